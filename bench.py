@@ -1,0 +1,192 @@
+#!/usr/bin/env python
+"""bench.py -- MPix/s fwd+bwd of the MI355X rasterizer on BASELINE.json's headline config.
+
+Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): 1.5M synthetic Gaussians, SH degree 3,
+1920x1080, one rasterizer forward + backward per step through the drop-in
+diff_gaussian_rasterization._C (libgsr.so, hand-written gfx950 HIP).  With --gpus N > 1 (one
+process per GPU, launched by torch.distributed.run) every rank renders its own view of its own
+scene shard-seed (weak scaling: view-parallel data parallelism) and the per-Gaussian
+gradients of the step are summed over ranks with one RCCL all-reduce.
+
+Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * W * H / step time (max over
+ranks).  roofline: the dominant kernel (stage) by HIP-event time inside the timed region, with
+its algorithmic bytes per launch / its average duration.  cpu_baseline: the C
+oracle (oracle/, a scalar port of the reference algorithm) timed on this host on a bounded
+sample (full preprocess + binning + preprocess backward, render fwd+bwd on 64 random tiles,
+extrapolated by tile count).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "relightable3dgaussians-w_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+METRIC = "MPix/s fwd+bwd, 1.5M Gaussians @1080p; train iters/s at 1/2/4/8 GPUs"
+
+
+def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
+    """SURVEY §8d per-stage compulsory HBM bytes (each array touched once)."""
+    S = 12 * M if M else 12
+    return {
+        "preprocess": P * 12 + Pv * (32 + S) + P * 8 + Pv * 67,
+        "render_fwd": T * 8 + R * 40 + Npix * 20,
+        "render_bwd": T * 8 + R * 40 + Npix * 20 + Pv * 44,
+        "preprocess_bwd": P * 4 + Pv * (12 + 12 + 12 + 12 + 3 + 12 + 16 + 24 + 12 * M) + Pv * (12 + 12 + 16 + 12 * M),
+        "tile_sort": R * 24,
+        "duplicate": P * 4 + Pv * 16 + R * 12,
+    }.get(stage)
+
+
+def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
+    from oracle import oracle as orc
+    n = lambda t: t.detach().cpu().numpy().astype(np.float32)
+    W, H = cam.image_width, cam.image_height
+    bg = np.zeros(3, np.float32)
+    t0 = time.perf_counter()
+    geom = orc.preprocess(n(gs_cpu["means3D"]), n(gs_cpu["scales"]), n(gs_cpu["rotations"]),
+                          n(gs_cpu["opacities"]).reshape(-1), n(gs_cpu["shs"]), None, None, n(cam.world_view_transform),
+                          n(cam.full_proj_transform), n(cam.camera_center), W, H, cam.tanfovx, cam.tanfovy, 1.0, deg)
+    R, keys, vals, ranges = orc.binning(geom, W, H)
+    t1 = time.perf_counter()
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    T = gx * gy
+    tiles = np.random.default_rng(seed).choice(T, size=min(ntiles, T), replace=False).astype(np.int32)
+    t2 = time.perf_counter()
+    color, fT, nc = orc.render_fwd(ranges, vals, geom["means2D"], geom["rgb"], geom["conic_opacity"], bg, W, H,
+                                   tiles=tiles)
+    g = orc.render_bwd(geom["radii"].shape[0], ranges, vals, bg, geom["means2D"], geom["conic_opacity"], geom["rgb"],
+                       fT, nc, dout_np, W, H, tiles=tiles)
+    t3 = time.perf_counter()
+    fwd = dict(geom)
+    fwd["cov3D_used"] = geom["cov3D"]
+    orc.preprocess_bwd(fwd, n(gs_cpu["means3D"]), n(gs_cpu["shs"]), deg, n(gs_cpu["scales"]), n(gs_cpu["rotations"]),
+                       1.0, n(cam.world_view_transform), n(cam.full_proj_transform), W, H, cam.tanfovx, cam.tanfovy,
+                       n(cam.camera_center), g["dL_dmean2D"], g["dL_dconic"], g["dL_dcolors"])
+    t4 = time.perf_counter()
+    est = (t1 - t0) + (t3 - t2) * T / len(tiles) + (t4 - t3)
+    return dict(value=W * H / est / 1e6, unit="MPix/s", cores=1, kind="port",
+                sample=(f"cfg2 ({gs_cpu['means3D'].shape[0]} Gaussians, {W}x{H}, SH{deg}): full preprocess + binning "
+                        f"(R={R}) + preprocess backward, render fwd+bwd on {len(tiles)}/{T} random tiles (seed {seed}) "
+                        f"extrapolated by tile count; single-threaded C oracle; measured {t4 - t0:.1f} s"),
+                seconds_estimated_full=est)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--P", type=int, default=None)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-tiles", type=int, default=64)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from diff_gaussian_rasterization import _C
+    from gsr import _lib, scenes
+
+    cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
+    W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
+    P = gs_cpu["means3D"].shape[0]
+    g = {k: v.to(dev) for k, v in gs_cpu.items()}
+    M = g["shs"].shape[1]
+    e = torch.empty(0, device=dev)
+    bg = torch.zeros(3, device=dev)
+    vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
+    gen = torch.Generator().manual_seed(1)
+    dout_cpu = torch.randn(3, H, W, generator=gen)
+    dout = dout_cpu.to(dev)
+    state = {}
+
+    def step():
+        R, color, radii, geom, binb, img = _C.rasterize_gaussians(
+            bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx,
+            cam.tanfovy, H, W, g["shs"], deg, cp, False)
+        grads = _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm,
+                                                pm, cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb,
+                                                img)
+        if dist is not None:
+            # one bucket: dL/d(means3D, sh, opacity, scales, rotations) summed over the view-parallel ranks
+            flat = torch.cat([grads[3].reshape(-1), grads[5].reshape(-1), grads[2].reshape(-1),
+                              grads[6].reshape(-1), grads[7].reshape(-1)])
+            dist.all_reduce(flat)
+        state["R"], state["radii"] = R, radii
+        return grads
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    _lib.profile_read(reset=True)
+    _lib.profile_enable(True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    t1 = time.perf_counter()
+    _lib.profile_enable(False)
+    stages = _lib.profile_read(reset=True)
+    ms = (t1 - t0) * 1e3 / args.steps
+    if dist is not None:
+        t = torch.tensor([ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+
+    R = int(state["R"])
+    Pv = int((state["radii"] > 0).sum().item())
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    per_stage = {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1] > 0}
+    dom = max(((k, v[0] / max(v[1], 1)) for k, v in stages.items() if v[1] > 0 and
+               algorithmic_bytes(k, P, Pv, R, T, W * H, M) is not None), key=lambda kv: kv[1])
+    dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
+    achieved = dom_bytes / (dom[1] * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom[0],
+                "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom[1], 4)}
+    out = {
+        "metric": METRIC, "value": round(world * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"{args.config}: {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view"
+                   + (", RCCL grad all-reduce" if world > 1 else ""), "gaussians": P, "width": W, "height": H,
+                   "sh_degree": deg, "num_rendered": R, "visible": Pv, "parallelism": f"views x{world}"},
+        "roofline": roofline,
+        "stage_ms": per_stage,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb = cpu_baseline(cam, gs_cpu, M, deg, dout_cpu.numpy(), ntiles=args.cpu_tiles)
+        out["cpu_baseline"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cb.items()
+                               if k != "seconds_estimated_full"}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,119 @@
+/*
+ * gsr.h -- C ABI of libgsr.so, the MI355X-native (gfx950) differentiable Gaussian
+ * rasterizer and relighting shade.  Plain pointers and sizes only; every float / int
+ * pointer is DEVICE memory unless stated; `stream` is a hipStream_t (NULL = default).
+ *
+ * Each entry point replaces one reference interface (paths relative to the reference
+ * checkout, submodules/diff-gaussian-rasterization/ abbreviated "dgr/"):
+ *
+ *   gsr_forward        dgr/cuda_rasterizer/rasterizer.h:33-55  Rasterizer::forward
+ *                      (driven from dgr/rasterize_points.cu:35-113 RasterizeGaussiansCUDA)
+ *   gsr_backward       dgr/cuda_rasterizer/rasterizer.h:57-82  Rasterizer::backward
+ *                      (driven from dgr/rasterize_points.cu:115-192)
+ *   gsr_mark_visible   dgr/cuda_rasterizer/rasterizer.h:23-29  Rasterizer::markVisible
+ *                      (dgr/rasterize_points.cu:194-213)
+ *   gsr_shade_forward  scene/NVDIFFREC/light.py:131-193 EnvironmentLight.shade (forward)
+ *   gsr_shade_backward autograd backward of the same (PyTorch + nvdiffrast in the reference)
+ *
+ * Error convention: every function returns 0 on success and a negative GSR_E* code on
+ * failure; gsr_last_error() returns a thread-local message.  The reference's conditions
+ * map as follows: AT_ERROR on a bad means3D shape is raised by the host wrapper; a
+ * prefiltered point that fails the near test (the reference's device printf + __trap,
+ * auxiliary.h:156-160) returns GSR_E_PREFILTERED instead of killing the context.
+ */
+#ifndef GSR_H_INCLUDED
+#define GSR_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_OK 0
+#define GSR_E_HIP (-1)
+#define GSR_E_ARG (-2)
+#define GSR_E_PREFILTERED (-3)
+#define GSR_E_ALLOC (-4)
+#define GSR_E_OVERFLOW (-5)
+
+/* Buffer growth callback: must return a device pointer to at least `nbytes` bytes that
+ * stays valid until the matching backward call (the reference's resizeFunctional,
+ * dgr/rasterize_points.cu:27-33, which resizes a torch uint8 tensor). */
+typedef void* (*gsr_resize_fn)(void* ctx, size_t nbytes);
+
+/* Forward rasterization.  Absent inputs are NULL (the reference passes empty tensors,
+ * i.e. nullptr data pointers).  out_color [3,H,W] and radii [P] are fully written.
+ * *num_rendered receives R, the number of (Gaussian, tile) instances. */
+int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer, void* binning_ctx,
+                gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M, const float* background, int width,
+                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                float tan_fovx, float tan_fovy, int prefiltered, float* out_color, int* radii, void* stream,
+                int* num_rendered);
+
+/* Backward rasterization.  geom/binning/img buffers are the ones the forward filled.
+ * dL_dpix is [3,H,W].  All nine gradient outputs are fully written (no zero-fill needed):
+ * dL_dmean2D [P,3] (z = 0), dL_dconic [P,2,2], dL_dopacity [P], dL_dcolor [P,3],
+ * dL_dmean3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3] (may be NULL if M == 0),
+ * dL_dscale [P,3], dL_drot [P,4]. */
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                 void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                 float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream);
+
+/* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+/* Relighting shade for N foreground Gaussians (light.py:131-193).  pos, normal, albedo,
+ * view_pos: [N,3]; kr: [N]; km: [N] or NULL (F0 = 0.04); base: [(deg+1)^2, 3];
+ * fg_lut: [256,256,2] (the split-sum LUT).  Outputs rgb, diffuse, specular: [N,3]. */
+int gsr_shade_forward(int N, int deg, const float* pos, const float* normal, const float* albedo,
+                      const float* view_pos, const float* kr, const float* km, const float* base,
+                      const float* fg_lut, int specular, float* rgb, float* diffuse, float* specular_out,
+                      void* stream);
+
+/* Backward of gsr_shade_forward given upstream gradients g_rgb, g_diffuse, g_specular
+ * ([N,3] each, any may be NULL = zero).  Outputs (any may be NULL = not needed):
+ * d_pos, d_normal, d_albedo, d_view_pos [N,3]; d_kr, d_km [N]; d_base [(deg+1)^2,3]
+ * (reduced over N; fully written).  `workspace` must hold gsr_shade_workspace_bytes(N, deg)
+ * bytes of device memory. */
+size_t gsr_shade_workspace_bytes(int N, int deg);
+int gsr_shade_backward(int N, int deg, const float* pos, const float* normal, const float* albedo,
+                       const float* view_pos, const float* kr, const float* km, const float* base,
+                       const float* fg_lut, int specular, const float* g_rgb, const float* g_diffuse,
+                       const float* g_specular, float* d_pos, float* d_normal, float* d_albedo, float* d_view_pos,
+                       float* d_kr, float* d_km, float* d_base, void* workspace, void* stream);
+
+/* Private-buffer introspection for tests and profiling: byte offsets of the arrays the
+ * forward leaves in its three buffers (layout is private between forward and backward). */
+typedef struct gsr_layout {
+    size_t geom_bytes, img_bytes, bin_bytes;
+    size_t geom_radii, geom_tiles, geom_depth_key, geom_rect, geom_rec, geom_acc;
+    size_t img_final_T, img_n_contrib, img_ranges;
+    size_t bin_point_list, bin_tile_keys;
+} gsr_layout;
+int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
+
+/* Stage profiling: when enabled, every stage (preprocess, compact, depth_sort, offsets_scan,
+ * duplicate, tile_sort, ranges, render_fwd, bwd_zero, render_bwd, preprocess_bwd, shade_fwd,
+ * shade_bwd) is bracketed by hipEvents on the call's stream.  gsr_profile_read() waits for
+ * the recorded events and returns accumulated milliseconds and launch counts per stage. */
+int gsr_profile_enable(int on);
+int gsr_profile_stage_count(void);
+const char* gsr_profile_stage_name(int i);
+int gsr_profile_read(double* ms, long long* counts, int n, int reset);
+
+const char* gsr_last_error(void);
+const char* gsr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSR_H_INCLUDED */

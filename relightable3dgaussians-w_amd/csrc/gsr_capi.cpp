@@ -1,0 +1,500 @@
+// gsr_capi.cpp -- C ABI (include/gsr.h): buffer layout and stage orchestration of the
+// forward / backward rasterizer (rasterizer_impl.cu:198-433 re-designed):
+//
+//   forward:  preprocess -> visibility compaction (+ R and P_v totals) -> ONE D2H sync
+//             -> depth sort of the P_v visible Gaussians (32-bit keys, 4 passes)
+//             -> depth-order exclusive scan of tiles_touched -> instance emission
+//             -> stable tile-id sort of the R instances (ceil(log2 T / 8) passes)
+//             -> tile ranges -> LDS-staged tile compositing
+//   backward: zero the per-Gaussian accumulator -> tile replay -> fused per-Gaussian
+//             cov2D / projection / SH / cov3D backward writing all nine outputs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gsr.h"
+#include "gsr_kernels.hpp"
+#include "gsr_shade.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+}  // namespace
+
+int gsr_fail_hip(hipError_t e, int line) {
+    return fail(GSR_E_HIP, "HIP error %d (%s) at gsr_capi.cpp:%d", (int)e, hipGetErrorString(e), line);
+}
+
+namespace {
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+
+struct Carver {
+    size_t o = 0;
+    size_t take(size_t bytes) {
+        const size_t r = o;
+        o = align_up(o + bytes, 256);
+        return r;
+    }
+};
+
+struct GeomLayout {
+    size_t totals, radii, tiles, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, offsets,
+        scan_tmp, sort_tmp, total;
+};
+struct ImgLayout {
+    size_t final_T, n_contrib, ranges, total;
+};
+struct BinLayout {
+    size_t tile_keys, tile_keys_alt, point, point_alt, sort_tmp, total;
+};
+
+GeomLayout geom_layout(long long P) {
+    Carver c;
+    GeomLayout L;
+    L.totals = c.take(64);
+    L.radii = c.take(4 * P);
+    L.tiles = c.take(4 * P);
+    L.depth_key = c.take(4 * P);
+    L.rect = c.take(8 * P);
+    L.rec = c.take(sizeof(gsr::Rec) * P);
+    L.acc = c.take(4 * gsr::ACC_STRIDE * P);
+    L.vis_key = c.take(4 * P);
+    L.vis_val = c.take(4 * P);
+    L.vis_key_alt = c.take(4 * P);
+    L.vis_val_alt = c.take(4 * P);
+    L.offsets = c.take(4 * P);
+    L.scan_tmp = c.take(16 * (size_t)gsr::scan_blocks(P) + 16);
+    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(P));
+    L.total = c.o + 256;
+    return L;
+}
+
+unsigned tiles_x(int W) { return (unsigned)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X); }
+unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y); }
+
+ImgLayout img_layout(int W, int H) {
+    Carver c;
+    ImgLayout L;
+    const size_t N = (size_t)W * H;
+    const size_t T = (size_t)tiles_x(W) * tiles_y(H);
+    L.final_T = c.take(4 * N);
+    L.n_contrib = c.take(4 * N);
+    L.ranges = c.take(8 * T);
+    L.total = c.o + 256;
+    return L;
+}
+
+BinLayout bin_layout(long long R) {
+    Carver c;
+    BinLayout L;
+    L.tile_keys = c.take(4 * R);
+    L.tile_keys_alt = c.take(4 * R);
+    L.point = c.take(4 * R);
+    L.point_alt = c.take(4 * R);
+    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(R));
+    L.total = c.o + 256;
+    return L;
+}
+
+// rasterizer_impl.cu:35-50
+uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4;
+    uint32_t step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step;
+        else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+int tile_sort_bits(int W, int H) { return (int)higher_msb(tiles_x(W) * tiles_y(H)); }
+
+// where the tile-sorted instance list ends up (the sort ping-pongs)
+bool point_list_in_alt(long long R, int W, int H) {
+    const int bits = tile_sort_bits(W, H);
+    if (R <= 1 || bits <= 0) return false;
+    return (((bits + 7) / 8) & 1) == 1;
+}
+
+template <typename T>
+T* at(void* base, size_t off) {
+    return reinterpret_cast<T*>(reinterpret_cast<char*>(base) + off);
+}
+
+char* align_base(void* p) { return reinterpret_cast<char*>(align_up(reinterpret_cast<size_t>(p), 256)); }
+
+struct PinnedHost {
+    unsigned long long* p = nullptr;
+    ~PinnedHost() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+thread_local PinnedHost g_pinned;
+
+#define HIP_OK(x)                                              \
+    do {                                                       \
+        hipError_t _e = (x);                                   \
+        if (_e != hipSuccess) return gsr_fail_hip(_e, __LINE__); \
+    } while (0)
+
+// ---- stage profiling: hipEvents recorded on the call's stream around each stage ----------
+enum Stage {
+    ST_PREPROCESS, ST_COMPACT, ST_DEPTH_SORT, ST_OFFSETS, ST_DUPLICATE, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD,
+    ST_BWD_ZERO, ST_RENDER_BWD, ST_PREPROCESS_BWD, ST_SHADE_FWD, ST_SHADE_BWD, ST_COUNT
+};
+const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "duplicate",
+                                     "tile_sort",   "ranges",       "render_fwd",     "bwd_zero",     "render_bwd",
+                                     "preprocess_bwd", "shade_fwd", "shade_bwd"};
+struct Prof {
+    bool on = false;
+    std::vector<hipEvent_t> pool;
+    struct Rec { hipEvent_t a, b; int stage; };
+    std::vector<Rec> pending;
+    double ms[ST_COUNT] = {0};
+    long long n[ST_COUNT] = {0};
+    hipEvent_t get() {
+        if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+        hipEvent_t e;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+};
+Prof g_prof;
+
+struct StageTimer {
+    hipEvent_t a = nullptr;
+    int stage;
+    hipStream_t s;
+    StageTimer(int st, hipStream_t ss) : stage(st), s(ss) {
+        if (g_prof.on) { a = g_prof.get(); (void)hipEventRecord(a, s); }
+    }
+    ~StageTimer() {
+        if (a) {
+            hipEvent_t b = g_prof.get();
+            (void)hipEventRecord(b, s);
+            g_prof.pending.push_back({a, b, stage});
+        }
+    }
+};
+#define GSR_STAGE(st) StageTimer _timer_##st(st, s)
+
+}  // namespace
+
+extern "C" {
+
+const char* gsr_last_error(void) { return g_err.c_str(); }
+
+const char* gsr_version(void) { return "gsr 0.1 gfx950"; }
+
+int gsr_profile_enable(int on) {
+    g_prof.on = on != 0;
+    return GSR_OK;
+}
+
+int gsr_profile_stage_count(void) { return ST_COUNT; }
+
+const char* gsr_profile_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : ""; }
+
+int gsr_profile_read(double* ms, long long* counts, int n, int reset) {
+    for (auto& r : g_prof.pending) {
+        HIP_OK(hipEventSynchronize(r.b));
+        float t = 0.f;
+        HIP_OK(hipEventElapsedTime(&t, r.a, r.b));
+        g_prof.ms[r.stage] += t;
+        g_prof.n[r.stage] += 1;
+        g_prof.pool.push_back(r.a);
+        g_prof.pool.push_back(r.b);
+    }
+    g_prof.pending.clear();
+    for (int i = 0; i < n && i < ST_COUNT; i++) {
+        if (ms) ms[i] = g_prof.ms[i];
+        if (counts) counts[i] = g_prof.n[i];
+    }
+    if (reset)
+        for (int i = 0; i < ST_COUNT; i++) { g_prof.ms[i] = 0; g_prof.n[i] = 0; }
+    return GSR_OK;
+}
+
+int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
+    if (!out || P < 0 || R < 0 || width < 0 || height < 0) return fail(GSR_E_ARG, "gsr_get_layout: bad arguments");
+    const GeomLayout g = geom_layout(P);
+    const ImgLayout im = img_layout(width, height);
+    const BinLayout b = bin_layout(R);
+    out->geom_bytes = g.total;
+    out->img_bytes = im.total;
+    out->bin_bytes = b.total;
+    out->geom_radii = g.radii;
+    out->geom_tiles = g.tiles;
+    out->geom_depth_key = g.depth_key;
+    out->geom_rect = g.rect;
+    out->geom_rec = g.rec;
+    out->geom_acc = g.acc;
+    out->img_final_T = im.final_T;
+    out->img_n_contrib = im.n_contrib;
+    out->img_ranges = im.ranges;
+    out->bin_point_list = point_list_in_alt(R, width, height) ? b.point_alt : b.point;
+    out->bin_tile_keys = point_list_in_alt(R, width, height) ? b.tile_keys_alt : b.tile_keys;
+    return GSR_OK;
+}
+
+int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer, void* binning_ctx,
+                gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M, const float* background, int width,
+                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                float tan_fovx, float tan_fovy, int prefiltered, float* out_color, int* radii, void* stream_,
+                int* num_rendered) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    if (num_rendered) *num_rendered = 0;
+    if (P < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_forward: bad sizes P=%d W=%d H=%d", P, width, height);
+    if (!geometry_buffer || !binning_buffer || !image_buffer) return fail(GSR_E_ARG, "gsr_forward: missing buffer callbacks");
+    if (!colors_precomp && !shs && P > 0)
+        return fail(GSR_E_ARG, "For non-RGB, provide precomputed Gaussian colors!");
+    if (!cov3D_precomp && (!scales || !rotations) && P > 0)
+        return fail(GSR_E_ARG, "gsr_forward: need scales+rotations or cov3D_precomp");
+    if (tiles_x(width) > 65535u || tiles_y(height) > 65535u) return fail(GSR_E_ARG, "gsr_forward: image too large");
+
+    // rasterizer_impl.cu:221-222 (host float arithmetic == device float arithmetic)
+    const float focal_y = height / (2.0f * tan_fovy);
+    const float focal_x = width / (2.0f * tan_fovx);
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(width, height);
+    char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
+    char* img = reinterpret_cast<char*>(image_buffer(image_ctx, il.total));
+    if (!geom || !img) return fail(GSR_E_ALLOC, "gsr_forward: buffer allocation failed");
+    geom = align_base(geom);
+    img = align_base(img);
+    const unsigned gx = tiles_x(width), gy = tiles_y(height);
+    const int T = (int)(gx * gy);
+    if (!radii) radii = at<int>(geom, gl.radii);
+
+    unsigned long long* totals = at<unsigned long long>(geom, gl.totals);
+    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 2);
+    HIP_OK(hipMemsetAsync(err_flag, 0, 4, s));
+
+    gsr::PreprocessArgs pa;
+    pa.P = P; pa.D = D; pa.M = M;
+    pa.means3D = means3D; pa.scales = scales; pa.scale_modifier = scale_modifier; pa.rotations = rotations;
+    pa.opacities = opacities; pa.shs = shs; pa.cov3D_precomp = cov3D_precomp; pa.colors_precomp = colors_precomp;
+    pa.viewmatrix = viewmatrix; pa.projmatrix = projmatrix; pa.campos = cam_pos;
+    pa.W = width; pa.H = height; pa.tan_fovx = tan_fovx; pa.tan_fovy = tan_fovy;
+    pa.focal_x = focal_x; pa.focal_y = focal_y; pa.grid_x = gx; pa.grid_y = gy; pa.prefiltered = prefiltered;
+    pa.radii = radii;
+    pa.tiles = at<uint32_t>(geom, gl.tiles);
+    pa.depth_key = at<uint32_t>(geom, gl.depth_key);
+    pa.rect = at<uint2>(geom, gl.rect);
+    pa.rec = at<gsr::Rec>(geom, gl.rec);
+    pa.err_flag = err_flag;
+    {
+        GSR_STAGE(ST_PREPROCESS);
+        gsr::launch_preprocess(pa, s);
+    }
+    GSR_LAUNCH_CHECK();
+
+    uint32_t* vis_key = at<uint32_t>(geom, gl.vis_key);
+    uint32_t* vis_val = at<uint32_t>(geom, gl.vis_val);
+    {
+        GSR_STAGE(ST_COMPACT);
+        gsr::launch_compact_visible(P, pa.tiles, pa.depth_key, vis_key, vis_val,
+                                    at<unsigned long long>(geom, gl.scan_tmp), totals, s);
+    }
+    GSR_LAUNCH_CHECK();
+
+    if (!g_pinned.p) HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 64, hipHostMallocDefault));
+    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, 24, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    const unsigned long long Pv = g_pinned.p[0], R64 = g_pinned.p[1];
+    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 2)[0];
+    if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
+    const long long R = (long long)R64;
+
+    const BinLayout bl = bin_layout(R);
+    char* bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
+    if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
+    bin = align_base(bin);
+
+    // depth sort of the visible Gaussians (stable: ties keep index order)
+    int flip;
+    {
+        GSR_STAGE(ST_DEPTH_SORT);
+        flip = gsr::radix_sort_pairs((long long)Pv, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
+                                     at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s);
+    }
+    GSR_LAUNCH_CHECK();
+    const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
+    uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
+    {
+        GSR_STAGE(ST_OFFSETS);
+        gsr::launch_exclusive_scan_u32((long long)Pv, pa.tiles, sorted_ids, offsets,
+                                       at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
+    }
+    GSR_LAUNCH_CHECK();
+    uint32_t* tk = at<uint32_t>(bin, bl.tile_keys);
+    uint32_t* pt = at<uint32_t>(bin, bl.point);
+    {
+        GSR_STAGE(ST_DUPLICATE);
+        gsr::launch_duplicate((int)Pv, sorted_ids, offsets, pa.rect, gx, tk, pt, s);
+    }
+    GSR_LAUNCH_CHECK();
+    const int bits = tile_sort_bits(width, height);
+    int flip2;
+    {
+        GSR_STAGE(ST_TILE_SORT);
+        flip2 = gsr::radix_sort_pairs(R, tk, pt, at<uint32_t>(bin, bl.tile_keys_alt), at<uint32_t>(bin, bl.point_alt),
+                                      bits, at<void>(bin, bl.sort_tmp), s);
+    }
+    GSR_LAUNCH_CHECK();
+    if ((flip2 != 0) != point_list_in_alt(R, width, height)) return fail(GSR_E_ARG, "internal: sort parity mismatch");
+    const uint32_t* point_list = flip2 ? at<uint32_t>(bin, bl.point_alt) : pt;
+    const uint32_t* sorted_tiles = flip2 ? at<uint32_t>(bin, bl.tile_keys_alt) : tk;
+    uint2* ranges = at<uint2>(img, il.ranges);
+    {
+        GSR_STAGE(ST_RANGES);
+        gsr::launch_ranges(R, T, sorted_tiles, ranges, s);
+    }
+    GSR_LAUNCH_CHECK();
+
+    gsr::RenderFwdArgs ra;
+    ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
+    ra.ranges = ranges; ra.point_list = point_list; ra.rec = pa.rec; ra.bg = background;
+    ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
+    {
+        GSR_STAGE(ST_RENDER_FWD);
+        gsr::launch_render_fwd(ra, s);
+    }
+    GSR_LAUNCH_CHECK();
+    if (num_rendered) *num_rendered = (int)R;
+    return GSR_OK;
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                 void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                 float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream_) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    if (P < 0 || R < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_backward: bad sizes");
+    if (P == 0) return GSR_OK;
+    if (!geom_buffer || !img_buffer || (R > 0 && !binning_buffer)) return fail(GSR_E_ARG, "gsr_backward: missing buffers");
+    const float focal_y = height / (2.0f * tan_fovy);
+    const float focal_x = width / (2.0f * tan_fovx);
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(width, height);
+    const BinLayout bl = bin_layout(R);
+    char* geom = align_base(geom_buffer);
+    char* img = align_base(img_buffer);
+    char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
+    const unsigned gx = tiles_x(width), gy = tiles_y(height);
+    if (!radii) radii = at<int>(geom, gl.radii);
+    float* acc = at<float>(geom, gl.acc);
+    {
+        GSR_STAGE(ST_BWD_ZERO);
+        HIP_OK(hipMemsetAsync(acc, 0, sizeof(float) * gsr::ACC_STRIDE * (size_t)P, s));
+    }
+
+    if (R > 0) {
+        gsr::RenderBwdArgs ra;
+        ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
+        ra.ranges = at<uint2>(img, il.ranges);
+        ra.point_list = point_list_in_alt(R, width, height) ? at<uint32_t>(bin, bl.point_alt) : at<uint32_t>(bin, bl.point);
+        ra.rec = at<gsr::Rec>(geom, gl.rec);
+        ra.colors = colors_precomp;
+        ra.bg = background;
+        ra.final_T = at<float>(img, il.final_T);
+        ra.n_contrib = at<uint32_t>(img, il.n_contrib);
+        ra.dL_dpix = dL_dpix;
+        ra.acc = acc;
+        {
+            GSR_STAGE(ST_RENDER_BWD);
+            gsr::launch_render_bwd(ra, s);
+        }
+        GSR_LAUNCH_CHECK();
+    }
+    gsr::PreprocessBwdArgs pb;
+    pb.P = P; pb.D = D; pb.M = M;
+    pb.means3D = means3D; pb.radii = radii; pb.shs = shs; pb.scales = scales; pb.rotations = rotations;
+    pb.scale_modifier = scale_modifier; pb.cov3D_precomp = cov3D_precomp;
+    pb.viewmatrix = viewmatrix; pb.projmatrix = projmatrix; pb.campos = campos;
+    pb.tan_fovx = tan_fovx; pb.tan_fovy = tan_fovy; pb.focal_x = focal_x; pb.focal_y = focal_y;
+    pb.acc = acc;
+    pb.dL_dmean2D = dL_dmean2D; pb.dL_dconic = dL_dconic; pb.dL_dopacity = dL_dopacity; pb.dL_dcolor = dL_dcolor;
+    pb.dL_dmean3D = dL_dmean3D; pb.dL_dcov3D = dL_dcov3D; pb.dL_dsh = M > 0 ? dL_dsh : nullptr;
+    pb.dL_dscale = dL_dscale; pb.dL_drot = dL_drot;
+    if ((dL_dscale == nullptr) != (dL_drot == nullptr)) return fail(GSR_E_ARG, "gsr_backward: dL_dscale/dL_drot must both be given");
+    {
+        GSR_STAGE(ST_PREPROCESS_BWD);
+        gsr::launch_preprocess_bwd(pb, s);
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
+                     void* stream_) {
+    (void)projmatrix;
+    if (P < 0) return fail(GSR_E_ARG, "gsr_mark_visible: bad P");
+    gsr::launch_mark_visible(P, means3D, viewmatrix, reinterpret_cast<bool*>(present),
+                             reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+size_t gsr_shade_workspace_bytes(int N, int deg) { return gsr::shade_workspace_bytes(N, deg); }
+
+int gsr_shade_forward(int N, int deg, const float* pos, const float* normal, const float* albedo,
+                      const float* view_pos, const float* kr, const float* km, const float* base,
+                      const float* fg_lut, int specular, float* rgb, float* diffuse, float* specular_out,
+                      void* stream_) {
+    if (N < 0 || deg < 2 || deg > 5) return fail(GSR_E_ARG, "gsr_shade_forward: bad N=%d deg=%d (2..5: the diffuse term reads base[0..8])", N, deg);
+    if (N == 0) return GSR_OK;
+    gsr::ShadeArgs a{N, deg, pos, normal, albedo, view_pos, kr, km, base, fg_lut, specular};
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    {
+        GSR_STAGE(ST_SHADE_FWD);
+        gsr::launch_shade_fwd(a, rgb, diffuse, specular_out, s);
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_shade_backward(int N, int deg, const float* pos, const float* normal, const float* albedo,
+                       const float* view_pos, const float* kr, const float* km, const float* base,
+                       const float* fg_lut, int specular, const float* g_rgb, const float* g_diffuse,
+                       const float* g_specular, float* d_pos, float* d_normal, float* d_albedo, float* d_view_pos,
+                       float* d_kr, float* d_km, float* d_base, void* workspace, void* stream_) {
+    if (N < 0 || deg < 2 || deg > 5) return fail(GSR_E_ARG, "gsr_shade_backward: bad N=%d deg=%d (2..5)", N, deg);
+    gsr::ShadeArgs a{N, deg, pos, normal, albedo, view_pos, kr, km, base, fg_lut, specular};
+    gsr::ShadeGrads g{g_rgb, g_diffuse, g_specular, d_pos, d_normal, d_albedo, d_view_pos, d_kr, d_km, d_base};
+    if (d_base && !workspace && N > 0) return fail(GSR_E_ARG, "gsr_shade_backward: workspace required for d_base");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    {
+        GSR_STAGE(ST_SHADE_BWD);
+        gsr::launch_shade_bwd(a, g, workspace, s);
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,74 @@
+// gsr_common.hpp -- shared device helpers for the MI355X (gfx950) Gaussian rasterizer.
+//
+// The preprocess / binning math must be bit-identical to the reference's
+// (cuda_rasterizer/auxiliary.h, forward.cu) as restated in oracle/gsr_oracle.c, so every
+// translation unit that includes this header with GSR_EXACT defined compiles its float
+// arithmetic with FMA contraction off and IEEE (correctly rounded) div/sqrt.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GSR_BLOCK_X 16
+#define GSR_BLOCK_Y 16
+#define GSR_TILE_PIX 256
+
+namespace gsr {
+
+// auxiliary.h:22-39 (same decimal literals as the reference)
+__device__ constexpr float SH_C0 = 0.28209479177387814f;
+__device__ constexpr float SH_C1 = 0.4886025119029199f;
+__device__ constexpr float SH_C2_0 = 1.0925484305920792f;
+__device__ constexpr float SH_C2_1 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_2 = 0.31539156525252005f;
+__device__ constexpr float SH_C2_3 = -1.0925484305920792f;
+__device__ constexpr float SH_C2_4 = 0.5462742152960396f;
+__device__ constexpr float SH_C3_0 = -0.5900435899266435f;
+__device__ constexpr float SH_C3_1 = 2.890611442640554f;
+__device__ constexpr float SH_C3_2 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_3 = 0.3731763325901154f;
+__device__ constexpr float SH_C3_4 = -0.4570457994644658f;
+__device__ constexpr float SH_C3_5 = 1.445305721320277f;
+__device__ constexpr float SH_C3_6 = -0.5900435899266435f;
+
+// Render record: one 48-byte row per Gaussian, written by preprocess, gathered by the
+// tile passes into LDS.  a = (x, y, conic.a, conic.b), b = (conic.c, opacity, r, g),
+// c = (b, ln(255*opacity), 0, 0).
+struct __align__(16) Rec {
+    float4 a, b, c;
+};
+
+// Per-Gaussian gradient accumulator line (64 B, one atomic request per line):
+// [0] dL/dmean2D.x [1] .y [2] dL/dconic.x [3] .y [4] .w [5] dL/dopacity [6..8] dL/dcolor
+constexpr int ACC_STRIDE = 16;
+
+// float -> int exactly as v_cvt_i32_f32 / the reference's implicit conversions
+// (forward.cu:235, :251): truncation, saturation, NaN -> 0.
+__device__ __forceinline__ int f2i(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483647.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)v;
+}
+
+// glm::mat3, column-major m[c][r]
+struct M3 {
+    float m[3][3];
+};
+
+__device__ __forceinline__ M3 mcols(float a0, float a1, float a2, float b0, float b1, float b2, float c0, float c1,
+                                    float c2) {
+    M3 R;
+    R.m[0][0] = a0; R.m[0][1] = a1; R.m[0][2] = a2;
+    R.m[1][0] = b0; R.m[1][1] = b1; R.m[1][2] = b2;
+    R.m[2][0] = c0; R.m[2][1] = c1; R.m[2][2] = c2;
+    return R;
+}
+
+}  // namespace gsr
+
+// HIP error plumbing for the C ABI (gsr_capi.cpp)
+#define GSR_LAUNCH_CHECK()                                       \
+    do {                                                         \
+        hipError_t _e = hipGetLastError();                       \
+        if (_e != hipSuccess) return gsr_fail_hip(_e, __LINE__); \
+    } while (0)

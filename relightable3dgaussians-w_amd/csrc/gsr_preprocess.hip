@@ -1,0 +1,92 @@
+// gsr_preprocess.hip -- forward per-Gaussian preprocess (forward.cu:155-256) and
+// checkFrustum (rasterizer_impl.cu:54-66), re-designed for gfx950:
+//  * one thread per Gaussian, 256-thread blocks (4 waves of 64);
+//  * camera matrices are wave-uniform scalar loads;
+//  * output is one packed 48-B render record per Gaussian (Rec) + a 32-bit depth key
+//    + a packed tile rect, so the binning and tile passes gather one row per Gaussian;
+//  * FMA contraction is OFF in this TU: radii, rects, depths, conics and SH colours are
+//    bit-identical to oracle/gsr_oracle.c (the reference's op order).
+#pragma clang fp contract(off)
+#include "gsr_exact.hpp"
+#include "gsr_kernels.hpp"
+
+namespace gsr {
+
+__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    a.radii[idx] = 0;
+    a.tiles[idx] = 0;
+    const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    // in_frustum (auxiliary.h:139-164): near cull only
+    const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
+    if (p_view.z <= 0.2f) {
+        if (a.prefiltered) atomicOr(a.err_flag, 1u);
+        return;
+    }
+    const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
+    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+    const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
+
+    float cov3[6];
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        const float4 rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        cov3d_from(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, rot, cov3);
+    }
+    const float3 cov = cov2d_from(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3, a.viewmatrix);
+    const float det = (cov.x * cov.z - cov.y * cov.y);
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+    const float mid = 0.5f * (cov.x + cov.z);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const float2 point_image = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
+    uint2 rmin, rmax;
+    const int irad = f2i(my_radius);
+    get_rect(point_image, irad, a.grid_x, a.grid_y, rmin, rmax);
+    const unsigned area = (rmax.x - rmin.x) * (rmax.y - rmin.y);
+    if (area == 0) return;
+
+    float3 rgb;
+    if (a.colors_precomp) {
+        rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
+    } else {
+        const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, a.shs + (size_t)idx * a.M * 3);
+        rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
+    }
+    const float opacity = a.opacities[idx];
+    Rec r;
+    r.a = make_float4(point_image.x, point_image.y, conic.x, conic.y);
+    r.b = make_float4(conic.z, opacity, rgb.x, rgb.y);
+    r.c = make_float4(rgb.z, __logf(255.0f * opacity), 0.f, 0.f);
+    a.rec[idx] = r;
+    a.depth_key[idx] = __float_as_uint(p_view.z);
+    a.rect[idx] = make_uint2(rmin.x | (rmax.x << 16), rmin.y | (rmax.y << 16));
+    a.radii[idx] = irad;
+    a.tiles[idx] = area;
+}
+
+__global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,
+                                                       bool* present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const float3 p = make_float3(means3D[3 * idx], means3D[3 * idx + 1], means3D[3 * idx + 2]);
+    present[idx] = !(xform_point4x3(p, viewmatrix).z <= 0.2f);
+}
+
+void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
+    if (a.P == 0) return;
+    hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+}
+
+void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_mark_visible, dim3((P + 255) / 256), dim3(256), 0, s, P, means3D, viewmatrix, present);
+}
+
+}  // namespace gsr

@@ -1,0 +1,312 @@
+// gsr_preprocess_bwd.hip -- fused per-Gaussian backward: computeCov2DCUDA
+// (backward.cu:144-274) + preprocessCUDA (backward.cu:346-396) with the SH backward
+// (:20-139) and the cov3D backward (:278-341), plus the unpacking of the render
+// backward's 64-B accumulator line into the reference's output tensors.
+//
+// One kernel instead of two + nine memsets: every output element is written here
+// (zeros for culled Gaussians), so the caller's buffers need no zero-fill.  cov3D and
+// the SH clamp flags are recomputed with the forward's exact (contraction-off) code
+// instead of being stored and re-read.
+#pragma clang fp contract(off)
+#include "gsr_exact.hpp"
+#include "gsr_kernels.hpp"
+
+namespace gsr {
+
+// auxiliary.h:107-117
+__device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
+    const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+    const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+    float3 o;
+    o.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+    o.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+    o.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+    return o;
+}
+
+__global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= a.P) return;
+    // ---- unpack the render-backward accumulator line ------------------------------
+    const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
+    const float4 l0 = line[0], l1 = line[1];
+    const float l2 = a.acc[(size_t)idx * ACC_STRIDE + 8];
+    const float dm2x = l0.x, dm2y = l0.y, dcx = l0.z, dcy = l0.w, dcw = l1.x, dop = l1.y;
+    const float dcol0 = l1.z, dcol1 = l1.w, dcol2 = l2;
+    a.dL_dmean2D[3 * idx + 0] = dm2x;
+    a.dL_dmean2D[3 * idx + 1] = dm2y;
+    a.dL_dmean2D[3 * idx + 2] = 0.f;
+    *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
+    a.dL_dopacity[idx] = dop;
+    a.dL_dcolor[3 * idx + 0] = dcol0;
+    a.dL_dcolor[3 * idx + 1] = dcol1;
+    a.dL_dcolor[3 * idx + 2] = dcol2;
+
+    float* dcov = a.dL_dcov3D + 6 * idx;
+    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * a.M * 3 : nullptr;
+    if (!(a.radii[idx] > 0)) {
+        a.dL_dmean3D[3 * idx + 0] = 0.f;
+        a.dL_dmean3D[3 * idx + 1] = 0.f;
+        a.dL_dmean3D[3 * idx + 2] = 0.f;
+#pragma unroll
+        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+        if (dsh)
+            for (int i = 0; i < a.M * 3; i++) dsh[i] = 0.f;
+        if (a.dL_dscale) {
+            a.dL_dscale[3 * idx + 0] = 0.f;
+            a.dL_dscale[3 * idx + 1] = 0.f;
+            a.dL_dscale[3 * idx + 2] = 0.f;
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
+    const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    float cov3[6];
+    float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
+    float3 scl = make_float3(0.f, 0.f, 0.f);
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        scl = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+        cov3d_from(scl.x, scl.y, scl.z, a.scale_modifier, rot, cov3);
+    }
+
+    // ---- computeCov2DCUDA (backward.cu:144-274) --------------------------------------
+    const float* v = a.viewmatrix;
+    const float h_x = a.focal_x, h_y = a.focal_y;
+    float3 t = xform_point4x3(mean, v);
+    const float limx = 1.3f * a.tan_fovx;
+    const float limy = 1.3f * a.tan_fovy;
+    const float txtz = t.x / t.z;
+    const float tytz = t.y / t.z;
+    t.x = fminf(limx, fmaxf(-limx, txtz)) * t.z;
+    t.y = fminf(limy, fmaxf(-limy, tytz)) * t.z;
+    const float x_grad_mul = txtz < -limx || txtz > limx ? 0.f : 1.f;
+    const float y_grad_mul = tytz < -limy || tytz > limy ? 0.f : 1.f;
+    const M3 J = mcols(h_x / t.z, 0.0f, -(h_x * t.x) / (t.z * t.z), 0.0f, h_y / t.z, -(h_y * t.y) / (t.z * t.z), 0.f,
+                       0.f, 0.f);
+    const M3 W = mcols(v[0], v[4], v[8], v[1], v[5], v[9], v[2], v[6], v[10]);
+    const M3 Vrk = mcols(cov3[0], cov3[1], cov3[2], cov3[1], cov3[3], cov3[4], cov3[2], cov3[4], cov3[5]);
+    const M3 T = mmul(W, J);
+    M3 cov2D = mmul(mmul(mtrans(T), mtrans(Vrk)), T);
+    const float ca = cov2D.m[0][0] += 0.3f;
+    const float cb = cov2D.m[0][1];
+    const float cc = cov2D.m[1][1] += 0.3f;
+    const float denom = ca * cc - cb * cb;
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+#define TT(i, j) T.m[i][j]
+    if (denom2inv != 0.f) {
+        dL_da = denom2inv * (-cc * cc * dcx + 2 * cb * cc * dcy + (denom - ca * cc) * dcw);
+        dL_dc = denom2inv * (-ca * ca * dcw + 2 * ca * cb * dcy + (denom - ca * cc) * dcx);
+        dL_db = denom2inv * 2 * (cb * cc * dcx - (denom + 2 * cb * cb) * dcy + ca * cb * dcw);
+        dcov[0] = (TT(0, 0) * TT(0, 0) * dL_da + TT(0, 0) * TT(1, 0) * dL_db + TT(1, 0) * TT(1, 0) * dL_dc);
+        dcov[3] = (TT(0, 1) * TT(0, 1) * dL_da + TT(0, 1) * TT(1, 1) * dL_db + TT(1, 1) * TT(1, 1) * dL_dc);
+        dcov[5] = (TT(0, 2) * TT(0, 2) * dL_da + TT(0, 2) * TT(1, 2) * dL_db + TT(1, 2) * TT(1, 2) * dL_dc);
+        dcov[1] = 2 * TT(0, 0) * TT(0, 1) * dL_da + (TT(0, 0) * TT(1, 1) + TT(0, 1) * TT(1, 0)) * dL_db +
+                  2 * TT(1, 0) * TT(1, 1) * dL_dc;
+        dcov[2] = 2 * TT(0, 0) * TT(0, 2) * dL_da + (TT(0, 0) * TT(1, 2) + TT(0, 2) * TT(1, 0)) * dL_db +
+                  2 * TT(1, 0) * TT(1, 2) * dL_dc;
+        dcov[4] = 2 * TT(0, 2) * TT(0, 1) * dL_da + (TT(0, 1) * TT(1, 2) + TT(0, 2) * TT(1, 1)) * dL_db +
+                  2 * TT(1, 1) * TT(1, 2) * dL_dc;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+    }
+#define VV(i, j) Vrk.m[i][j]
+    const float dL_dT00 = 2 * (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_da +
+                          (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_db;
+    const float dL_dT01 = 2 * (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_da +
+                          (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_db;
+    const float dL_dT02 = 2 * (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_da +
+                          (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_db;
+    const float dL_dT10 = 2 * (TT(1, 0) * VV(0, 0) + TT(1, 1) * VV(0, 1) + TT(1, 2) * VV(0, 2)) * dL_dc +
+                          (TT(0, 0) * VV(0, 0) + TT(0, 1) * VV(0, 1) + TT(0, 2) * VV(0, 2)) * dL_db;
+    const float dL_dT11 = 2 * (TT(1, 0) * VV(1, 0) + TT(1, 1) * VV(1, 1) + TT(1, 2) * VV(1, 2)) * dL_dc +
+                          (TT(0, 0) * VV(1, 0) + TT(0, 1) * VV(1, 1) + TT(0, 2) * VV(1, 2)) * dL_db;
+    const float dL_dT12 = 2 * (TT(1, 0) * VV(2, 0) + TT(1, 1) * VV(2, 1) + TT(1, 2) * VV(2, 2)) * dL_dc +
+                          (TT(0, 0) * VV(2, 0) + TT(0, 1) * VV(2, 1) + TT(0, 2) * VV(2, 2)) * dL_db;
+#undef VV
+#undef TT
+#define WW(i, j) W.m[i][j]
+    const float dL_dJ00 = WW(0, 0) * dL_dT00 + WW(0, 1) * dL_dT01 + WW(0, 2) * dL_dT02;
+    const float dL_dJ02 = WW(2, 0) * dL_dT00 + WW(2, 1) * dL_dT01 + WW(2, 2) * dL_dT02;
+    const float dL_dJ11 = WW(1, 0) * dL_dT10 + WW(1, 1) * dL_dT11 + WW(1, 2) * dL_dT12;
+    const float dL_dJ12 = WW(2, 0) * dL_dT10 + WW(2, 1) * dL_dT11 + WW(2, 2) * dL_dT12;
+#undef WW
+    const float tz = 1.f / t.z;
+    const float tz2 = tz * tz;
+    const float tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -h_x * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
+    const float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t.x) * tz3 * dL_dJ02 +
+                         (2 * h_y * t.y) * tz3 * dL_dJ12;
+    float3 dm = make_float3(v[0] * dL_dtx + v[1] * dL_dty + v[2] * dL_dtz, v[4] * dL_dtx + v[5] * dL_dty + v[6] * dL_dtz,
+                            v[8] * dL_dtx + v[9] * dL_dty + v[10] * dL_dtz);
+
+    // ---- preprocessCUDA backward (backward.cu:366-396) -------------------------------
+    const float* proj = a.projmatrix;
+    const float4 m_hom = xform_point4x4(mean, proj);
+    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+    const float mul1 = (proj[0] * mean.x + proj[4] * mean.y + proj[8] * mean.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * mean.x + proj[5] * mean.y + proj[9] * mean.z + proj[13]) * m_w * m_w;
+    dm.x += (proj[0] * m_w - proj[3] * mul1) * dm2x + (proj[1] * m_w - proj[3] * mul2) * dm2y;
+    dm.y += (proj[4] * m_w - proj[7] * mul1) * dm2x + (proj[5] * m_w - proj[7] * mul2) * dm2y;
+    dm.z += (proj[8] * m_w - proj[11] * mul1) * dm2x + (proj[9] * m_w - proj[11] * mul2) * dm2y;
+
+    if (a.shs) {
+        // backward.cu:20-139
+        const float* sh = a.shs + (size_t)idx * a.M * 3;
+        const float3 raw = sh_to_rgb_raw(a.D, mean, a.campos, sh);  // clamp flags, as the forward
+        const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
+        const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+        float g[3] = {dcol0 * (raw.x < 0 ? 0 : 1), dcol1 * (raw.y < 0 ? 0 : 1), dcol2 * (raw.z < 0 ? 0 : 1)};
+        float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
+        const int deg = a.D;
+#define SHC(k, c) sh[3 * (k) + (c)]
+#pragma unroll
+        for (int c = 0; c < 3; c++) dsh[c] = SH_C0 * g[c];
+        if (deg > 0) {
+            const float b1 = -SH_C1 * y, b2 = SH_C1 * z, b3 = -SH_C1 * x;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                dsh[3 + c] = b1 * g[c];
+                dsh[6 + c] = b2 * g[c];
+                dsh[9 + c] = b3 * g[c];
+                ddx[c] = -SH_C1 * SHC(3, c);
+                ddy[c] = -SH_C1 * SHC(1, c);
+                ddz[c] = SH_C1 * SHC(2, c);
+            }
+            if (deg > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+                const float b4 = SH_C2_0 * xy, b5 = SH_C2_1 * yz, b6 = SH_C2_2 * (2.f * zz - xx - yy);
+                const float b7 = SH_C2_3 * xz, b8 = SH_C2_4 * (xx - yy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    dsh[12 + c] = b4 * g[c];
+                    dsh[15 + c] = b5 * g[c];
+                    dsh[18 + c] = b6 * g[c];
+                    dsh[21 + c] = b7 * g[c];
+                    dsh[24 + c] = b8 * g[c];
+                    ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
+                              SH_C2_4 * 2.f * x * SHC(8, c);
+                    ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
+                              SH_C2_4 * 2.f * -y * SHC(8, c);
+                    ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
+                }
+                if (deg > 2) {
+                    const float b9 = SH_C3_0 * y * (3.f * xx - yy);
+                    const float b10 = SH_C3_1 * xy * z;
+                    const float b11 = SH_C3_2 * y * (4.f * zz - xx - yy);
+                    const float b12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                    const float b13 = SH_C3_4 * x * (4.f * zz - xx - yy);
+                    const float b14 = SH_C3_5 * z * (xx - yy);
+                    const float b15 = SH_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                    for (int c = 0; c < 3; c++) {
+                        dsh[27 + c] = b9 * g[c];
+                        dsh[30 + c] = b10 * g[c];
+                        dsh[33 + c] = b11 * g[c];
+                        dsh[36 + c] = b12 * g[c];
+                        dsh[39 + c] = b13 * g[c];
+                        dsh[42 + c] = b14 * g[c];
+                        dsh[45 + c] = b15 * g[c];
+                        ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
+                                   SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
+                                   SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
+                                   SH_C3_5 * SHC(14, c) * 2.f * xz + SH_C3_6 * SHC(15, c) * 3.f * (xx - yy));
+                        ddy[c] += (SH_C3_0 * SHC(9, c) * 3.f * (xx - yy) + SH_C3_1 * SHC(10, c) * xz +
+                                   SH_C3_2 * SHC(11, c) * (-3.f * yy + 4.f * zz - xx) +
+                                   SH_C3_3 * SHC(12, c) * -3.f * 2.f * yz + SH_C3_4 * SHC(13, c) * -2.f * xy +
+                                   SH_C3_5 * SHC(14, c) * -2.f * yz + SH_C3_6 * SHC(15, c) * -3.f * 2.f * xy);
+                        ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
+                                   SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
+                                   SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
+                    }
+                }
+            }
+        }
+#undef SHC
+        // coefficients above the evaluated degree get zero gradient (torch::zeros in the reference)
+        for (int k = (deg + 1) * (deg + 1); k < a.M; k++) {
+            dsh[3 * k] = 0.f;
+            dsh[3 * k + 1] = 0.f;
+            dsh[3 * k + 2] = 0.f;
+        }
+        const float3 dL_ddir = make_float3(ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2],
+                                           ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2],
+                                           ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2]);
+        const float3 d = dnormvdv3(dir_orig, dL_ddir);
+        dm.x += d.x;
+        dm.y += d.y;
+        dm.z += d.z;
+    } else if (dsh) {
+        for (int i = 0; i < a.M * 3; i++) dsh[i] = 0.f;
+    }
+    a.dL_dmean3D[3 * idx + 0] = dm.x;
+    a.dL_dmean3D[3 * idx + 1] = dm.y;
+    a.dL_dmean3D[3 * idx + 2] = dm.z;
+
+    if (a.dL_dscale) {
+        if (!a.scales) {
+            a.dL_dscale[3 * idx + 0] = 0.f;
+            a.dL_dscale[3 * idx + 1] = 0.f;
+            a.dL_dscale[3 * idx + 2] = 0.f;
+            *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+            return;
+        }
+        // ---- computeCov3D backward (backward.cu:278-341) ------------------------------
+        const float r = rot.x, x = rot.y, y = rot.z, z = rot.w;
+        const M3 R = mcols(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                           2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                           2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+        M3 S = mcols(1.0f, 0.f, 0.f, 0.f, 1.0f, 0.f, 0.f, 0.f, 1.0f);
+        const float s0 = a.scale_modifier * scl.x, s1 = a.scale_modifier * scl.y, s2 = a.scale_modifier * scl.z;
+        S.m[0][0] = s0;
+        S.m[1][1] = s1;
+        S.m[2][2] = s2;
+        const M3 M = mmul(S, R);
+        const M3 dL_dSigma = mcols(dcov[0], 0.5f * dcov[1], 0.5f * dcov[2], 0.5f * dcov[1], dcov[3], 0.5f * dcov[4],
+                                   0.5f * dcov[2], 0.5f * dcov[4], dcov[5]);
+        M3 M2;
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) M2.m[i][j] = 2.0f * M.m[i][j];
+        const M3 dL_dM = mmul(M2, dL_dSigma);
+        const M3 Rt = mtrans(R);
+        M3 D = mtrans(dL_dM);
+        float* ds = a.dL_dscale + 3 * idx;
+        ds[0] = Rt.m[0][0] * D.m[0][0] + Rt.m[0][1] * D.m[0][1] + Rt.m[0][2] * D.m[0][2];
+        ds[1] = Rt.m[1][0] * D.m[1][0] + Rt.m[1][1] * D.m[1][1] + Rt.m[1][2] * D.m[1][2];
+        ds[2] = Rt.m[2][0] * D.m[2][0] + Rt.m[2][1] * D.m[2][1] + Rt.m[2][2] * D.m[2][2];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            D.m[0][j] *= s0;
+            D.m[1][j] *= s1;
+            D.m[2][j] *= s2;
+        }
+#define DD(i, j) D.m[i][j]
+        float4 dq;
+        dq.x = 2 * z * (DD(0, 1) - DD(1, 0)) + 2 * y * (DD(2, 0) - DD(0, 2)) + 2 * x * (DD(1, 2) - DD(2, 1));
+        dq.y = 2 * y * (DD(1, 0) + DD(0, 1)) + 2 * z * (DD(2, 0) + DD(0, 2)) + 2 * r * (DD(1, 2) - DD(2, 1)) -
+               4 * x * (DD(2, 2) + DD(1, 1));
+        dq.z = 2 * x * (DD(1, 0) + DD(0, 1)) + 2 * r * (DD(2, 0) - DD(0, 2)) + 2 * z * (DD(1, 2) + DD(2, 1)) -
+               4 * y * (DD(2, 2) + DD(0, 0));
+        dq.w = 2 * r * (DD(0, 1) - DD(1, 0)) + 2 * x * (DD(2, 0) + DD(0, 2)) + 2 * y * (DD(1, 2) + DD(2, 1)) -
+               4 * z * (DD(1, 1) + DD(0, 0));
+#undef DD
+        *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = dq;
+    }
+}
+
+void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {
+    if (a.P == 0) return;
+    hipLaunchKernelGGL(k_preprocess_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace gsr

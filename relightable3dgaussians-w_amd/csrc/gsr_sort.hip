@@ -1,0 +1,160 @@
+// gsr_sort.hip -- stable LSD radix sort of (u32 key, u32 value) pairs, wave64-native.
+//
+// Replaces cub::DeviceRadixSort::SortPairs (rasterizer_impl.cu:303-308).  The binning
+// stage sorts (a) the visible Gaussians by their 32-bit depth key and (b) the
+// (tile, gaussian) instances by tile id only -- never the reference's 64-bit keys -- so
+// the instance sort needs ceil(log2(T)/8) = 2 passes instead of 6.  Stability of every
+// pass gives the reference's total order (tile, depth, gaussian index).
+//
+// One pass = 3 launches (reduce-then-scan):
+//   k_radix_hist    per-4096-key tile digit histogram (wave ballot-match counting)
+//   scan            exclusive scan of the digit-major histogram -> global offsets
+//   k_radix_scatter per-tile stable ranking: each wave ranks its 1024 contiguous keys
+//                   with 8 ballots per 64-key row (peer masks, leader lane bumps the
+//                   per-wave LDS counter), waves combine through LDS, the tile is
+//                   reordered in LDS and written out in digit runs (coalesced).
+#include "gsr_block.hpp"
+#include "gsr_kernels.hpp"
+
+namespace gsr {
+
+constexpr int WAVE_ITEMS = SORT_TILE / 4;  // 1024 contiguous keys per wave
+
+__device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bb = __ballot(bit);
+        m &= bit ? bb : ~bb;
+    }
+    return valid ? m : 0ull;
+}
+
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const uint32_t* keys, int shift,
+                                                               uint32_t mask, uint32_t* hist, int nb) {
+    __shared__ uint32_t cnt[4][256];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const long long base = (long long)blockIdx.x * SORT_TILE + wave * WAVE_ITEMS;
+    volatile uint32_t* wc = cnt[wave];
+#pragma unroll 4
+    for (int k = 0; k < SORT_ITEMS; k++) {
+        const long long i = base + k * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = valid ? ((keys[i] >> shift) & mask) : 0u;
+        const uint64_t m = peer_mask(d, valid);
+        if (valid && lane == (int)(__ffsll((unsigned long long)m) - 1)) wc[d] = wc[d] + (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    const int d = threadIdx.x;
+    hist[(long long)d * nb + blockIdx.x] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
+}
+
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
+                                                                  const uint32_t* vals_in, int shift, uint32_t mask,
+                                                                  const uint32_t* offsets, int nb, uint32_t* keys_out,
+                                                                  uint32_t* vals_out) {
+    __shared__ uint32_t s_keys[SORT_TILE];
+    __shared__ uint32_t s_vals[SORT_TILE];
+    __shared__ uint32_t wh[4][256];
+    __shared__ uint32_t dstart[256];
+    __shared__ uint32_t goff[256];
+    __shared__ uint32_t scan_sh[4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&wh[0][0])[i] = 0;
+    __syncthreads();
+    const long long tile_base = (long long)blockIdx.x * SORT_TILE;
+    const long long base = tile_base + wave * WAVE_ITEMS;
+    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
+    volatile uint32_t* wc = wh[wave];
+    const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+#pragma unroll
+    for (int k = 0; k < SORT_ITEMS; k++) {
+        const long long i = base + k * 64 + lane;
+        const bool valid = i < n;
+        key[k] = valid ? keys_in[i] : 0u;
+        val[k] = valid ? vals_in[i] : 0u;
+        const uint32_t d = (key[k] >> shift) & mask;
+        const uint64_t m = peer_mask(d, valid);
+        const int leader = valid ? (int)(__ffsll((unsigned long long)m) - 1) : lane;
+        uint32_t old = 0;
+        if (valid && lane == leader) {
+            old = wc[d];
+            wc[d] = old + (uint32_t)__popcll(m);
+        }
+        old = __shfl(old, leader, 64);
+        rank[k] = old + (uint32_t)__popcll(m & lt);
+    }
+    __syncthreads();
+    {
+        const int d = threadIdx.x;
+        const uint32_t c0 = wh[0][d], c1 = wh[1][d], c2 = wh[2][d], c3 = wh[3][d];
+        const uint32_t start = block256_exclusive_scan(c0 + c1 + c2 + c3, scan_sh, (uint32_t*)nullptr);
+        wh[0][d] = start;
+        wh[1][d] = start + c0;
+        wh[2][d] = start + c0 + c1;
+        wh[3][d] = start + c0 + c1 + c2;
+        dstart[d] = start;
+        goff[d] = offsets[(long long)d * nb + blockIdx.x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SORT_ITEMS; k++) {
+        const long long i = base + k * 64 + lane;
+        if (i < n) {
+            const uint32_t d = (key[k] >> shift) & mask;
+            const uint32_t p = wh[wave][d] + rank[k];
+            s_keys[p] = key[k];
+            s_vals[p] = val[k];
+        }
+    }
+    __syncthreads();
+    const long long count = (n - tile_base) < SORT_TILE ? (n - tile_base) : SORT_TILE;
+#pragma unroll
+    for (int k = 0; k < SORT_ITEMS; k++) {
+        const int p = k * SORT_THREADS + threadIdx.x;
+        if (p < count) {
+            const uint32_t kk = s_keys[p];
+            const uint32_t d = (kk >> shift) & mask;
+            const uint32_t g = goff[d] + (uint32_t)(p - dstart[d]);
+            keys_out[g] = kk;
+            vals_out[g] = s_vals[p];
+        }
+    }
+}
+
+size_t radix_sort_temp_bytes(long long n) {
+    const long long nb = sort_blocks(n);
+    const long long h = 256 * nb;
+    return (size_t)(4 * (h + scan_blocks(h)) + 256);
+}
+
+int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                     int end_bit, void* temp, hipStream_t s) {
+    if (n <= 1 || end_bit <= 0) return 0;
+    const int nb = sort_blocks(n);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
+    uint32_t* spine = hist + 256LL * nb;
+    uint32_t* kin = keys;
+    uint32_t* vin = vals;
+    uint32_t* kout = keys_alt;
+    uint32_t* vout = vals_alt;
+    int flips = 0;
+    for (int shift = 0; shift < end_bit; shift += 8) {
+        const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
+        const uint32_t mask = (1u << nbits) - 1u;
+        hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
+        launch_exclusive_scan_u32(256LL * nb, hist, nullptr, hist, spine, nullptr, s);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask, hist, nb,
+                           kout, vout);
+        uint32_t* t;
+        t = kin; kin = kout; kout = t;
+        t = vin; vin = vout; vout = t;
+        flips ^= 1;
+    }
+    return flips;
+}
+
+}  // namespace gsr

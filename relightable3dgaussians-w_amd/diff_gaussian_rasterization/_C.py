@@ -1,0 +1,111 @@
+"""diff_gaussian_rasterization._C -- the extension module the reference binds in
+submodules/diff-gaussian-rasterization/ext.cpp:15-19, implemented over the C ABI of
+libgsr.so (include/gsr.h) instead of a pybind11/libtorch extension.
+
+Same three functions, same positional arguments and return tuples as
+rasterize_points.h:18-64.  Every call runs the hand-written gfx950 kernels; there is no
+CPU path (a CPU tensor raises).
+"""
+import ctypes as C
+import os
+import sys
+
+import torch
+
+_here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if _here not in sys.path:
+    sys.path.insert(0, _here)
+
+from gsr import _lib  # noqa: E402
+
+NUM_CHANNELS = 3
+
+
+def _f32(t):
+    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                        prefiltered):
+    """rasterize_points.cu:35-113 RasterizeGaussiansCUDA ->
+    (num_rendered, color[3,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _lib.require_gpu_tensor(means3D, "means3D")
+    dev = means3D.device
+    P, H, W = means3D.size(0), int(image_height), int(image_width)
+    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    bs = _lib.BufferSet(dev)
+    if P == 0:
+        return 0, torch.zeros((NUM_CHANNELS, H, W), dtype=torch.float32, device=dev), radii, *bs.bufs
+    out_color = torch.empty((NUM_CHANNELS, H, W), dtype=torch.float32, device=dev)
+    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    keep = [_f32(x) for x in (background, means3D, sh, colors, opacity, scales, rotations, cov3D_precomp, viewmatrix,
+                              projmatrix, campos)]
+    bg_, m_, sh_, col_, op_, sc_, rot_, cov_, vm_, pm_, cp_ = keep
+    for name, t in (("background", bg_), ("viewmatrix", vm_), ("projmatrix", pm_), ("campos", cp_)):
+        _lib.require_gpu_tensor(t, name)
+    rc = _lib.ResizeContexts(bs)
+    nr = C.c_int(0)
+    try:
+        ret = _lib.lib().gsr_forward(
+            _lib.RESIZE, rc.ctx[0], _lib.RESIZE, rc.ctx[1], _lib.RESIZE, rc.ctx[2], P, int(degree), M,
+            _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(sh_), _lib.fptr(col_), _lib.fptr(op_), _lib.fptr(sc_),
+            float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
+            float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out_color.data_ptr(), radii.data_ptr(),
+            _lib.stream_of(dev), C.byref(nr))
+    finally:
+        rc.close()
+    _lib.check(ret, "rasterize_gaussians")
+    return int(nr.value), out_color, radii, bs.bufs[0], bs.bufs[1], bs.bufs[2]
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer):
+    """rasterize_points.cu:115-192 RasterizeGaussiansBackwardCUDA -> (dL_dmeans2D, dL_dcolors,
+    dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    _lib.require_gpu_tensor(means3D, "means3D")
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = dL_dout_color.size(1), dL_dout_color.size(2)
+    M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
+    alloc = torch.zeros if P == 0 else torch.empty
+    f = dict(dtype=torch.float32, device=dev)
+    dL_dmeans2D = alloc((P, 3), **f)
+    dL_dcolors = alloc((P, NUM_CHANNELS), **f)
+    dL_dconic = alloc((P, 2, 2), **f)
+    dL_dopacity = alloc((P, 1), **f)
+    dL_dmeans3D = alloc((P, 3), **f)
+    dL_dcov3D = alloc((P, 6), **f)
+    dL_dsh = alloc((P, M, 3), **f)
+    dL_dscales = alloc((P, 3), **f)
+    dL_drotations = alloc((P, 4), **f)
+    if P != 0:
+        keep = [_f32(x) for x in (background, means3D, sh, colors, scales, rotations, cov3D_precomp, viewmatrix,
+                                  projmatrix, campos, dL_dout_color)]
+        bg_, m_, sh_, col_, sc_, rot_, cov_, vm_, pm_, cp_, dout_ = keep
+        radii_ = radii.contiguous()
+        ptr = lambda t: t.data_ptr() if t.numel() else None
+        ret = _lib.lib().gsr_backward(
+            P, int(degree), M, int(R), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(sh_), _lib.fptr(col_),
+            _lib.fptr(sc_), float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_),
+            _lib.fptr(cp_), float(tan_fovx), float(tan_fovy), radii_.data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
+            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(),
+            dL_dopacity.data_ptr(), dL_dcolors.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
+            dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(), _lib.stream_of(dev))
+        _lib.check(ret, "rasterize_gaussians_backward")
+    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """rasterize_points.cu:194-213 markVisible -> bool[P]."""
+    _lib.require_gpu_tensor(means3D, "means3D")
+    P = means3D.size(0)
+    present = torch.zeros(P, dtype=torch.bool, device=means3D.device)
+    if P != 0:
+        m_, vm_, pm_ = _f32(means3D), _f32(viewmatrix), _f32(projmatrix)
+        _lib.check(_lib.lib().gsr_mark_visible(P, m_.data_ptr(), vm_.data_ptr(), pm_.data_ptr(), present.data_ptr(),
+                                               _lib.stream_of(means3D.device)), "mark_visible")
+    return present

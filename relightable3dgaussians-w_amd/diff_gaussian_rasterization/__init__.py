@@ -1,0 +1,101 @@
+"""Drop-in `diff_gaussian_rasterization` package for MI355X.
+
+Public surface identical to the reference package
+(submodules/diff-gaussian-rasterization/diff_gaussian_rasterization/__init__.py:17-195),
+so gaussian_renderer/__init__.py:15 `from diff_gaussian_rasterization import
+GaussianRasterizationSettings, GaussianRasterizer` and everything built on it run
+unchanged.  The extension module `_C` is backed by libgsr.so (hand-written gfx950 HIP).
+"""
+from typing import NamedTuple
+
+import torch
+import torch.nn as nn
+
+from . import _C
+
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians"]
+
+
+class GaussianRasterizationSettings(NamedTuple):
+    """Camera + render settings (reference __init__.py:133-144).  viewmatrix is the
+    camera's world_view_transform, projmatrix its full_proj_transform (row-vector
+    convention, scene/cameras.py:77-79)."""
+    image_height: int
+    image_width: int
+    tanfovx: float
+    tanfovy: float
+    bg: torch.Tensor
+    scale_modifier: float
+    viewmatrix: torch.Tensor
+    projmatrix: torch.Tensor
+    sh_degree: int
+    campos: torch.Tensor
+    prefiltered: bool
+
+
+def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                        raster_settings):
+    return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
+                                     cov3Ds_precomp, raster_settings)
+
+
+def _forward_args(s, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp, sh):
+    # positional order of _C.rasterize_gaussians (rasterize_points.h:18-37)
+    return (s.bg, means3D, colors_precomp, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, sh, s.sh_degree,
+            s.campos, s.prefiltered)
+
+
+class _RasterizeGaussians(torch.autograd.Function):
+    """Autograd node (reference __init__.py:40-131).  means2D is an input only so that its
+    .grad receives dL/d(screen-space mean) for densification; the forward never reads it."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                raster_settings):
+        num_rendered, color, radii, geom_buf, bin_buf, img_buf = _C.rasterize_gaussians(
+            *_forward_args(raster_settings, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
+                           sh))
+        ctx.raster_settings = raster_settings
+        ctx.num_rendered = num_rendered
+        ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom_buf,
+                              bin_buf, img_buf)
+        return color, radii
+
+    @staticmethod
+    def backward(ctx, grad_out_color, _grad_radii):
+        s = ctx.raster_settings
+        colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom_buf, bin_buf, img_buf = \
+            ctx.saved_tensors
+        (g_means2D, g_colors, g_opacities, g_means3D, g_cov3D, g_sh, g_scales, g_rotations) = \
+            _C.rasterize_gaussians_backward(s.bg, means3D, radii, colors_precomp, scales, rotations,
+                                            s.scale_modifier, cov3Ds_precomp, s.viewmatrix, s.projmatrix, s.tanfovx,
+                                            s.tanfovy, grad_out_color, sh, s.sh_degree, s.campos, geom_buf,
+                                            ctx.num_rendered, bin_buf, img_buf)
+        # gradients in the order of forward()'s inputs; None for raster_settings
+        return g_means3D, g_means2D, g_sh, g_colors, g_opacities, g_scales, g_rotations, g_cov3D, None
+
+
+class GaussianRasterizer(nn.Module):
+    """reference __init__.py:146-195"""
+
+    def __init__(self, raster_settings):
+        super().__init__()
+        self.raster_settings = raster_settings
+
+    def markVisible(self, positions):
+        with torch.no_grad():
+            s = self.raster_settings
+            return _C.mark_visible(positions, s.viewmatrix, s.projmatrix)
+
+    def forward(self, means3D, means2D, opacities, shs=None, colors_precomp=None, scales=None, rotations=None,
+                cov3D_precomp=None):
+        if (shs is None) == (colors_precomp is None):
+            raise Exception('Please provide excatly one of either SHs or precomputed colors!')
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        empty = torch.Tensor([])
+        pick = lambda t: empty if t is None else t
+        return rasterize_gaussians(means3D, means2D, pick(shs), pick(colors_precomp), opacities, pick(scales),
+                                   pick(rotations), pick(cov3D_precomp), self.raster_settings)

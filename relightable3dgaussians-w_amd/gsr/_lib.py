@@ -1,0 +1,154 @@
+"""ctypes binding of libgsr.so (C ABI: include/gsr.h).
+
+The product path: every call lands in hand-written HIP for gfx950.  There is no CPU or
+PyTorch fallback -- if the library or a GPU is missing, calls raise.
+"""
+import ctypes as C
+import os
+import subprocess
+import threading
+
+import torch
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libgsr.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+RESIZE_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
+
+_lib = None
+_lock = threading.Lock()
+
+
+class Layout(C.Structure):
+    _fields_ = [(n, C.c_size_t) for n in (
+        "geom_bytes", "img_bytes", "bin_bytes", "geom_radii", "geom_tiles", "geom_depth_key", "geom_rect",
+        "geom_rec", "geom_acc", "img_final_T", "img_n_contrib", "img_ranges", "bin_point_list", "bin_tile_keys")]
+
+
+def build(jobs=8, arch="gfx950"):
+    """Compile libgsr.so in-tree (hipcc --offload-arch=gfx950)."""
+    subprocess.check_call(["make", "-s", "-C", CSRC, f"-j{jobs}", f"ARCH={arch}"])
+
+
+def _declare(lib):
+    vp, i, f, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+    lib.gsr_forward.argtypes = [RESIZE_FN, vp, RESIZE_FN, vp, RESIZE_FN, vp, i, i, i, vp, i, i, vp, vp, vp, vp, vp, f,
+                                vp, vp, vp, vp, vp, f, f, i, vp, vp, vp, C.POINTER(C.c_int)]
+    lib.gsr_backward.argtypes = [i, i, i, i, vp, i, i, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp, vp, vp,
+                                 vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
+    lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                       vp, vp, vp]
+    lib.gsr_shade_workspace_bytes.argtypes = [i, i]
+    lib.gsr_shade_workspace_bytes.restype = sz
+    lib.gsr_get_layout.argtypes = [i, C.c_longlong, i, i, C.POINTER(Layout)]
+    lib.gsr_profile_enable.argtypes = [i]
+    lib.gsr_profile_stage_count.restype = i
+    lib.gsr_profile_stage_name.argtypes = [i]
+    lib.gsr_profile_stage_name.restype = C.c_char_p
+    lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
+    lib.gsr_last_error.restype = C.c_char_p
+    lib.gsr_version.restype = C.c_char_p
+    for fn in ("gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward", "gsr_shade_backward",
+               "gsr_get_layout"):
+        getattr(lib, fn).restype = C.c_int
+
+
+def lib():
+    """Load (never silently substitute) libgsr.so."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(f"libgsr.so not built ({LIB_PATH}); run __graft_entry__.build() "
+                                       "or `make -C relightable3dgaussians-w_amd/csrc`")
+                L = C.CDLL(LIB_PATH)
+                _declare(L)
+                _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().gsr_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def require_gpu_tensor(t, name):
+    if not isinstance(t, torch.Tensor) or t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be a GPU (HIP) tensor; this rasterizer has no CPU path")
+
+
+def fptr(t):
+    """Device pointer of a float32 tensor, or None for an empty tensor (= 'absent', as the
+    reference's data<float>() of an empty tensor)."""
+    if t is None or t.numel() == 0:
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"expected float32 tensor, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError("internal: pointer of a non-contiguous tensor")
+    return t.data_ptr()
+
+
+def stream_of(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def profile_enable(on=True):
+    lib().gsr_profile_enable(int(bool(on)))
+
+
+def profile_read(reset=True):
+    """{stage: (total_ms, launches)} accumulated since the last reset (waits for the events)."""
+    L = lib()
+    n = L.gsr_profile_stage_count()
+    ms = (C.c_double * n)()
+    cnt = (C.c_longlong * n)()
+    check(L.gsr_profile_read(ms, cnt, n, int(bool(reset))), "gsr_profile_read")
+    return {L.gsr_profile_stage_name(k).decode(): (ms[k], cnt[k]) for k in range(n)}
+
+
+def layout(P, R, W, H):
+    L = Layout()
+    check(lib().gsr_get_layout(int(P), int(R), int(W), int(H), C.byref(L)), "gsr_get_layout")
+    return L
+
+
+class BufferSet:
+    """Owns the three growable byte buffers of one forward call (the reference's
+    geomBuffer / binningBuffer / imgBuffer torch.uint8 tensors, rasterize_points.cu:70-77)."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = [torch.empty(0, dtype=torch.uint8, device=device) for _ in range(3)]
+
+
+_live = {}
+_next = [1]
+
+
+def _resize(ctx, n):
+    key = int(ctx)
+    bs = _live[key >> 2]
+    t = torch.empty(int(n), dtype=torch.uint8, device=bs.device)
+    bs.bufs[key & 3] = t
+    return t.data_ptr()
+
+
+RESIZE = RESIZE_FN(_resize)
+
+
+class ResizeContexts:
+    def __init__(self, bs):
+        with _lock:
+            self.id = _next[0]
+            _next[0] += 1
+        _live[self.id] = bs
+        self.ctx = [C.c_void_p((self.id << 2) | k) for k in range(3)]
+
+    def close(self):
+        _live.pop(self.id, None)

@@ -1,0 +1,53 @@
+"""CPU checks of the drop-in boundary: libgsr.so loads and exports every symbol that
+include/gsr.h declares; the Python package imports and refuses CPU tensors (no fallback)."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    src = open(os.path.join(ROOT, "include", "gsr.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(gsr_[a-z_]+)\s*\(", src)) - {"gsr_resize_fn"})
+
+
+def test_header_declares_the_reference_entry_points():
+    syms = declared_symbols()
+    for s in ("gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward", "gsr_shade_backward"):
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol():
+    from gsr import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        _lib.build()
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(L, s)]
+    assert not missing, missing
+    assert _lib.lib().gsr_version().decode().startswith("gsr")
+
+
+def test_layout_query_is_consistent():
+    from gsr import _lib
+    L = _lib.layout(1000, 12345, 1920, 1080)
+    assert L.geom_bytes > 1000 * (48 + 64) and L.bin_bytes > 12345 * 16 and L.img_bytes >= 1920 * 1080 * 8
+    for off in (L.geom_rec, L.geom_acc, L.img_ranges, L.bin_point_list):
+        assert off % 256 == 0
+
+
+def test_cpu_tensors_are_rejected():
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+    e = torch.empty(0)
+    with pytest.raises(RuntimeError, match="GPU"):
+        _C.rasterize_gaussians(torch.zeros(3), torch.zeros(10, 3), e, e, e, e, 1.0, e, torch.eye(4), torch.eye(4), 1.0,
+                               1.0, 8, 8, e, 0, torch.zeros(3), False)
+    assert hasattr(dgr, "GaussianRasterizationSettings") and hasattr(dgr, "_RasterizeGaussians")
+    assert dgr.GaussianRasterizationSettings._fields == (
+        "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
+        "sh_degree", "campos", "prefiltered")

@@ -1,0 +1,247 @@
+"""GPU parity: libgsr.so (through the C ABI via diff_gaussian_rasterization._C) vs the CPU
+oracle on the same seeded inputs.
+
+Bar (BASELINE.json north_star): bit-exact on tile/key indexing -- radii, tiles_touched,
+screen means, conics, depth keys, num_rendered, the sorted instance list and the tile
+ranges -- and within 1e-4 relative on rendered RGB and on every gradient (relative L2
+over the tensor: the GPU sums gradients in a different order than the reference's
+atomics, so elementwise bits cannot match; the tolerance is tied to the tensor norm)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_case, np32, rel_l2
+from oracle import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+RGB_TOL = 1e-4
+GRAD_TOL = 1e-4
+
+
+def _dgr():
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+    from gsr import _lib
+    return dgr, _C, _lib
+
+
+def _view(buf, off, n, dtype):
+    base = buf.data_ptr()
+    shift = (-base) % 256
+    nbytes = n * torch.empty(0, dtype=dtype).element_size()
+    return buf[shift + off: shift + off + nbytes].view(dtype)
+
+
+def run_gpu(cam, gs, mode="colors", bg=(0.0, 0.0, 0.0), scale_modifier=1.0, sh_degree=0, prefiltered=False,
+            cov=False):
+    _, _C, _lib = _dgr()
+    dev = torch.device("cuda")
+    P = gs["means3D"].shape[0]
+    W, H = cam.image_width, cam.image_height
+    e = torch.empty(0, device=dev)
+    means = gs["means3D"].to(dev)
+    colors = gs["colors"].to(dev) if mode == "colors" else e
+    sh = gs["shs"].to(dev) if mode == "sh" else e
+    if cov:
+        cov3 = torch.tensor(orc.preprocess(np32(gs["means3D"]), np32(gs["scales"]), np32(gs["rotations"]),
+                                           np32(gs["opacities"]).reshape(-1), None, np.zeros((P, 3), np.float32),
+                                           None, np.eye(4, dtype=np.float32), np.eye(4, dtype=np.float32),
+                                           np.zeros(3, np.float32), 16, 16, 1.0, 1.0, scale_modifier)["cov3D"],
+                            device=dev)
+        scales, rots = e, e
+    else:
+        cov3 = e
+        scales, rots = gs["scales"].to(dev), gs["rotations"].to(dev)
+    bg_t = torch.tensor(bg, dtype=torch.float32, device=dev)
+    vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
+    R, color, radii, geom, binb, img = _C.rasterize_gaussians(
+        bg_t, means, colors, gs["opacities"].to(dev), scales, rots, scale_modifier, cov3, vm, pm, cam.tanfovx,
+        cam.tanfovy, H, W, sh, sh_degree, cp, prefiltered)
+    torch.cuda.synchronize()
+    L = _lib.layout(P, R, W, H)
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    st = dict(R=R, color=color, radii=radii, geom=geom, binb=binb, img=img, bg=bg_t, means=means, colors=colors,
+              sh=sh, scales=scales, rots=rots, cov3=cov3, vm=vm, pm=pm, cp=cp)
+    st["rec"] = _view(geom, L.geom_rec, 12 * P, torch.float32).view(P, 12).cpu().numpy()
+    st["tiles"] = _view(geom, L.geom_tiles, P, torch.int32).cpu().numpy().view(np.uint32)
+    st["depth_key"] = _view(geom, L.geom_depth_key, P, torch.int32).cpu().numpy().view(np.uint32)
+    st["point_list"] = _view(binb, L.bin_point_list, R, torch.int32).cpu().numpy().view(np.uint32)
+    st["ranges"] = _view(img, L.img_ranges, 2 * gx * gy, torch.int32).cpu().numpy().view(np.uint32).reshape(-1, 2)
+    st["final_T"] = _view(img, L.img_final_T, W * H, torch.float32).cpu().numpy()
+    st["n_contrib"] = _view(img, L.img_n_contrib, W * H, torch.int32).cpu().numpy().view(np.uint32)
+    return st
+
+
+def run_oracle(cam, gs, mode="colors", bg=(0.0, 0.0, 0.0), scale_modifier=1.0, sh_degree=0, cov3=None):
+    W, H = cam.image_width, cam.image_height
+    return orc.forward(np.asarray(bg, np.float32), np32(gs["means3D"]), np32(gs["colors"]) if mode == "colors" else None,
+                       np32(gs["opacities"]), None if cov3 is not None else np32(gs["scales"]),
+                       None if cov3 is not None else np32(gs["rotations"]), scale_modifier, cov3,
+                       np32(cam.world_view_transform), np32(cam.full_proj_transform), cam.tanfovx, cam.tanfovy, H, W,
+                       np32(gs["shs"]) if mode == "sh" else None, sh_degree, np32(cam.camera_center))
+
+
+def check_forward(st, ref, W, H):
+    vis = ref["radii"] > 0
+    np.testing.assert_array_equal(st["radii"].cpu().numpy(), ref["radii"])
+    np.testing.assert_array_equal(st["tiles"], ref["tiles_touched"])
+    rec = st["rec"]
+    # bit-exact screen-space geometry of every visible Gaussian
+    np.testing.assert_array_equal(rec[vis, 0:2], ref["means2D"][vis])
+    np.testing.assert_array_equal(rec[vis, 2:4], ref["conic_opacity"][vis, 0:2])
+    np.testing.assert_array_equal(rec[vis, 4:6], ref["conic_opacity"][vis, 2:4])
+    np.testing.assert_array_equal(rec[vis, 6:9], ref["features"][vis])
+    np.testing.assert_array_equal(st["depth_key"][vis], ref["depths"][vis].view(np.uint32))
+    assert st["R"] == ref["num_rendered"]
+    np.testing.assert_array_equal(st["point_list"], ref["point_list"])
+    np.testing.assert_array_equal(st["ranges"], ref["ranges"])
+    color = st["color"].cpu().numpy()
+    e = rel_l2(color, ref["color"])
+    assert e <= RGB_TOL, f"rgb rel L2 {e:.3e}"
+    # borderline exp() decisions may flip a handful of pixels; everything else agrees to 1e-4
+    bad = np.abs(color - ref["color"]) > 1e-4 * max(1.0, np.abs(ref["color"]).max())
+    assert bad.mean() < 1e-3, f"{bad.sum()} rgb values off by > 1e-4"
+    nc_match = (st["n_contrib"] == ref["n_contrib"]).mean()
+    assert nc_match > 0.999, nc_match
+    return e
+
+
+CASES = [
+    dict(name="cfg1_small_sh0", P=3000, W=128, H=128, mode="sh", sh_degree=0),
+    dict(name="colors_ragged", P=2500, W=100, H=75, mode="colors"),
+    dict(name="sh3_orbit_bg", P=2500, W=96, H=64, mode="sh", sh_degree=3, camera="orbit", bg=(0.2, 0.5, 1.0)),
+    dict(name="sh1_scale_mod", P=2000, W=64, H=64, mode="sh", sh_degree=1, scale_modifier=1.7),
+    dict(name="sh2_cov_precomp", P=2000, W=80, H=48, mode="sh", sh_degree=2, cov=True),
+    dict(name="dense_small", P=20000, W=64, H=64, mode="colors"),
+]
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_forward_parity(case):
+    cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
+                        camera=case.get("camera", "identity"))
+    kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), scale_modifier=case.get("scale_modifier", 1.0),
+              sh_degree=case.get("sh_degree", 0))
+    st = run_gpu(cam, gs, cov=case.get("cov", False), **kw)
+    ref = run_oracle(cam, gs, cov3=st["cov3"].cpu().numpy() if case.get("cov") else None, **kw)
+    check_forward(st, ref, cam.image_width, cam.image_height)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_backward_parity(case):
+    _, _C, _ = _dgr()
+    cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
+                        camera=case.get("camera", "identity"))
+    kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), scale_modifier=case.get("scale_modifier", 1.0),
+              sh_degree=case.get("sh_degree", 0))
+    st = run_gpu(cam, gs, cov=case.get("cov", False), **kw)
+    cov3 = st["cov3"].cpu().numpy() if case.get("cov") else None
+    ref = run_oracle(cam, gs, cov3=cov3, **kw)
+    W, H = cam.image_width, cam.image_height
+    g = torch.Generator().manual_seed(1)
+    dout = torch.randn(3, H, W, generator=g)
+    grads = _C.rasterize_gaussians_backward(
+        st["bg"], st["means"], st["radii"], st["colors"], st["scales"], st["rots"], kw["scale_modifier"], st["cov3"],
+        st["vm"], st["pm"], cam.tanfovx, cam.tanfovy, dout.cuda(), st["sh"], kw["sh_degree"], st["cp"], st["geom"],
+        st["R"], st["binb"], st["img"])
+    names = ["dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    gref = orc.backward(ref, np.asarray(kw["bg"], np.float32), np32(gs["means3D"]),
+                        np32(gs["colors"]) if kw["mode"] == "colors" else None,
+                        None if cov3 is not None else np32(gs["scales"]),
+                        None if cov3 is not None else np32(gs["rotations"]), kw["scale_modifier"], cov3,
+                        np32(cam.world_view_transform), np32(cam.full_proj_transform), cam.tanfovx, cam.tanfovy,
+                        dout.numpy(), np32(gs["shs"]) if kw["mode"] == "sh" else None, kw["sh_degree"],
+                        np32(cam.camera_center))
+    errs = {}
+    for n, gt in zip(names, grads):
+        r = gref[n]
+        if n == "dL_dcolors" and kw["mode"] == "sh":
+            pass  # still returned by the reference (grad w.r.t. the absent colors_precomp)
+        mine = gt.detach().cpu().numpy().reshape(r.shape)
+        if n in ("dL_dscales", "dL_drotations") and cov3 is not None:
+            assert np.abs(mine).max() == 0.0
+            continue
+        if n == "dL_dcov3D" and cov3 is None:
+            pass
+        if np.abs(r).max() == 0:
+            assert np.abs(mine).max() == 0.0, n
+            continue
+        errs[n] = rel_l2(mine, r)
+    bad = {k: v for k, v in errs.items() if v > GRAD_TOL}
+    assert not bad, f"gradient rel L2 errors above {GRAD_TOL}: {bad} (all: {errs})"
+
+
+def test_autograd_module_path():
+    """The drop-in GaussianRasterizer as gaussian_renderer.render() uses it (colors_precomp,
+    sh_degree=-1, scales/rotations, means2D with retain_grad)."""
+    dgr, _, _ = _dgr()
+    cam, gs = make_case(P=3000, W=96, H=96, sh_degree=0)
+    dev = "cuda"
+    s = dgr.GaussianRasterizationSettings(image_height=96, image_width=96, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+                                          bg=torch.zeros(3, device=dev), scale_modifier=1.0,
+                                          viewmatrix=cam.world_view_transform.to(dev),
+                                          projmatrix=cam.full_proj_transform.to(dev), sh_degree=-1,
+                                          campos=cam.camera_center.to(dev), prefiltered=False)
+    rast = dgr.GaussianRasterizer(raster_settings=s)
+    leaves = {k: gs[k].to(dev).requires_grad_(True) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+    means2D = torch.zeros_like(leaves["means3D"], requires_grad=True) + 0
+    means2D.retain_grad()
+    img, radii = rast(means3D=leaves["means3D"], means2D=means2D, shs=None, colors_precomp=leaves["colors"],
+                      opacities=leaves["opacities"], scales=leaves["scales"], rotations=leaves["rotations"],
+                      cov3D_precomp=None)
+    assert img.shape == (3, 96, 96) and radii.shape == (3000,)
+    (img * torch.linspace(0, 1, 96, device=dev)).sum().backward()
+    for k, v in leaves.items():
+        assert v.grad is not None and torch.isfinite(v.grad).all(), k
+    assert means2D.grad is not None and (means2D.grad[:, :2].abs().sum() > 0)
+    vis = rast.markVisible(leaves["means3D"].detach())
+    assert vis.dtype == torch.bool and vis.all()  # every synthetic point is in front of the camera
+    with pytest.raises(Exception):
+        rast(means3D=leaves["means3D"], means2D=means2D, opacities=leaves["opacities"])
+
+
+def test_empty_and_fully_culled():
+    _, _C, _ = _dgr()
+    cam, gs = make_case(P=100, W=32, H=32)
+    dev = "cuda"
+    e = torch.empty(0, device=dev)
+    args = lambda m, c, o, s, r: (torch.zeros(3, device=dev), m, c, o, s, r, 1.0, e, cam.world_view_transform.cuda(),
+                                  cam.full_proj_transform.cuda(), cam.tanfovx, cam.tanfovy, 32, 32, e, 0,
+                                  cam.camera_center.cuda(), False)
+    z = torch.zeros((0, 3), device=dev)
+    R, color, radii, *_ = _C.rasterize_gaussians(*args(z, z, torch.zeros((0, 1), device=dev), z,
+                                                       torch.zeros((0, 4), device=dev)))
+    assert R == 0 and color.abs().max() == 0 and radii.numel() == 0
+    behind = gs["means3D"].clone()
+    behind[:, 2] = -behind[:, 2]
+    R, color, radii, *_ = _C.rasterize_gaussians(*args(behind.cuda(), gs["colors"].cuda(), gs["opacities"].cuda(),
+                                                       gs["scales"].cuda(), gs["rotations"].cuda()))
+    assert R == 0 and (radii == 0).all() and color.abs().max() == 0
+
+
+def test_prefiltered_error_is_reported():
+    _, _C, _ = _dgr()
+    cam, gs = make_case(P=64, W=32, H=32)
+    behind = gs["means3D"].clone()
+    behind[:5, 2] = -1.0
+    dev = "cuda"
+    e = torch.empty(0, device=dev)
+    with pytest.raises(RuntimeError, match="prefiltered"):
+        _C.rasterize_gaussians(torch.zeros(3, device=dev), behind.cuda(), gs["colors"].cuda(), gs["opacities"].cuda(),
+                               gs["scales"].cuda(), gs["rotations"].cuda(), 1.0, e, cam.world_view_transform.cuda(),
+                               cam.full_proj_transform.cuda(), cam.tanfovx, cam.tanfovy, 32, 32, e, 0,
+                               cam.camera_center.cuda(), True)
+
+
+def test_bad_means_shape():
+    _, _C, _ = _dgr()
+    dev = "cuda"
+    e = torch.empty(0, device=dev)
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        _C.rasterize_gaussians(torch.zeros(3, device=dev), torch.zeros(10, 4, device=dev), e, e, e, e, 1.0, e,
+                               torch.eye(4, device=dev), torch.eye(4, device=dev), 1.0, 1.0, 8, 8, e, 0,
+                               torch.zeros(3, device=dev), False)
