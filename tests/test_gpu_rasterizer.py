@@ -162,6 +162,8 @@ def test_backward_parity(case):
         if n == "dL_dcolors" and kw["mode"] == "sh":
             pass  # still returned by the reference (grad w.r.t. the absent colors_precomp)
         mine = gt.detach().cpu().numpy().reshape(r.shape)
+        if r.size == 0:
+            continue
         if n in ("dL_dscales", "dL_drotations") and cov3 is not None:
             assert np.abs(mine).max() == 0.0
             continue
