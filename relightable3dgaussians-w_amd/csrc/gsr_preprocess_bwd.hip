@@ -13,6 +13,8 @@
 
 namespace gsr {
 
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* s_sh, int sh_stride);
+
 // auxiliary.h:107-117
 __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
     const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
@@ -24,9 +26,34 @@ __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
     return o;
 }
 
+// SH rows ([M][3] floats = 192 B at degree 3) are moved between HBM and LDS by whole rows
+// (coalesced), processed per thread from LDS (stride M*3+1: conflict-free), and the
+// gradient rows go back out the same way.
+__device__ __forceinline__ void copy_rows(float* dst, int dst_stride, const float* src, int src_stride, int rows,
+                                          int width) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+    for (int r = wave; r < rows; r += nw)
+        for (int e = lane; e < width; e += 64) dst[r * dst_stride + e] = src[r * src_stride + e];
+}
+
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+    extern __shared__ float s_sh[];
+    const int M3 = a.M * 3, sh_stride = M3 + 1;
+    const int g0 = blockIdx.x * blockDim.x;
+    const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
+    if (a.shs) {
+        copy_rows(s_sh, sh_stride, a.shs + (size_t)g0 * M3, M3, rows, M3);
+        __syncthreads();
+    }
+    const int idx = g0 + threadIdx.x;
+    if (idx < a.P) preprocess_bwd_one(a, idx, s_sh, sh_stride);
+    if (a.dL_dsh) {
+        __syncthreads();
+        copy_rows(a.dL_dsh + (size_t)g0 * M3, M3, s_sh, sh_stride, rows, M3);
+    }
+}
+
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* s_sh, int sh_stride) {
     // ---- unpack the render-backward accumulator line ------------------------------
     const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
     const float4 l0 = line[0], l1 = line[1];
@@ -43,7 +70,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     a.dL_dcolor[3 * idx + 2] = dcol2;
 
     float* dcov = a.dL_dcov3D + 6 * idx;
-    float* dsh = a.dL_dsh ? a.dL_dsh + (size_t)idx * a.M * 3 : nullptr;
+    float* dsh = a.dL_dsh ? s_sh + threadIdx.x * sh_stride : nullptr;  // LDS row, written back by the caller
     if (!(a.radii[idx] > 0)) {
         a.dL_dmean3D[3 * idx + 0] = 0.f;
         a.dL_dmean3D[3 * idx + 1] = 0.f;
@@ -157,8 +184,9 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     dm.z += (proj[8] * m_w - proj[11] * mul1) * dm2x + (proj[9] * m_w - proj[11] * mul2) * dm2y;
 
     if (a.shs) {
-        // backward.cu:20-139
-        const float* sh = a.shs + (size_t)idx * a.M * 3;
+        // backward.cu:20-139 on this Gaussian's LDS row (coalesced in/out, see below);
+        // each degree block reads its coefficients before overwriting them with dL/dsh.
+        float* sh = s_sh + threadIdx.x * sh_stride;
         const float3 raw = sh_to_rgb_raw(a.D, mean, a.campos, sh);  // clamp flags, as the forward
         const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
         const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
@@ -166,6 +194,7 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         float g[3] = {dcol0 * (raw.x < 0 ? 0 : 1), dcol1 * (raw.y < 0 ? 0 : 1), dcol2 * (raw.z < 0 ? 0 : 1)};
         float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
         const int deg = a.D;
+        float* dsh = sh;
 #define SHC(k, c) sh[3 * (k) + (c)]
 #pragma unroll
         for (int c = 0; c < 3; c++) dsh[c] = SH_C0 * g[c];
@@ -173,12 +202,12 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
             const float b1 = -SH_C1 * y, b2 = SH_C1 * z, b3 = -SH_C1 * x;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
-                dsh[3 + c] = b1 * g[c];
-                dsh[6 + c] = b2 * g[c];
-                dsh[9 + c] = b3 * g[c];
                 ddx[c] = -SH_C1 * SHC(3, c);
                 ddy[c] = -SH_C1 * SHC(1, c);
                 ddz[c] = SH_C1 * SHC(2, c);
+                dsh[3 + c] = b1 * g[c];
+                dsh[6 + c] = b2 * g[c];
+                dsh[9 + c] = b3 * g[c];
             }
             if (deg > 1) {
                 const float xx = x * x, yy = y * y, zz = z * z;
@@ -187,16 +216,16 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
                 const float b7 = SH_C2_3 * xz, b8 = SH_C2_4 * (xx - yy);
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    dsh[12 + c] = b4 * g[c];
-                    dsh[15 + c] = b5 * g[c];
-                    dsh[18 + c] = b6 * g[c];
-                    dsh[21 + c] = b7 * g[c];
-                    dsh[24 + c] = b8 * g[c];
                     ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
                               SH_C2_4 * 2.f * x * SHC(8, c);
                     ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
                               SH_C2_4 * 2.f * -y * SHC(8, c);
                     ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
+                    dsh[12 + c] = b4 * g[c];
+                    dsh[15 + c] = b5 * g[c];
+                    dsh[18 + c] = b6 * g[c];
+                    dsh[21 + c] = b7 * g[c];
+                    dsh[24 + c] = b8 * g[c];
                 }
                 if (deg > 2) {
                     const float b9 = SH_C3_0 * y * (3.f * xx - yy);
@@ -208,13 +237,6 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
                     const float b15 = SH_C3_6 * x * (xx - 3.f * yy);
 #pragma unroll
                     for (int c = 0; c < 3; c++) {
-                        dsh[27 + c] = b9 * g[c];
-                        dsh[30 + c] = b10 * g[c];
-                        dsh[33 + c] = b11 * g[c];
-                        dsh[36 + c] = b12 * g[c];
-                        dsh[39 + c] = b13 * g[c];
-                        dsh[42 + c] = b14 * g[c];
-                        dsh[45 + c] = b15 * g[c];
                         ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
                                    SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
                                    SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
@@ -226,13 +248,21 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
                         ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
                                    SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
                                    SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
+                        dsh[27 + c] = b9 * g[c];
+                        dsh[30 + c] = b10 * g[c];
+                        dsh[33 + c] = b11 * g[c];
+                        dsh[36 + c] = b12 * g[c];
+                        dsh[39 + c] = b13 * g[c];
+                        dsh[42 + c] = b14 * g[c];
+                        dsh[45 + c] = b15 * g[c];
                     }
                 }
             }
         }
 #undef SHC
         // coefficients above the evaluated degree get zero gradient (torch::zeros in the reference)
-        for (int k = (deg + 1) * (deg + 1); k < a.M; k++) {
+        const int kmin = deg < 0 ? 0 : (deg > 3 ? 16 : (deg + 1) * (deg + 1));
+        for (int k = kmin; k < a.M; k++) {
             dsh[3 * k] = 0.f;
             dsh[3 * k + 1] = 0.f;
             dsh[3 * k + 2] = 0.f;
@@ -244,8 +274,6 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         dm.x += d.x;
         dm.y += d.y;
         dm.z += d.z;
-    } else if (dsh) {
-        for (int i = 0; i < a.M * 3; i++) dsh[i] = 0.f;
     }
     a.dL_dmean3D[3 * idx + 0] = dm.x;
     a.dL_dmean3D[3 * idx + 1] = dm.y;
@@ -306,7 +334,10 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {
     if (a.P == 0) return;
-    hipLaunchKernelGGL(k_preprocess_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    // 256 Gaussians per workgroup while their SH rows fit 64 KiB of LDS, else 64
+    const size_t row = a.shs ? (size_t)(a.M * 3 + 1) * sizeof(float) : 0;
+    const int threads = row * 256 <= 65536 ? 256 : 64;
+    hipLaunchKernelGGL(k_preprocess_bwd, dim3((a.P + threads - 1) / threads), dim3(threads), row * threads, s, a);
 }
 
 }  // namespace gsr

@@ -1,0 +1,79 @@
+// gsr_tile.hpp -- helpers shared by the forward and backward tile passes.
+#pragma once
+#include "gsr_common.hpp"
+
+namespace gsr {
+
+// bijective XCD-aware block -> tile remap: blocks b and b+8 run on the same XCD (private
+// L2), so each XCD gets a contiguous band of tiles whose Gaussian records overlap.
+__device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned n) {
+    const unsigned q = n >> 3, r = n & 7u, x = b & 7u;
+    const unsigned base = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    return base + (b >> 3);
+}
+
+// exp as the tile loops evaluate it, identical in forward and backward so that the
+// backward replays exactly the forward's blend decisions (v_exp_f32 on x*log2(e)).
+__device__ __forceinline__ float tile_exp(float x) { return __expf(x); }
+
+// Minimum over the pixel box [dx0,dx1]x[dy0,dy1] (offsets from the Gaussian centre) of
+// q(d) = a dx^2 + 2 b dx dy + c dy^2, for a positive-definite conic (a, b, c).
+__device__ __forceinline__ float qmin_box(float a, float b, float c, float dx0, float dx1, float dy0, float dy1) {
+    if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return 0.f;
+    // edges dx = const: argmin dy = -b dx / c ; edges dy = const: argmin dx = -b dy / a
+    const float ic = 1.f / c, ia = 1.f / a;
+    float q = 3.4e38f;
+    {
+        const float X = dx0;
+        const float y = fminf(fmaxf(-b * X * ic, dy0), dy1);
+        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
+    }
+    {
+        const float X = dx1;
+        const float y = fminf(fmaxf(-b * X * ic, dy0), dy1);
+        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
+    }
+    {
+        const float Y = dy0;
+        const float x = fminf(fmaxf(-b * Y * ia, dx0), dx1);
+        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
+    }
+    {
+        const float Y = dy1;
+        const float x = fminf(fmaxf(-b * Y * ia, dx0), dx1);
+        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
+    }
+    return q;
+}
+
+// Conservative test: can this Gaussian reach alpha >= 1/255 at any integer pixel of the
+// box?  The render loops evaluate alpha = min(0.99, o * exp(-q/2)) and skip alpha < 1/255,
+// so a Gaussian with o * exp(-qmin/2) < 1/255 contributes nothing to any pixel of the box
+// (in the forward, the backward, n_contrib or T).  `lnthr` = ln(255 * o).  The margin
+// covers the float rounding of q at the pixels (relative to the magnitude of its terms)
+// and of the exp/threshold evaluation, so the skip is never wrong.
+__device__ __forceinline__ bool box_reachable(float a, float b, float c, float lnthr, float dx0, float dx1, float dy0,
+                                              float dy1) {
+    const float q = qmin_box(a, b, c, dx0, dx1, dy0, dy1);
+    const float mx = fmaxf(fabsf(dx0), fabsf(dx1)), my = fmaxf(fabsf(dy0), fabsf(dy1));
+    const float S = a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my;
+    return q <= 2.f * lnthr + 1e-2f + 1e-4f * S;
+}
+
+// All-lane wave64 float sum on the VALU: 4 DPP row steps + the gfx950 permlane swaps.
+template <int ctrl>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp<0x124>(v);  // row_ror:4
+    v += dpp<0x128>(v);  // row_ror:8   -> every lane holds its 16-lane row sum
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(s[0]) + __uint_as_float(s[1]);  // rows (0,1) and (2,3)
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // halves
+}
+
+}  // namespace gsr
