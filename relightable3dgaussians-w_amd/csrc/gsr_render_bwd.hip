@@ -5,10 +5,9 @@
 //  * the replay starts at the tile's largest n_contrib (positions past every pixel's last
 //    contributor are skipped by the reference too) and stages records from the back with
 //    the forward's conservative tile/quadrant culling and ballot compaction;
-//  * per Gaussian, the wave's 64 lanes reduce their 9 partial gradients on the VALU
-//    (DPP row steps + gfx950 permlane swaps, wave_sum) -- skipped when no lane of the
-//    wave contributes -- and 9 lanes add the 9 sums into a per-tile LDS row in one
-//    ds_add instruction;
+//  * per Gaussian, each 16-lane row of the wave reduces its 9 partial gradients on the
+//    VALU (4 fused DPP adds per value) -- skipped when no lane of the wave contributes --
+//    and 36 lanes (9 per row) add the row sums into the tile's LDS row with one ds_add;
 //  * after each batch the tile flushes one 9-float row per Gaussian to the 64-B
 //    per-Gaussian accumulator line; one wave-instruction covers 4 whole lines.
 #include "gsr_block.hpp"
@@ -154,26 +153,29 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
                 }
             }
             if (__ballot(active) != 0ull) {
-                g0 = wave_sum(g0);
-                g1 = wave_sum(g1);
-                g2 = wave_sum(g2);
-                g3 = wave_sum(g3);
-                g4 = wave_sum(g4);
-                g5 = wave_sum(g5);
-                g6 = wave_sum(g6);
-                g7 = wave_sum(g7);
-                g8 = wave_sum(g8);
-                if (lane < 9) {
+                // 16-lane row sums on the VALU, then lanes c < 9 of every row add component c
+                // of their row into the tile's LDS row (one ds_add_f32, 4 rows per address)
+                g0 = row_sum(g0);
+                g1 = row_sum(g1);
+                g2 = row_sum(g2);
+                g3 = row_sum(g3);
+                g4 = row_sum(g4);
+                g5 = row_sum(g5);
+                g6 = row_sum(g6);
+                g7 = row_sum(g7);
+                g8 = row_sum(g8);
+                const int c = lane & 15;
+                if (c < 9) {
                     float v = g0;
-                    v = lane == 1 ? g1 : v;
-                    v = lane == 2 ? g2 : v;
-                    v = lane == 3 ? g3 : v;
-                    v = lane == 4 ? g4 : v;
-                    v = lane == 5 ? g5 : v;
-                    v = lane == 6 ? g6 : v;
-                    v = lane == 7 ? g7 : v;
-                    v = lane == 8 ? g8 : v;
-                    atomicAdd(&s_acc[k][lane], v);
+                    v = c == 1 ? g1 : v;
+                    v = c == 2 ? g2 : v;
+                    v = c == 3 ? g3 : v;
+                    v = c == 4 ? g4 : v;
+                    v = c == 5 ? g5 : v;
+                    v = c == 6 ? g6 : v;
+                    v = c == 7 ? g7 : v;
+                    v = c == 8 ? g8 : v;
+                    atomicAdd(&s_acc[k][c], v);
                 }
             }
         }

@@ -33,19 +33,25 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
 
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const uint32_t* keys, int shift,
                                                                uint32_t mask, uint32_t* hist, int nb) {
+    // per-wave LDS sub-histograms (ds_add_u32), keys read 16 B per lane
     __shared__ uint32_t cnt[4][256];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    const long long base = (long long)blockIdx.x * SORT_TILE + wave * WAVE_ITEMS;
-    volatile uint32_t* wc = cnt[wave];
-#pragma unroll 4
-    for (int k = 0; k < SORT_ITEMS; k++) {
-        const long long i = base + k * 64 + lane;
-        const bool valid = i < n;
-        const uint32_t d = valid ? ((keys[i] >> shift) & mask) : 0u;
-        const uint64_t m = peer_mask(d, valid);
-        if (valid && lane == (int)(__ffsll((unsigned long long)m) - 1)) wc[d] = wc[d] + (uint32_t)__popcll(m);
+    const long long tile_base = (long long)blockIdx.x * SORT_TILE;
+    uint32_t* wc = cnt[wave];
+    if (tile_base + SORT_TILE <= n) {
+        const uint4* k4 = reinterpret_cast<const uint4*>(keys + tile_base);
+#pragma unroll
+        for (int r = 0; r < SORT_ITEMS / 4; r++) {
+            const uint4 v = k4[r * SORT_THREADS + threadIdx.x];
+            atomicAdd(&wc[(v.x >> shift) & mask], 1u);
+            atomicAdd(&wc[(v.y >> shift) & mask], 1u);
+            atomicAdd(&wc[(v.z >> shift) & mask], 1u);
+            atomicAdd(&wc[(v.w >> shift) & mask], 1u);
+        }
+    } else {
+        for (long long i = tile_base + threadIdx.x; i < n; i += SORT_THREADS) atomicAdd(&wc[(keys[i] >> shift) & mask], 1u);
     }
     __syncthreads();
     const int d = threadIdx.x;

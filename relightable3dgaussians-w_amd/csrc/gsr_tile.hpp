@@ -65,6 +65,13 @@ template <int ctrl>
 __device__ __forceinline__ float dpp(float v) {
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xf, 0xf, true));
 }
+// Every lane receives the sum over its 16-lane DPP row (4 fused v_add_f32_dpp).
+__device__ __forceinline__ float row_sum(float v) {
+    v += dpp<0xB1>(v);
+    v += dpp<0x4E>(v);
+    v += dpp<0x124>(v);
+    return v + dpp<0x128>(v);
+}
 __device__ __forceinline__ float wave_sum(float v) {
     v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
