@@ -42,8 +42,6 @@ def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
         "render_fwd": T * 8 + R * 40 + Npix * 20,
         "render_bwd": T * 8 + R * 40 + Npix * 20 + Pv * 44,
         "preprocess_bwd": P * 4 + Pv * (12 + 12 + 12 + 12 + 3 + 12 + 16 + 24 + 12 * M) + Pv * (12 + 12 + 16 + 12 * M),
-        "tile_sort": R * 24,
-        "duplicate": P * 4 + Pv * 16 + R * 12,
     }.get(stage)
 
 

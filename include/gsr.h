@@ -102,7 +102,7 @@ typedef struct gsr_layout {
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
 
 /* Stage profiling: when enabled, every stage (preprocess, compact, depth_sort, offsets_scan,
- * duplicate, tile_sort, ranges, render_fwd, bwd_zero, render_bwd, preprocess_bwd, shade_fwd,
+ * st_emit, st_sort, tile_lists, render_fwd, bwd_zero, render_bwd, preprocess_bwd, shade_fwd,
  * shade_bwd) is bracketed by hipEvents on the call's stream.  gsr_profile_read() waits for
  * the recorded events and returns accumulated milliseconds and launch counts per stage. */
 int gsr_profile_enable(int on);

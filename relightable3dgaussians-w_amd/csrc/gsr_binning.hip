@@ -1,32 +1,45 @@
-// gsr_binning.hip -- instance emission and tile ranges (rasterizer_impl.cu:70-138).
+// gsr_binning.hip -- instance lists per tile (rasterizer_impl.cu:70-138 re-designed).
 //
-// Differences from the reference, with identical results:
-//  * instances are emitted in DEPTH order (after sorting the visible Gaussians by their
-//    depth key), carrying the tile id alone as the sort key; the stable tile-only sort
-//    then reproduces the reference's (tile, depth, index) order exactly;
-//  * ranges are produced for the T tiles only (the reference sizes its image buffer by
-//    pixel count, :172-179, but only T entries are ever used).
+// The reference emits one 64-bit key (tile << 32 | depth) per (Gaussian, tile) pair --
+// R of them, ~28M at 1.5M Gaussians/1080p -- and radix-sorts all R on 32+13 bits.  Here:
+//   1. the P_v visible Gaussians are sorted once by depth (gsr_sort.hip);
+//   2. in that order every Gaussian emits one entry per SUPER-TILE (8x4 tiles) its rect
+//      touches (k_st_emit: S ~ 1.3 P_v entries instead of R);
+//   3. the S entries are stably sorted by super-tile id (one 8-bit pass at 1080p);
+//   4. each super-tile list is cut into 1024-entry segments (k_seg_table); one workgroup
+//      per segment keeps, for each of the super-tile's 32 tiles, the entries whose rect
+//      covers it with an order-preserving wave-ballot compaction.  A count pass
+//      (k_seg_lists<false>), a per-tile prefix over segments (k_seg_prefix), a scan over
+//      tiles (= the reference's ranges) and a write pass (k_seg_lists<true>) produce
+//      point_list directly, in coalesced runs.
+// Every step is stable, so each tile's list is exactly the reference's order
+// (depth-bits ascending, Gaussian index ascending on ties), bit-exact.
+#include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
 
 namespace gsr {
 
-// One wave emits the instances of 64 consecutive depth-sorted Gaussians as one flat,
-// contiguous run: lane i writes instance i, i+64, ... (coalesced 4-B stores), finding its
-// Gaussian by binary search over the wave's inclusive tile-count prefix in LDS.
-__global__ void __launch_bounds__(256) k_duplicate(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets,
-                                                    const uint2* rect, unsigned grid_x, uint32_t* tile_keys,
-                                                    uint32_t* gauss_vals) {
+// ---- 2. super-tile emission -----------------------------------------------------------
+// One wave emits the entries of 64 consecutive depth-sorted Gaussians as one contiguous
+// run: lane i writes entry i, i+64, ... (coalesced), locating its Gaussian by binary
+// search over the wave's inclusive count prefix in LDS.
+__global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets,
+                                                  const uint2* rect, unsigned gsx, uint32_t* st_keys,
+                                                  uint32_t* st_vals) {
     __shared__ uint32_t s_inc[4][64];
     __shared__ uint32_t s_id[4][64];
-    __shared__ uint2 s_rect[4][64];
+    __shared__ uint2 s_srect[4][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t idx = 0, cnt = 0;
-    uint2 r = make_uint2(0, 0);
+    uint2 sr = make_uint2(0, 0);
     if (s < Pv) {
         idx = sorted_ids[s];
-        r = rect[idx];
-        cnt = ((r.x >> 16) - (r.x & 0xffffu)) * ((r.y >> 16) - (r.y & 0xffffu));
+        const uint2 r = rect[idx];
+        const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
+        const uint32_t sy0 = (r.y & 0xffffu) / GSR_ST_H, sy1 = ((r.y >> 16) + GSR_ST_H - 1) / GSR_ST_H;
+        sr = make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
+        cnt = (sx1 - sx0) * (sy1 - sy0);
     }
     uint32_t inc = cnt;
 #pragma unroll
@@ -36,31 +49,31 @@ __global__ void __launch_bounds__(256) k_duplicate(int Pv, const uint32_t* sorte
     }
     s_inc[wave][lane] = inc;
     s_id[wave][lane] = idx;
-    s_rect[wave][lane] = r;
+    s_srect[wave][lane] = sr;
     const int s0 = blockIdx.x * blockDim.x + wave * 64;
     const uint32_t base = s0 < Pv ? offsets[s0] : 0u;
     const uint32_t total = __shfl(inc, 63, 64);
     __syncthreads();
     for (uint32_t i = lane; i < total; i += 64) {
-        // first j with s_inc[j] > i
-        int lo = 0, hi = 63;
+        int lo = 0, hi = 63;  // first j with s_inc[j] > i
         while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (s_inc[wave][mid] > i) hi = mid;
             else lo = mid + 1;
         }
         const uint32_t k = i - (lo ? s_inc[wave][lo - 1] : 0u);
-        const uint2 rr = s_rect[wave][lo];
+        const uint2 rr = s_srect[wave][lo];
         const uint32_t x0 = rr.x & 0xffffu, w = (rr.x >> 16) - x0, y0 = rr.y & 0xffffu;
         const uint32_t yy = k / w, xx = k - yy * w;
-        tile_keys[base + i] = (y0 + yy) * grid_x + (x0 + xx);
-        gauss_vals[base + i] = s_id[wave][lo];
+        st_keys[base + i] = (y0 + yy) * gsx + (x0 + xx);
+        st_vals[base + i] = s_id[wave][lo];
     }
 }
 
-__global__ void __launch_bounds__(256) k_ranges(long long R, const uint32_t* keys, uint2* ranges) {
+// super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
+__global__ void __launch_bounds__(256) k_seg_ranges(long long n, const uint32_t* keys, uint2* ranges) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= R) return;
+    if (i >= n) return;
     const uint32_t cur = keys[i];
     if (i == 0) {
         ranges[cur].x = 0;
@@ -71,20 +84,207 @@ __global__ void __launch_bounds__(256) k_ranges(long long R, const uint32_t* key
             ranges[cur].x = (uint32_t)i;
         }
     }
-    if (i == R - 1) ranges[cur].y = (uint32_t)R;
+    if (i == n - 1) ranges[cur].y = (uint32_t)n;
 }
 
-void launch_duplicate(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect,
-                      unsigned grid_x, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s) {
+// ---- 4. per-super-tile tile filters ------------------------------------------------------
+constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32
+
+struct StGeom {
+    unsigned tx0, ty0, nx, ny;
+};
+__device__ __forceinline__ StGeom st_geom(unsigned st, unsigned gsx, unsigned gx, unsigned gy) {
+    StGeom g;
+    g.tx0 = (st % gsx) * GSR_ST_W;
+    g.ty0 = (st / gsx) * GSR_ST_H;
+    g.nx = min(GSR_ST_W, gx - g.tx0);
+    g.ny = min(GSR_ST_H, gy - g.ty0);
+    return g;
+}
+
+// Segment table: every super-tile list is cut into segments of SEG entries; segment g
+// covers entries [seg_e0[g], min(seg_e0[g] + SEG, end of its super-tile)).
+constexpr uint32_t SEG = 1024;
+
+__global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_ranges, uint32_t* seg_st,
+                                                    uint32_t* seg_e0, uint32_t* st_seg0, uint32_t* nseg_total) {
+    // single workgroup: exclusive scan of per-super-tile segment counts, then fill the table
+    __shared__ uint32_t sh[4];
+    uint32_t carry = 0;
+    for (int c = 0; c < nst; c += 256) {
+        const int st = c + threadIdx.x;
+        uint32_t n = 0;
+        uint2 r = make_uint2(0, 0);
+        if (st < nst) {
+            r = st_ranges[st];
+            n = (r.y - r.x + SEG - 1) / SEG;
+        }
+        uint32_t tot;
+        const uint32_t off = carry + block256_exclusive_scan(n, sh, &tot);
+        if (st < nst) {
+            st_seg0[st] = off;
+            for (uint32_t k = 0; k < n; k++) {
+                seg_st[off + k] = (uint32_t)st;
+                seg_e0[off + k] = r.x + k * SEG;
+            }
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        st_seg0[nst] = carry;
+        *nseg_total = carry;
+    }
+}
+
+// Count (WRITE = false) or write (WRITE = true) one segment: for each of the super-tile's
+// 32 tiles, the entries whose rect covers it, ranked in list order by wave ballots.
+template <bool WRITE>
+__global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, const uint32_t* seg_st,
+                                                    const uint32_t* seg_e0, const uint2* st_ranges,
+                                                    const uint32_t* st_vals, const uint2* rect, unsigned gx,
+                                                    unsigned gy, unsigned gsx, uint32_t* seg_cnt,
+                                                    const uint32_t* seg_base, uint32_t* point_list) {
+    __shared__ uint32_t s_wc[4][ST_TILES];
+    __shared__ uint32_t s_run[ST_TILES];
+    const uint32_t gseg = blockIdx.x;
+    if (gseg >= *nseg_total) return;
+    const unsigned st = seg_st[gseg];
+    const StGeom g = st_geom(st, gsx, gx, gy);
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    const uint32_t e0 = seg_e0[gseg];
+    const uint32_t e1 = min(e0 + SEG, st_ranges[st].y);
+    if (tid < ST_TILES) s_run[tid] = WRITE ? seg_base[(size_t)gseg * ST_TILES + tid] : 0u;
+    __syncthreads();
+    for (uint32_t b = e0; b < e1; b += 256) {
+        const uint32_t e = b + tid;
+        const bool valid = e < e1;
+        uint32_t id = 0, mask = 0;
+        if (valid) {
+            id = st_vals[e];
+            const uint2 r = rect[id];
+            // local tile coverage mask (bit t = (t / 8) row, (t % 8) column)
+            const int cx0 = max((int)(r.x & 0xffffu) - (int)g.tx0, 0), cx1 = min((int)(r.x >> 16) - (int)g.tx0, (int)g.nx);
+            const int cy0 = max((int)(r.y & 0xffffu) - (int)g.ty0, 0), cy1 = min((int)(r.y >> 16) - (int)g.ty0, (int)g.ny);
+            if (cx1 > cx0 && cy1 > cy0) {
+                const uint32_t row = ((1u << cx1) - 1u) & ~((1u << cx0) - 1u);
+                for (int y = cy0; y < cy1; y++) mask |= row << (GSR_ST_W * y);
+            }
+        }
+        uint64_t bal[ST_TILES];
+#pragma unroll
+        for (int t = 0; t < ST_TILES; t++) bal[t] = __ballot((mask >> t) & 1u);
+        if (lane < ST_TILES) {
+            uint64_t mine = 0;
+#pragma unroll
+            for (int t = 0; t < ST_TILES; t++) mine = lane == t ? bal[t] : mine;
+            s_wc[wave][lane] = (uint32_t)__popcll(mine);
+        }
+        __syncthreads();
+        if (WRITE && mask) {
+#pragma unroll
+            for (int t = 0; t < ST_TILES; t++) {
+                if ((mask >> t) & 1u) {
+                    uint32_t p = s_run[t] + (uint32_t)__popcll(bal[t] & lt);
+                    for (int w = 0; w < wave; w++) p += s_wc[w][t];
+                    point_list[p] = id;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid < ST_TILES) s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
+        __syncthreads();
+    }
+    if (!WRITE && tid < ST_TILES) seg_cnt[(size_t)gseg * ST_TILES + tid] = s_run[tid];
+}
+
+// Per (super-tile, local tile): prefix of the segment counts -> segment-relative bases,
+// and the tile's total count.
+__global__ void __launch_bounds__(256) k_seg_prefix(int nst, const uint32_t* st_seg0, unsigned gx, unsigned gy,
+                                                     unsigned gsx, uint32_t* seg_cnt_to_base, uint32_t* tile_cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nst * (int)ST_TILES) return;
+    const unsigned st = i / ST_TILES, t = i % ST_TILES;
+    const StGeom g = st_geom(st, gsx, gx, gy);
+    const unsigned lx = t % GSR_ST_W, ly = t / GSR_ST_W;
+    uint32_t run = 0;
+    for (uint32_t k = st_seg0[st]; k < st_seg0[st + 1]; k++) {
+        const uint32_t c = seg_cnt_to_base[(size_t)k * ST_TILES + t];
+        seg_cnt_to_base[(size_t)k * ST_TILES + t] = run;
+        run += c;
+    }
+    if (lx < g.nx && ly < g.ny) tile_cnt[(g.ty0 + ly) * gx + g.tx0 + lx] = run;
+}
+
+// segment bases become absolute: += tile_start of the tile
+__global__ void __launch_bounds__(256) k_seg_absolute(const uint32_t* nseg_total, const uint32_t* seg_st, unsigned gx,
+                                                       unsigned gy, unsigned gsx, const uint32_t* tile_start,
+                                                       uint32_t* seg_base, long long max_items) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= max_items || i >= (long long)(*nseg_total) * ST_TILES) return;
+    const uint32_t gseg = (uint32_t)(i / ST_TILES), t = (uint32_t)(i % ST_TILES);
+    const StGeom g = st_geom(seg_st[gseg], gsx, gx, gy);
+    const unsigned lx = t % GSR_ST_W, ly = t / GSR_ST_W;
+    if (lx < g.nx && ly < g.ny) seg_base[i] += tile_start[(g.ty0 + ly) * gx + g.tx0 + lx];
+}
+
+// ranges[t] = [start, start + cnt), (0, 0) for empty tiles (rasterizer_impl.cu:310-318)
+__global__ void __launch_bounds__(256) k_tile_ranges(int T, const uint32_t* tile_cnt, const uint32_t* tile_start,
+                                                      uint2* ranges) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t c = tile_cnt[t];
+    ranges[t] = c ? make_uint2(tile_start[t], tile_start[t] + c) : make_uint2(0u, 0u);
+}
+
+// ---- host launchers ---------------------------------------------------------------------
+void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
+                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s) {
     if (Pv == 0) return;
-    hipLaunchKernelGGL(k_duplicate, dim3((Pv + 255) / 256), dim3(256), 0, s, Pv, sorted_ids, offsets, rect, grid_x,
-                       tile_keys, gauss_vals);
+    hipLaunchKernelGGL(k_st_emit, dim3((Pv + 255) / 256), dim3(256), 0, s, Pv, sorted_ids, offsets, rect, gsx, st_keys,
+                       st_vals);
 }
 
-void launch_ranges(long long R, int T, const uint32_t* sorted_tile_keys, uint2* ranges, hipStream_t s) {
-    hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)T, s);
-    if (R == 0) return;
-    hipLaunchKernelGGL(k_ranges, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, s, R, sorted_tile_keys, ranges);
+void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s) {
+    (void)hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)nseg, s);
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_seg_ranges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, sorted_keys, ranges);
+}
+
+size_t tile_lists_temp_bytes(long long S, int nst) {
+    const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
+    return 4 * (2 * G + (nst + 1) + 1 + G * ST_TILES) + 256;
+}
+
+void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_vals, const uint2* rect,
+                       unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
+                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s) {
+    const int T = (int)(gx * gy);
+    const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
+    uint32_t* seg_st = reinterpret_cast<uint32_t*>(temp);
+    uint32_t* seg_e0 = seg_st + G;
+    uint32_t* st_seg0 = seg_e0 + G;
+    uint32_t* nseg_total = st_seg0 + nst + 1;
+    uint32_t* seg_cnt = nseg_total + 1;  // [G][32], becomes the segment bases in place
+    hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total);
+    if (G > 0) {
+        hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
+                           st_ranges, st_vals, rect, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
+                           (uint32_t*)nullptr);
+    }
+    (void)hipMemsetAsync(tile_cnt, 0, sizeof(uint32_t) * (size_t)T, s);
+    const int np = nst * (int)ST_TILES;
+    hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, st_seg0, gx, gy, gsx, seg_cnt,
+                       tile_cnt);
+    launch_exclusive_scan_u32(T, tile_cnt, nullptr, tile_start, scan_tmp, nullptr, s);
+    hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, T, tile_cnt, tile_start, ranges);
+    if (G > 0) {
+        const long long items = (long long)G * ST_TILES;
+        hipLaunchKernelGGL(k_seg_absolute, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, nseg_total, seg_st,
+                           gx, gy, gsx, tile_start, seg_cnt, items);
+        hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
+                           st_ranges, st_vals, rect, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, point_list);
+    }
 }
 
 }  // namespace gsr

@@ -55,14 +55,15 @@ struct Carver {
 };
 
 struct GeomLayout {
-    size_t totals, radii, tiles, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, offsets,
-        scan_tmp, sort_tmp, total;
+    size_t totals, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt,
+        offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, total;
 };
 struct BinLayout {
-    size_t tile_keys, tile_keys_alt, point, point_alt, sort_tmp, total;
+    size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_ranges, tile_cnt, tile_start, scan_tmp,
+        lists_tmp, total;
 };
 
 GeomLayout geom_layout(long long P) {
@@ -71,6 +72,7 @@ GeomLayout geom_layout(long long P) {
     L.totals = c.take(64);
     L.radii = c.take(4 * P);
     L.tiles = c.take(4 * P);
+    L.st_count = c.take(4 * P);
     L.depth_key = c.take(4 * P);
     L.rect = c.take(8 * P);
     L.rec = c.take(sizeof(gsr::Rec) * P);
@@ -80,7 +82,7 @@ GeomLayout geom_layout(long long P) {
     L.vis_key_alt = c.take(4 * P);
     L.vis_val_alt = c.take(4 * P);
     L.offsets = c.take(4 * P);
-    L.scan_tmp = c.take(16 * (size_t)gsr::scan_blocks(P) + 16);
+    L.scan_tmp = c.take(24 * (size_t)gsr::scan_blocks(P) + 16);
     L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(P));
     L.total = c.o + 256;
     return L;
@@ -101,14 +103,25 @@ ImgLayout img_layout(int W, int H) {
     return L;
 }
 
-BinLayout bin_layout(long long R) {
+unsigned st_x(int W) { return (tiles_x(W) + GSR_ST_W - 1) / GSR_ST_W; }
+unsigned st_y(int H) { return (tiles_y(H) + GSR_ST_H - 1) / GSR_ST_H; }
+
+// point_list first: the backward needs only it (offset 0, independent of S)
+BinLayout bin_layout(long long R, long long S, int W, int H) {
     Carver c;
     BinLayout L;
-    L.tile_keys = c.take(4 * R);
-    L.tile_keys_alt = c.take(4 * R);
+    const size_t NS = (size_t)st_x(W) * st_y(H), T = (size_t)tiles_x(W) * tiles_y(H);
     L.point = c.take(4 * R);
-    L.point_alt = c.take(4 * R);
-    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(R));
+    L.st_keys = c.take(4 * S);
+    L.st_vals = c.take(4 * S);
+    L.st_keys_alt = c.take(4 * S);
+    L.st_vals_alt = c.take(4 * S);
+    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(S));
+    L.st_ranges = c.take(8 * NS);
+    L.tile_cnt = c.take(4 * T);
+    L.tile_start = c.take(4 * T);
+    L.scan_tmp = c.take(4 * (size_t)gsr::scan_blocks((long long)T) + 16);
+    L.lists_tmp = c.take(gsr::tile_lists_temp_bytes(S, (int)NS));
     L.total = c.o + 256;
     return L;
 }
@@ -124,15 +137,6 @@ uint32_t higher_msb(uint32_t n) {
     }
     if (n >> msb) msb++;
     return msb;
-}
-
-int tile_sort_bits(int W, int H) { return (int)higher_msb(tiles_x(W) * tiles_y(H)); }
-
-// where the tile-sorted instance list ends up (the sort ping-pongs)
-bool point_list_in_alt(long long R, int W, int H) {
-    const int bits = tile_sort_bits(W, H);
-    if (R <= 1 || bits <= 0) return false;
-    return (((bits + 7) / 8) & 1) == 1;
 }
 
 template <typename T>
@@ -161,8 +165,8 @@ enum Stage {
     ST_PREPROCESS, ST_COMPACT, ST_DEPTH_SORT, ST_OFFSETS, ST_DUPLICATE, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD,
     ST_BWD_ZERO, ST_RENDER_BWD, ST_PREPROCESS_BWD, ST_SHADE_FWD, ST_SHADE_BWD, ST_COUNT
 };
-const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "duplicate",
-                                     "tile_sort",   "ranges",       "render_fwd",     "bwd_zero",     "render_bwd",
+const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "st_emit",
+                                     "st_sort",     "tile_lists",       "render_fwd",     "bwd_zero",     "render_bwd",
                                      "preprocess_bwd", "shade_fwd", "shade_bwd"};
 struct Prof {
     bool on = false;
@@ -238,7 +242,7 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     if (!out || P < 0 || R < 0 || width < 0 || height < 0) return fail(GSR_E_ARG, "gsr_get_layout: bad arguments");
     const GeomLayout g = geom_layout(P);
     const ImgLayout im = img_layout(width, height);
-    const BinLayout b = bin_layout(R);
+    const BinLayout b = bin_layout(R, 0, width, height);
     out->geom_bytes = g.total;
     out->img_bytes = im.total;
     out->bin_bytes = b.total;
@@ -251,8 +255,8 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     out->img_final_T = im.final_T;
     out->img_n_contrib = im.n_contrib;
     out->img_ranges = im.ranges;
-    out->bin_point_list = point_list_in_alt(R, width, height) ? b.point_alt : b.point;
-    out->bin_tile_keys = point_list_in_alt(R, width, height) ? b.tile_keys_alt : b.tile_keys;
+    out->bin_point_list = b.point;
+    out->bin_tile_keys = b.st_keys;
     return GSR_OK;
 }
 
@@ -288,7 +292,7 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     if (!radii) radii = at<int>(geom, gl.radii);
 
     unsigned long long* totals = at<unsigned long long>(geom, gl.totals);
-    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 2);
+    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 3);
     HIP_OK(hipMemsetAsync(err_flag, 0, 4, s));
 
     gsr::PreprocessArgs pa;
@@ -300,6 +304,7 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     pa.focal_x = focal_x; pa.focal_y = focal_y; pa.grid_x = gx; pa.grid_y = gy; pa.prefiltered = prefiltered;
     pa.radii = radii;
     pa.tiles = at<uint32_t>(geom, gl.tiles);
+    pa.st_count = at<uint32_t>(geom, gl.st_count);
     pa.depth_key = at<uint32_t>(geom, gl.depth_key);
     pa.rect = at<uint2>(geom, gl.rect);
     pa.rec = at<gsr::Rec>(geom, gl.rec);
@@ -314,21 +319,21 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     uint32_t* vis_val = at<uint32_t>(geom, gl.vis_val);
     {
         GSR_STAGE(ST_COMPACT);
-        gsr::launch_compact_visible(P, pa.tiles, pa.depth_key, vis_key, vis_val,
+        gsr::launch_compact_visible(P, pa.tiles, pa.st_count, pa.depth_key, vis_key, vis_val,
                                     at<unsigned long long>(geom, gl.scan_tmp), totals, s);
     }
     GSR_LAUNCH_CHECK();
 
     if (!g_pinned.p) HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 64, hipHostMallocDefault));
-    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, 24, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, 32, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    const unsigned long long Pv = g_pinned.p[0], R64 = g_pinned.p[1];
-    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 2)[0];
+    const unsigned long long Pv = g_pinned.p[0], R64 = g_pinned.p[1], S64 = g_pinned.p[2];
+    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 3)[0];
     if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
-    const long long R = (long long)R64;
+    const long long R = (long long)R64, S = (long long)S64;
 
-    const BinLayout bl = bin_layout(R);
+    const BinLayout bl = bin_layout(R, S, width, height);
     char* bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
     if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
     bin = align_base(bin);
@@ -345,32 +350,37 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
     {
         GSR_STAGE(ST_OFFSETS);
-        gsr::launch_exclusive_scan_u32((long long)Pv, pa.tiles, sorted_ids, offsets,
+        gsr::launch_exclusive_scan_u32((long long)Pv, pa.st_count, sorted_ids, offsets,
                                        at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
     }
     GSR_LAUNCH_CHECK();
-    uint32_t* tk = at<uint32_t>(bin, bl.tile_keys);
-    uint32_t* pt = at<uint32_t>(bin, bl.point);
+    const unsigned gsx = st_x(width), gsy = st_y(height);
+    const int NS = (int)(gsx * gsy);
+    uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
+    uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
     {
         GSR_STAGE(ST_DUPLICATE);
-        gsr::launch_duplicate((int)Pv, sorted_ids, offsets, pa.rect, gx, tk, pt, s);
+        gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
     }
     GSR_LAUNCH_CHECK();
-    const int bits = tile_sort_bits(width, height);
     int flip2;
     {
         GSR_STAGE(ST_TILE_SORT);
-        flip2 = gsr::radix_sort_pairs(R, tk, pt, at<uint32_t>(bin, bl.tile_keys_alt), at<uint32_t>(bin, bl.point_alt),
-                                      bits, at<void>(bin, bl.sort_tmp), s);
+        flip2 = gsr::radix_sort_pairs(S, stk, stv, at<uint32_t>(bin, bl.st_keys_alt), at<uint32_t>(bin, bl.st_vals_alt),
+                                      (int)higher_msb((uint32_t)NS), at<void>(bin, bl.sort_tmp), s);
     }
     GSR_LAUNCH_CHECK();
-    if ((flip2 != 0) != point_list_in_alt(R, width, height)) return fail(GSR_E_ARG, "internal: sort parity mismatch");
-    const uint32_t* point_list = flip2 ? at<uint32_t>(bin, bl.point_alt) : pt;
-    const uint32_t* sorted_tiles = flip2 ? at<uint32_t>(bin, bl.tile_keys_alt) : tk;
+    const uint32_t* st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
+    const uint32_t* st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
     uint2* ranges = at<uint2>(img, il.ranges);
+    uint32_t* point_list = at<uint32_t>(bin, bl.point);
     {
         GSR_STAGE(ST_RANGES);
-        gsr::launch_ranges(R, T, sorted_tiles, ranges, s);
+        uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
+        gsr::launch_seg_ranges(S, NS, st_sorted_keys, st_ranges, s);
+        gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_vals, pa.rect, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
+                               at<uint32_t>(bin, bl.tile_start), ranges, at<uint32_t>(bin, bl.scan_tmp),
+                               at<void>(bin, bl.lists_tmp), point_list, s);
     }
     GSR_LAUNCH_CHECK();
 
@@ -402,7 +412,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     const float focal_x = width / (2.0f * tan_fovx);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R);
+    const BinLayout bl = bin_layout(R, 0, width, height);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
@@ -418,7 +428,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         gsr::RenderBwdArgs ra;
         ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
         ra.ranges = at<uint2>(img, il.ranges);
-        ra.point_list = point_list_in_alt(R, width, height) ? at<uint32_t>(bin, bl.point_alt) : at<uint32_t>(bin, bl.point);
+        ra.point_list = at<uint32_t>(bin, bl.point);
         ra.rec = at<gsr::Rec>(geom, gl.rec);
         ra.colors = colors_precomp;
         ra.bg = background;

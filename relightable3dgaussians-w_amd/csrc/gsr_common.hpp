@@ -11,6 +11,9 @@
 #define GSR_BLOCK_X 16
 #define GSR_BLOCK_Y 16
 #define GSR_TILE_PIX 256
+// super-tile (binning granularity) in tiles
+#define GSR_ST_W 8u
+#define GSR_ST_H 4u
 
 namespace gsr {
 

@@ -29,6 +29,7 @@ struct PreprocessArgs {
     // outputs
     int* radii;
     uint32_t* tiles;
+    uint32_t* st_count;  // super-tiles touched (binning entries)
     uint32_t* depth_key;
     uint2* rect;
     Rec* rec;
@@ -46,11 +47,11 @@ inline int scan_blocks(long long n) { return (int)((n + SCAN_TILE - 1) / SCAN_TI
 
 // Visibility compaction: tiles[i] > 0 <=> visible.  Produces, in index order (stable),
 // vis_key[j] = depth_key[i], vis_val[j] = i for the j-th visible Gaussian, and
-// totals[0] = number of visible Gaussians, totals[1..2] = 64-bit sum of tiles.
-// block_tmp: scan_blocks(P) * 8 bytes (u64).
-void launch_compact_visible(int P, const uint32_t* tiles, const uint32_t* depth_key, uint32_t* vis_key,
-                            uint32_t* vis_val, unsigned long long* block_tmp, unsigned long long* totals,
-                            hipStream_t s);
+// totals[0] = number of visible Gaussians, totals[1] = sum of tiles (R),
+// totals[2] = sum of st_count (S).  block_tmp: scan_blocks(P) * 24 bytes.
+void launch_compact_visible(int P, const uint32_t* tiles, const uint32_t* st_count, const uint32_t* depth_key,
+                            uint32_t* vis_key, uint32_t* vis_val, unsigned long long* block_tmp,
+                            unsigned long long* totals, hipStream_t s);
 
 // Exclusive scan (u32) of in[0..n) -> out; block_tmp: scan_blocks(n) u32;
 // total (optional) receives the sum.  If gather != nullptr the input is in[gather[i]].
@@ -71,12 +72,18 @@ int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys
                      int end_bit, void* temp, hipStream_t s);
 
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
-// For the depth-sorted visible Gaussians: emit one (tile, gaussian) pair per touched tile,
-// y-major then x, at offsets[s] (exclusive scan of tiles in depth order).
-void launch_duplicate(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect,
-                      unsigned grid_x, uint32_t* tile_keys, uint32_t* gauss_vals, hipStream_t s);
-// ranges[t] = [first, last+1) over the tile-sorted keys; untouched tiles (0, 0).
-void launch_ranges(long long R, int T, const uint32_t* sorted_tile_keys, uint2* ranges, hipStream_t s);
+// In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
+// super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
+void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
+                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
+// ranges[k] = [first, last+1) of key k in a sorted key array; (0, 0) for absent keys.
+void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s);
+// Per-super-tile tile filters over 1024-entry segments: tile counts, tile starts (scan),
+// ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).
+size_t tile_lists_temp_bytes(long long S, int nst);
+void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_vals, const uint2* rect,
+                       unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
+                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s);
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 struct RenderFwdArgs {

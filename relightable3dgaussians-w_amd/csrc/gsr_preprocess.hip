@@ -17,6 +17,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     if (idx >= a.P) return;
     a.radii[idx] = 0;
     a.tiles[idx] = 0;
+    a.st_count[idx] = 0;
     const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     // in_frustum (auxiliary.h:139-164): near cull only
     const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
@@ -69,6 +70,8 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.rect[idx] = make_uint2(rmin.x | (rmax.x << 16), rmin.y | (rmax.y << 16));
     a.radii[idx] = irad;
     a.tiles[idx] = area;
+    a.st_count[idx] = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
+                      ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
 }
 
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,

@@ -10,11 +10,11 @@
 namespace gsr {
 
 // ---------------- visibility compaction ----------------------------------------------
-__global__ void __launch_bounds__(SCAN_THREADS) k_vis_reduce(int P, const uint32_t* tiles,
+__global__ void __launch_bounds__(SCAN_THREADS) k_vis_reduce(int P, const uint32_t* tiles, const uint32_t* stc,
                                                                unsigned long long* block_tmp) {
-    __shared__ unsigned long long sh[4];
+    __shared__ unsigned long long sh[3][4];
     const long long base = (long long)blockIdx.x * SCAN_TILE + (long long)threadIdx.x * SCAN_ITEMS;
-    unsigned long long cnt = 0, sum = 0;
+    unsigned long long cnt = 0, sum = 0, ssum = 0;
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
         const long long i = base + k;
@@ -22,40 +22,47 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_vis_reduce(int P, const uint32
             const uint32_t t = tiles[i];
             cnt += t > 0;
             sum += t;
+            ssum += stc[i];
         }
     }
-    // reduce both: count in the high 24 bits is not safe for large tiles; reduce separately
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     cnt = wave_reduce_sum(cnt);
     sum = wave_reduce_sum(sum);
-    __shared__ unsigned long long sh2[4];
-    if (lane == 0) { sh[wave] = cnt; sh2[wave] = sum; }
+    ssum = wave_reduce_sum(ssum);
+    if (lane == 0) {
+        sh[0][wave] = cnt;
+        sh[1][wave] = sum;
+        sh[2][wave] = ssum;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        block_tmp[2 * blockIdx.x] = sh[0] + sh[1] + sh[2] + sh[3];
-        block_tmp[2 * blockIdx.x + 1] = sh2[0] + sh2[1] + sh2[2] + sh2[3];
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        block_tmp[3 * blockIdx.x + k] = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
     }
 }
 
 __global__ void __launch_bounds__(SCAN_THREADS) k_vis_spine(int nb, unsigned long long* block_tmp,
                                                               unsigned long long* totals) {
     __shared__ unsigned long long sh[4];
-    unsigned long long carry = 0, tsum = 0;
+    unsigned long long carry = 0, tsum = 0, ssum = 0;
     for (int c = 0; c < nb; c += SCAN_THREADS) {
         const int i = c + threadIdx.x;
-        unsigned long long v = i < nb ? block_tmp[2 * i] : 0ull;
-        unsigned long long t = i < nb ? block_tmp[2 * i + 1] : 0ull;
-        unsigned long long tot;
+        unsigned long long v = i < nb ? block_tmp[3 * i] : 0ull;
+        unsigned long long t = i < nb ? block_tmp[3 * i + 1] : 0ull;
+        unsigned long long u = i < nb ? block_tmp[3 * i + 2] : 0ull;
+        unsigned long long tot, tt, uu;
         unsigned long long ex = block256_exclusive_scan(v, sh, &tot);
-        unsigned long long tt;
         block256_exclusive_scan(t, sh, &tt);
-        if (i < nb) block_tmp[2 * i] = carry + ex;
+        block256_exclusive_scan(u, sh, &uu);
+        if (i < nb) block_tmp[3 * i] = carry + ex;
         carry += tot;
         tsum += tt;
+        ssum += uu;
     }
     if (threadIdx.x == 0) {
         totals[0] = carry;
         totals[1] = tsum;
+        totals[2] = ssum;
     }
 }
 
@@ -74,7 +81,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_vis_scatter(int P, const uint3
         cnt += t[k] > 0;
     }
     unsigned long long pos = block256_exclusive_scan(cnt, sh, (unsigned long long*)nullptr) +
-                             block_tmp[2 * blockIdx.x];
+                             block_tmp[3 * blockIdx.x];
 #pragma unroll
     for (int k = 0; k < SCAN_ITEMS; k++) {
         if (t[k] > 0) {
@@ -86,15 +93,15 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_vis_scatter(int P, const uint3
     }
 }
 
-void launch_compact_visible(int P, const uint32_t* tiles, const uint32_t* depth_key, uint32_t* vis_key,
-                            uint32_t* vis_val, unsigned long long* block_tmp, unsigned long long* totals,
-                            hipStream_t s) {
+void launch_compact_visible(int P, const uint32_t* tiles, const uint32_t* st_count, const uint32_t* depth_key,
+                            uint32_t* vis_key, uint32_t* vis_val, unsigned long long* block_tmp,
+                            unsigned long long* totals, hipStream_t s) {
     const int nb = scan_blocks(P);
     if (nb == 0) {
-        hipMemsetAsync(totals, 0, 2 * sizeof(unsigned long long), s);
+        (void)hipMemsetAsync(totals, 0, 3 * sizeof(unsigned long long), s);
         return;
     }
-    hipLaunchKernelGGL(k_vis_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, P, tiles, block_tmp);
+    hipLaunchKernelGGL(k_vis_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, P, tiles, st_count, block_tmp);
     hipLaunchKernelGGL(k_vis_spine, dim3(1), dim3(SCAN_THREADS), 0, s, nb, block_tmp, totals);
     hipLaunchKernelGGL(k_vis_scatter, dim3(nb), dim3(SCAN_THREADS), 0, s, P, tiles, depth_key, vis_key, vis_val,
                        block_tmp);
@@ -160,7 +167,7 @@ void launch_exclusive_scan_u32(long long n, const uint32_t* in, const uint32_t* 
                                uint32_t* block_tmp, uint32_t* total, hipStream_t s) {
     const int nb = scan_blocks(n);
     if (nb == 0) {
-        if (total) hipMemsetAsync(total, 0, sizeof(uint32_t), s);
+        if (total) (void)hipMemsetAsync(total, 0, sizeof(uint32_t), s);
         return;
     }
     hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, s, n, in, gather, block_tmp);

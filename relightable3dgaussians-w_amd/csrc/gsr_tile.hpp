@@ -83,4 +83,93 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // halves
 }
 
+// ---- batch staging shared by the forward and backward tile passes ---------------------
+struct TileStageLDS {
+    float4 a[256];           // (x, y, conic.a, conic.b)
+    float4 b[256];           // (conic.c, opacity, r, g)
+    float c[256];            // b
+    uint32_t pos[256];       // position in the tile's range
+    uint32_t id[256];        // Gaussian index
+    uint16_t qidx[4][256];   // per-quadrant lists of slots, in range order
+    uint32_t qcnt[4];        // per-quadrant list length
+    uint32_t cnt;            // slots used
+    uint32_t wcnt[4][5];     // per-wave ballot counts: kept, quadrant 0..3
+};
+
+struct TileStage {
+    int px, py;
+    bool inside;
+    float pfx, pfy, tx0, ty0, wmax, hmax;
+    uint64_t lt;
+
+    __device__ __forceinline__ void init(unsigned tile, unsigned gx, int W, int H) {
+        const unsigned bx = tile % gx, by = tile / gx;
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        px = bx * GSR_BLOCK_X + (wave & 1) * 8 + (lane & 7);
+        py = by * GSR_BLOCK_Y + (wave >> 1) * 8 + (lane >> 3);
+        inside = px < W && py < H;
+        pfx = (float)px;
+        pfy = (float)py;
+        tx0 = (float)(bx * GSR_BLOCK_X);
+        ty0 = (float)(by * GSR_BLOCK_Y);
+        wmax = (float)(W - 1);
+        hmax = (float)(H - 1);
+        lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    }
+
+    // Gather this thread's candidate record (if `valid`), keep it if it can reach any pixel
+    // of a quadrant, and compact the survivors (in thread order, i.e. range order) into the
+    // LDS slots and the four quadrant lists.  Contains two workgroup barriers; the caller
+    // must have passed a barrier since the previous batch's last read of `sm`.
+    // `qlimit` (optional, LDS): quadrant q only keeps positions < qlimit[q].
+    __device__ __forceinline__ void stage(TileStageLDS& sm, bool valid, uint32_t position, uint32_t gid,
+                                          const Rec* rec, const uint32_t* qlimit = nullptr) {
+        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+        Rec r;
+        uint32_t qmask = 0;
+        if (valid) {
+            r = rec[gid];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const float qx0 = tx0 + (q & 1) * 8.f, qy0 = ty0 + (q >> 1) * 8.f;
+                const float qx1 = fminf(qx0 + 7.f, wmax), qy1 = fminf(qy0 + 7.f, hmax);
+                if (qx0 <= wmax && qy0 <= hmax && (!qlimit || position < qlimit[q]) &&
+                    box_reachable(r.a.z, r.a.w, r.b.x, r.c.y, qx0 - r.a.x, qx1 - r.a.x, qy0 - r.a.y, qy1 - r.a.y))
+                    qmask |= 1u << q;
+            }
+        }
+        const bool keep = qmask != 0;
+        const uint64_t bk = __ballot(keep);
+        uint64_t bq[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) bq[q] = __ballot((qmask >> q) & 1u);
+        if (lane == 0) {
+            sm.wcnt[wave][0] = (uint32_t)__popcll(bk);
+#pragma unroll
+            for (int q = 0; q < 4; q++) sm.wcnt[wave][1 + q] = (uint32_t)__popcll(bq[q]);
+        }
+        __syncthreads();
+        if (keep) {
+            uint32_t slot = (uint32_t)__popcll(bk & lt);
+            for (int w = 0; w < wave; w++) slot += sm.wcnt[w][0];
+            sm.a[slot] = r.a;
+            sm.b[slot] = r.b;
+            sm.c[slot] = r.c.x;
+            sm.pos[slot] = position;
+            sm.id[slot] = gid;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if ((qmask >> q) & 1u) {
+                    uint32_t qp = (uint32_t)__popcll(bq[q] & lt);
+                    for (int w = 0; w < wave; w++) qp += sm.wcnt[w][1 + q];
+                    sm.qidx[q][qp] = (uint16_t)slot;
+                }
+            }
+        }
+        if (tid < 4) sm.qcnt[tid] = sm.wcnt[0][1 + tid] + sm.wcnt[1][1 + tid] + sm.wcnt[2][1 + tid] + sm.wcnt[3][1 + tid];
+        if (tid == 4) sm.cnt = sm.wcnt[0][0] + sm.wcnt[1][0] + sm.wcnt[2][0] + sm.wcnt[3][0];
+        __syncthreads();
+    }
+};
+
 }  // namespace gsr
