@@ -45,6 +45,24 @@ def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
     }.get(stage)
 
 
+STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "render_bwd": "k_render_bwd",
+                "preprocess_bwd": "k_preprocess_bwd"}
+
+
+def pmc_traffic(stage):
+    """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC pass
+    (profiles/<tag>_hbm_traffic.json, written by tools/profile_summary.py from separate
+    --pmc FETCH_SIZE / WRITE_SIZE runs of this same bench command, corrected as
+    MI355X_MICROARCH.md prescribes).  None when no such profile exists."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    k = d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {})
+    return k.get("traffic_bytes"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
     from oracle import oracle as orc
     n = lambda t: t.detach().cpu().numpy().astype(np.float32)
@@ -103,6 +121,7 @@ def main():
 
     from diff_gaussian_rasterization import _C
     from gsr import _lib, scenes
+    from gsr import dp as gdp
 
     cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
     W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
@@ -126,9 +145,8 @@ def main():
                                                 img)
         if dist is not None:
             # one bucket: dL/d(means3D, sh, opacity, scales, rotations) summed over the view-parallel ranks
-            flat = torch.cat([grads[3].reshape(-1), grads[5].reshape(-1), grads[2].reshape(-1),
-                              grads[6].reshape(-1), grads[7].reshape(-1)])
-            dist.all_reduce(flat)
+            ts = [grads[3], grads[5], grads[2], grads[6], grads[7]]
+            state["bucket"] = gdp.all_reduce_grads(ts, bucket=state.get("bucket"))
         state["R"], state["radii"] = R, radii
         return grads
 
@@ -163,8 +181,11 @@ def main():
                algorithmic_bytes(k, P, Pv, R, T, W * H, M) is not None), key=lambda kv: kv[1])
     dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
     achieved = dom_bytes / (dom[1] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom[0])
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None, "kernel": dom[0],
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
+                "kernel": dom[0],
                 "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom[1], 4)}
     out = {
         "metric": METRIC, "value": round(world * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "n_gpus": world,

@@ -1,0 +1,112 @@
+"""View-parallel data parallelism for the rasterizer path.
+
+The reference trains on one camera per iteration (train.py:95-160): render -> loss ->
+backward -> densification statistics -> Adam.  The only part of that loop that touches
+every Gaussian on every view is the per-Gaussian gradient and the densification statistics,
+so the MI355X design shards *views* over ranks (one process per GPU, weak scaling) and adds
+exactly one exchange step per iteration:
+
+  * the per-Gaussian gradients of all parameters are flattened into ONE contiguous bucket
+    and summed with a single all-reduce (RCCL over xGMI on the GPU box, gloo in the CPU
+    tests).  Summing N single-view gradients is what the reference computes by accumulating
+    N iterations of batch 1 before a step.  One large bucket beats many small ones on xGMI:
+    at cfg2 the bucket is 1.5M x 59 floats = 354 MB, which amortises ring latency.
+  * the densification statistics: ``xyz_gradient_accum`` and ``denom``
+    (gaussian_model.py:627-629) are SUMmed, ``max_radii2D`` (train.py:130) is MAXed.  Each
+    rank accumulates its own views' norms first, so the reduced statistics equal the
+    sequential reference's after the same set of views.
+
+No collective touches the rasterizer itself: every rank calls the same libgsr.so on its own
+view.  The helpers take any process group, so the gloo world_size-2 tests in
+tests/test_dp_gloo.py exercise the same code the nccl bench path runs.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+def shard_views(n_views: int, rank: int, world: int) -> List[int]:
+    """Round-robin view assignment: rank r renders views r, r+world, ... (disjoint, covering)."""
+    if world <= 0 or not (0 <= rank < world):
+        raise ValueError(f"bad rank/world {rank}/{world}")
+    return list(range(rank, n_views, world))
+
+
+class GradBucket:
+    """One flat buffer holding several gradient tensors back to back.
+
+    ``pack`` copies the tensors in, ``all_reduce`` runs one collective over the whole buffer,
+    and ``unpack`` copies the reduced values back into the original tensors, in place.  The
+    buffer is allocated once and reused, so a training step does not allocate.
+    """
+
+    def __init__(self, like: Sequence[torch.Tensor]):
+        if not like:
+            raise ValueError("GradBucket needs at least one tensor")
+        dt, dev = like[0].dtype, like[0].device
+        for t in like:
+            if t.dtype != dt or t.device != dev:
+                raise ValueError("GradBucket tensors must share dtype and device")
+        self.shapes = [tuple(t.shape) for t in like]
+        self.sizes = [t.numel() for t in like]
+        self.flat = torch.empty(sum(self.sizes), dtype=dt, device=dev)
+
+    def views(self) -> List[torch.Tensor]:
+        out, o = [], 0
+        for n, shp in zip(self.sizes, self.shapes):
+            out.append(self.flat[o:o + n].view(shp))
+            o += n
+        return out
+
+    def pack(self, tensors: Sequence[torch.Tensor]) -> None:
+        if [tuple(t.shape) for t in tensors] != self.shapes:
+            raise ValueError("GradBucket.pack: shapes differ from the bucket layout")
+        for v, t in zip(self.views(), tensors):
+            v.copy_(t)
+
+    def unpack(self, tensors: Sequence[torch.Tensor]) -> None:
+        for v, t in zip(self.views(), tensors):
+            t.copy_(v)
+
+    def all_reduce(self, group=None, average: bool = False) -> None:
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=group)
+        if average:
+            self.flat.div_(dist.get_world_size(group))
+
+
+def all_reduce_grads(tensors: Sequence[torch.Tensor], bucket: Optional[GradBucket] = None, group=None,
+                     average: bool = False) -> GradBucket:
+    """Sum (or average) ``tensors`` over the group with a single collective, in place."""
+    if bucket is None:
+        bucket = GradBucket(tensors)
+    bucket.pack(tensors)
+    bucket.all_reduce(group=group, average=average)
+    bucket.unpack(tensors)
+    return bucket
+
+
+def reduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Tensor, max_radii2D: torch.Tensor,
+                               group=None) -> None:
+    """In place: SUM the gradient-norm accumulator and the view counter, MAX the screen radii.
+
+    Mirrors gaussian_model.py:627-629 (accum += ||dL/dmean2D[:, :2]||, denom += 1 on the
+    visibility filter) and train.py:130 (max_radii2D = max(max_radii2D, radii)) across ranks.
+    The two sums travel in one buffer.
+    """
+    sums = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    n = xyz_gradient_accum.numel()
+    xyz_gradient_accum.copy_(sums[:n].view_as(xyz_gradient_accum))
+    denom.copy_(sums[n:].view_as(denom))
+    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)
+
+
+def accumulate_view_stats(stats: Dict[str, torch.Tensor], mean2D_grad: torch.Tensor, radii: torch.Tensor) -> None:
+    """Per-rank, per-view densification update (train.py:130, gaussian_model.py:627-629)."""
+    vis = radii > 0
+    stats["max_radii2D"][vis] = torch.max(stats["max_radii2D"][vis], radii[vis].to(stats["max_radii2D"].dtype))
+    stats["xyz_gradient_accum"][vis] += torch.norm(mean2D_grad[vis, :2], dim=-1, keepdim=True)
+    stats["denom"][vis] += 1

@@ -1,0 +1,91 @@
+#!/usr/bin/env python
+"""Turn one round's rocprofv3 outputs (tools/profile_round.sh) into the committed evidence under
+profiles/:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_hbm_traffic.json   per kernel: calls, avg duration, FETCH_SIZE / WRITE_SIZE per
+                                    launch and the corrected HBM bytes per launch
+  profiles/<tag>_summary.md         the same as a table, plus the bench line printed under the
+                                    profiler (its stage_ms must agree with the kernel averages)
+
+HBM correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are KiB; on gfx950
+FETCH_SIZE reports 1/2 of the bytes of wide streaming reads, so
+    traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024  bytes per launch.
+The factor is calibrated for 16-B-per-lane streaming loads; gathers of 48-B records are not
+calibrated, so the read half is an estimate (ratios between kernel variants are exact).
+"""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("gsr::", "").replace("void ", "")
+
+
+def counters(pattern):
+    acc = defaultdict(list)
+    for f in glob.glob(pattern):
+        for r in csv.DictReader(open(f)):
+            acc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return acc
+
+
+def main(tag="r01"):
+    out_dir = os.path.join(ROOT, "profiles")
+    os.makedirs(out_dir, exist_ok=True)
+    g = os.path.join(ROOT, "gpurun_out")
+    ks = sorted(glob.glob(os.path.join(g, f"prof_{tag}_kt", "*", "*_kernel_stats.csv")))
+    if not ks:
+        sys.exit(f"no kernel stats for {tag}")
+    rows = list(csv.DictReader(open(ks[-1])))
+    with open(os.path.join(out_dir, f"{tag}_kernel_stats.csv"), "w") as f:
+        f.write(open(ks[-1]).read())
+    fetch = counters(os.path.join(g, f"prof_{tag}_fetch", "*", "*_counter_collection.csv"))
+    write = counters(os.path.join(g, f"prof_{tag}_write", "*", "*_counter_collection.csv"))
+    res = {}
+    for r in rows:
+        k = short(r["Name"])
+        fr = fetch.get((k, "FETCH_SIZE"))
+        wr = write.get((k, "WRITE_SIZE"))
+        fk = statistics.mean(fr) if fr else None
+        wk = statistics.mean(wr) if wr else None
+        res[k] = dict(calls=int(r["Calls"]), avg_ms=float(r["AverageNs"]) / 1e6, pct=float(r["Percentage"]),
+                      fetch_kib=fk, write_kib=wk,
+                      traffic_bytes=(None if fk is None or wk is None else (2 * fk + wk) * 1024.0))
+    bench = None
+    log = os.path.join(g, f"prof_{tag}_kt.log")
+    if os.path.exists(log):
+        for line in open(log):
+            if line.startswith("{\"metric\""):
+                bench = json.loads(line)
+    json.dump(dict(tag=tag, correction="traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch (gfx950)",
+                   command="rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
+                           "--no-cpu-baseline; separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes",
+                   kernels=res, bench_under_profiler=bench),
+              open(os.path.join(out_dir, f"{tag}_hbm_traffic.json"), "w"), indent=1)
+    with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
+        f.write(f"# rocprofv3 summary {tag}\n\nbench.py cfg2 (1.5M Gaussians, SH3, 1920x1080) under rocprofv3; "
+                "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch.\n\n")
+        f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s |\n|---|---|---|---|---|---|---|---|\n")
+        for k, v in sorted(res.items(), key=lambda kv: -kv[1]["pct"]):
+            tb = v["traffic_bytes"]
+            f.write(f"| {k} | {v['calls']} | {v['avg_ms']:.4f} | {v['pct']:.1f} | "
+                    f"{'' if v['fetch_kib'] is None else round(v['fetch_kib'])} | "
+                    f"{'' if v['write_kib'] is None else round(v['write_kib'])} | "
+                    f"{'' if tb is None else round(tb / 1e6, 2)} | "
+                    f"{'' if tb is None else round(tb / (v['avg_ms'] * 1e-3) / 1e9, 1)} |\n")
+        if bench:
+            f.write(f"\nbench line under the profiler: value {bench['value']} MPix/s, ms/step {bench['ms_per_step']}"
+                    f"\n\nstage_ms (HIP events): {json.dumps(bench.get('stage_ms'))}\n")
+    print(open(os.path.join(out_dir, f"{tag}_summary.md")).read())
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
