@@ -8,7 +8,10 @@
 //   3. the S entries are stably sorted by super-tile id (one 8-bit pass at 1080p);
 //   4. each super-tile list is cut into 1024-entry segments (k_seg_table); one workgroup
 //      per segment keeps, for each of the super-tile's 32 tiles, the entries whose rect
-//      covers it with an order-preserving wave-ballot compaction.  A count pass
+//      covers it with an order-preserving wave-ballot compaction.  The entry's coverage of
+//      its super-tile (a local tile rect, 10 bits) rides in the key's top bits through the
+//      sort (which only orders bits [0, log2 NS)), so the filters read one coalesced word per
+//      entry instead of gathering the Gaussian's rect.  A count pass
 //      (k_seg_lists<false>), a per-tile prefix over segments (k_seg_prefix), a scan over
 //      tiles (= the reference's ranges) and a write pass (k_seg_lists<true>) produce
 //      point_list directly, in coalesced runs.
@@ -18,6 +21,23 @@
 #include "gsr_kernels.hpp"
 
 namespace gsr {
+
+// Local tile rect of a Gaussian inside super-tile (sx, sy): cx0 | (cx1-1) << 3 | cy0 << 6 |
+// (cy1-1) << 8, where [cx0, cx1) x [cy0, cy1) are tile offsets within the 8x4 super-tile.
+__device__ __forceinline__ uint32_t local_rect_code(uint2 r, uint32_t sx, uint32_t sy) {
+    const int tx0 = (int)(sx * GSR_ST_W), ty0 = (int)(sy * GSR_ST_H);
+    const int cx0 = max((int)(r.x & 0xffffu) - tx0, 0), cx1 = min((int)(r.x >> 16) - tx0, (int)GSR_ST_W);
+    const int cy0 = max((int)(r.y & 0xffffu) - ty0, 0), cy1 = min((int)(r.y >> 16) - ty0, (int)GSR_ST_H);
+    return (uint32_t)cx0 | ((uint32_t)(cx1 - 1) << 3) | ((uint32_t)cy0 << 6) | ((uint32_t)(cy1 - 1) << 8);
+}
+__device__ __forceinline__ uint32_t local_rect_mask(uint32_t code) {
+    const uint32_t cx0 = code & 7u, cx1 = ((code >> 3) & 7u) + 1u, cy0 = (code >> 6) & 3u, cy1 = ((code >> 8) & 3u) + 1u;
+    const uint32_t row = ((1u << cx1) - 1u) & ~((1u << cx0) - 1u);
+    uint32_t m = 0;
+#pragma unroll
+    for (uint32_t y = 0; y < GSR_ST_H; y++) m |= (y >= cy0 && y < cy1) ? row << (GSR_ST_W * y) : 0u;
+    return m;
+}
 
 // ---- 2. super-tile emission -----------------------------------------------------------
 // One wave emits the entries of 64 consecutive depth-sorted Gaussians as one contiguous
@@ -29,13 +49,14 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
     __shared__ uint32_t s_inc[4][64];
     __shared__ uint32_t s_id[4][64];
     __shared__ uint2 s_srect[4][64];
+    __shared__ uint2 s_rect[4][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t idx = 0, cnt = 0;
-    uint2 sr = make_uint2(0, 0);
+    uint2 sr = make_uint2(0, 0), r = make_uint2(0, 0);
     if (s < Pv) {
         idx = sorted_ids[s];
-        const uint2 r = rect[idx];
+        r = rect[idx];
         const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
         const uint32_t sy0 = (r.y & 0xffffu) / GSR_ST_H, sy1 = ((r.y >> 16) + GSR_ST_H - 1) / GSR_ST_H;
         sr = make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
@@ -50,6 +71,7 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
     s_inc[wave][lane] = inc;
     s_id[wave][lane] = idx;
     s_srect[wave][lane] = sr;
+    s_rect[wave][lane] = r;
     const int s0 = blockIdx.x * blockDim.x + wave * 64;
     const uint32_t base = s0 < Pv ? offsets[s0] : 0u;
     const uint32_t total = __shfl(inc, 63, 64);
@@ -65,7 +87,8 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
         const uint2 rr = s_srect[wave][lo];
         const uint32_t x0 = rr.x & 0xffffu, w = (rr.x >> 16) - x0, y0 = rr.y & 0xffffu;
         const uint32_t yy = k / w, xx = k - yy * w;
-        st_keys[base + i] = (y0 + yy) * gsx + (x0 + xx);
+        const uint32_t sx = x0 + xx, sy = y0 + yy;
+        st_keys[base + i] = (sy * gsx + sx) | (local_rect_code(s_rect[wave][lo], sx, sy) << ST_KEY_BITS);
         st_vals[base + i] = s_id[wave][lo];
     }
 }
@@ -74,11 +97,11 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
 __global__ void __launch_bounds__(256) k_seg_ranges(long long n, const uint32_t* keys, uint2* ranges) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t cur = keys[i];
+    const uint32_t cur = keys[i] & ST_KEY_MASK;
     if (i == 0) {
         ranges[cur].x = 0;
     } else {
-        const uint32_t prev = keys[i - 1];
+        const uint32_t prev = keys[i - 1] & ST_KEY_MASK;
         if (cur != prev) {
             ranges[prev].y = (uint32_t)i;
             ranges[cur].x = (uint32_t)i;
@@ -141,7 +164,7 @@ __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_rang
 template <bool WRITE>
 __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, const uint32_t* seg_st,
                                                     const uint32_t* seg_e0, const uint2* st_ranges,
-                                                    const uint32_t* st_vals, const uint2* rect, unsigned gx,
+                                                    const uint32_t* st_keys, const uint32_t* st_vals, unsigned gx,
                                                     unsigned gy, unsigned gsx, uint32_t* seg_cnt,
                                                     const uint32_t* seg_base, uint32_t* point_list) {
     __shared__ uint32_t s_wc[4][ST_TILES];
@@ -161,15 +184,9 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
         const bool valid = e < e1;
         uint32_t id = 0, mask = 0;
         if (valid) {
-            id = st_vals[e];
-            const uint2 r = rect[id];
             // local tile coverage mask (bit t = (t / 8) row, (t % 8) column)
-            const int cx0 = max((int)(r.x & 0xffffu) - (int)g.tx0, 0), cx1 = min((int)(r.x >> 16) - (int)g.tx0, (int)g.nx);
-            const int cy0 = max((int)(r.y & 0xffffu) - (int)g.ty0, 0), cy1 = min((int)(r.y >> 16) - (int)g.ty0, (int)g.ny);
-            if (cx1 > cx0 && cy1 > cy0) {
-                const uint32_t row = ((1u << cx1) - 1u) & ~((1u << cx0) - 1u);
-                for (int y = cy0; y < cy1; y++) mask |= row << (GSR_ST_W * y);
-            }
+            mask = local_rect_mask(st_keys[e] >> ST_KEY_BITS);
+            if (WRITE) id = st_vals[e];
         }
         uint64_t bal[ST_TILES];
 #pragma unroll
@@ -256,7 +273,7 @@ size_t tile_lists_temp_bytes(long long S, int nst) {
     return 4 * (2 * G + (nst + 1) + 1 + G * ST_TILES) + 256;
 }
 
-void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_vals, const uint2* rect,
+void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s) {
     const int T = (int)(gx * gy);
@@ -269,7 +286,7 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
     hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total);
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
-                           st_ranges, st_vals, rect, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
+                           st_ranges, st_keys, st_vals, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
                            (uint32_t*)nullptr);
     }
     (void)hipMemsetAsync(tile_cnt, 0, sizeof(uint32_t) * (size_t)T, s);
@@ -283,7 +300,7 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
         hipLaunchKernelGGL(k_seg_absolute, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, nseg_total, seg_st,
                            gx, gy, gsx, tile_start, seg_cnt, items);
         hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
-                           st_ranges, st_vals, rect, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, point_list);
+                           st_ranges, st_keys, st_vals, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, point_list);
     }
 }
 

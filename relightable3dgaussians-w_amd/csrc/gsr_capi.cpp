@@ -275,7 +275,9 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
         return fail(GSR_E_ARG, "For non-RGB, provide precomputed Gaussian colors!");
     if (!cov3D_precomp && (!scales || !rotations) && P > 0)
         return fail(GSR_E_ARG, "gsr_forward: need scales+rotations or cov3D_precomp");
-    if (tiles_x(width) > 65535u || tiles_y(height) > 65535u) return fail(GSR_E_ARG, "gsr_forward: image too large");
+    if (tiles_x(width) > 65535u || tiles_y(height) > 65535u ||
+        (unsigned long long)st_x(width) * st_y(height) >= (1ull << gsr::ST_KEY_BITS))
+        return fail(GSR_E_ARG, "gsr_forward: image too large");
 
     // rasterizer_impl.cu:221-222 (host float arithmetic == device float arithmetic)
     const float focal_y = height / (2.0f * tan_fovy);
@@ -378,7 +380,7 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
         GSR_STAGE(ST_RANGES);
         uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
         gsr::launch_seg_ranges(S, NS, st_sorted_keys, st_ranges, s);
-        gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_vals, pa.rect, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
+        gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
                                at<uint32_t>(bin, bl.tile_start), ranges, at<uint32_t>(bin, bl.scan_tmp),
                                at<void>(bin, bl.lists_tmp), point_list, s);
     }

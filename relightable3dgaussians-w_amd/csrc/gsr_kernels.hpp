@@ -76,12 +76,16 @@ int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys
 // super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
                     uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
+// Super-tile keys: id in bits [0, ST_KEY_BITS), the entry's local tile rect above (so at
+// most 2^20 super-tiles; the sort orders only the id bits).
+constexpr int ST_KEY_BITS = 20;
+constexpr uint32_t ST_KEY_MASK = (1u << ST_KEY_BITS) - 1u;
 // ranges[k] = [first, last+1) of key k in a sorted key array; (0, 0) for absent keys.
 void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s);
 // Per-super-tile tile filters over 1024-entry segments: tile counts, tile starts (scan),
 // ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).
 size_t tile_lists_temp_bytes(long long S, int nst);
-void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_vals, const uint2* rect,
+void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s);
 

@@ -2,148 +2,149 @@
 //
 // gfx950 design (the reference issues 9 float atomics to global memory per contributing
 // (pixel, Gaussian) pair, backward.cu:523,545-554):
-//  * the replay starts at the tile's largest n_contrib (positions past every pixel's last
-//    contributor are skipped by the reference too) and stages records from the back with
-//    the forward's conservative quadrant culling into per-quadrant LDS lists (TileStage);
-//  * the per-pixel recurrence (T, accum_rec, last_alpha, last_color) is evaluated
-//    branch-free with predicated updates;
-//  * per Gaussian, each 16-lane row of the wave reduces its 9 partial gradients on the
-//    VALU (4 fused DPP adds per value) -- skipped when no lane of the wave contributes --
-//    and 36 lanes (9 per row) add the row sums into the tile's LDS row with one ds_add;
-//  * after each batch the tile flushes one 9-float row per Gaussian to the 64-B
-//    per-Gaussian accumulator line; one wave-instruction covers 4 whole lines.
+//  * one wave per 16x16 tile (WaveTile), each lane owns one pixel of each 8x8 quadrant;
+//    quadrant q replays only positions below its largest n_contrib (positions past every
+//    pixel's last contributor are skipped by the reference too);
+//  * batches of 64 list entries, back to front: each lane gathers one record and tests it
+//    against the four quadrants (box_reachable, limited by the quadrant's n_contrib); the
+//    wave walks the surviving lanes (s_ff1 + v_readlane broadcasts);
+//  * per Gaussian, the reachable quadrants run the reference's per-pixel recurrence
+//    (T, accum_rec, last_alpha, last_color) branch-free with predicated updates and sum
+//    their 9 partial gradients in-lane; the wave then reduces the 9 values once: 16-lane
+//    DPP row sums (4 fused v_add_f32_dpp each), lane c of each row keeps value c, and two
+//    permlane swaps add the four rows.  Lanes 0..8 issue one 9-lane atomic to the
+//    Gaussian's 64-B accumulator line -- one request per (tile, Gaussian).
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
 namespace gsr {
 
-__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
-    TileStage st;
-    __shared__ TileStageLDS sm;
-    __shared__ float s_acc[256][9];
-    __shared__ uint32_t s_qmax[4];
+__global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
     const unsigned ntile = a.grid_x * a.grid_y;
     const unsigned tile = xcd_remap(blockIdx.x, ntile);
-    st.init(tile, a.grid_x, a.W, a.H);
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    WaveTile wt;
+    wt.init(tile, a.grid_x, a.W, a.H);
+    const int lane = threadIdx.x;
     const uint2 range = a.ranges[tile];
-    const int pix = a.W * st.py + st.px;
     const int HW = a.H * a.W;
 
-    const float T_final = st.inside ? a.final_T[pix] : 0.f;
-    float T = T_final;
-    const uint32_t last_contributor = st.inside ? a.n_contrib[pix] : 0u;
-    float dpx0 = 0.f, dpx1 = 0.f, dpx2 = 0.f;
-    if (st.inside) {
-        dpx0 = a.dL_dpix[pix];
-        dpx1 = a.dL_dpix[HW + pix];
-        dpx2 = a.dL_dpix[2 * HW + pix];
-    }
-    const float bg_dot = a.bg[0] * dpx0 + a.bg[1] * dpx1 + a.bg[2] * dpx2;
-    float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f;
-    float lc0 = 0.f, lc1 = 0.f, lc2 = 0.f;
-    float last_alpha = 0.f;
-    const float ddelx_dx = 0.5f * a.W;
-    const float ddely_dy = 0.5f * a.H;
-
-    uint32_t m = last_contributor;
+    const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    // per quadrant pixel state: T, dL/dpix, the background term, and the recurrence of
+    // backward.cu:514-537 carried as dot products with dL/dpix (accum_rec . dL/dpix and
+    // last_color . dL/dpix) plus last_alpha
+    float T[4], Tb[4], dp0[4], dp1[4], dp2[4], AD[4], LD[4], la[4];
+    uint32_t last[4], qlim[4];
+    uint32_t nmax = 0;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t t = __shfl_xor(m, o, 64);
-        m = t > m ? t : m;
+    for (int q = 0; q < 4; q++) {
+        const bool in = wt.inside(q, a.W, a.H);
+        const int pix = in ? wt.pixel(q, a.W) : 0;
+        const float Tf = in ? a.final_T[pix] : 0.f;
+        last[q] = in ? a.n_contrib[pix] : 0u;
+        dp0[q] = in ? a.dL_dpix[pix] : 0.f;
+        dp1[q] = in ? a.dL_dpix[HW + pix] : 0.f;
+        dp2[q] = in ? a.dL_dpix[2 * HW + pix] : 0.f;
+        T[q] = Tf;
+        // -T_final * bg . dL/dpix, the background term of dL/dalpha (backward.cu:533-537)
+        Tb[q] = -Tf * (a.bg[0] * dp0[q] + a.bg[1] * dp1[q] + a.bg[2] * dp2[q]);
+        AD[q] = LD[q] = la[q] = 0.f;
+        qlim[q] = wave_max_u32(last[q]);
+        nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
-    // each quadrant (wave) only replays positions below its own largest n_contrib
-    if (lane == 0) s_qmax[wave] = m;
-    __syncthreads();
-    const int nmax = (int)max(max(s_qmax[0], s_qmax[1]), max(s_qmax[2], s_qmax[3]));
+    // Reduction layout (see the end of the loop): lane 16 r + j, j < 2, ends up holding
+    // value kVal[j][r] of the Gaussian's 9 gradient sums; lane 0 + 2 holds value 8.
+    const int row = lane >> 4, col = lane & 15;
+    const int vidx = col == 0 ? (row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3)
+                     : col == 1 ? (row == 0 ? 4 : row == 1 ? 6 : row == 2 ? 5 : 7)
+                     : (col == 2 && row == 0) ? 8 : -1;
+    // per-value scale: dL/dmean2D gets op * (W/2, H/2), dL/dconic -op/2, the rest 1
+    const float vscale = vidx == 0 ? 0.5f * a.W : vidx == 1 ? 0.5f * a.H : vidx <= 4 ? -0.5f : 1.f;
+    const bool vop = vidx >= 0 && vidx <= 4;
 
-    for (int b0 = 0; b0 < nmax; b0 += 256) {
-        const int nb = (nmax - b0) < 256 ? (nmax - b0) : 256;
-        __syncthreads();  // the previous batch's flush is done with sm / s_acc
-        const int p = nmax - 1 - (b0 + tid);
-        uint32_t id = 0;
-        if (tid < nb) id = a.point_list[range.x + p];
+    // software pipeline: list ids run two batches ahead, records one batch ahead
+    uint32_t id_cur = 0, id_next = 0;
+    Rec r_next = {};
+    if ((uint32_t)lane < nmax) {
+        id_cur = a.point_list[range.x + nmax - 1u - lane];
+        r_next = a.rec[id_cur];
+    }
+    if (64u + lane < nmax) id_next = a.point_list[range.x + nmax - 65u - lane];
+    for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
+        const uint32_t i = b0 + lane;
+        const uint32_t p = nmax - 1u - i;  // back to front
+        const Rec r = r_next;
+        const uint32_t id = id_cur;
+        id_cur = id_next;
+        if (i + 64u < nmax) r_next = a.rec[id_cur];
+        if (i + 128u < nmax) id_next = a.point_list[range.x + p - 128u];
+        const uint32_t qm = i < nmax ? wt.reach(r, p, qlim) : 0u;
+        const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
+        uint64_t todo = __ballot(qm != 0);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = bcast(qm, k);
+            const float ax = bcast(r.a.x, k), ay = bcast(r.a.y, k);
+            const float ka = bcast(na, k), kb = bcast(nb, k), kc = bcast(nc, k), op = bcast(r.b.y, k);
+            const float c0 = bcast(r.b.z, k), c1 = bcast(r.b.w, k), c2 = bcast(r.c.x, k);
+            const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
+            // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
+            // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
+            // S6..8 = sum alpha T dL/dpix
+            float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f, S6 = 0.f, S7 = 0.f, S8 = 0.f;
+            bool any = false;
 #pragma unroll
-        for (int v = 0; v < 9; v++) s_acc[tid][v] = 0.f;
-        st.stage(sm, tid < nb, (uint32_t)p, id, a.rec, s_qmax);
-        const int cnt = sm.qcnt[wave];
-        for (int k = 0; k < cnt; k++) {
-            const int s = sm.qidx[wave][k];
-            const float4 A = sm.a[s];
-            const float4 B = sm.b[s];
-            const float c2 = sm.c[s];
-            const uint32_t pos = sm.pos[s];
-            const float dx = A.x - st.pfx, dy = A.y - st.pfy;
-            const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-            const float G = tile_exp(power);
-            const float alpha = fminf(0.99f, B.y * G);
-            const bool active = pos < last_contributor && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-            if (__ballot(active) == 0ull) continue;  // wave-uniform
-            const float inv = __builtin_amdgcn_rcpf(1.f - alpha);
-            const float Tn = T * inv;
-            const float dchannel_dcolor = alpha * Tn;
-            const float c0 = B.z, c1 = B.w;
-            const float na0 = last_alpha * lc0 + (1.f - last_alpha) * acc0;
-            const float na1 = last_alpha * lc1 + (1.f - last_alpha) * acc1;
-            const float na2 = last_alpha * lc2 + (1.f - last_alpha) * acc2;
-            float dL_dalpha = ((c0 - na0) * dpx0 + (c1 - na1) * dpx1 + (c2 - na2) * dpx2) * Tn;
-            dL_dalpha += (-T_final * inv) * bg_dot;
-            const float dL_dG = B.y * dL_dalpha;
-            const float gdx = G * dx;
-            const float gdy = G * dy;
-            const float dG_ddelx = -gdx * A.z - gdy * A.w;
-            const float dG_ddely = -gdy * B.x - gdx * A.w;
-            const float h = -0.5f * dL_dG;
-            float g0 = active ? dL_dG * dG_ddelx * ddelx_dx : 0.f;
-            float g1 = active ? dL_dG * dG_ddely * ddely_dy : 0.f;
-            float g2 = active ? h * gdx * dx : 0.f;
-            float g3 = active ? h * gdx * dy : 0.f;
-            float g4 = active ? h * gdy * dy : 0.f;
-            float g5 = active ? G * dL_dalpha : 0.f;
-            float g6 = active ? dchannel_dcolor * dpx0 : 0.f;
-            float g7 = active ? dchannel_dcolor * dpx1 : 0.f;
-            float g8 = active ? dchannel_dcolor * dpx2 : 0.f;
-            T = active ? Tn : T;
-            acc0 = active ? na0 : acc0;
-            acc1 = active ? na1 : acc1;
-            acc2 = active ? na2 : acc2;
-            lc0 = active ? c0 : lc0;
-            lc1 = active ? c1 : lc1;
-            lc2 = active ? c2 : lc2;
-            last_alpha = active ? alpha : last_alpha;
-            // 16-lane row sums on the VALU; lanes c < 9 of every row add component c of their
-            // row into the tile's LDS row (one ds_add_f32, 4 rows per address)
-            g0 = row_sum(g0);
-            g1 = row_sum(g1);
-            g2 = row_sum(g2);
-            g3 = row_sum(g3);
-            g4 = row_sum(g4);
-            g5 = row_sum(g5);
-            g6 = row_sum(g6);
-            g7 = row_sum(g7);
-            g8 = row_sum(g8);
-            const int c = lane & 15;
-            if (c < 9) {
-                float v = g0;
-                v = c == 1 ? g1 : v;
-                v = c == 2 ? g2 : v;
-                v = c == 3 ? g3 : v;
-                v = c == 4 ? g4 : v;
-                v = c == 5 ? g5 : v;
-                v = c == 6 ? g6 : v;
-                v = c == 7 ? g7 : v;
-                v = c == 8 ? g8 : v;
-                atomicAdd(&s_acc[s][c], v);
+            for (int q = 0; q < 4; q++) {
+                if (!((m >> q) & 1u)) continue;
+                const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
+                const float power = gauss_power(ka, kb, kc, dx, dy);
+                const float G = tile_exp(power);
+                const float alpha = fminf(0.99f, op * G);
+                const bool active = pos < last[q] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+                if (__ballot(active) == 0ull) continue;  // wave-uniform
+                any = true;
+                // inactive lanes run the same code with alpha = G = 0: T, the sums and
+                // the gradients stay unchanged
+                const float ae = active ? alpha : 0.f;
+                const float Ge = active ? G : 0.f;
+                const float inv = __builtin_amdgcn_rcpf(1.f - ae);
+                const float Tn = T[q] * inv;
+                const float dch = ae * Tn;
+                const float cdp = __builtin_fmaf(c2, dp2[q], __builtin_fmaf(c1, dp1[q], c0 * dp0[q]));
+                const float nAD = __builtin_fmaf(la[q], LD[q] - AD[q], AD[q]);
+                const float dLda = __builtin_fmaf(Tn, cdp - nAD, inv * Tb[q]);
+                const float Gd = Ge * dLda;
+                S5 += Gd;
+                const float wdx = Gd * dx, wdy = Gd * dy;
+                M1 += wdx;
+                M2 += wdy;
+                S2 = __builtin_fmaf(wdx, dx, S2);
+                S3 = __builtin_fmaf(wdx, dy, S3);
+                S4 = __builtin_fmaf(wdy, dy, S4);
+                S6 = __builtin_fmaf(dch, dp0[q], S6);
+                S7 = __builtin_fmaf(dch, dp1[q], S7);
+                S8 = __builtin_fmaf(dch, dp2[q], S8);
+                T[q] = Tn;
+                AD[q] = active ? nAD : AD[q];
+                LD[q] = active ? cdp : LD[q];
+                la[q] = active ? alpha : la[q];
             }
-        }
-        __syncthreads();
-        const int used = (int)sm.cnt;
-        for (int q = tid; q < used * 16; q += 256) {
-            const int j = q >> 4, c = q & 15;
-            if (c < 9) {
-                const float v = s_acc[j][c];
-                if (v != 0.f) atomicAdd(a.acc + (size_t)sm.id[j] * ACC_STRIDE + c, v);
-            }
+            if (!any) continue;
+            // conic part of dL/dmean2D (backward.cu:540-545): -(a M1 + b M2), -(b M1 + c M2)
+            const float S0 = __builtin_fmaf(ka, M1 + M1, kb * M2);
+            const float S1 = __builtin_fmaf(kc, M2 + M2, kb * M1);
+            // wave reduction: permlane32 swaps pair (S0,S1),(S2,S3),(S4,S5),(S6,S7),(S8,-)
+            // into half-wave sums, permlane16 swaps pair those into row sums of four values
+            // per register, then 16-lane DPP row sums
+            float P0 = swap32_sum(S0, S1), P1 = swap32_sum(S2, S3), P2 = swap32_sum(S4, S5);
+            float P3 = swap32_sum(S6, S7), P4 = swap32_sum(S8, S8);
+            float Q0 = swap16_sum(P0, P1), Q1 = swap16_sum(P2, P3), Q2 = swap16_sum(P4, P4);
+            Q0 = row_sum(Q0);
+            Q1 = row_sum(Q1);
+            Q2 = row_sum(Q2);
+            float v = col == 0 ? Q0 : (col == 1 ? Q1 : Q2);
+            v *= vop ? op * vscale : vscale;
+            if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)bcast(id, k) * ACC_STRIDE + vidx, v);
         }
     }
 }
@@ -151,7 +152,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdArgs a) {
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(ntile), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_render_bwd, dim3(ntile), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

@@ -1,82 +1,108 @@
 // gsr_render_fwd.hip -- per-tile front-to-back alpha compositing (forward.cu:261-374).
 //
 // gfx950 design:
-//  * one 256-thread workgroup per 16x16 tile, each wave owns an 8x8 quadrant (compact
-//    footprint -> coherent early exit); tiles are remapped so each XCD's L2 serves a
-//    contiguous band of the image (xcd_remap);
-//  * staging: each thread gathers one 48-B record of the batch and tests it
-//    conservatively against the four quadrants (box_reachable).  Survivors are compacted
-//    into LDS with wave ballots, and every quadrant gets its own index list, so each wave
-//    iterates only over Gaussians that can reach alpha >= 1/255 somewhere in its 8x8
-//    pixels.  The original range position travels with the record, so n_contrib (the
-//    reference's last_contributor) is unchanged;
-//  * inner loop: branch-free (predicated) blend on broadcast LDS reads, v_exp_f32, colour
-//    from LDS (the reference re-reads colours from global memory per pixel); the wave
-//    leaves the loop as soon as all its pixels are saturated;
-//  * block-wide early exit with __syncthreads_count exactly as the reference.
+//  * one wave per 16x16 tile (WaveTile): each lane owns 4 pixels, one per 8x8 quadrant;
+//    tiles are remapped so each XCD's L2 serves a contiguous band of the image (xcd_remap);
+//  * batches of 64 list entries: each lane gathers one 48-B record and tests it
+//    conservatively against the four quadrants (box_reachable); the wave then walks the
+//    surviving lanes in list order (s_ff1), broadcasting each record with v_readlane, and
+//    blends it only into the quadrants it can reach (wave-uniform branches).  The range
+//    position travels with the record, so n_contrib (the reference's last_contributor)
+//    is unchanged;
+//  * a quadrant leaves the loop as soon as all its pixels are saturated, the tile as soon
+//    as all four are (the reference's block-wide __syncthreads_count exit).
+// Blend decisions and arithmetic order per pixel are the reference's, so colours, T and
+// n_contrib match it exactly.
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
 namespace gsr {
 
-__global__ void __launch_bounds__(256) k_render_fwd(RenderFwdArgs a) {
-    TileStage st;
-    __shared__ TileStageLDS sm;
+__global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
     const unsigned ntile = a.grid_x * a.grid_y;
     const unsigned tile = xcd_remap(blockIdx.x, ntile);
-    st.init(tile, a.grid_x, a.W, a.H);
-    const int tid = threadIdx.x, wave = tid >> 6;
+    WaveTile wt;
+    wt.init(tile, a.grid_x, a.W, a.H);
+    const int lane = threadIdx.x;
     const uint2 range = a.ranges[tile];
     const int n = (int)(range.y - range.x);
-    bool done = !st.inside;
-    float T = 1.0f;
-    uint32_t last_contributor = 0;
-    float C0 = 0.f, C1 = 0.f, C2 = 0.f;
-    for (int b0 = 0; b0 < n; b0 += 256) {
-        if (__syncthreads_count(done) == 256) break;
-        const int j = b0 + tid;
-        uint32_t id = 0;
-        if (j < n) id = a.point_list[range.x + j];
-        st.stage(sm, j < n, j, id, a.rec);
-        if (!__all(done)) {
-            const int cnt = sm.qcnt[wave];
-            for (int k = 0; k < cnt; k++) {
-                const int s = sm.qidx[wave][k];
-                const float4 A = sm.a[s];
-                const float4 B = sm.b[s];
-                const float dx = A.x - st.pfx, dy = A.y - st.pfy;
-                const float power = -0.5f * (A.z * dx * dx + B.x * dy * dy) - A.w * dx * dy;
-                const float alpha = fminf(0.99f, B.y * tile_exp(power));
-                const bool hit = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                const float test_T = T * (1 - alpha);
+
+    const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    float T[4], C0[4], C1[4], C2[4];
+    float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
+    uint32_t last[4];
+    uint32_t live = 0;  // quadrants with a pixel still blending (wave-uniform)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        T[q] = 1.f;
+        C0[q] = C1[q] = C2[q] = 0.f;
+        last[q] = 0;
+        const bool in = wt.inside(q, a.W, a.H);
+        lim[q] = in ? 1.0f / 255.0f : __builtin_inff();
+        if (__ballot(in)) live |= 1u << q;
+    }
+    // software pipeline: list ids run two batches ahead, records one batch ahead
+    uint32_t id_next = lane < n ? a.point_list[range.x + lane] : 0u;
+    Rec r_next = {};
+    if (lane < n) r_next = a.rec[id_next];
+    id_next = 64 + lane < n ? a.point_list[range.x + 64 + lane] : 0u;
+    for (int b0 = 0; b0 < n && live; b0 += 64) {
+        const int j = b0 + lane;
+        Rec r = r_next;
+        if (j + 64 < n) r_next = a.rec[id_next];
+        if (j + 128 < n) id_next = a.point_list[range.x + j + 128];
+        const uint32_t qm = j < n ? wt.reach(r, (uint32_t)j, nullptr) : 0u;
+        const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
+        uint64_t todo = __ballot((qm & live) != 0);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t m = bcast(qm, k) & live;
+            if (!m) continue;
+            const float ax = bcast(r.a.x, k), ay = bcast(r.a.y, k);
+            const float ka = bcast(na, k), kb = bcast(nb, k), kc = bcast(nc, k), op = bcast(r.b.y, k);
+            const float col0 = bcast(r.b.z, k), col1 = bcast(r.b.w, k), col2 = bcast(r.c.x, k);
+            const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!((m >> q) & 1u)) continue;
+                const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
+                const float power = gauss_power(ka, kb, kc, dx, dy);
+                const float alpha = fminf(0.99f, op * tile_exp(power));
+                const bool hit = !(power > 0.0f) && alpha >= lim[q];
+                const float test_T = T[q] * (1 - alpha);
                 const bool sat = hit && test_T < 0.0001f;  // saturating Gaussian is not blended
                 const bool blend = hit && !sat;
-                done = done || sat;
-                const float w = blend ? alpha * T : 0.f;
-                C0 += B.z * w;
-                C1 += B.w * w;
-                C2 += sm.c[s] * w;
-                T = blend ? test_T : T;
-                last_contributor = blend ? sm.pos[s] + 1u : last_contributor;
-                if (__all(done)) break;
+                const float w = blend ? alpha * T[q] : 0.f;
+                C0[q] += col0 * w;
+                C1[q] += col1 * w;
+                C2[q] += col2 * w;
+                T[q] = blend ? test_T : T[q];
+                last[q] = blend ? pos1 : last[q];
+                lim[q] = sat ? __builtin_inff() : lim[q];
+                if (__ballot(sat) && !__ballot(lim[q] < 1.f)) live &= ~(1u << q);
             }
+            if (!live) break;
         }
     }
-    if (st.inside) {
-        const int pix = a.W * st.py + st.px;
-        a.final_T[pix] = T;
-        a.n_contrib[pix] = last_contributor;
-        const int HW = a.H * a.W;
-        a.out_color[pix] = C0 + T * a.bg[0];
-        a.out_color[HW + pix] = C1 + T * a.bg[1];
-        a.out_color[2 * HW + pix] = C2 + T * a.bg[2];
+    const int HW = a.H * a.W;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (wt.inside(q, a.W, a.H)) {
+            const int pix = wt.pixel(q, a.W);
+            a.final_T[pix] = T[q];
+            a.n_contrib[pix] = last[q];
+            a.out_color[pix] = C0[q] + T[q] * a.bg[0];
+            a.out_color[HW + pix] = C1[q] + T[q] * a.bg[1];
+            a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
+        }
     }
 }
 
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(ntile), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(ntile), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

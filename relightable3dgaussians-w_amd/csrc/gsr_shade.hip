@@ -432,7 +432,7 @@ void launch_shade_fwd(const ShadeArgs& a, float* rgb, float* diffuse, float* spe
 
 void launch_shade_bwd(const ShadeArgs& a, const ShadeGrads& g, void* workspace, hipStream_t s) {
     if (a.N == 0) {
-        if (g.d_base) hipMemsetAsync(g.d_base, 0, sizeof(float) * 3 * (a.deg + 1) * (a.deg + 1), s);
+        if (g.d_base) (void)hipMemsetAsync(g.d_base, 0, sizeof(float) * 3 * (a.deg + 1) * (a.deg + 1), s);
         return;
     }
     const int nb = (a.N + SHADE_THREADS - 1) / SHADE_THREADS;

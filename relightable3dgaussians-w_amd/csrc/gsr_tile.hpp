@@ -20,8 +20,10 @@ __device__ __forceinline__ float tile_exp(float x) { return __expf(x); }
 // q(d) = a dx^2 + 2 b dx dy + c dy^2, for a positive-definite conic (a, b, c).
 __device__ __forceinline__ float qmin_box(float a, float b, float c, float dx0, float dx1, float dy0, float dy1) {
     if (dx0 <= 0.f && dx1 >= 0.f && dy0 <= 0.f && dy1 >= 0.f) return 0.f;
-    // edges dx = const: argmin dy = -b dx / c ; edges dy = const: argmin dx = -b dy / a
-    const float ic = 1.f / c, ia = 1.f / a;
+    // edges dx = const: argmin dy = -b dx / c ; edges dy = const: argmin dx = -b dy / a.
+    // v_rcp_f32 (1 ulp) only moves the candidate point along the edge, where q is
+    // stationary; the margin in box_reachable absorbs the second-order change.
+    const float ic = __builtin_amdgcn_rcpf(c), ia = __builtin_amdgcn_rcpf(a);
     float q = 3.4e38f;
     {
         const float X = dx0;
@@ -72,6 +74,16 @@ __device__ __forceinline__ float row_sum(float v) {
     v += dpp<0x124>(v);
     return v + dpp<0x128>(v);
 }
+// permlane32 swap of (a, b) + add: lanes 0-31 get a[l] + a[l+32], lanes 32-63 b[l-32] + b[l].
+__device__ __forceinline__ float swap32_sum(float a, float b) {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
+// permlane16 swap of (a, b) + add: rows 0/2 get a's row pair sums, rows 1/3 b's.
+__device__ __forceinline__ float swap16_sum(float a, float b) {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+    return __uint_as_float(s[0]) + __uint_as_float(s[1]);
+}
 __device__ __forceinline__ float wave_sum(float v) {
     v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
@@ -83,93 +95,70 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // halves
 }
 
-// ---- batch staging shared by the forward and backward tile passes ---------------------
-struct TileStageLDS {
-    float4 a[256];           // (x, y, conic.a, conic.b)
-    float4 b[256];           // (conic.c, opacity, r, g)
-    float c[256];            // b
-    uint32_t pos[256];       // position in the tile's range
-    uint32_t id[256];        // Gaussian index
-    uint16_t qidx[4][256];   // per-quadrant lists of slots, in range order
-    uint32_t qcnt[4];        // per-quadrant list length
-    uint32_t cnt;            // slots used
-    uint32_t wcnt[4][5];     // per-wave ballot counts: kept, quadrant 0..3
-};
-
-struct TileStage {
+// ---- one wave per 16x16 tile --------------------------------------------------------
+// Lane l owns pixel (l % 8, l / 8) of each of the tile's four 8x8 quadrants q (offset
+// (8 (q & 1), 8 (q >> 1))), so a wave holds the whole tile and every per-Gaussian quadrant
+// decision is wave-uniform.  Batches of 64 candidates live in registers (one per lane);
+// the inner loop walks the surviving lanes with s_ff1 and broadcasts each record with
+// v_readlane, so the tile passes need no LDS and no workgroup barriers.
+struct WaveTile {
+    float pfx, pfy;          // quadrant-0 pixel of this lane
+    float tx0, ty0, wmax, hmax;
     int px, py;
-    bool inside;
-    float pfx, pfy, tx0, ty0, wmax, hmax;
-    uint64_t lt;
 
     __device__ __forceinline__ void init(unsigned tile, unsigned gx, int W, int H) {
+        const int lane = threadIdx.x & 63;
         const unsigned bx = tile % gx, by = tile / gx;
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        px = bx * GSR_BLOCK_X + (wave & 1) * 8 + (lane & 7);
-        py = by * GSR_BLOCK_Y + (wave >> 1) * 8 + (lane >> 3);
-        inside = px < W && py < H;
+        px = (int)(bx * GSR_BLOCK_X) + (lane & 7);
+        py = (int)(by * GSR_BLOCK_Y) + (lane >> 3);
         pfx = (float)px;
         pfy = (float)py;
         tx0 = (float)(bx * GSR_BLOCK_X);
         ty0 = (float)(by * GSR_BLOCK_Y);
         wmax = (float)(W - 1);
         hmax = (float)(H - 1);
-        lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     }
+    __device__ __forceinline__ bool inside(int q, int W, int H) const {
+        return px + 8 * (q & 1) < W && py + 8 * (q >> 1) < H;
+    }
+    __device__ __forceinline__ int pixel(int q, int W) const { return W * (py + 8 * (q >> 1)) + px + 8 * (q & 1); }
 
-    // Gather this thread's candidate record (if `valid`), keep it if it can reach any pixel
-    // of a quadrant, and compact the survivors (in thread order, i.e. range order) into the
-    // LDS slots and the four quadrant lists.  Contains two workgroup barriers; the caller
-    // must have passed a barrier since the previous batch's last read of `sm`.
-    // `qlimit` (optional, LDS): quadrant q only keeps positions < qlimit[q].
-    __device__ __forceinline__ void stage(TileStageLDS& sm, bool valid, uint32_t position, uint32_t gid,
-                                          const Rec* rec, const uint32_t* qlimit = nullptr) {
-        const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-        Rec r;
-        uint32_t qmask = 0;
-        if (valid) {
-            r = rec[gid];
+    // Quadrants (bit q) the record can reach with alpha >= 1/255 (conservative, see
+    // box_reachable); `limit[q]`: only positions < limit[q] are kept for quadrant q.
+    __device__ __forceinline__ uint32_t reach(const Rec& r, uint32_t position, const uint32_t* limit) const {
+        uint32_t m = 0;
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const float qx0 = tx0 + (q & 1) * 8.f, qy0 = ty0 + (q >> 1) * 8.f;
-                const float qx1 = fminf(qx0 + 7.f, wmax), qy1 = fminf(qy0 + 7.f, hmax);
-                if (qx0 <= wmax && qy0 <= hmax && (!qlimit || position < qlimit[q]) &&
-                    box_reachable(r.a.z, r.a.w, r.b.x, r.c.y, qx0 - r.a.x, qx1 - r.a.x, qy0 - r.a.y, qy1 - r.a.y))
-                    qmask |= 1u << q;
-            }
+        for (int q = 0; q < 4; q++) {
+            const float qx0 = tx0 + (q & 1) * 8.f, qy0 = ty0 + (q >> 1) * 8.f;
+            const float qx1 = fminf(qx0 + 7.f, wmax), qy1 = fminf(qy0 + 7.f, hmax);
+            if (qx0 <= wmax && qy0 <= hmax && (!limit || position < limit[q]) &&
+                box_reachable(r.a.z, r.a.w, r.b.x, r.c.y, qx0 - r.a.x, qx1 - r.a.x, qy0 - r.a.y, qy1 - r.a.y))
+                m |= 1u << q;
         }
-        const bool keep = qmask != 0;
-        const uint64_t bk = __ballot(keep);
-        uint64_t bq[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) bq[q] = __ballot((qmask >> q) & 1u);
-        if (lane == 0) {
-            sm.wcnt[wave][0] = (uint32_t)__popcll(bk);
-#pragma unroll
-            for (int q = 0; q < 4; q++) sm.wcnt[wave][1 + q] = (uint32_t)__popcll(bq[q]);
-        }
-        __syncthreads();
-        if (keep) {
-            uint32_t slot = (uint32_t)__popcll(bk & lt);
-            for (int w = 0; w < wave; w++) slot += sm.wcnt[w][0];
-            sm.a[slot] = r.a;
-            sm.b[slot] = r.b;
-            sm.c[slot] = r.c.x;
-            sm.pos[slot] = position;
-            sm.id[slot] = gid;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if ((qmask >> q) & 1u) {
-                    uint32_t qp = (uint32_t)__popcll(bq[q] & lt);
-                    for (int w = 0; w < wave; w++) qp += sm.wcnt[w][1 + q];
-                    sm.qidx[q][qp] = (uint16_t)slot;
-                }
-            }
-        }
-        if (tid < 4) sm.qcnt[tid] = sm.wcnt[0][1 + tid] + sm.wcnt[1][1 + tid] + sm.wcnt[2][1 + tid] + sm.wcnt[3][1 + tid];
-        if (tid == 4) sm.cnt = sm.wcnt[0][0] + sm.wcnt[1][0] + sm.wcnt[2][0] + sm.wcnt[3][0];
-        __syncthreads();
+        return m;
     }
 };
+
+// Exponent of the Gaussian at offset (dx, dy) from its centre, with the conic prepared as
+// (na, nb, nc) = (-a/2, -b, -c/2): power = -(a dx^2 + c dy^2)/2 - b dx dy.  The forward and
+// backward tile passes evaluate it with this exact operation sequence, so the backward
+// replays the forward's blend decisions bit for bit.
+__device__ __forceinline__ float gauss_power(float na, float nb, float nc, float dx, float dy) {
+    return __builtin_fmaf(na * dx, dx, __builtin_fmaf(nc * dy, dy, (nb * dx) * dy));
+}
+
+__device__ __forceinline__ float bcast(float v, int k) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+__device__ __forceinline__ uint32_t bcast(uint32_t v, int k) { return (uint32_t)__builtin_amdgcn_readlane((int)v, k); }
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t m) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t t = __shfl_xor(m, o, 64);
+        m = t > m ? t : m;
+    }
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)m);
+}
 
 }  // namespace gsr

@@ -3,6 +3,7 @@
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 TAG="${1:-pmc}"
+KRE="${2:-k_render|k_radix|k_preprocess}"
 cd /tmp && export TMPDIR=/tmp
 mkdir -p "$R/gpurun_out"
 i=0
@@ -10,7 +11,7 @@ for CT in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_B
           "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VMEM_RD SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS" \
           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $CT --kernel-include-regex "k_render|k_radix|k_preprocess" --output-format csv \
+  timeout -k 10 300 rocprofv3 --pmc $CT --kernel-include-regex "$KRE" --output-format csv \
     -d "$R/gpurun_out/${TAG}_$i" -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
     > "$R/gpurun_out/${TAG}_$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$R/gpurun_out/${TAG}_$i.log"; exit $rc; }
