@@ -26,14 +26,45 @@ __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
     return o;
 }
 
-// SH rows ([M][3] floats = 192 B at degree 3) are moved between HBM and LDS by whole rows
-// (coalesced), processed per thread from LDS (stride M*3+1: conflict-free), and the
-// gradient rows go back out the same way.
-__device__ __forceinline__ void copy_rows(float* dst, int dst_stride, const float* src, int src_stride, int rows,
-                                          int width) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-    for (int r = wave; r < rows; r += nw)
-        for (int e = lane; e < width; e += 64) dst[r * dst_stride + e] = src[r * src_stride + e];
+// SH rows ([M][3] floats = 192 B at degree 3) of the workgroup's Gaussians are one
+// contiguous block in HBM: it is moved as a flat array of 16-B words (every lane busy,
+// many loads in flight) and scattered into LDS rows of stride M*3+1 (odd: conflict-free
+// per-thread row access); the gradient rows go back out the same way.
+__device__ __forceinline__ void load_rows(float* s, int stride, const float* g, int rows, int width) {
+    const int n = rows * width;
+    if ((width & 3) == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(g);
+        for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
+            const float4 v = g4[f];
+            const int e0 = f * 4, r = e0 / width, e = e0 - r * width;
+            float* d = s + r * stride + e;
+            d[0] = v.x;
+            d[1] = v.y;
+            d[2] = v.z;
+            d[3] = v.w;
+        }
+    } else {
+        for (int f = threadIdx.x; f < n; f += blockDim.x) {
+            const int r = f / width;
+            s[r * stride + f - r * width] = g[f];
+        }
+    }
+}
+__device__ __forceinline__ void store_rows(float* g, const float* s, int stride, int rows, int width) {
+    const int n = rows * width;
+    if ((width & 3) == 0) {
+        float4* g4 = reinterpret_cast<float4*>(g);
+        for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
+            const int e0 = f * 4, r = e0 / width, e = e0 - r * width;
+            const float* d = s + r * stride + e;
+            g4[f] = make_float4(d[0], d[1], d[2], d[3]);
+        }
+    } else {
+        for (int f = threadIdx.x; f < n; f += blockDim.x) {
+            const int r = f / width;
+            g[f] = s[r * stride + f - r * width];
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
@@ -42,14 +73,14 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     const int g0 = blockIdx.x * blockDim.x;
     const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
     if (a.shs) {
-        copy_rows(s_sh, sh_stride, a.shs + (size_t)g0 * M3, M3, rows, M3);
+        load_rows(s_sh, sh_stride, a.shs + (size_t)g0 * M3, rows, M3);
         __syncthreads();
     }
     const int idx = g0 + threadIdx.x;
     if (idx < a.P) preprocess_bwd_one(a, idx, s_sh, sh_stride);
     if (a.dL_dsh) {
         __syncthreads();
-        copy_rows(a.dL_dsh + (size_t)g0 * M3, M3, s_sh, sh_stride, rows, M3);
+        store_rows(a.dL_dsh + (size_t)g0 * M3, s_sh, sh_stride, rows, M3);
     }
 }
 
