@@ -19,6 +19,14 @@
 
 namespace gsr {
 
+#ifdef GSR_RENDER_STATS
+__device__ unsigned long long g_bwd_stats[8];
+__device__ unsigned long long g_bwd_times[3 * 65536];  // per tile: start, end (s_memrealtime), hw id
+#define BWD_STAT(k, v) st[k] += (v)
+#else
+#define BWD_STAT(k, v)
+#endif
+
 __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
     const unsigned ntile = a.grid_x * a.grid_y;
     const unsigned tile = xcd_remap(blockIdx.x, ntile);
@@ -69,6 +77,10 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
         r_next = a.rec[id_cur];
     }
     if (64u + lane < nmax) id_next = a.point_list[range.x + nmax - 65u - lane];
+#ifdef GSR_RENDER_STATS
+    unsigned long long st[8] = {};
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
         const uint32_t i = b0 + lane;
         const uint32_t p = nmax - 1u - i;  // back to front
@@ -80,6 +92,8 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
         const uint32_t qm = i < nmax ? wt.reach(r, p, qlim) : 0u;
         const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
         uint64_t todo = __ballot(qm != 0);
+        BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
+        BWD_STAT(1, __popcll(todo));
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -96,12 +110,15 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
+                BWD_STAT(2, 1);
                 const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
                 const float power = gauss_power(ka, kb, kc, dx, dy);
                 const float G = tile_exp(power);
                 const float alpha = fminf(0.99f, op * G);
                 const bool active = pos < last[q] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
                 if (__ballot(active) == 0ull) continue;  // wave-uniform
+                BWD_STAT(3, 1);
+                BWD_STAT(4, __popcll(__ballot(active)));
                 any = true;
                 // inactive lanes run the same code with alpha = G = 0: T, the sums and
                 // the gradients stay unchanged
@@ -130,6 +147,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
                 la[q] = active ? alpha : la[q];
             }
             if (!any) continue;
+            BWD_STAT(5, 1);
             // conic part of dL/dmean2D (backward.cu:540-545): -(a M1 + b M2), -(b M1 + c M2)
             const float S0 = __builtin_fmaf(ka, M1 + M1, kb * M2);
             const float S1 = __builtin_fmaf(kc, M2 + M2, kb * M1);
@@ -147,7 +165,32 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
             if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)bcast(id, k) * ACC_STRIDE + vidx, v);
         }
     }
+#ifdef GSR_RENDER_STATS
+    if (lane == 0) {
+        for (int k = 0; k < 6; k++) atomicAdd(&g_bwd_stats[k], st[k]);
+        if (tile < 65536) {
+            g_bwd_times[3 * tile] = t_start;
+            g_bwd_times[3 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+            g_bwd_times[3 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                                        ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+        }
+    }
+#endif
 }
+
+#ifdef GSR_RENDER_STATS
+extern "C" int gsr_debug_bwd_times(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_times), sizeof(unsigned long long) * 3 * n) == hipSuccess ? 0 : -1;
+}
+extern "C" int gsr_debug_bwd_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stats), sizeof(g_bwd_stats)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_bwd_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;

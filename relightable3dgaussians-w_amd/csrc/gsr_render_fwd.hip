@@ -18,6 +18,13 @@
 
 namespace gsr {
 
+#ifdef GSR_RENDER_STATS
+__device__ unsigned long long g_fwd_stats[8];
+#define FWD_STAT(k, v) st[k] += (v)
+#else
+#define FWD_STAT(k, v)
+#endif
+
 __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
     const unsigned ntile = a.grid_x * a.grid_y;
     const unsigned tile = xcd_remap(blockIdx.x, ntile);
@@ -46,6 +53,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
     Rec r_next = {};
     if (lane < n) r_next = a.rec[id_next];
     id_next = 64 + lane < n ? a.point_list[range.x + 64 + lane] : 0u;
+#ifdef GSR_RENDER_STATS
+    unsigned long long st[8] = {};
+#endif
     for (int b0 = 0; b0 < n && live; b0 += 64) {
         const int j = b0 + lane;
         Rec r = r_next;
@@ -54,6 +64,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
         const uint32_t qm = j < n ? wt.reach(r, (uint32_t)j, nullptr) : 0u;
         const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
         uint64_t todo = __ballot((qm & live) != 0);
+        FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
+        FWD_STAT(1, __popcll(todo));
         while (todo) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -70,6 +82,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
                 const float power = gauss_power(ka, kb, kc, dx, dy);
                 const float alpha = fminf(0.99f, op * tile_exp(power));
                 const bool hit = !(power > 0.0f) && alpha >= lim[q];
+                FWD_STAT(2, 1);
+                FWD_STAT(3, __ballot(hit) != 0ull);
+                FWD_STAT(4, __popcll(__ballot(hit)));
                 const float test_T = T[q] * (1 - alpha);
                 const bool sat = hit && test_T < 0.0001f;  // saturating Gaussian is not blended
                 const bool blend = hit && !sat;
@@ -85,6 +100,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
             if (!live) break;
         }
     }
+#ifdef GSR_RENDER_STATS
+    if (lane == 0)
+        for (int k = 0; k < 5; k++) atomicAdd(&g_fwd_stats[k], st[k]);
+#endif
     const int HW = a.H * a.W;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -98,6 +117,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
         }
     }
 }
+
+#ifdef GSR_RENDER_STATS
+extern "C" int gsr_debug_fwd_stats(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_stats), sizeof(g_fwd_stats)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fwd_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;

@@ -11,7 +11,7 @@ import threading
 import torch
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libgsr.so")
+LIB_PATH = os.environ.get("GSR_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libgsr.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 RESIZE_FN = C.CFUNCTYPE(C.c_void_p, C.c_void_p, C.c_size_t)
