@@ -19,6 +19,7 @@
 // (depth-bits ascending, Gaussian index ascending on ties), bit-exact.
 #include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
+#include "gsr_tile.hpp"
 
 namespace gsr {
 
@@ -160,7 +161,9 @@ __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_rang
 }
 
 // Count (WRITE = false) or write (WRITE = true) one segment: for each of the super-tile's
-// 32 tiles, the entries whose rect covers it, ranked in list order by wave ballots.
+// 32 tiles, the entries whose rect covers it, ranked in list order by wave ballots.  Lane t
+// of every wave holds the wave's output base for tile t, so a rank is one readlane plus
+// a lane-masked popcount; lanes covering tile t store to consecutive addresses.
 template <bool WRITE>
 __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, const uint32_t* seg_st,
                                                     const uint32_t* seg_e0, const uint2* st_ranges,
@@ -168,51 +171,53 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
                                                     unsigned gy, unsigned gsx, uint32_t* seg_cnt,
                                                     const uint32_t* seg_base, uint32_t* point_list) {
     __shared__ uint32_t s_wc[4][ST_TILES];
-    __shared__ uint32_t s_run[ST_TILES];
     const uint32_t gseg = blockIdx.x;
     if (gseg >= *nseg_total) return;
     const unsigned st = seg_st[gseg];
-    const StGeom g = st_geom(st, gsx, gx, gy);
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     const uint32_t e0 = seg_e0[gseg];
     const uint32_t e1 = min(e0 + SEG, st_ranges[st].y);
-    if (tid < ST_TILES) s_run[tid] = WRITE ? seg_base[(size_t)gseg * ST_TILES + tid] : 0u;
-    __syncthreads();
+    // lane t < 32: running output position of tile t (block-uniform across waves)
+    uint32_t run = (WRITE && lane < ST_TILES) ? seg_base[(size_t)gseg * ST_TILES + lane] : 0u;
     for (uint32_t b = e0; b < e1; b += 256) {
         const uint32_t e = b + tid;
-        const bool valid = e < e1;
         uint32_t id = 0, mask = 0;
-        if (valid) {
+        if (e < e1) {
             // local tile coverage mask (bit t = (t / 8) row, (t % 8) column)
             mask = local_rect_mask(st_keys[e] >> ST_KEY_BITS);
             if (WRITE) id = st_vals[e];
         }
         uint64_t bal[ST_TILES];
+        uint32_t mine = 0;
 #pragma unroll
-        for (int t = 0; t < ST_TILES; t++) bal[t] = __ballot((mask >> t) & 1u);
-        if (lane < ST_TILES) {
-            uint64_t mine = 0;
-#pragma unroll
-            for (int t = 0; t < ST_TILES; t++) mine = lane == t ? bal[t] : mine;
-            s_wc[wave][lane] = (uint32_t)__popcll(mine);
+        for (int t = 0; t < ST_TILES; t++) {
+            bal[t] = __ballot((mask >> t) & 1u);
+            mine = lane == t ? (uint32_t)__popcll(bal[t]) : mine;
         }
+        if (lane < ST_TILES) s_wc[wave][lane] = mine;
         __syncthreads();
-        if (WRITE && mask) {
+        uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+        if (lane < ST_TILES) {
+            c0 = s_wc[0][lane];
+            c1 = s_wc[1][lane];
+            c2 = s_wc[2][lane];
+            c3 = s_wc[3][lane];
+        }
+        if (WRITE) {
+            const uint32_t wbase = run + (wave > 0 ? c0 : 0u) + (wave > 1 ? c1 : 0u) + (wave > 2 ? c2 : 0u);
 #pragma unroll
             for (int t = 0; t < ST_TILES; t++) {
                 if ((mask >> t) & 1u) {
-                    uint32_t p = s_run[t] + (uint32_t)__popcll(bal[t] & lt);
-                    for (int w = 0; w < wave; w++) p += s_wc[w][t];
-                    point_list[p] = id;
+                    const uint32_t lo = (uint32_t)bal[t], hi = (uint32_t)(bal[t] >> 32);
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+                    point_list[bcast(wbase, t) + r] = id;
                 }
             }
         }
-        __syncthreads();
-        if (tid < ST_TILES) s_run[tid] += s_wc[0][tid] + s_wc[1][tid] + s_wc[2][tid] + s_wc[3][tid];
+        run += c0 + c1 + c2 + c3;
         __syncthreads();
     }
-    if (!WRITE && tid < ST_TILES) seg_cnt[(size_t)gseg * ST_TILES + tid] = s_run[tid];
+    if (!WRITE && wave == 0 && lane < ST_TILES) seg_cnt[(size_t)gseg * ST_TILES + lane] = run;
 }
 
 // Per (super-tile, local tile): prefix of the segment counts -> segment-relative bases,
