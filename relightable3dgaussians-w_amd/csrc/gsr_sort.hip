@@ -7,9 +7,10 @@
 // pass gives the reference's total order (tile, depth, gaussian index).
 //
 // One pass = 3 launches (reduce-then-scan):
-//   k_radix_hist    per-4096-key tile digit histogram (wave ballot-match counting)
-//   scan            exclusive scan of the digit-major histogram -> global offsets
-//   k_radix_scatter per-tile stable ranking: each wave ranks its 1024 contiguous keys
+//   k_radix_hist    per-tile digit histogram (per-wave LDS counters)
+//   k_digit_scan    one workgroup per digit: exclusive scan of that digit's per-tile
+//                   counts (contiguous in the digit-major table) + the digit's total
+//   k_radix_scatter per-tile stable ranking: each wave ranks its contiguous keys
 //                   with 8 ballots per 64-key row (peer masks, leader lane bumps the
 //                   per-wave LDS counter), waves combine through LDS, the tile is
 //                   reordered in LDS and written out in digit runs (coalesced).
@@ -58,10 +59,26 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const 
     hist[(long long)d * nb + blockIdx.x] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
 }
 
+// hist[d][0..nb) -> exclusive prefix within digit d; digit_tot[d] = the digit's total
+__global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int nb, uint32_t* digit_tot) {
+    __shared__ uint32_t sh[4];
+    uint32_t* h = hist + (long long)blockIdx.x * nb;
+    uint32_t carry = 0;
+    for (int c = 0; c < nb; c += SORT_THREADS) {
+        const int i = c + threadIdx.x;
+        const uint32_t v = i < nb ? h[i] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block256_exclusive_scan(v, sh, &tot);
+        if (i < nb) h[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+}
+
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
-                                                                  const uint32_t* offsets, int nb, uint32_t* keys_out,
-                                                                  uint32_t* vals_out) {
+                                                                  const uint32_t* offsets, const uint32_t* digit_tot,
+                                                                  int nb, uint32_t* keys_out, uint32_t* vals_out) {
     __shared__ uint32_t s_keys[SORT_TILE];
     __shared__ uint32_t s_vals[SORT_TILE];
     __shared__ uint32_t wh[4][256];
@@ -76,12 +93,17 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
     volatile uint32_t* wc = wh[wave];
     const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
+    // all loads first (32 per lane in flight), then the ranking
+#pragma unroll
+    for (int k = 0; k < SORT_ITEMS; k++) {
+        const long long i = base + k * 64 + lane;
+        key[k] = i < n ? keys_in[i] : 0u;
+        val[k] = i < n ? vals_in[i] : 0u;
+    }
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
         const long long i = base + k * 64 + lane;
         const bool valid = i < n;
-        key[k] = valid ? keys_in[i] : 0u;
-        val[k] = valid ? vals_in[i] : 0u;
         const uint32_t d = (key[k] >> shift) & mask;
         const uint64_t m = peer_mask(d, valid);
         const int leader = valid ? (int)(__ffsll((unsigned long long)m) - 1) : lane;
@@ -103,7 +125,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         wh[2][d] = start + c0 + c1;
         wh[3][d] = start + c0 + c1 + c2;
         dstart[d] = start;
-        goff[d] = offsets[(long long)d * nb + blockIdx.x];
+        const uint32_t dbase = block256_exclusive_scan(digit_tot[d], scan_sh, (uint32_t*)nullptr);
+        goff[d] = dbase + offsets[(long long)d * nb + blockIdx.x];
     }
     __syncthreads();
 #pragma unroll
@@ -134,7 +157,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
 size_t radix_sort_temp_bytes(long long n) {
     const long long nb = sort_blocks(n);
     const long long h = 256 * nb;
-    return (size_t)(4 * (h + scan_blocks(h)) + 256);
+    return (size_t)(4 * (h + 256) + 256);
 }
 
 int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
@@ -142,7 +165,7 @@ int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys
     if (n <= 1 || end_bit <= 0) return 0;
     const int nb = sort_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* spine = hist + 256LL * nb;
+    uint32_t* digit_tot = hist + 256LL * nb;
     uint32_t* kin = keys;
     uint32_t* vin = vals;
     uint32_t* kout = keys_alt;
@@ -152,9 +175,9 @@ int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
         const uint32_t mask = (1u << nbits) - 1u;
         hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
-        launch_exclusive_scan_u32(256LL * nb, hist, nullptr, hist, spine, nullptr, s);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask, hist, nb,
-                           kout, vout);
+        hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask, hist,
+                           digit_tot, nb, kout, vout);
         uint32_t* t;
         t = kin; kin = kout; kout = t;
         t = vin; vin = vout; vout = t;
