@@ -27,9 +27,7 @@ __device__ unsigned long long g_bwd_times[3 * 65536];  // per tile: start, end (
 #define BWD_STAT(k, v)
 #endif
 
-__global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
-    const unsigned ntile = a.grid_x * a.grid_y;
-    const unsigned tile = xcd_remap(blockIdx.x, ntile);
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -69,14 +67,6 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
     const float vscale = vidx == 0 ? 0.5f * a.W : vidx == 1 ? 0.5f * a.H : vidx <= 4 ? -0.5f : 1.f;
     const bool vop = vidx >= 0 && vidx <= 4;
 
-    // software pipeline: list ids run two batches ahead, records one batch ahead
-    uint32_t id_cur = 0, id_next = 0;
-    Rec r_next = {};
-    if ((uint32_t)lane < nmax) {
-        id_cur = a.point_list[range.x + nmax - 1u - lane];
-        r_next = a.rec[id_cur];
-    }
-    if (64u + lane < nmax) id_next = a.point_list[range.x + nmax - 65u - lane];
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
@@ -84,13 +74,18 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
     for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
         const uint32_t i = b0 + lane;
         const uint32_t p = nmax - 1u - i;  // back to front
-        const Rec r = r_next;
-        const uint32_t id = id_cur;
-        id_cur = id_next;
-        if (i + 64u < nmax) r_next = a.rec[id_cur];
-        if (i + 128u < nmax) id_next = a.point_list[range.x + p - 128u];
-        const uint32_t qm = i < nmax ? wt.reach(r, p, qlim) : 0u;
-        const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
+        uint32_t id = 0, qm = 0;
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+        float rc = 0.f;
+        if (i < nmax) {
+            id = a.point_list[range.x + p];
+            const Rec r = a.rec[id];
+            qm = wt.reach(r, p, qlim);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2)
+            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
+            rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
+            rc = r.c.x;
+        }
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
         BWD_STAT(1, __popcll(todo));
@@ -98,9 +93,9 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
             const uint32_t m = bcast(qm, k);
-            const float ax = bcast(r.a.x, k), ay = bcast(r.a.y, k);
-            const float ka = bcast(na, k), kb = bcast(nb, k), kc = bcast(nc, k), op = bcast(r.b.y, k);
-            const float c0 = bcast(r.b.z, k), c1 = bcast(r.b.w, k), c2 = bcast(r.c.x, k);
+            const float ax = bcast(ra.x, k), ay = bcast(ra.y, k);
+            const float ka = bcast(ra.z, k), kb = bcast(ra.w, k), kc = bcast(rb.x, k), op = bcast(rb.y, k);
+            const float c0 = bcast(rb.z, k), c1 = bcast(rb.w, k), c2 = bcast(rc, k);
             const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
             // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
             // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
@@ -115,15 +110,16 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
                 const float power = gauss_power(ka, kb, kc, dx, dy);
                 const float G = tile_exp(power);
                 const float alpha = fminf(0.99f, op * G);
-                const bool active = pos < last[q] && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
-                if (__ballot(active) == 0ull) continue;  // wave-uniform
+                // active: pos < last && !(power > 0) && !(alpha < 1/255)
+                const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();
+                if (act == 0ull) continue;  // wave-uniform
                 BWD_STAT(3, 1);
-                BWD_STAT(4, __popcll(__ballot(active)));
+                BWD_STAT(4, __popcll(act));
                 any = true;
                 // inactive lanes run the same code with alpha = G = 0: T, the sums and
                 // the gradients stay unchanged
-                const float ae = active ? alpha : 0.f;
-                const float Ge = active ? G : 0.f;
+                const float ae = sel(act, alpha, 0.f);
+                const float Ge = sel(act, G, 0.f);
                 const float inv = __builtin_amdgcn_rcpf(1.f - ae);
                 const float Tn = T[q] * inv;
                 const float dch = ae * Tn;
@@ -142,9 +138,9 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
                 S7 = __builtin_fmaf(dch, dp1[q], S7);
                 S8 = __builtin_fmaf(dch, dp2[q], S8);
                 T[q] = Tn;
-                AD[q] = active ? nAD : AD[q];
-                LD[q] = active ? cdp : LD[q];
-                la[q] = active ? alpha : la[q];
+                AD[q] = sel(act, nAD, AD[q]);
+                LD[q] = sel(act, cdp, LD[q]);
+                la[q] = sel(act, alpha, la[q]);
             }
             if (!any) continue;
             BWD_STAT(5, 1);
@@ -176,6 +172,21 @@ __global__ void __launch_bounds__(64) k_render_bwd(RenderBwdArgs a) {
         }
     }
 #endif
+}
+
+
+// One workgroup per tile, dispatched heaviest-first: block b takes position b / 8 of XCD
+// band (b mod 8)'s queue (launch_tile_order), so the hardware dispatcher, which deals blocks
+// round-robin over the XCDs and starts them as slots free up, runs a longest-first
+// schedule with each XCD on its own band of the image.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {
+    const unsigned ntile = a.grid_x * a.grid_y;
+    unsigned lo, len;
+    band_of(blockIdx.x & 7u, ntile, lo, len);
+    const unsigned b = blockIdx.x >> 3;
+    // blocks past a short band's end (bands differ by at most one tile) take the remainder
+    const unsigned tile = b < len ? a.order[lo + b] : xcd_remap(blockIdx.x, ntile);
+    render_bwd_tile(a, tile);
 }
 
 #ifdef GSR_RENDER_STATS

@@ -25,9 +25,7 @@ __device__ unsigned long long g_fwd_stats[8];
 #define FWD_STAT(k, v)
 #endif
 
-__global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
-    const unsigned ntile = a.grid_x * a.grid_y;
-    const unsigned tile = xcd_remap(blockIdx.x, ntile);
+__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -48,21 +46,22 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
         lim[q] = in ? 1.0f / 255.0f : __builtin_inff();
         if (__ballot(in)) live |= 1u << q;
     }
-    // software pipeline: list ids run two batches ahead, records one batch ahead
-    uint32_t id_next = lane < n ? a.point_list[range.x + lane] : 0u;
-    Rec r_next = {};
-    if (lane < n) r_next = a.rec[id_next];
-    id_next = 64 + lane < n ? a.point_list[range.x + 64 + lane] : 0u;
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
 #endif
     for (int b0 = 0; b0 < n && live; b0 += 64) {
         const int j = b0 + lane;
-        Rec r = r_next;
-        if (j + 64 < n) r_next = a.rec[id_next];
-        if (j + 128 < n) id_next = a.point_list[range.x + j + 128];
-        const uint32_t qm = j < n ? wt.reach(r, (uint32_t)j, nullptr) : 0u;
-        const float na = -0.5f * r.a.z, nb = -r.a.w, nc = -0.5f * r.b.x;
+        uint32_t qm = 0;
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+        float rc = 0.f;
+        if (j < n) {
+            const Rec r = a.rec[a.point_list[range.x + j]];
+            qm = wt.reach(r, (uint32_t)j, nullptr);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2)
+            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
+            rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
+            rc = r.c.x;
+        }
         uint64_t todo = __ballot((qm & live) != 0);
         FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
         FWD_STAT(1, __popcll(todo));
@@ -71,9 +70,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
             todo &= todo - 1;
             const uint32_t m = bcast(qm, k) & live;
             if (!m) continue;
-            const float ax = bcast(r.a.x, k), ay = bcast(r.a.y, k);
-            const float ka = bcast(na, k), kb = bcast(nb, k), kc = bcast(nc, k), op = bcast(r.b.y, k);
-            const float col0 = bcast(r.b.z, k), col1 = bcast(r.b.w, k), col2 = bcast(r.c.x, k);
+            const float ax = bcast(ra.x, k), ay = bcast(ra.y, k);
+            const float ka = bcast(ra.z, k), kb = bcast(ra.w, k), kc = bcast(rb.x, k), op = bcast(rb.y, k);
+            const float col0 = bcast(rb.z, k), col1 = bcast(rb.w, k), col2 = bcast(rc, k);
             const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -116,6 +115,28 @@ __global__ void __launch_bounds__(64) k_render_fwd(RenderFwdArgs a) {
             a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
         }
     }
+    uint32_t nm = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t m = wave_max_u32(last[q]);
+        nm = m > nm ? m : nm;
+    }
+    if (lane == 0) a.tile_nmax[tile] = nm;
+}
+
+
+// One workgroup per tile, dispatched heaviest-first: block b takes position b / 8 of XCD
+// band (b mod 8)'s queue (launch_tile_order), so the hardware dispatcher, which deals blocks
+// round-robin over the XCDs and starts them as slots free up, runs a longest-first
+// schedule with each XCD on its own band of the image.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5, 5))) k_render_fwd(RenderFwdArgs a) {
+    const unsigned ntile = a.grid_x * a.grid_y;
+    unsigned lo, len;
+    band_of(blockIdx.x & 7u, ntile, lo, len);
+    const unsigned b = blockIdx.x >> 3;
+    // blocks past a short band's end (bands differ by at most one tile) take the remainder
+    const unsigned tile = b < len ? a.order[lo + b] : xcd_remap(blockIdx.x, ntile);
+    render_fwd_tile(a, tile);
 }
 
 #ifdef GSR_RENDER_STATS

@@ -12,6 +12,50 @@ __device__ __forceinline__ unsigned xcd_remap(unsigned b, unsigned n) {
     return base + (b >> 3);
 }
 
+// band x of xcd_remap: tiles [lo, lo + len)
+__device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, unsigned& len) {
+    const unsigned q = n >> 3, r = n & 7u;
+    lo = x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q;
+    len = q + (x < r ? 1u : 0u);
+}
+
+// Persistent-pass tile source (one wave per workgroup): pulls tiles from this XCD's queue
+// (launch_tile_order), then from the other seven.  Wave-uniform; false once all are empty.
+struct TileQueue {
+    unsigned ntile, q;
+    int tries;
+    const uint32_t* order;
+    uint32_t* queue;
+
+    __device__ __forceinline__ void init(unsigned n, const uint32_t* ord, uint32_t* qu) {
+        ntile = n;
+        order = ord;
+        queue = qu;
+        tries = 0;
+#ifdef GSR_QUEUE_BLOCKID
+        q = blockIdx.x & 7u;
+#else
+        q = (unsigned)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7u;  // HW_REG_XCC_ID
+#endif
+    }
+    __device__ __forceinline__ bool next(unsigned& tile) {
+        while (tries < 8) {
+            unsigned lo, len;
+            band_of(q, ntile, lo, len);
+            uint32_t idx = 0;
+            if ((threadIdx.x & 63) == 0) idx = atomicAdd(&queue[q], 1u);
+            idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
+            if (idx < len) {
+                tile = (unsigned)__builtin_amdgcn_readfirstlane((int)order[lo + idx]);
+                return true;
+            }
+            q = (q + 1) & 7u;
+            tries++;
+        }
+        return false;
+    }
+};
+
 // exp as the tile loops evaluate it, identical in forward and backward so that the
 // backward replays exactly the forward's blend decisions (v_exp_f32 on x*log2(e)).
 __device__ __forceinline__ float tile_exp(float x) { return __expf(x); }
@@ -146,6 +190,43 @@ struct WaveTile {
 __device__ __forceinline__ float gauss_power(float na, float nb, float nc, float dx, float dy) {
     return __builtin_fmaf(na * dx, dx, __builtin_fmaf(nc * dy, dy, (nb * dx) * dy));
 }
+
+// Lane masks in SGPR pairs and selects on them (v_cmp_*_e64 / v_cndmask_b32_e64).  On
+// gfx950 a v_cndmask_b32 that reads its mask from VCC (the VOP2 form the compiler picks
+// for `c ? a : b`) issues ~5x slower than the VOP3 form reading any other SGPR pair
+// (tools/micro/vcmp.hip), so the tile loops build masks and selects explicitly.
+typedef uint64_t lmask;
+__device__ __forceinline__ lmask m_gt0(float a) {  // a > 0
+    lmask m;
+    asm("v_cmp_lt_f32_e64 %0, 0, %1" : "=s"(m) : "v"(a));
+    return m;
+}
+__device__ __forceinline__ lmask m_ge(float a, float b) {  // a >= b (false on NaN)
+    lmask m;
+    asm("v_cmp_ge_f32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ lmask m_lt(float a, float b) {  // a < b
+    lmask m;
+    asm("v_cmp_lt_f32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ lmask m_ult(uint32_t a, uint32_t b) {  // a < b, a wave-uniform
+    lmask m;
+    asm("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "s"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ float sel(lmask m, float t, float f) {  // m ? t : f per lane
+    float r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+__device__ __forceinline__ uint32_t sel(lmask m, uint32_t t, uint32_t f) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
+    return r;
+}
+__device__ __forceinline__ lmask exec_mask() { return __builtin_amdgcn_read_exec(); }
 
 __device__ __forceinline__ float bcast(float v, int k) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));

@@ -46,7 +46,9 @@ def main(cfg="cfg2"):
         out[name] = {"entries_per_tile": v[0] / T, "survivors_per_tile": v[1] / T, "quad_evals_per_tile": v[2] / T,
                      "quad_evals_with_work_per_tile": v[3] / T,
                      "lanes_per_working_eval": v[4] / max(v[3], 1),
-                     "gaussians_with_work_per_tile": (v[5] / T) if name == "bwd" else None}
+                     "gaussians_with_work_per_tile": (v[5] / T) if name == "bwd" else None,
+                     "queue_wait_us_total": v[6] / 100.0 if name == "bwd" else None,
+                     "tiles_via_queue": v[7] if name == "bwd" else None}
     n = T
     tb = (C.c_ulonglong * (3 * n))()
     L.gsr_debug_bwd_times(tb, n)
