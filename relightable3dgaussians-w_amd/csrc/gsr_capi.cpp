@@ -59,7 +59,7 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, queues, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, total;
 };
 struct BinLayout {
     size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_ranges, tile_cnt, tile_start, scan_tmp,
@@ -102,7 +102,6 @@ ImgLayout img_layout(int W, int H) {
     L.tile_nmax = c.take(4 * T);
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    L.queues = c.take(4 * 16);
     L.total = c.o + 256;
     return L;
 }
@@ -394,11 +393,11 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
     ra.ranges = ranges; ra.point_list = point_list; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
-    ra.order = at<uint32_t>(img, il.order_fwd); ra.queue = at<uint32_t>(img, il.queues);
+    ra.order = at<uint32_t>(img, il.order_fwd);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     {
         GSR_STAGE(ST_RENDER_FWD);
-        gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), ra.queue, s);
+        gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), s);
         gsr::launch_render_fwd(ra, s);
     }
     GSR_LAUNCH_CHECK();
@@ -446,11 +445,10 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         ra.dL_dpix = dL_dpix;
         ra.acc = acc;
         ra.order = at<uint32_t>(img, il.order_bwd);
-        ra.queue = at<uint32_t>(img, il.queues) + 8;
         {
             GSR_STAGE(ST_RENDER_BWD);
             gsr::launch_tile_order(gx * gy, ra.ranges, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
-                                   ra.queue, s);
+                                   s);
             gsr::launch_render_bwd(ra, s);
         }
         GSR_LAUNCH_CHECK();

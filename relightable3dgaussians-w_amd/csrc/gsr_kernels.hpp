@@ -89,13 +89,10 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s);
 
-// ---- tile queues (gsr_schedule.hip) ------------------------------------------------------
+// ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of
-// the tile's list length when cost is null); queue: 8 counters, zeroed here.
-void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* queue,
-                       hipStream_t s);
-// waves the device holds at `per_simd` waves per SIMD (grid size of a persistent pass)
-int resident_waves(int per_simd);
+// the tile's list length when cost is null).
+void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, hipStream_t s);
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 struct RenderFwdArgs {
@@ -108,8 +105,7 @@ struct RenderFwdArgs {
     float* out_color;
     float* final_T;
     uint32_t* n_contrib;
-    const uint32_t* order;  // tile queues (launch_tile_order)
-    uint32_t* queue;
+    const uint32_t* order;  // dispatch order (launch_tile_order)
     uint32_t* tile_nmax;    // out: per tile, the largest n_contrib (the backward's cost)
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
@@ -126,8 +122,7 @@ struct RenderBwdArgs {
     const uint32_t* n_contrib;
     const float* dL_dpix;
     float* acc;  // [P][ACC_STRIDE]
-    const uint32_t* order;  // tile queues (launch_tile_order)
-    uint32_t* queue;
+    const uint32_t* order;  // dispatch order (launch_tile_order)
 };
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 

@@ -176,7 +176,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 
 // One workgroup per tile, dispatched heaviest-first: block b takes position b / 8 of XCD
-// band (b mod 8)'s queue (launch_tile_order), so the hardware dispatcher, which deals blocks
+// band (b mod 8)'s order (launch_tile_order), so the hardware dispatcher, which deals blocks
 // round-robin over the XCDs and starts them as slots free up, runs a longest-first
 // schedule with each XCD on its own band of the image.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {

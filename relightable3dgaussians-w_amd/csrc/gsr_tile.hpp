@@ -19,43 +19,6 @@ __device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, un
     len = q + (x < r ? 1u : 0u);
 }
 
-// Persistent-pass tile source (one wave per workgroup): pulls tiles from this XCD's queue
-// (launch_tile_order), then from the other seven.  Wave-uniform; false once all are empty.
-struct TileQueue {
-    unsigned ntile, q;
-    int tries;
-    const uint32_t* order;
-    uint32_t* queue;
-
-    __device__ __forceinline__ void init(unsigned n, const uint32_t* ord, uint32_t* qu) {
-        ntile = n;
-        order = ord;
-        queue = qu;
-        tries = 0;
-#ifdef GSR_QUEUE_BLOCKID
-        q = blockIdx.x & 7u;
-#else
-        q = (unsigned)__builtin_amdgcn_s_getreg(20 | (0 << 6) | (3 << 11)) & 7u;  // HW_REG_XCC_ID
-#endif
-    }
-    __device__ __forceinline__ bool next(unsigned& tile) {
-        while (tries < 8) {
-            unsigned lo, len;
-            band_of(q, ntile, lo, len);
-            uint32_t idx = 0;
-            if ((threadIdx.x & 63) == 0) idx = atomicAdd(&queue[q], 1u);
-            idx = (uint32_t)__builtin_amdgcn_readfirstlane((int)idx);
-            if (idx < len) {
-                tile = (unsigned)__builtin_amdgcn_readfirstlane((int)order[lo + idx]);
-                return true;
-            }
-            q = (q + 1) & 7u;
-            tries++;
-        }
-        return false;
-    }
-};
-
 // exp as the tile loops evaluate it, identical in forward and backward so that the
 // backward replays exactly the forward's blend decisions (v_exp_f32 on x*log2(e)).
 __device__ __forceinline__ float tile_exp(float x) { return __expf(x); }
