@@ -33,6 +33,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     const int n = (int)(range.y - range.x);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    __shared__ float4 s_a[64], s_b[64];
+    __shared__ float2 s_c[64];
     float T[4], C0[4], C1[4], C2[4];
     float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
     uint32_t last[4];
@@ -62,24 +64,36 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
+        // the batch's records go to LDS; the walk below reads each survivor's record with
+        // broadcast LDS loads (LDS pipe) instead of 11 v_readlane (VALU), the next
+        // survivor's loads issued before the current one is blended
+        __syncthreads();
+        s_a[lane] = ra;
+        s_b[lane] = rb;
+        s_c[lane] = make_float2(rc, __uint_as_float(qm));
+        __syncthreads();
         uint64_t todo = __ballot((qm & live) != 0);
         FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
         FWD_STAT(1, __popcll(todo));
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
+        if (!todo) continue;
+        int k = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        float4 A = s_a[k], B = s_b[k];
+        float2 Cq = s_c[k];
+        for (;;) {
+            const bool more = todo != 0ull;
+            const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
-            const uint32_t m = bcast(qm, k) & live;
-            if (!m) continue;
-            const float ax = bcast(ra.x, k), ay = bcast(ra.y, k);
-            const float ka = bcast(ra.z, k), kb = bcast(ra.w, k), kc = bcast(rb.x, k), op = bcast(rb.y, k);
-            const float col0 = bcast(rb.z, k), col1 = bcast(rb.w, k), col2 = bcast(rc, k);
+            const float4 An = s_a[kn], Bn = s_b[kn];
+            const float2 Cn = s_c[kn];
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
             const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
-                const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
-                const float power = gauss_power(ka, kb, kc, dx, dy);
-                const float alpha = fminf(0.99f, op * tile_exp(power));
+                const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
+                const float power = gauss_power(A.z, A.w, B.x, dx, dy);
+                const float alpha = fminf(0.99f, B.y * tile_exp(power));
                 const bool hit = !(power > 0.0f) && alpha >= lim[q];
                 FWD_STAT(2, 1);
                 FWD_STAT(3, __ballot(hit) != 0ull);
@@ -88,15 +102,19 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 const bool sat = hit && test_T < 0.0001f;  // saturating Gaussian is not blended
                 const bool blend = hit && !sat;
                 const float w = blend ? alpha * T[q] : 0.f;
-                C0[q] += col0 * w;
-                C1[q] += col1 * w;
-                C2[q] += col2 * w;
+                C0[q] += B.z * w;
+                C1[q] += B.w * w;
+                C2[q] += Cq.x * w;
                 T[q] = blend ? test_T : T[q];
                 last[q] = blend ? pos1 : last[q];
                 lim[q] = sat ? __builtin_inff() : lim[q];
                 if (__ballot(sat) && !__ballot(lim[q] < 1.f)) live &= ~(1u << q);
             }
-            if (!live) break;
+            if (!live || !more) break;
+            k = kn;
+            A = An;
+            B = Bn;
+            Cq = Cn;
         }
     }
 #ifdef GSR_RENDER_STATS
@@ -129,7 +147,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 // band (b mod 8)'s order (launch_tile_order), so the hardware dispatcher, which deals blocks
 // round-robin over the XCDs and starts them as slots free up, runs a longest-first
 // schedule with each XCD on its own band of the image.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5, 5))) k_render_fwd(RenderFwdArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 6))) k_render_fwd(RenderFwdArgs a) {
     const unsigned ntile = a.grid_x * a.grid_y;
     unsigned lo, len;
     band_of(blockIdx.x & 7u, ntile, lo, len);
