@@ -35,6 +35,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const int HW = a.H * a.W;
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    __shared__ float4 s_a[64], s_b[64], s_c[64];
     // per quadrant pixel state: T, dL/dpix, the background term, and the recurrence of
     // backward.cu:514-537 carried as dot products with dL/dpix (accum_rec . dL/dpix and
     // last_color . dL/dpix) plus last_alpha
@@ -86,16 +87,28 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
+        // records to LDS; survivors are read back with broadcast LDS loads (LDS pipe)
+        // instead of v_readlane (VALU), the next survivor's issued before the current one
+        __syncthreads();
+        s_a[lane] = ra;
+        s_b[lane] = rb;
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
+        __syncthreads();
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
         BWD_STAT(1, __popcll(todo));
-        while (todo) {
-            const int k = __builtin_ctzll(todo);
+        if (!todo) continue;
+        int k = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
+        for (;;) {
+            const bool more = todo != 0ull;
+            const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
-            const uint32_t m = bcast(qm, k);
-            const float ax = bcast(ra.x, k), ay = bcast(ra.y, k);
-            const float ka = bcast(ra.z, k), kb = bcast(ra.w, k), kc = bcast(rb.x, k), op = bcast(rb.y, k);
-            const float c0 = bcast(rb.z, k), c1 = bcast(rb.w, k), c2 = bcast(rc, k);
+            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
+            const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
+            const float c0 = B.z, c1 = B.w, c2 = Cq.x;
             const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
             // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
             // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
@@ -142,7 +155,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 LD[q] = sel(act, cdp, LD[q]);
                 la[q] = sel(act, alpha, la[q]);
             }
-            if (!any) continue;
+            if (any) {
             BWD_STAT(5, 1);
             // conic part of dL/dmean2D (backward.cu:540-545): -(a M1 + b M2), -(b M1 + c M2)
             const float S0 = __builtin_fmaf(ka, M1 + M1, kb * M2);
@@ -158,7 +171,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             Q2 = row_sum(Q2);
             float v = col == 0 ? Q0 : (col == 1 ? Q1 : Q2);
             v *= vop ? op * vscale : vscale;
-            if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)bcast(id, k) * ACC_STRIDE + vidx, v);
+            if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
+            }
+            if (!more) break;
+            k = kn;
+            A = An;
+            B = Bn;
+            Cq = Cn;
         }
     }
 #ifdef GSR_RENDER_STATS
