@@ -116,13 +116,40 @@ CASES = [
     dict(name="sh1_scale_mod", P=2000, W=64, H=64, mode="sh", sh_degree=1, scale_modifier=1.7),
     dict(name="sh2_cov_precomp", P=2000, W=80, H=48, mode="sh", sh_degree=2, cov=True),
     dict(name="dense_small", P=20000, W=64, H=64, mode="colors"),
+    # edge cases: sub-tile image, Gaussians larger than the image, near-threshold and opaque
+    # opacities (early saturation), a cloud half outside the frustum, SH degree 3 + colours
+    dict(name="tiny_7x5", P=400, W=7, H=5, mode="colors"),
+    dict(name="huge_gaussians", P=300, W=96, H=80, mode="colors", mutate="huge"),
+    dict(name="faint_opacity", P=3000, W=80, H=64, mode="colors", mutate="faint"),
+    dict(name="opaque_stack", P=6000, W=64, H=64, mode="sh", sh_degree=1, mutate="opaque"),
+    dict(name="half_outside", P=3000, W=96, H=96, mode="sh", sh_degree=3, mutate="shift"),
 ]
+
+
+def mutate(gs, how):
+    """Edge-case variants of a synthetic cloud (deterministic)."""
+    if how is None:
+        return gs
+    gs = {k: v.clone() for k, v in gs.items()}
+    g = torch.Generator().manual_seed(11)
+    if how == "huge":  # screen radii beyond the image: rects clamp to the grid, R ~ P * T
+        gs["scales"] *= 25.0
+    elif how == "faint":  # opacities straddling 1/255: alpha-threshold decisions everywhere
+        gs["opacities"] = torch.empty_like(gs["opacities"]).uniform_(0.5 / 255, 3.0 / 255, generator=g)
+    elif how == "opaque":  # opaque and large: most pixels saturate (T < 1e-4) early
+        gs["opacities"].fill_(0.99)
+        gs["scales"] *= 3.0
+    elif how == "shift":  # half the cloud left of the frustum, some behind the near plane
+        gs["means3D"][:, 0] -= 0.6 * gs["means3D"][:, 2]
+        gs["means3D"][: gs["means3D"].shape[0] // 10, 2] = 0.1
+    return gs
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_forward_parity(case):
     cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
                         camera=case.get("camera", "identity"))
+    gs = mutate(gs, case.get("mutate"))
     kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), scale_modifier=case.get("scale_modifier", 1.0),
               sh_degree=case.get("sh_degree", 0))
     st = run_gpu(cam, gs, cov=case.get("cov", False), **kw)
@@ -135,6 +162,7 @@ def test_backward_parity(case):
     _, _C, _ = _dgr()
     cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
                         camera=case.get("camera", "identity"))
+    gs = mutate(gs, case.get("mutate"))
     kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), scale_modifier=case.get("scale_modifier", 1.0),
               sh_degree=case.get("sh_degree", 0))
     st = run_gpu(cam, gs, cov=case.get("cov", False), **kw)
