@@ -49,6 +49,19 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "ren
                 "preprocess_bwd": "k_preprocess_bwd"}
 
 
+VALU_NS_PER_INST = 1.16  # wave64 v_fma_f32 issue cost per SIMD at 8 waves/SIMD (tools/micro/pk_fma.hip, vops.hip)
+
+
+def pmc_kernel(stage):
+    """The newest committed rocprofv3 record (profiles/r*_hbm_traffic.json) of the stage's kernel."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
+    if not files:
+        return {}, None
+    d = json.load(open(files[-1]))
+    return d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {}), os.path.relpath(files[-1], ROOT)
+
+
 def pmc_traffic(stage):
     """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC pass
     (profiles/<tag>_hbm_traffic.json, written by tools/profile_summary.py from separate
@@ -187,6 +200,16 @@ def main():
                 "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                 "kernel": dom[0],
                 "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom[1], 4)}
+    kinfo, ksrc = pmc_kernel(dom[0])
+    if kinfo.get("valu_insts"):
+        # the tile passes are VALU-issue-bound: instruction throughput against the measured
+        # wave64 VALU issue rate of the chip
+        n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        peak = n_simd / (VALU_NS_PER_INST * 1e-9) / 1e9
+        ach = kinfo["valu_insts"] / (dom[1] * 1e-3) / 1e9
+        roofline["valu"] = {"insts_per_launch": int(kinfo["valu_insts"]), "achieved_ginst_s": round(ach, 1),
+                            "peak_ginst_s": round(peak, 1), "frac": round(ach / peak, 4), "source": ksrc,
+                            "peak_basis": f"{n_simd} SIMDs x 1 wave64 v_fma_f32 per {VALU_NS_PER_INST} ns"}
     out = {
         "metric": METRIC, "value": round(world * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,

@@ -49,6 +49,7 @@ def main(tag="r01"):
         f.write(open(ks[-1]).read())
     fetch = counters(os.path.join(g, f"prof_{tag}_fetch", "*", "*_counter_collection.csv"))
     write = counters(os.path.join(g, f"prof_{tag}_write", "*", "*_counter_collection.csv"))
+    valu = counters(os.path.join(g, f"prof_{tag}_valu", "*", "*_counter_collection.csv"))
     res = {}
     for r in rows:
         k = short(r["Name"])
@@ -56,9 +57,14 @@ def main(tag="r01"):
         wr = write.get((k, "WRITE_SIZE"))
         fk = statistics.mean(fr) if fr else None
         wk = statistics.mean(wr) if wr else None
+        vi = valu.get((k, "SQ_INSTS_VALU"))
+        si = valu.get((k, "SQ_INSTS_SALU"))
+        wv = valu.get((k, "SQ_WAVES"))
         res[k] = dict(calls=int(r["Calls"]), avg_ms=float(r["AverageNs"]) / 1e6, pct=float(r["Percentage"]),
                       fetch_kib=fk, write_kib=wk,
-                      traffic_bytes=(None if fk is None or wk is None else (2 * fk + wk) * 1024.0))
+                      traffic_bytes=(None if fk is None or wk is None else (2 * fk + wk) * 1024.0),
+                      valu_insts=statistics.mean(vi) if vi else None, salu_insts=statistics.mean(si) if si else None,
+                      waves=statistics.mean(wv) if wv else None)
     bench = None
     log = os.path.join(g, f"prof_{tag}_kt.log")
     if os.path.exists(log):
@@ -73,14 +79,16 @@ def main(tag="r01"):
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary {tag}\n\nbench.py cfg2 (1.5M Gaussians, SH3, 1920x1080) under rocprofv3; "
                 "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch.\n\n")
-        f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s |\n|---|---|---|---|---|---|---|---|\n")
+        f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s | VALU Minst/launch |\n"
+                "|---|---|---|---|---|---|---|---|---|\n")
         for k, v in sorted(res.items(), key=lambda kv: -kv[1]["pct"]):
             tb = v["traffic_bytes"]
             f.write(f"| {k} | {v['calls']} | {v['avg_ms']:.4f} | {v['pct']:.1f} | "
                     f"{'' if v['fetch_kib'] is None else round(v['fetch_kib'])} | "
                     f"{'' if v['write_kib'] is None else round(v['write_kib'])} | "
                     f"{'' if tb is None else round(tb / 1e6, 2)} | "
-                    f"{'' if tb is None else round(tb / (v['avg_ms'] * 1e-3) / 1e9, 1)} |\n")
+                    f"{'' if tb is None else round(tb / (v['avg_ms'] * 1e-3) / 1e9, 1)} | "
+                    f"{'' if v['valu_insts'] is None else round(v['valu_insts'] / 1e6, 2)} |\n")
         if bench:
             f.write(f"\nbench line under the profiler: value {bench['value']} MPix/s, ms/step {bench['ms_per_step']}"
                     f"\n\nstage_ms (HIP events): {json.dumps(bench.get('stage_ms'))}\n")
