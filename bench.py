@@ -110,6 +110,86 @@ def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
                 seconds_estimated_full=est)
 
 
+def bench_relight(args, dev):
+    """cfg3: the relightable render() step -- fused PBR shade of the foreground
+    Gaussians, then render()'s six rasterizer calls over one geometry (main image, diffuse,
+    specular, depth, normal, alpha; gaussian_renderer/__init__.py:160-264) and a training-
+    style loss backward through all of them.  value = views/s with the geometry cache on;
+    the same step with the cache off is reported beside it."""
+    import diff_gaussian_rasterization as dgr
+    import relit_shade
+    from gsr import scenes
+    P_fg = args.P or 1_000_000
+    P = P_fg + P_fg // 10  # + 10 % sky Gaussians
+    cam, gs, c = scenes.build_config("cfg2", device="cpu", seed=0, P=P)
+    W, H = cam.image_width, cam.image_height
+    g = {k: v.to(dev) for k, v in gs.items()}
+    gen = torch.Generator().manual_seed(7)
+    mat = {"albedo": torch.rand(P_fg, 3, generator=gen), "kr": torch.rand(P_fg, 1, generator=gen) * 0.9 + 0.05,
+           "km": torch.rand(P_fg, 1, generator=gen),
+           "normal": torch.nn.functional.normalize(torch.randn(P_fg, 3, generator=gen), dim=1)}
+    mat = {k: v.to(dev) for k, v in mat.items()}
+    base = (torch.randn(25, 3, generator=gen) * 0.3).to(dev)
+    base[0] = 1.0
+    sky_col = torch.rand(P - P_fg, 3, generator=gen).to(dev)
+    vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
+    light = relit_shade.EnvironmentLight(base.clone(), sh_degree=4)
+    zero3 = torch.zeros(3, device=dev)
+    settings = dgr.GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=cam.tanfovx,
+                                                 tanfovy=cam.tanfovy, bg=zero3, scale_modifier=1.0, viewmatrix=vm,
+                                                 projmatrix=pm, sh_degree=-1, campos=cp, prefiltered=False)
+    dweights = [torch.randn(3, H, W, generator=gen).to(dev) for _ in range(6)]
+
+    def step():
+        means3D = g["means3D"].detach().requires_grad_(True)
+        opac = g["opacities"].detach().requires_grad_(True)
+        scales = g["scales"].detach().requires_grad_(True)
+        rots = g["rotations"].detach().requires_grad_(True)
+        albedo = mat["albedo"].detach().requires_grad_(True)
+        kr = mat["kr"].detach().requires_grad_(True)
+        km = mat["km"].detach().requires_grad_(True)
+        light.base = base.detach().clone().requires_grad_(True)
+        means2D = torch.zeros_like(means3D, requires_grad=True)
+        fg = means3D[:P_fg]
+        view_pos = cp.expand(P_fg, 3)
+        rgb, ex = light.shade(fg[None, None], mat["normal"][None, None], albedo[None, None], view_pos[None, None],
+                              kr[None, None], km[None, None])
+        rgb, dif, spe = rgb[0, 0], ex["diffuse"][0, 0], ex["specular"][0, 0]
+        cat = lambda x: torch.cat([x, sky_col], 0)
+        depth = (means3D @ vm[:3, :3] + vm[3, :3])[:, 2:3].expand(P, 3)
+        nrm = cat(0.5 * mat["normal"] + 0.5)
+        colours = [cat(rgb), cat(dif), cat(spe), depth, nrm, torch.ones(P, 3, device=dev)]
+        rast = dgr.GaussianRasterizer(settings)
+        loss = 0.0
+        for col, w in zip(colours, dweights):
+            img, _ = rast(means3D=means3D, means2D=means2D, opacities=opac, colors_precomp=col, scales=scales,
+                          rotations=rots)
+            loss = loss + (img * w).sum()
+        loss.backward()
+
+    res = {}
+    for cached in (True, False):
+        dgr.geometry_cache(cached)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        res[cached] = (time.perf_counter() - t0) * 1e3 / args.steps
+    dgr.geometry_cache(True)
+    ms = res[True]
+    print(json.dumps({
+        "metric": "relit render() views/s (shade + 6 rasterizer calls + backward)", "value": round(1e3 / ms, 3),
+        "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"cfg3: {P_fg} foreground + {P - P_fg} sky Gaussians, {W}x{H}, env SH deg 4",
+                   "gaussians": P, "width": W, "height": H},
+        "geometry_cache": {"on_ms": round(res[True], 4), "off_ms": round(res[False], 4),
+                           "speedup": round(res[False] / res[True], 3)}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -131,6 +211,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if args.config == "cfg3":
+        bench_relight(args, dev)
+        return
 
     from diff_gaussian_rasterization import _C
     from gsr import _lib, scenes

@@ -54,6 +54,21 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
                 float tan_fovx, float tan_fovy, int prefiltered, float* out_color, int* radii, void* stream,
                 int* num_rendered);
 
+/* Forward rasterization of NEW colours over the geometry of an earlier gsr_forward call
+ * (the reference's render() rasterizes the same Gaussians 6-10 times per view with
+ * different colors_precomp, gaussian_renderer/__init__.py:160-264).  src_geom_buffer,
+ * binning_buffer and image_buffer are that call's buffers, src_radii its radii; every
+ * input that shapes the geometry (means, scales, rotations, cov3D, opacities, matrices,
+ * image size, scale_modifier) must be unchanged -- the caller owns that check.  Writes a new
+ * geometry buffer (colours replaced in the render records; the binning and image buffers
+ * are shared, read-only except for identical re-writes of final_T / n_contrib),
+ * out_color [3,H,W] and radii [P].  Output equals a full gsr_forward call bit for bit.
+ * The returned geometry buffer pairs with the shared binning/image buffers in gsr_backward. */
+int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const void* src_geom_buffer,
+                      const int* src_radii, void* binning_buffer, void* image_buffer, int P, int R,
+                      const float* background, int width, int height, const float* colors_precomp, float* out_color,
+                      int* radii, void* stream);
+
 /* Backward rasterization.  geom/binning/img buffers are the ones the forward filled.
  * dL_dpix is [3,H,W].  All nine gradient outputs are fully written (no zero-fill needed):
  * dL_dmean2D [P,3] (z = 0), dL_dconic [P,2,2], dL_dopacity [P], dL_dcolor [P,3],

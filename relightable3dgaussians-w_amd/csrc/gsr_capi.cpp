@@ -405,6 +405,47 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     return GSR_OK;
 }
 
+int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const void* src_geom_buffer,
+                      const int* src_radii, void* binning_buffer, void* image_buffer, int P, int R,
+                      const float* background, int width, int height, const float* colors_precomp, float* out_color,
+                      int* radii, void* stream_) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    if (P < 0 || R < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_forward_reuse: bad sizes");
+    if (!geometry_buffer || !src_geom_buffer || !src_radii || !image_buffer || !colors_precomp || !radii ||
+        (R > 0 && !binning_buffer))
+        return fail(GSR_E_ARG, "gsr_forward_reuse: missing buffers");
+    if (P == 0) return GSR_OK;
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(width, height);
+    const BinLayout bl = bin_layout(R, 0, width, height);
+    char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
+    if (!geom) return fail(GSR_E_ALLOC, "gsr_forward_reuse: buffer allocation failed");
+    geom = align_base(geom);
+    const char* src = align_base(const_cast<void*>(src_geom_buffer));
+    char* img = align_base(image_buffer);
+    char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
+    {
+        GSR_STAGE(ST_PREPROCESS);
+        gsr::launch_recolor(P, src_radii, reinterpret_cast<const gsr::Rec*>(src + gl.rec), colors_precomp,
+                            at<gsr::Rec>(geom, gl.rec), radii, s);
+    }
+    GSR_LAUNCH_CHECK();
+    const unsigned gx = tiles_x(width), gy = tiles_y(height);
+    gsr::RenderFwdArgs ra;  // with R == 0 every range is empty: background everywhere
+    ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
+    ra.ranges = at<uint2>(img, il.ranges); ra.point_list = bin ? at<uint32_t>(bin, bl.point) : nullptr;
+    ra.rec = at<gsr::Rec>(geom, gl.rec); ra.bg = background;
+    ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
+    ra.order = at<uint32_t>(img, il.order_fwd);
+    ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
+    {
+        GSR_STAGE(ST_RENDER_FWD);
+        gsr::launch_render_fwd(ra, s);  // the cached call's dispatch order is still valid
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
                  const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
                  const float* rotations, const float* cov3D_precomp, const float* viewmatrix,

@@ -38,6 +38,8 @@ struct PreprocessArgs {
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s);
+void launch_recolor(int P, const int* radii_src, const Rec* src, const float* colors, Rec* dst, int* radii_out,
+                    hipStream_t s);
 
 // ---- scans (gsr_scan.hip) -----------------------------------------------------------
 constexpr int SCAN_THREADS = 256;

@@ -82,6 +82,29 @@ __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3
     present[idx] = !(xform_point4x3(p, viewmatrix).z <= 0.2f);
 }
 
+// Same geometry, new colours (the geometry cache across a render()'s rasterizer calls):
+// copy each visible Gaussian's record with its colour replaced, and the radii.
+__global__ void __launch_bounds__(256) k_recolor(int P, const int* radii_src, const Rec* src, const float* colors,
+                                                  Rec* dst, int* radii_out) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const int r = radii_src[idx];
+    radii_out[idx] = r;
+    if (r > 0) {
+        Rec v = src[idx];
+        v.b.z = colors[3 * idx];
+        v.b.w = colors[3 * idx + 1];
+        v.c.x = colors[3 * idx + 2];
+        dst[idx] = v;
+    }
+}
+
+void launch_recolor(int P, const int* radii_src, const Rec* src, const float* colors, Rec* dst, int* radii_out,
+                    hipStream_t s) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_recolor, dim3((P + 255) / 256), dim3(256), 0, s, P, radii_src, src, colors, dst, radii_out);
+}
+
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, s, a);

@@ -61,6 +61,35 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return int(nr.value), out_color, radii, bs.bufs[0], bs.bufs[1], bs.bufs[2]
 
 
+def _rasterize_reuse(background, colors, image_height, image_width, src_geom, src_radii, R, binningBuffer,
+                     imageBuffer):
+    """Colours-only forward over the geometry of an earlier rasterize_gaussians call
+    (gsr_forward_reuse): same outputs as a full call whose geometry inputs are unchanged.
+    Returns (num_rendered, color, radii, geomBuffer, binningBuffer, imageBuffer); the binning
+    and image buffers are the earlier call's (shared, read-only)."""
+    _lib.require_gpu_tensor(colors, "colors_precomp")
+    dev = colors.device
+    P, H, W = src_radii.size(0), int(image_height), int(image_width)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    out_color = torch.empty((NUM_CHANNELS, H, W), dtype=torch.float32, device=dev)
+    bs = _lib.BufferSet(dev)
+    if P == 0:
+        out_color.zero_()
+        return 0, out_color, radii, bs.bufs[0], binningBuffer, imageBuffer
+    bg_, col_ = _f32(background), _f32(colors)
+    rc = _lib.ResizeContexts(bs)
+    ptr = lambda t: t.data_ptr() if t.numel() else None
+    try:
+        ret = _lib.lib().gsr_forward_reuse(_lib.RESIZE, rc.ctx[0], src_geom.data_ptr(), src_radii.data_ptr(),
+                                           ptr(binningBuffer), imageBuffer.data_ptr(), P, int(R), _lib.fptr(bg_), W, H,
+                                           _lib.fptr(col_), out_color.data_ptr(), radii.data_ptr(),
+                                           _lib.stream_of(dev))
+    finally:
+        rc.close()
+    _lib.check(ret, "rasterize_gaussians (geometry reuse)")
+    return int(R), out_color, radii, bs.bufs[0], binningBuffer, imageBuffer
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
                                  campos, geomBuffer, R, binningBuffer, imageBuffer):

@@ -6,6 +6,7 @@ so gaussian_renderer/__init__.py:15 `from diff_gaussian_rasterization import
 GaussianRasterizationSettings, GaussianRasterizer` and everything built on it run
 unchanged.  The extension module `_C` is backed by libgsr.so (hand-written gfx950 HIP).
 """
+import os
 from typing import NamedTuple
 
 import torch
@@ -13,7 +14,57 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians",
+           "geometry_cache"]
+
+
+class _GeometryCache:
+    """Geometry reuse across rasterizer calls that differ only in colours.
+
+    render() (gaussian_renderer/__init__.py:160-264) rasterizes the same Gaussians 6-10 times
+    per view -- the main image, diffuse/specular/depth/normal extras and the alpha mask --
+    with different colors_precomp and background.  Preprocess, depth sort, binning and the
+    tile ranges depend only on the geometry, so a call whose geometry inputs are the same
+    tensors, unmodified (data pointer, version counter, shape, strides), with the same camera
+    and image settings, re-renders colours over the previous call's binning
+    (gsr_forward_reuse).  The outputs are bit-identical to a full call.  The cache holds
+    references to the keyed tensors, so their memory cannot be recycled into a false hit
+    while it lives.  Only the colors_precomp path is cached (SH colours depend on campos).
+    Disable with GSR_GEOMETRY_CACHE=0 or geometry_cache(False)."""
+
+    def __init__(self):
+        self.enabled = os.environ.get("GSR_GEOMETRY_CACHE", "1") != "0"
+        self.clear()
+
+    def clear(self):
+        self.key = None
+        self.refs = None
+        self.entry = None
+        self.hits = 0
+        self.misses = 0
+
+    @staticmethod
+    def _tkey(t):
+        if t is None or t.numel() == 0:
+            return None
+        return (t.data_ptr(), t._version, tuple(t.shape), t.stride(), t.dtype, str(t.device))
+
+    def key_of(self, s, means3D, opacities, scales, rotations, cov3Ds_precomp):
+        tensors = (means3D, opacities, scales, rotations, cov3Ds_precomp, s.viewmatrix, s.projmatrix)
+        return (tuple(self._tkey(t) for t in tensors),
+                (int(s.image_height), int(s.image_width), float(s.tanfovx), float(s.tanfovy),
+                 float(s.scale_modifier), bool(s.prefiltered))), tensors
+
+
+_geometry_cache = _GeometryCache()
+
+
+def geometry_cache(enabled=None):
+    """Query or switch the geometry cache; returns the cache (hits/misses counters)."""
+    if enabled is not None:
+        _geometry_cache.enabled = bool(enabled)
+        _geometry_cache.clear()
+    return _geometry_cache
 
 
 class GaussianRasterizationSettings(NamedTuple):
@@ -53,9 +104,24 @@ class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                 raster_settings):
-        num_rendered, color, radii, geom_buf, bin_buf, img_buf = _C.rasterize_gaussians(
-            *_forward_args(raster_settings, means3D, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
-                           sh))
+        cache = _geometry_cache
+        key = None
+        if cache.enabled and colors_precomp.numel() != 0 and sh.numel() == 0 and means3D.is_cuda:
+            key, refs = cache.key_of(raster_settings, means3D, opacities, scales, rotations, cov3Ds_precomp)
+        if key is not None and key == cache.key:
+            cache.hits += 1
+            R0, radii0, geom0, bin0, img0 = cache.entry
+            num_rendered, color, radii, geom_buf, bin_buf, img_buf = _C._rasterize_reuse(
+                raster_settings.bg, colors_precomp, raster_settings.image_height, raster_settings.image_width, geom0,
+                radii0, R0, bin0, img0)
+        else:
+            num_rendered, color, radii, geom_buf, bin_buf, img_buf = _C.rasterize_gaussians(
+                *_forward_args(raster_settings, means3D, colors_precomp, opacities, scales, rotations,
+                               cov3Ds_precomp, sh))
+            if key is not None:
+                cache.misses += 1
+                cache.key, cache.refs = key, refs
+                cache.entry = (num_rendered, radii, geom_buf, bin_buf, img_buf)
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh, geom_buf,

@@ -38,6 +38,7 @@ def _declare(lib):
     lib.gsr_backward.argtypes = [i, i, i, i, vp, i, i, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp, vp, vp,
                                  vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    lib.gsr_forward_reuse.argtypes = [RESIZE_FN, vp, vp, vp, vp, vp, i, i, vp, i, i, vp, vp, vp, vp]
     lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
     lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                        vp, vp, vp]
@@ -51,7 +52,8 @@ def _declare(lib):
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_last_error.restype = C.c_char_p
     lib.gsr_version.restype = C.c_char_p
-    for fn in ("gsr_forward", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward", "gsr_shade_backward",
+    for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
+               "gsr_shade_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 
