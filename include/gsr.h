@@ -14,6 +14,9 @@
  *                      (dgr/rasterize_points.cu:194-213)
  *   gsr_shade_forward  scene/NVDIFFREC/light.py:131-193 EnvironmentLight.shade (forward)
  *   gsr_shade_backward autograd backward of the same (PyTorch + nvdiffrast in the reference)
+ *   gsr_forward_reuse  colours-only re-render over an earlier call's geometry (the 6-10
+ *                      same-geometry calls of gaussian_renderer/__init__.py:160-264)
+ *   gsr_knn_mean_dist  submodules/simple-knn/spatial.cu:14-26 distCUDA2
  *
  * Error convention: every function returns 0 on success and a negative GSR_E* code on
  * failure; gsr_last_error() returns a thread-local message.  The reference's conditions
@@ -105,6 +108,13 @@ int gsr_shade_backward(int N, int deg, const float* pos, const float* normal, co
                        const float* fg_lut, int specular, const float* g_rgb, const float* g_diffuse,
                        const float* g_specular, float* d_pos, float* d_normal, float* d_albedo, float* d_view_pos,
                        float* d_kr, float* d_km, float* d_base, void* workspace, void* stream);
+
+/* Mean squared distance to the 3 nearest other points, for P points [P,3] (simple-knn's
+ * distCUDA2, submodules/simple-knn/spatial.cu:14-26 -> simple_knn.cu:185-220, used by
+ * gaussian_model.py:189,249).  Same Morton/box algorithm and arithmetic, bit-identical
+ * output.  `workspace`: gsr_knn_workspace_bytes(P) bytes of device memory. */
+size_t gsr_knn_workspace_bytes(int P);
+int gsr_knn_mean_dist(int P, const float* points, float* mean_dists, void* workspace, void* stream);
 
 /* Private-buffer introspection for tests and profiling: byte offsets of the arrays the
  * forward leaves in its three buffers (layout is private between forward and backward). */

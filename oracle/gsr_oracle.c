@@ -1067,3 +1067,95 @@ void orc_shade_bwd(int N, int deg, const REAL* pos, const REAL* nrm, const REAL*
     for (int k = 0; k < K * 3; k++) d_base[k] = (REAL)db[k];
     free(db);
 }
+
+/* ---------------- simple-knn distCUDA2 (submodules/simple-knn/simple_knn.cu:119-220) --------
+ * Sequential restatement of SimpleKNN::knn: bounds seeded with 0 (cub Reduce init, :190-200),
+ * 10-bit Morton codes (:53-71), stable sort by code, 1024-point boxes (:79-113), +-3
+ * neighbour rejection bound and the box scan in index order (:144-181).  Float arithmetic
+ * only; sums of squares as fma(z, z, fma(y, y, x * x)) -- the contraction nvcc applies to
+ * `x*x + y*y + z*z` (parity w.r.t. nvcc's contraction choice is unpinned).  Test
+ * infrastructure only. */
+#define KNN_BOX 1024
+static float knn_sq3(float x, float y, float z) { return fmaf(z, z, fmaf(y, y, x * x)); }
+static uint32_t knn_prep(uint32_t x) {
+    x = (x | (x << 16)) & 0x030000FFu;
+    x = (x | (x << 8)) & 0x0300F00Fu;
+    x = (x | (x << 4)) & 0x030C30C3u;
+    x = (x | (x << 2)) & 0x09249249u;
+    return x;
+}
+static uint32_t knn_f2u(float f) {
+    if (!(f > 0.f)) return 0u;
+    if (f >= 4294967296.f) return 0xFFFFFFFFu;
+    return (uint32_t)f;
+}
+static float knn_box_dist(const float* mn, const float* mx, const float* p) {
+    float d[3] = {0.f, 0.f, 0.f};
+    for (int k = 0; k < 3; k++)
+        if (p[k] < mn[k] || p[k] > mx[k]) d[k] = fminf(fabsf(p[k] - mn[k]), fabsf(p[k] - mx[k]));
+    return knn_sq3(d[0], d[1], d[2]);
+}
+static void knn_update(const float* ref, const float* p, float* best) {
+    float d = knn_sq3(p[0] - ref[0], p[1] - ref[1], p[2] - ref[2]);
+    for (int j = 0; j < 3; j++)
+        if (best[j] > d) {
+            float t = best[j];
+            best[j] = d;
+            d = t;
+        }
+}
+void orc_knn(int P, const float* pts, float* dists) {
+    if (P <= 0) return;
+    float mn[3] = {0.f, 0.f, 0.f}, mx[3] = {0.f, 0.f, 0.f};
+    for (int i = 0; i < P; i++)
+        for (int k = 0; k < 3; k++) {
+            mn[k] = fminf(mn[k], pts[3 * i + k]);
+            mx[k] = fmaxf(mx[k], pts[3 * i + k]);
+        }
+    uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * P);
+    uint32_t* ids = (uint32_t*)malloc(sizeof(uint32_t) * P);
+    for (int i = 0; i < P; i++) {
+        uint32_t c[3];
+        for (int k = 0; k < 3; k++) c[k] = knn_prep(knn_f2u(((pts[3 * i + k] - mn[k]) / (mx[k] - mn[k])) * 1023.f));
+        keys[i] = c[0] | (c[1] << 1) | (c[2] << 2);
+        ids[i] = (uint32_t)i;
+    }
+    radix_sort_pairs(keys, ids, P, 30);
+    float* sp = (float*)malloc(sizeof(float) * 3 * P);
+    for (int i = 0; i < P; i++)
+        for (int k = 0; k < 3; k++) sp[3 * i + k] = pts[3 * ids[i] + k];
+    const int nbox = (P + KNN_BOX - 1) / KNN_BOX;
+    float* bmn = (float*)malloc(sizeof(float) * 3 * nbox);
+    float* bmx = (float*)malloc(sizeof(float) * 3 * nbox);
+    for (int b = 0; b < nbox; b++) {
+        for (int k = 0; k < 3; k++) {
+            bmn[3 * b + k] = 3.402823466e+38f;
+            bmx[3 * b + k] = -3.402823466e+38f;
+        }
+        for (int i = b * KNN_BOX; i < P && i < (b + 1) * KNN_BOX; i++)
+            for (int k = 0; k < 3; k++) {
+                bmn[3 * b + k] = fminf(bmn[3 * b + k], sp[3 * i + k]);
+                bmx[3 * b + k] = fmaxf(bmx[3 * b + k], sp[3 * i + k]);
+            }
+    }
+    for (int idx = 0; idx < P; idx++) {
+        const float* point = sp + 3 * idx;
+        float best[3] = {3.402823466e+38f, 3.402823466e+38f, 3.402823466e+38f};
+        for (int i = (idx - 3 > 0 ? idx - 3 : 0); i <= (P - 1 < idx + 3 ? P - 1 : idx + 3); i++)
+            if (i != idx) knn_update(point, sp + 3 * i, best);
+        const float reject = best[2];
+        best[0] = best[1] = best[2] = 3.402823466e+38f;
+        for (int b = 0; b < nbox; b++) {
+            const float dist = knn_box_dist(bmn + 3 * b, bmx + 3 * b, point);
+            if (dist > reject || dist > best[2]) continue;
+            for (int i = b * KNN_BOX; i < P && i < (b + 1) * KNN_BOX; i++)
+                if (i != idx) knn_update(point, sp + 3 * i, best);
+        }
+        dists[ids[idx]] = (best[0] + best[1] + best[2]) / 3.0f;
+    }
+    free(keys);
+    free(ids);
+    free(sp);
+    free(bmn);
+    free(bmx);
+}

@@ -249,3 +249,13 @@ def shade_bwd(pos, nrm, albedo, view_pos, kr, km, base, lut, g_rgb, g_diff, g_sp
                             C.c_int(int(specular)), *[_p(x) for x in gs], _p(d["pos"]), _p(d["normal"]),
                             _p(d["albedo"]), _p(d["view_pos"]), _p(d["kr"]), _p(d["km"]), _p(d["base"]))
     return d
+
+
+def knn(points):
+    """submodules/simple-knn distCUDA2: mean squared distance to the 3 nearest other points
+    (orc_knn, the reference's Morton/box algorithm, float arithmetic)."""
+    L = _lib(False)
+    pts = _arr(points, np.float32).reshape(-1, 3)
+    out = np.zeros(pts.shape[0], np.float32)
+    L.orc_knn(C.c_int(pts.shape[0]), _p(pts), _p(out))
+    return out

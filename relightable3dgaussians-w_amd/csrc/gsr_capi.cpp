@@ -523,6 +523,17 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return GSR_OK;
 }
 
+size_t gsr_knn_workspace_bytes(int P) { return gsr::knn_workspace_bytes(P); }
+
+int gsr_knn_mean_dist(int P, const float* points, float* mean_dists, void* workspace, void* stream_) {
+    if (P < 0) return fail(GSR_E_ARG, "gsr_knn_mean_dist: bad P");
+    if (P == 0) return GSR_OK;
+    if (!points || !mean_dists || !workspace) return fail(GSR_E_ARG, "gsr_knn_mean_dist: missing buffers");
+    gsr::launch_knn(P, points, mean_dists, workspace, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 size_t gsr_shade_workspace_bytes(int N, int deg) { return gsr::shade_workspace_bytes(N, deg); }
 
 int gsr_shade_forward(int N, int deg, const float* pos, const float* normal, const float* albedo,

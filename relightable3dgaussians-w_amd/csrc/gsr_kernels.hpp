@@ -155,4 +155,8 @@ struct PreprocessBwdArgs {
 };
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 
+// ---- 3-nearest-neighbour mean distance (gsr_knn.hip) ------------------------------------
+size_t knn_workspace_bytes(int P);
+void launch_knn(int P, const float* pts, float* dists, void* ws, hipStream_t s);
+
 }  // namespace gsr

@@ -38,6 +38,9 @@ def _declare(lib):
     lib.gsr_backward.argtypes = [i, i, i, i, vp, i, i, vp, vp, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp, vp, vp,
                                  vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.gsr_mark_visible.argtypes = [i, vp, vp, vp, vp, vp]
+    lib.gsr_knn_workspace_bytes.argtypes = [i]
+    lib.gsr_knn_workspace_bytes.restype = sz
+    lib.gsr_knn_mean_dist.argtypes = [i, vp, vp, vp, vp]
     lib.gsr_forward_reuse.argtypes = [RESIZE_FN, vp, vp, vp, vp, vp, i, i, vp, i, i, vp, vp, vp, vp]
     lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
     lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -52,7 +55,7 @@ def _declare(lib):
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_last_error.restype = C.c_char_p
     lib.gsr_version.restype = C.c_char_p
-    for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
+    for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
                "gsr_shade_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
