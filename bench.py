@@ -199,6 +199,9 @@ def main():
     ap.add_argument("--P", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-tiles", type=int, default=64)
+    ap.add_argument("--ply", default=None, help="a trained scene (GaussianModel.save_ply layout) instead of cfg2's "
+                                               "synthetic cloud; camera looks at the foreground's median from "
+                                               "2x its extent, 1920x1080, focal 1400")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -219,7 +222,10 @@ def main():
     from gsr import _lib, scenes
     from gsr import dp as gdp
 
-    cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
+    if args.ply:
+        cam, gs_cpu, cfg = scenes.ply_config(args.ply)
+    else:
+        cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
     W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
     P = gs_cpu["means3D"].shape[0]
     g = {k: v.to(dev) for k, v in gs_cpu.items()}

@@ -59,7 +59,7 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, nheavy, total;
 };
 struct BinLayout {
     size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_ranges, tile_cnt, tile_start, scan_tmp,
@@ -102,6 +102,7 @@ ImgLayout img_layout(int W, int H) {
     L.tile_nmax = c.take(4 * T);
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
+    L.nheavy = c.take(4 * 16);  // forward [0..8), backward [8..16)
     L.total = c.o + 256;
     return L;
 }
@@ -394,10 +395,13 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     ra.ranges = ranges; ra.point_list = point_list; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
+    ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     {
         GSR_STAGE(ST_RENDER_FWD);
-        gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), s);
+        gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), at<uint32_t>(img, il.nheavy),
+                               gsr::FWD_HEAVY_BITS, s);
+        HIP_OK(hipMemsetAsync(ra.tile_nmax, 0, 4 * (size_t)T, s));
         gsr::launch_render_fwd(ra, s);
     }
     GSR_LAUNCH_CHECK();
@@ -437,7 +441,8 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.rec = at<gsr::Rec>(geom, gl.rec); ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
-    ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
+    ra.nheavy = at<uint32_t>(img, il.nheavy);
+    ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     {
         GSR_STAGE(ST_RENDER_FWD);
         gsr::launch_render_fwd(ra, s);  // the cached call's dispatch order is still valid
@@ -486,10 +491,11 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
         ra.dL_dpix = dL_dpix;
         ra.acc = acc;
         ra.order = at<uint32_t>(img, il.order_bwd);
+        ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         {
             GSR_STAGE(ST_RENDER_BWD);
             gsr::launch_tile_order(gx * gy, ra.ranges, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
-                                   s);
+                                   at<uint32_t>(img, il.nheavy) + 8, gsr::BWD_HEAVY_BITS, s);
             gsr::launch_render_bwd(ra, s);
         }
         GSR_LAUNCH_CHECK();

@@ -93,8 +93,12 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of
-// the tile's list length when cost is null).
-void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, hipStream_t s);
+// the tile's list length when cost is null); nheavy[8]: per band, the leading tiles with
+// cost >= 2^heavy_bits.
+void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
+                       int heavy_bits, hipStream_t s);
+constexpr int FWD_HEAVY_BITS = 13;  // list length >= 8192
+constexpr int BWD_HEAVY_BITS = 11;  // largest n_contrib >= 2048
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 struct RenderFwdArgs {
@@ -108,7 +112,8 @@ struct RenderFwdArgs {
     float* final_T;
     uint32_t* n_contrib;
     const uint32_t* order;  // dispatch order (launch_tile_order)
-    uint32_t* tile_nmax;    // out: per tile, the largest n_contrib (the backward's cost)
+    const uint32_t* nheavy;
+    uint32_t* tile_nmax;    // out (atomicMax; zeroed by the caller)    // out: per tile, the largest n_contrib (the backward's cost)
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -125,6 +130,7 @@ struct RenderBwdArgs {
     const float* dL_dpix;
     float* acc;  // [P][ACC_STRIDE]
     const uint32_t* order;  // dispatch order (launch_tile_order)
+    const uint32_t* nheavy;
 };
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 

@@ -27,7 +27,7 @@ __device__ unsigned long long g_bwd_times[3 * 65536];  // per tile: start, end (
 #define BWD_STAT(k, v)
 #endif
 
-__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile) {
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -55,7 +55,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         // -T_final * bg . dL/dpix, the background term of dL/dalpha (backward.cu:533-537)
         Tb[q] = -Tf * (a.bg[0] * dp0[q] + a.bg[1] * dp1[q] + a.bg[2] * dp2[q]);
         AD[q] = LD[q] = la[q] = 0.f;
-        qlim[q] = wave_max_u32(last[q]);
+        qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;  // other quadrants: another wave
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
     // Reduction layout (see the end of the loop): lane 16 r + j, j < 2, ends up holding
@@ -89,11 +89,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         }
         // records to LDS; survivors are read back with broadcast LDS loads (LDS pipe)
         // instead of v_readlane (VALU), the next survivor's issued before the current one
-        __syncthreads();
+        wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
-        __syncthreads();
+        wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
         BWD_STAT(1, __popcll(todo));
@@ -194,18 +194,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 }
 
 
-// One workgroup per tile, dispatched heaviest-first: block b takes position b / 8 of XCD
-// band (b mod 8)'s order (launch_tile_order), so the hardware dispatcher, which deals blocks
-// round-robin over the XCDs and starts them as slots free up, runs a longest-first
-// schedule with each XCD on its own band of the image.
+// One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
+// whole tile.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {
-    const unsigned ntile = a.grid_x * a.grid_y;
-    unsigned lo, len;
-    band_of(blockIdx.x & 7u, ntile, lo, len);
-    const unsigned b = blockIdx.x >> 3;
-    // blocks past a short band's end (bands differ by at most one tile) take the remainder
-    const unsigned tile = b < len ? a.order[lo + b] : xcd_remap(blockIdx.x, ntile);
-    render_bwd_tile(a, tile);
+    unsigned tile;
+    uint32_t qallow;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_bwd_tile(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -225,7 +220,8 @@ extern "C" int gsr_debug_bwd_stats(unsigned long long* out, int reset) {
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(ntile), dim3(64), 0, s, a);
+    // one block per unit of the longest band (heavy tiles count four); the rest exit
+    hipLaunchKernelGGL(k_render_bwd, dim3(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP)), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

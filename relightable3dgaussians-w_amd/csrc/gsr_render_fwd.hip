@@ -25,7 +25,7 @@ __device__ unsigned long long g_fwd_stats[8];
 #define FWD_STAT(k, v)
 #endif
 
-__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile) {
+__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -46,7 +46,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         last[q] = 0;
         const bool in = wt.inside(q, a.W, a.H);
         lim[q] = in ? 1.0f / 255.0f : __builtin_inff();
-        if (__ballot(in)) live |= 1u << q;
+        if (((qallow >> q) & 1u) && __ballot(in)) live |= 1u << q;
     }
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
@@ -67,11 +67,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         // the batch's records go to LDS; the walk below reads each survivor's record with
         // broadcast LDS loads (LDS pipe) instead of 11 v_readlane (VALU), the next
         // survivor's loads issued before the current one is blended
-        __syncthreads();
+        wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_c[lane] = make_float2(rc, __uint_as_float(qm));
-        __syncthreads();
+        wave_lds_sync();
         uint64_t todo = __ballot((qm & live) != 0);
         FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
         FWD_STAT(1, __popcll(todo));
@@ -124,7 +124,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     const int HW = a.H * a.W;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        if (wt.inside(q, a.W, a.H)) {
+        if (((qallow >> q) & 1u) && wt.inside(q, a.W, a.H)) {
             const int pix = wt.pixel(q, a.W);
             a.final_T[pix] = T[q];
             a.n_contrib[pix] = last[q];
@@ -136,25 +136,20 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     uint32_t nm = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        const uint32_t m = wave_max_u32(last[q]);
+        const uint32_t m = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nm = m > nm ? m : nm;
     }
-    if (lane == 0) a.tile_nmax[tile] = nm;
+    if (lane == 0) atomicMax(&a.tile_nmax[tile], nm);
 }
 
 
-// One workgroup per tile, dispatched heaviest-first: block b takes position b / 8 of XCD
-// band (b mod 8)'s order (launch_tile_order), so the hardware dispatcher, which deals blocks
-// round-robin over the XCDs and starts them as slots free up, runs a longest-first
-// schedule with each XCD on its own band of the image.
+// One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
+// whole tile.
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 6))) k_render_fwd(RenderFwdArgs a) {
-    const unsigned ntile = a.grid_x * a.grid_y;
-    unsigned lo, len;
-    band_of(blockIdx.x & 7u, ntile, lo, len);
-    const unsigned b = blockIdx.x >> 3;
-    // blocks past a short band's end (bands differ by at most one tile) take the remainder
-    const unsigned tile = b < len ? a.order[lo + b] : xcd_remap(blockIdx.x, ntile);
-    render_fwd_tile(a, tile);
+    unsigned tile;
+    uint32_t qallow;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_fwd_tile(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -171,7 +166,8 @@ extern "C" int gsr_debug_fwd_stats(unsigned long long* out, int reset) {
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(ntile), dim3(64), 0, s, a);
+    // one block per unit of the longest band (heavy tiles count four); the rest exit
+    hipLaunchKernelGGL(k_render_fwd, dim3(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP)), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

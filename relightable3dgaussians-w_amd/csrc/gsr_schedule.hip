@@ -4,7 +4,10 @@
 // (list length, early saturation).  Each XCD band of the image (the bands of xcd_remap:
 // neighbouring tiles share Gaussian records in that XCD's L2) is ordered heaviest-first by
 // a log2 bucketing of a cost estimate; the passes dispatch block b on position b / 8 of band
-// b mod 8, so the hardware dispatcher runs a longest-first schedule per XCD.
+// b mod 8, so the hardware dispatcher runs a longest-first schedule per XCD.  Tiles above a
+// cost threshold (lists in the thousands: dense centres of real scenes) are split over the
+// four waves of their workgroup, one 8x8 quadrant each; the rest run four to a workgroup,
+// one wave each (TileUnit in gsr_tile.hpp).
 // (A persistent variant pulling tiles from per-XCD atomic queues measured 2x slower: the
 // returning atomics cost ~13 us per pull under load.)
 #include "gsr_kernels.hpp"
@@ -12,9 +15,10 @@
 
 namespace gsr {
 
-// One workgroup per band: order[lo .. lo+len) = the band's tiles, cost buckets descending.
+// One workgroup per band: order[lo .. lo+len) = the band's tiles, cost buckets descending;
+// nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4 ways).
 __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost,
-                                                      uint32_t* order) {
+                                                      uint32_t* order, uint32_t* nheavy, int heavy_bits) {
     __shared__ uint32_t hist[33];
     __shared__ uint32_t cur[33];
     unsigned lo, len;
@@ -28,11 +32,13 @@ __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t run = 0;
+        uint32_t run = 0, heavy = 0;
         for (int b = 32; b >= 0; b--) {  // heaviest bucket first
             cur[b] = run;
             run += hist[b];
+            if (b > heavy_bits) heavy += hist[b];  // cost >= 2^heavy_bits
         }
+        nheavy[blockIdx.x] = heavy;
     }
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
@@ -46,9 +52,10 @@ __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2
     }
 }
 
-void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, hipStream_t s) {
+void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
+                       int heavy_bits, hipStream_t s) {
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, ntile, ranges, cost, order);
+    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, ntile, ranges, cost, order, nheavy, heavy_bits);
 }
 
 }  // namespace gsr

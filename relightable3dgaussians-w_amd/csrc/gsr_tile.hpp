@@ -19,6 +19,38 @@ __device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, un
     len = q + (x < r ? 1u : 0u);
 }
 
+// Work unit of a one-wave workgroup of the tile passes: block b serves unit b / 8 of XCD
+// band b mod 8.  The band's first min(nheavy, HEAVY_CAP) tiles (heaviest first) are split
+// into four units, one per 8x8 quadrant; every other tile is one unit.  Sets tile and the
+// quadrant mask; false when the block has nothing to do.  (Four-wave workgroups holding a
+// heavy tile's quadrants measured slower on balanced scenes: a workgroup waits for four
+// free wave slots on one CU, so single waves cannot backfill.)
+constexpr unsigned HEAVY_CAP = 64;  // split tiles per band
+__device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
+                                          unsigned& tile, uint32_t& qallow) {
+    const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
+    unsigned lo, len;
+    band_of(band, ntile, lo, len);
+    const unsigned h = min(nheavy[band], HEAVY_CAP);
+    unsigned pos;
+    if (u < 4u * h) {
+        pos = u >> 2;
+        qallow = 1u << (u & 3u);
+    } else {
+        pos = h + (u - 4u * h);
+        qallow = 15u;
+    }
+    if (pos >= len) return false;
+    tile = order[lo + pos];
+    return true;
+}
+// LDS ordering within one wave (the tile passes' waves share no LDS)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // exp as the tile loops evaluate it, identical in forward and backward so that the
 // backward replays exactly the forward's blend decisions (v_exp_f32 on x*log2(e)).
 __device__ __forceinline__ float tile_exp(float x) { return __expf(x); }

@@ -178,3 +178,55 @@ def build_config(name, device="cpu", seed=0, P=None, W=None, H=None):
     gs = synthetic_gaussians(c["P"], c["W"], c["H"], cam.tanfovx, cam.tanfovy, c["sh_degree"], seed=seed,
                              zrange=c["zrange"], log_z=c["log_z"], scale_mode=c["scale_mode"], device=device)
     return cam, gs, c
+
+
+def load_ply_gaussians(path, device="cpu"):
+    """A trained scene saved by GaussianModel.save_ply (scene/gaussian_model.py:296-355) as
+    rasterizer inputs, with the model's activations (gaussian_model.py:54-70):
+    means3D (sky Gaussians placed from their angles, :95-104), scales = exp, rotations =
+    normalised, opacities = sigmoid, colors = sigmoid(albedo), plus is_sky, roughness and
+    metalness (sigmoid).  Reads through the drop-in `plyfile` (plyfile.py)."""
+    import plyfile
+    v = plyfile.PlyData.read(path).elements[0]
+    names = [p.name for p in v.properties]
+    col = lambda prefix: np.stack([np.asarray(v[n], np.float32) for n in names if n.startswith(prefix)], 1)
+    xyz = np.stack([np.asarray(v[k], np.float32) for k in ("x", "y", "z")], 1)
+    is_sky = np.asarray(v["is_sky"]).astype(bool) if "is_sky" in names else np.zeros(len(xyz), bool)
+    if is_sky.any() and "sky_radius" in names:
+        ang = col("sky_angles_")[is_sky].astype(np.float64)
+        th = np.clip(ang[:, 0], 0, np.pi / 2)
+        ph = np.clip(ang[:, 1], -np.pi / 2, np.pi / 2)
+        r = float(np.asarray(v["sky_radius"])[0])
+        c = col("sky_gauss_center_")[0].astype(np.float64)
+        d = np.stack([np.sin(th) * np.sin(ph), -np.cos(th), np.sin(th) * np.cos(ph)], 1)
+        xyz[is_sky] = (r * d + c).astype(np.float32)
+    sig = lambda a: 1.0 / (1.0 + np.exp(-a))
+    rot = col("rot_")
+    rot = rot / np.maximum(np.linalg.norm(rot, axis=1, keepdims=True), 1e-12)
+    out = dict(means3D=xyz, scales=np.exp(col("scale_")), rotations=rot,
+               opacities=sig(np.asarray(v["opacity"], np.float32))[:, None], colors=sig(col("albedo_")),
+               is_sky=is_sky)
+    for k in ("roughness", "metalness"):
+        if k in names:
+            out[k] = sig(np.asarray(v[k], np.float32))[:, None]
+    return {k: torch.from_numpy(np.ascontiguousarray(a)).to(device=device,
+                                                            dtype=torch.bool if a.dtype == bool else torch.float32)
+            for k, a in out.items()}
+
+
+def ply_config(path, W=1920, H=1080, focal=1400.0):
+    """Bench inputs from a saved scene: the rasterizer's SH path at degree 0 with the albedo
+    as the DC colour (so bench.py's SH3 plumbing applies unchanged), camera at the
+    foreground median minus 2x the foreground extent along z, looking at it."""
+    g = load_ply_gaussians(path)
+    fg = g["means3D"][~g["is_sky"]] if (~g["is_sky"]).any() else g["means3D"]
+    med = fg.median(dim=0).values.double().numpy()
+    ext = float((fg.quantile(0.9, dim=0) - fg.quantile(0.1, dim=0)).norm())
+    pos = med - np.array([0.0, 0.0, 2.0 * max(ext, 1e-3)])
+    R, T = look_at_rotation(pos, med)
+    cam = focal_camera(W, H, focal, R=R, T=T)
+    P = g["means3D"].shape[0]
+    shs = rgb2sh(g["colors"]).reshape(P, 1, 3)
+    gs = dict(means3D=g["means3D"], scales=g["scales"], rotations=g["rotations"], opacities=g["opacities"],
+              shs=shs.contiguous(), colors=g["colors"])
+    return cam, gs, dict(P=P, W=W, H=H, sh_degree=0)
