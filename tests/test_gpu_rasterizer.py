@@ -123,6 +123,9 @@ CASES = [
     dict(name="faint_opacity", P=3000, W=80, H=64, mode="colors", mutate="faint"),
     dict(name="opaque_stack", P=6000, W=64, H=64, mode="sh", sh_degree=1, mutate="opaque"),
     dict(name="half_outside", P=3000, W=96, H=96, mode="sh", sh_degree=3, mutate="shift"),
+    # lists above the heavy-tile thresholds (>= 8192 entries, n_contrib >= 2048): the
+    # four-way quadrant split of the tile passes
+    dict(name="heavy_tiles", P=70000, W=64, H=48, mode="colors", mutate="thin"),
 ]
 
 
@@ -139,6 +142,9 @@ def mutate(gs, how):
     elif how == "opaque":  # opaque and large: most pixels saturate (T < 1e-4) early
         gs["opacities"].fill_(0.99)
         gs["scales"] *= 3.0
+    elif how == "thin":  # low opacity, wide: long lists that never saturate
+        gs["opacities"] = torch.empty_like(gs["opacities"]).uniform_(0.01, 0.03, generator=g)
+        gs["scales"] *= 2.0
     elif how == "shift":  # half the cloud left of the frustum, some behind the near plane
         gs["means3D"][:, 0] -= 0.6 * gs["means3D"][:, 2]
         gs["means3D"][: gs["means3D"].shape[0] // 10, 2] = 0.1
