@@ -1,7 +1,7 @@
 // gsr_capi.cpp -- C ABI (include/gsr.h): buffer layout and stage orchestration of the
 // forward / backward rasterizer (rasterizer_impl.cu:198-433 re-designed):
 //
-//   forward:  preprocess -> visibility compaction (+ R and P_v totals) -> ONE D2H sync
+//   forward:  preprocess (+ P_v, R, S totals) -> depth sort of all P -> ONE D2H sync
 //             -> depth sort of the P_v visible Gaussians (32-bit keys, 4 passes)
 //             -> depth-order exclusive scan of tiles_touched -> instance emission
 //             -> stable tile-id sort of the R instances (ceil(log2 T / 8) passes)
@@ -69,7 +69,7 @@ struct BinLayout {
 GeomLayout geom_layout(long long P) {
     Carver c;
     GeomLayout L;
-    L.totals = c.take(64);
+    L.totals = c.take(8 * (3 * gsr::TOTAL_SLOTS + 1));  // [slots][P_v, R, S] + error flag
     L.radii = c.take(4 * P);
     L.tiles = c.take(4 * P);
     L.st_count = c.take(4 * P);
@@ -298,8 +298,9 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     if (!radii) radii = at<int>(geom, gl.radii);
 
     unsigned long long* totals = at<unsigned long long>(geom, gl.totals);
-    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 3);
-    HIP_OK(hipMemsetAsync(err_flag, 0, 4, s));
+    const size_t totals_bytes = 8 * (3 * gsr::TOTAL_SLOTS + 1);
+    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 3 * gsr::TOTAL_SLOTS);
+    HIP_OK(hipMemsetAsync(totals, 0, totals_bytes, s));  // per-slot P_v, R, S (preprocess atomics) + error flag
 
     gsr::PreprocessArgs pa;
     pa.P = P; pa.D = D; pa.M = M;
@@ -315,26 +316,37 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     pa.rect = at<uint2>(geom, gl.rect);
     pa.rec = at<gsr::Rec>(geom, gl.rec);
     pa.err_flag = err_flag;
+    pa.totals = totals;
     {
         GSR_STAGE(ST_PREPROCESS);
         gsr::launch_preprocess(pa, s);
     }
     GSR_LAUNCH_CHECK();
 
+    // Depth sort of all P Gaussians: culled ones carry key 0xFFFFFFFF and sort last, so the
+    // first P_v sorted entries are the visible Gaussians in the reference's (depth, index)
+    // order -- no separate visibility compaction.  Runs before the one host sync.
     uint32_t* vis_key = at<uint32_t>(geom, gl.vis_key);
     uint32_t* vis_val = at<uint32_t>(geom, gl.vis_val);
+    int flip;
     {
-        GSR_STAGE(ST_COMPACT);
-        gsr::launch_compact_visible(P, pa.tiles, pa.st_count, pa.depth_key, vis_key, vis_val,
-                                    at<unsigned long long>(geom, gl.scan_tmp), totals, s);
+        GSR_STAGE(ST_DEPTH_SORT);
+        flip = gsr::radix_sort_pairs_from(P, pa.depth_key, nullptr, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
+                                          at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s);
     }
     GSR_LAUNCH_CHECK();
 
-    if (!g_pinned.p) HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 64, hipHostMallocDefault));
-    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, 32, hipMemcpyDeviceToHost, s));
+    if (!g_pinned.p)
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * (3 * gsr::TOTAL_SLOTS + 1), hipHostMallocDefault));
+    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, totals_bytes, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    const unsigned long long Pv = g_pinned.p[0], R64 = g_pinned.p[1], S64 = g_pinned.p[2];
-    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 3)[0];
+    unsigned long long Pv = 0, R64 = 0, S64 = 0;
+    for (int k = 0; k < gsr::TOTAL_SLOTS; k++) {
+        Pv += g_pinned.p[3 * k];
+        R64 += g_pinned.p[3 * k + 1];
+        S64 += g_pinned.p[3 * k + 2];
+    }
+    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 3 * gsr::TOTAL_SLOTS)[0];
     if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
     const long long R = (long long)R64, S = (long long)S64;
@@ -344,14 +356,6 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
     bin = align_base(bin);
 
-    // depth sort of the visible Gaussians (stable: ties keep index order)
-    int flip;
-    {
-        GSR_STAGE(ST_DEPTH_SORT);
-        flip = gsr::radix_sort_pairs((long long)Pv, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
-                                     at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s);
-    }
-    GSR_LAUNCH_CHECK();
     const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
     uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
     {

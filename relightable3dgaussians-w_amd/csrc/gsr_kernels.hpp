@@ -34,7 +34,9 @@ struct PreprocessArgs {
     uint2* rect;
     Rec* rec;
     unsigned* err_flag;
+    unsigned long long* totals;  // [TOTAL_SLOTS][3] += P_v, R, S (zeroed by the caller; the host sums)
 };
+constexpr int TOTAL_SLOTS = 64;  // spread of the totals' atomics (one slot per 1/64 of the blocks)
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s);
@@ -46,14 +48,6 @@ constexpr int SCAN_THREADS = 256;
 constexpr int SCAN_ITEMS = 16;
 constexpr int SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;  // 4096
 inline int scan_blocks(long long n) { return (int)((n + SCAN_TILE - 1) / SCAN_TILE); }
-
-// Visibility compaction: tiles[i] > 0 <=> visible.  Produces, in index order (stable),
-// vis_key[j] = depth_key[i], vis_val[j] = i for the j-th visible Gaussian, and
-// totals[0] = number of visible Gaussians, totals[1] = sum of tiles (R),
-// totals[2] = sum of st_count (S).  block_tmp: scan_blocks(P) * 24 bytes.
-void launch_compact_visible(int P, const uint32_t* tiles, const uint32_t* st_count, const uint32_t* depth_key,
-                            uint32_t* vis_key, uint32_t* vis_val, unsigned long long* block_tmp,
-                            unsigned long long* totals, hipStream_t s);
 
 // Exclusive scan (u32) of in[0..n) -> out; block_tmp: scan_blocks(n) u32;
 // total (optional) receives the sum.  If gather != nullptr the input is in[gather[i]].
@@ -72,6 +66,11 @@ size_t radix_sort_temp_bytes(long long n);
 // buffers, 0 if in the primary buffers.
 int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
                      int end_bit, void* temp, hipStream_t s);
+// The same with a separate, untouched input (keys_in, vals_in; vals_in == nullptr means
+// the values 0..n-1); the result lands in (keys, vals) or, when 1 is returned, the alt pair.
+int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
+                          uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int end_bit, void* temp,
+                          hipStream_t s);
 
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
 // In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per

@@ -12,12 +12,14 @@
 
 namespace gsr {
 
-__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= a.P) return;
+// One Gaussian; returns its tile and super-tile counts (0 when culled).
+__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, uint32_t& tiles,
+                                               uint32_t& stc) {
+    tiles = stc = 0;
     a.radii[idx] = 0;
     a.tiles[idx] = 0;
     a.st_count[idx] = 0;
+    a.depth_key[idx] = 0xFFFFFFFFu;  // culled Gaussians sort after every visible depth
     const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     // in_frustum (auxiliary.h:139-164): near cull only
     const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
@@ -70,8 +72,34 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     a.rect[idx] = make_uint2(rmin.x | (rmax.x << 16), rmin.y | (rmax.y << 16));
     a.radii[idx] = irad;
     a.tiles[idx] = area;
-    a.st_count[idx] = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
-                      ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
+    stc = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
+          ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
+    a.st_count[idx] = stc;
+    tiles = area;
+}
+
+// Preprocess + the frame totals (visible count P_v, instances R, super-tile entries S):
+// workgroup sums, one atomic per workgroup and total into one of TOTAL_SLOTS slots (a
+// single address per total serialises ~6k atomics; the host adds the slots).
+__global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
+    __shared__ unsigned long long sh[3][4];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t tiles = 0, stc = 0;
+    if (idx < a.P) preprocess_one(a, idx, tiles, stc);
+    unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+        if (lane == 0) sh[k][wave] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        const unsigned long long t = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
+        if (t) atomicAdd(a.totals + 3 * (blockIdx.x % TOTAL_SLOTS) + k, t);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,

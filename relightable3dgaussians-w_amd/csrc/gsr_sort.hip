@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     for (int k = 0; k < SORT_ITEMS; k++) {
         const long long i = base + k * 64 + lane;
         key[k] = i < n ? keys_in[i] : 0u;
-        val[k] = i < n ? vals_in[i] : 0u;
+        val[k] = i < n ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
@@ -160,30 +160,37 @@ size_t radix_sort_temp_bytes(long long n) {
     return (size_t)(4 * (h + 256) + 256);
 }
 
-int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
-                     int end_bit, void* temp, hipStream_t s) {
-    if (n <= 1 || end_bit <= 0) return 0;
+int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
+                          uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int end_bit, void* temp,
+                          hipStream_t s) {
+    if (n <= 0 || end_bit <= 0) return -1;
     const int nb = sort_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
     uint32_t* digit_tot = hist + 256LL * nb;
-    uint32_t* kin = keys;
-    uint32_t* vin = vals;
-    uint32_t* kout = keys_alt;
-    uint32_t* vout = vals_alt;
-    int flips = 0;
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = vals_in;
+    uint32_t* out_k[2] = {keys, keys_alt};
+    uint32_t* out_v[2] = {vals, vals_alt};
+    int cur = 0;
     for (int shift = 0; shift < end_bit; shift += 8) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
         const uint32_t mask = (1u << nbits) - 1u;
         hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
         hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
         hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask, hist,
-                           digit_tot, nb, kout, vout);
-        uint32_t* t;
-        t = kin; kin = kout; kout = t;
-        t = vin; vin = vout; vout = t;
-        flips ^= 1;
+                           digit_tot, nb, out_k[cur], out_v[cur]);
+        kin = out_k[cur];
+        vin = out_v[cur];
+        cur ^= 1;
     }
-    return flips;
+    return cur ^ 1;  // the buffer pair written last
+}
+
+int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,
+                     int end_bit, void* temp, hipStream_t s) {
+    if (n <= 1 || end_bit <= 0) return 0;
+    // first pass reads (keys, vals) and writes the alt pair, then they alternate
+    return radix_sort_pairs_from(n, keys, vals, keys_alt, vals_alt, keys, vals, end_bit, temp, s) ^ 1;
 }
 
 }  // namespace gsr
