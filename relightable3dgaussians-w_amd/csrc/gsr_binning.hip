@@ -94,6 +94,174 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
     }
 }
 
+// ---- 2+3 fused: super-tile entries emitted straight into super-tile order ----------------
+// The depth-sorted visible Gaussians are cut into blocks of ST_G.  k_st_hist counts each
+// block's entries per super-tile (digit-major table [NS][nb]) and stores the block's rects
+// in sorted order; k_digit_scan (gsr_sort.hip) turns every super-tile's row into
+// block offsets + a total; k_st_bases scans the totals into super-tile bases and ranges;
+// k_st_scatter re-enumerates each block's entries in (Gaussian, super-tile) order and
+// ranks them per super-tile with wave ballots, writing each entry at its final position.
+// Equivalent to emit + a stable counting sort by super-tile (the entry order within a
+// super-tile is the depth order), in four launches and no entry round trip through HBM.
+constexpr int ST_G = 1024;  // Gaussians per block (256 per wave in the scatter)
+
+__device__ __forceinline__ uint2 st_rect_of(uint2 r) {
+    const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
+    const uint32_t sy0 = (r.y & 0xffffu) / GSR_ST_H, sy1 = ((r.y >> 16) + GSR_ST_H - 1) / GSR_ST_H;
+    return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
+}
+
+__global__ void __launch_bounds__(256) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
+                                                  int NS, int nb, uint32_t* table, uint2* rect_sorted) {
+    extern __shared__ uint32_t hist[];
+    for (int i = threadIdx.x; i < NS; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
+    const int p0 = blk * ST_G;
+    for (int p = p0 + threadIdx.x; p < min(Pv, p0 + ST_G); p += blockDim.x) {
+        const uint2 r = rect[sorted_ids[p]];
+        rect_sorted[p] = r;
+        const uint2 sr = st_rect_of(r);
+        for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
+            for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&hist[sy * gsx + sx], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NS; i += blockDim.x) table[(size_t)i * nb + blk] = hist[i];
+}
+
+// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total)
+__global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, uint32_t* bases, uint2* ranges) {
+    __shared__ uint32_t sh[4];
+    uint32_t carry = 0;
+    for (int c = 0; c < NS; c += 256) {
+        const int i = c + threadIdx.x;
+        const uint32_t v = i < NS ? tot[i] : 0u;
+        uint32_t t;
+        const uint32_t ex = carry + block256_exclusive_scan(v, sh, &t);
+        if (i < NS) {
+            bases[i] = ex;
+            ranges[i] = v ? make_uint2(ex, ex + v) : make_uint2(0u, 0u);
+        }
+        carry += t;
+    }
+}
+
+// Per block of ST_G sorted Gaussians, four waves each own ST_G / 4 consecutive Gaussians,
+// one Gaussian per lane per 64-Gaussian chunk.  Pass 1 counts the wave's entries per
+// super-tile (LDS atomics over each lane's super-tile rect); the block then knows where each
+// wave's run of every super-tile starts (block offset from the table + the counts of the
+// waves before it).  Pass 2, per chunk: every lane ORs its bit into the 64-bit lane mask of
+// each super-tile it touches; an entry's rank in its run is the popcount of the mask's
+// lower lanes (a Gaussian touches a super-tile at most once, so the lanes in a mask are
+// exactly the entries of that super-tile in depth order); the lowest lane then advances
+// the run and clears the mask.  Order-independent atomics only, so the output is
+// deterministic, and each super-tile's entries come out in depth order.
+template <bool WRITE>
+__device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
+                                        unsigned gsx, uint32_t* wcnt, unsigned long long* wmask,
+                                        uint32_t* st_keys, uint32_t* st_vals) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long bit = 1ull << lane, lt = bit - 1ull;
+    for (int c0 = p0; c0 < p1; c0 += 64) {
+        const int p = c0 + lane;
+        uint2 r = make_uint2(0u, 0u), sr = r;
+        uint32_t gid = 0;
+        if (p < p1) {
+            r = rect_sorted[p];
+            sr = st_rect_of(r);
+            if (WRITE) gid = sorted_ids[p];
+        }
+        const uint32_t sx0 = sr.x & 0xffffu, sx1 = sr.x >> 16, sy0 = sr.y & 0xffffu, sy1 = sr.y >> 16;
+        if (!WRITE) {
+            for (uint32_t sy = sy0; sy < sy1; sy++)
+                for (uint32_t sx = sx0; sx < sx1; sx++) atomicAdd(&wcnt[sy * gsx + sx], 1u);
+            continue;
+        }
+        for (uint32_t sy = sy0; sy < sy1; sy++)
+            for (uint32_t sx = sx0; sx < sx1; sx++) atomicOr(&wmask[sy * gsx + sx], bit);
+        wave_lds_sync();
+        for (uint32_t sy = sy0; sy < sy1; sy++)
+            for (uint32_t sx = sx0; sx < sx1; sx++) {
+                const uint32_t sid = sy * gsx + sx;
+                const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
+                st_keys[pos] = sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS);
+                st_vals[pos] = gid;
+            }
+        wave_lds_sync();
+        for (uint32_t sy = sy0; sy < sy1; sy++)
+            for (uint32_t sx = sx0; sx < sx1; sx++) {
+                const uint32_t sid = sy * gsx + sx;
+                const unsigned long long m = wmask[sid];
+                if ((m & lt) == 0ull) {
+                    wcnt[sid] += (uint32_t)__popcll(m);
+                    wmask[sid] = 0ull;
+                }
+            }
+        wave_lds_sync();
+    }
+}
+
+__global__ void __launch_bounds__(256) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
+                                                     unsigned gsx, int NS, int nb, const uint32_t* table,
+                                                     const uint32_t* bases, uint32_t* st_keys, uint32_t* st_vals) {
+    extern __shared__ unsigned long long st_lds[];  // [4][NS] lane masks, then [4][NS] run counters
+    unsigned long long* wmask_all = st_lds;
+    uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + 4 * NS);
+    const int wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 4 * NS; i += 256) {
+        wmask_all[i] = 0ull;
+        wcnt_all[i] = 0u;
+    }
+    __syncthreads();
+    const unsigned blk = xcd_remap(blockIdx.x, nb);  // as k_st_hist: runs of neighbours merge in L2
+    const int g0 = blk * ST_G;
+    const int p0 = min(Pv, g0 + wave * (ST_G / 4)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / 4));
+    st_pass<false>(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, nullptr, nullptr, nullptr);
+    __syncthreads();
+    // each wave's run of super-tile s starts after the block's earlier waves
+    for (int i = threadIdx.x; i < NS; i += 256) {
+        uint32_t run = bases[i] + table[(size_t)i * nb + blk];
+        for (int w = 0; w < 4; w++) {
+            const uint32_t c = wcnt_all[w * NS + i];
+            wcnt_all[w * NS + i] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    st_pass<true>(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, st_keys,
+                  st_vals);
+}
+
+size_t st_bin_temp_bytes(long long Pv, int NS) {
+    const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
+    return 4 * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 4 * 256 + 1024;
+}
+
+bool st_bin_supported(int NS) { return NS <= 1024; }  // per-wave LDS masks + counters: 48 B x NS
+
+void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
+                   uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
+    (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
+    if (Pv <= 0) return;
+    const int nb = (Pv + ST_G - 1) / ST_G;
+    char* t = reinterpret_cast<char*>(temp);
+    auto take = [&](size_t bytes) {
+        char* p = t;
+        t += (bytes + 255) & ~(size_t)255;
+        return p;
+    };
+    uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
+    uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
+    uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
+    uint2* rect_sorted = reinterpret_cast<uint2*>(take(8 * (size_t)Pv));
+    hipLaunchKernelGGL(k_st_hist, dim3(nb), dim3(256), 4 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
+                       rect_sorted);
+    launch_digit_scan(NS, table, nb, tot, s);
+    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
+    hipLaunchKernelGGL(k_st_scatter, dim3(nb), dim3(256), 48 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS, nb,
+                       table, bases, st_keys, st_vals);
+}
+
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
 __global__ void __launch_bounds__(256) k_seg_ranges(long long n, const uint32_t* keys, uint2* ranges) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;

@@ -62,7 +62,8 @@ struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, nheavy, total;
 };
 struct BinLayout {
-    size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_ranges, tile_cnt, tile_start, scan_tmp,
+    size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_bin_tmp, st_ranges, tile_cnt, tile_start,
+        scan_tmp,
         lists_tmp, total;
 };
 
@@ -111,16 +112,19 @@ unsigned st_x(int W) { return (tiles_x(W) + GSR_ST_W - 1) / GSR_ST_W; }
 unsigned st_y(int H) { return (tiles_y(H) + GSR_ST_H - 1) / GSR_ST_H; }
 
 // point_list first: the backward needs only it (offset 0, independent of S)
-BinLayout bin_layout(long long R, long long S, int W, int H) {
+BinLayout bin_layout(long long R, long long S, int W, int H, long long Pv) {
     Carver c;
     BinLayout L;
     const size_t NS = (size_t)st_x(W) * st_y(H), T = (size_t)tiles_x(W) * tiles_y(H);
+    const bool fused = gsr::st_bin_supported((int)NS);
     L.point = c.take(4 * R);
     L.st_keys = c.take(4 * S);
     L.st_vals = c.take(4 * S);
-    L.st_keys_alt = c.take(4 * S);
-    L.st_vals_alt = c.take(4 * S);
-    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(S));
+    // emit + sort fallback for very large images (NS > 4096 super-tiles)
+    L.st_keys_alt = c.take(fused ? 0 : 4 * S);
+    L.st_vals_alt = c.take(fused ? 0 : 4 * S);
+    L.sort_tmp = c.take(fused ? 0 : gsr::radix_sort_temp_bytes(S));
+    L.st_bin_tmp = c.take(fused ? gsr::st_bin_temp_bytes(Pv, (int)NS) : 0);
     L.st_ranges = c.take(8 * NS);
     L.tile_cnt = c.take(4 * T);
     L.tile_start = c.take(4 * T);
@@ -246,7 +250,7 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     if (!out || P < 0 || R < 0 || width < 0 || height < 0) return fail(GSR_E_ARG, "gsr_get_layout: bad arguments");
     const GeomLayout g = geom_layout(P);
     const ImgLayout im = img_layout(width, height);
-    const BinLayout b = bin_layout(R, 0, width, height);
+    const BinLayout b = bin_layout(R, 0, width, height, 0);
     out->geom_bytes = g.total;
     out->img_bytes = im.total;
     out->bin_bytes = b.total;
@@ -351,43 +355,49 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
     const long long R = (long long)R64, S = (long long)S64;
 
-    const BinLayout bl = bin_layout(R, S, width, height);
+    const BinLayout bl = bin_layout(R, S, width, height, (long long)Pv);
     char* bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
     if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
     bin = align_base(bin);
 
     const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
-    uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
-    {
-        GSR_STAGE(ST_OFFSETS);
-        gsr::launch_exclusive_scan_u32((long long)Pv, pa.st_count, sorted_ids, offsets,
-                                       at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
-    }
-    GSR_LAUNCH_CHECK();
     const unsigned gsx = st_x(width), gsy = st_y(height);
     const int NS = (int)(gsx * gsy);
     uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
     uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
-    {
+    uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
+    const uint32_t* st_sorted_keys = stk;
+    const uint32_t* st_sorted_vals = stv;
+    if (gsr::st_bin_supported(NS)) {
         GSR_STAGE(ST_DUPLICATE);
-        gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
+        gsr::launch_st_bin((int)Pv, sorted_ids, pa.rect, gsx, NS, at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, s);
+    } else {
+        uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
+        {
+            GSR_STAGE(ST_OFFSETS);
+            gsr::launch_exclusive_scan_u32((long long)Pv, pa.st_count, sorted_ids, offsets,
+                                           at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
+        }
+        {
+            GSR_STAGE(ST_DUPLICATE);
+            gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
+        }
+        int flip2;
+        {
+            GSR_STAGE(ST_TILE_SORT);
+            flip2 = gsr::radix_sort_pairs(S, stk, stv, at<uint32_t>(bin, bl.st_keys_alt),
+                                          at<uint32_t>(bin, bl.st_vals_alt), (int)higher_msb((uint32_t)NS),
+                                          at<void>(bin, bl.sort_tmp), s);
+        }
+        st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
+        st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
+        gsr::launch_seg_ranges(S, NS, st_sorted_keys, st_ranges, s);
     }
     GSR_LAUNCH_CHECK();
-    int flip2;
-    {
-        GSR_STAGE(ST_TILE_SORT);
-        flip2 = gsr::radix_sort_pairs(S, stk, stv, at<uint32_t>(bin, bl.st_keys_alt), at<uint32_t>(bin, bl.st_vals_alt),
-                                      (int)higher_msb((uint32_t)NS), at<void>(bin, bl.sort_tmp), s);
-    }
-    GSR_LAUNCH_CHECK();
-    const uint32_t* st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
-    const uint32_t* st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
     uint2* ranges = at<uint2>(img, il.ranges);
     uint32_t* point_list = at<uint32_t>(bin, bl.point);
     {
         GSR_STAGE(ST_RANGES);
-        uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
-        gsr::launch_seg_ranges(S, NS, st_sorted_keys, st_ranges, s);
         gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
                                at<uint32_t>(bin, bl.tile_start), ranges, at<uint32_t>(bin, bl.scan_tmp),
                                at<void>(bin, bl.lists_tmp), point_list, s);
@@ -425,7 +435,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     if (P == 0) return GSR_OK;
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R, 0, width, height);
+    const BinLayout bl = bin_layout(R, 0, width, height, 0);
     char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
     if (!geom) return fail(GSR_E_ALLOC, "gsr_forward_reuse: buffer allocation failed");
     geom = align_base(geom);
@@ -470,7 +480,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     const float focal_x = width / (2.0f * tan_fovx);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R, 0, width, height);
+    const BinLayout bl = bin_layout(R, 0, width, height, 0);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;

@@ -72,7 +72,16 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
                           uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int end_bit, void* temp,
                           hipStream_t s);
 
+// table[d][0..nb) -> exclusive prefix within each of ndigits rows; digit_tot[d] = row total
+void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot, hipStream_t s);
+
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
+// Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
+// order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1024.
+size_t st_bin_temp_bytes(long long Pv, int NS);
+bool st_bin_supported(int NS);
+void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
+                   uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s);
 // In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
 // super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,

@@ -16,6 +16,7 @@
 //                   reordered in LDS and written out in digit runs (coalesced).
 #include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
+#include "gsr_tile.hpp"
 
 namespace gsr {
 
@@ -39,7 +40,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const 
     const int wave = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    const long long tile_base = (long long)blockIdx.x * SORT_TILE;
+    const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring tiles' digit runs merge in one L2
+    const long long tile_base = (long long)blk * SORT_TILE;
     uint32_t* wc = cnt[wave];
     if (tile_base + SORT_TILE <= n) {
         const uint4* k4 = reinterpret_cast<const uint4*>(keys + tile_base);
@@ -56,7 +58,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const 
     }
     __syncthreads();
     const int d = threadIdx.x;
-    hist[(long long)d * nb + blockIdx.x] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
+    hist[(long long)d * nb + blk] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
 }
 
 // hist[d][0..nb) -> exclusive prefix within digit d; digit_tot[d] = the digit's total
@@ -88,7 +90,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&wh[0][0])[i] = 0;
     __syncthreads();
-    const long long tile_base = (long long)blockIdx.x * SORT_TILE;
+    const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring tiles' digit runs merge in one L2
+    const long long tile_base = (long long)blk * SORT_TILE;
     const long long base = tile_base + wave * WAVE_ITEMS;
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
     volatile uint32_t* wc = wh[wave];
@@ -126,7 +129,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         wh[3][d] = start + c0 + c1 + c2;
         dstart[d] = start;
         const uint32_t dbase = block256_exclusive_scan(digit_tot[d], scan_sh, (uint32_t*)nullptr);
-        goff[d] = dbase + offsets[(long long)d * nb + blockIdx.x];
+        goff[d] = dbase + offsets[(long long)d * nb + blk];
     }
     __syncthreads();
 #pragma unroll
@@ -152,6 +155,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
             vals_out[g] = s_vals[p];
         }
     }
+}
+
+void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot, hipStream_t s) {
+    hipLaunchKernelGGL(k_digit_scan, dim3(ndigits), dim3(SORT_THREADS), 0, s, table, nb, digit_tot);
 }
 
 size_t radix_sort_temp_bytes(long long n) {
