@@ -103,7 +103,9 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
-constexpr int ST_G = 1024;  // Gaussians per block (256 per wave in the scatter)
+constexpr int ST_G = 1024;  // Gaussians per block
+constexpr int ST_W = 8;     // waves per block in k_st_hist / k_st_scatter (ST_G / ST_W Gaussians each)
+constexpr int ST_T = 64 * ST_W;
 
 __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
@@ -111,22 +113,33 @@ __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
 }
 
-__global__ void __launch_bounds__(256) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
-                                                  int NS, int nb, uint32_t* table, uint2* rect_sorted) {
-    extern __shared__ uint32_t hist[];
-    for (int i = threadIdx.x; i < NS; i += blockDim.x) hist[i] = 0;
+__global__ void __launch_bounds__(ST_T) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
+                                                  int NS, int nb, uint32_t* table, uint32_t* wcounts,
+                                                  uint2* rect_sorted) {
+    extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
+    for (int i = threadIdx.x; i < ST_W * NS; i += ST_T) hist[i] = 0;
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
-    const int p0 = blk * ST_G;
-    for (int p = p0 + threadIdx.x; p < min(Pv, p0 + ST_G); p += blockDim.x) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int g0 = blk * ST_G;
+    const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
+    uint32_t* wh = hist + wave * NS;
+    for (int p = p0 + lane; p < p1; p += 64) {
         const uint2 r = rect[sorted_ids[p]];
         rect_sorted[p] = r;
         const uint2 sr = st_rect_of(r);
         for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
-            for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&hist[sy * gsx + sx], 1u);
+            for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < NS; i += blockDim.x) table[(size_t)i * nb + blk] = hist[i];
+    uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
+    for (int i = threadIdx.x; i < ST_W * NS; i += ST_T) wc[i] = hist[i];
+    for (int i = threadIdx.x; i < NS; i += ST_T) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < ST_W; w++) t += hist[w * NS + i];
+        table[(size_t)i * nb + blk] = t;
+    }
 }
 
 // bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total)
@@ -146,40 +159,44 @@ __global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, u
     }
 }
 
-// Per block of ST_G sorted Gaussians, four waves each own ST_G / 4 consecutive Gaussians,
-// one Gaussian per lane per 64-Gaussian chunk.  Pass 1 counts the wave's entries per
-// super-tile (LDS atomics over each lane's super-tile rect); the block then knows where each
-// wave's run of every super-tile starts (block offset from the table + the counts of the
-// waves before it).  Pass 2, per chunk: every lane ORs its bit into the 64-bit lane mask of
-// each super-tile it touches; an entry's rank in its run is the popcount of the mask's
+// Orders a wave's LDS accesses across lanes (LDS executes one wave's instructions in order)
+// without the vmcnt wait a wavefront fence adds: the ranking must not wait for its own
+// scattered stores or the next chunk's prefetch.
+__device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Per block of ST_G sorted Gaussians, ST_W waves each own ST_G / ST_W consecutive Gaussians,
+// one Gaussian per lane per 64-Gaussian chunk.  k_st_hist counted each wave's entries per
+// super-tile, so each wave's run of every super-tile starts at the block offset from the
+// table + the counts of the block's earlier waves.  Per chunk: every lane ORs its bit into
+// the 64-bit lane mask of each super-tile it touches; an entry's rank in its run is the popcount of the mask's
 // lower lanes (a Gaussian touches a super-tile at most once, so the lanes in a mask are
 // exactly the entries of that super-tile in depth order); the lowest lane then advances
 // the run and clears the mask.  Order-independent atomics only, so the output is
 // deterministic, and each super-tile's entries come out in depth order.
-template <bool WRITE>
 __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
                                         unsigned gsx, uint32_t* wcnt, unsigned long long* wmask,
                                         uint32_t* st_keys, uint32_t* st_vals) {
     const int lane = threadIdx.x & 63;
     const unsigned long long bit = 1ull << lane, lt = bit - 1ull;
+    // the next chunk's rect and id are loaded while this chunk is ranked
+    uint2 r_nx = make_uint2(0u, 0u);
+    uint32_t gid_nx = 0;
+    if (p0 + lane < p1) {
+        r_nx = rect_sorted[p0 + lane];
+        gid_nx = sorted_ids[p0 + lane];
+    }
     for (int c0 = p0; c0 < p1; c0 += 64) {
-        const int p = c0 + lane;
-        uint2 r = make_uint2(0u, 0u), sr = r;
-        uint32_t gid = 0;
-        if (p < p1) {
-            r = rect_sorted[p];
-            sr = st_rect_of(r);
-            if (WRITE) gid = sorted_ids[p];
+        const uint2 r = r_nx;
+        const uint32_t gid = gid_nx;
+        const uint2 sr = (c0 + lane < p1) ? st_rect_of(r) : make_uint2(0u, 0u);
+        if (c0 + 64 + lane < p1) {
+            r_nx = rect_sorted[c0 + 64 + lane];
+            gid_nx = sorted_ids[c0 + 64 + lane];
         }
         const uint32_t sx0 = sr.x & 0xffffu, sx1 = sr.x >> 16, sy0 = sr.y & 0xffffu, sy1 = sr.y >> 16;
-        if (!WRITE) {
-            for (uint32_t sy = sy0; sy < sy1; sy++)
-                for (uint32_t sx = sx0; sx < sx1; sx++) atomicAdd(&wcnt[sy * gsx + sx], 1u);
-            continue;
-        }
         for (uint32_t sy = sy0; sy < sy1; sy++)
             for (uint32_t sx = sx0; sx < sx1; sx++) atomicOr(&wmask[sy * gsx + sx], bit);
-        wave_lds_sync();
+        lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
@@ -187,7 +204,7 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
                 st_keys[pos] = sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS);
                 st_vals[pos] = gid;
             }
-        wave_lds_sync();
+        lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
@@ -197,47 +214,44 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
                     wmask[sid] = 0ull;
                 }
             }
-        wave_lds_sync();
+        lds_order();
     }
 }
 
-__global__ void __launch_bounds__(256) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
+__global__ void __launch_bounds__(ST_T) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
                                                      unsigned gsx, int NS, int nb, const uint32_t* table,
-                                                     const uint32_t* bases, uint32_t* st_keys, uint32_t* st_vals) {
-    extern __shared__ unsigned long long st_lds[];  // [4][NS] lane masks, then [4][NS] run counters
+                                                     const uint32_t* wcounts, const uint32_t* bases,
+                                                     uint32_t* st_keys, uint32_t* st_vals) {
+    extern __shared__ unsigned long long st_lds[];  // [ST_W][NS] lane masks, then [ST_W][NS] run counters
     unsigned long long* wmask_all = st_lds;
-    uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + 4 * NS);
+    uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + ST_W * NS);
     const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 4 * NS; i += 256) {
-        wmask_all[i] = 0ull;
-        wcnt_all[i] = 0u;
-    }
-    __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // as k_st_hist: runs of neighbours merge in L2
     const int g0 = blk * ST_G;
-    const int p0 = min(Pv, g0 + wave * (ST_G / 4)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / 4));
-    st_pass<false>(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, nullptr, nullptr, nullptr);
-    __syncthreads();
-    // each wave's run of super-tile s starts after the block's earlier waves
-    for (int i = threadIdx.x; i < NS; i += 256) {
+    const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
+    // each wave's run of super-tile s starts after the block's earlier waves (k_st_hist's
+    // per-wave counts)
+    const uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
+    for (int i = threadIdx.x; i < NS; i += ST_T) {
         uint32_t run = bases[i] + table[(size_t)i * nb + blk];
-        for (int w = 0; w < 4; w++) {
-            const uint32_t c = wcnt_all[w * NS + i];
+        for (int w = 0; w < ST_W; w++) {
+            wmask_all[w * NS + i] = 0ull;
             wcnt_all[w * NS + i] = run;
-            run += c;
+            run += wc[w * NS + i];
         }
     }
     __syncthreads();
-    st_pass<true>(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, st_keys,
+    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, st_keys,
                   st_vals);
 }
 
 size_t st_bin_temp_bytes(long long Pv, int NS) {
     const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
-    return 4 * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 4 * 256 + 1024;
+    return (4 + 4 * ST_W) * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 5 * 256 + 1024;
 }
 
-bool st_bin_supported(int NS) { return NS <= 1024; }  // per-wave LDS masks + counters: 48 B x NS
+// per-wave LDS masks + counters: 12 B x ST_W x NS within a 64 KiB workgroup allocation
+bool st_bin_supported(int NS) { return 12 * ST_W * NS <= 65536; }
 
 void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
                    uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
@@ -254,12 +268,13 @@ void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsign
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint2* rect_sorted = reinterpret_cast<uint2*>(take(8 * (size_t)Pv));
-    hipLaunchKernelGGL(k_st_hist, dim3(nb), dim3(256), 4 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
-                       rect_sorted);
+    uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * ST_W * (size_t)NS * nb));
+    hipLaunchKernelGGL(k_st_hist, dim3(nb), dim3(ST_T), 4 * ST_W * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
+                       wcounts, rect_sorted);
     launch_digit_scan(NS, table, nb, tot, s);
     hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
-    hipLaunchKernelGGL(k_st_scatter, dim3(nb), dim3(256), 48 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS, nb,
-                       table, bases, st_keys, st_vals);
+    hipLaunchKernelGGL(k_st_scatter, dim3(nb), dim3(ST_T), 12 * ST_W * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS, nb,
+                       table, wcounts, bases, st_keys, st_vals);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)

@@ -2,10 +2,11 @@
 """Print the per-kernel summary (calls, average us, share) from a rocprofv3 rocpd database
 (the default output format): python tools/rocpd_top.py gpurun_out/<dir> [N]."""
 import glob
+import os
 import sqlite3
 import sys
 
-db = sorted(glob.glob(sys.argv[1] + "/**/*.db", recursive=True))[-1]
+db = max(glob.glob(sys.argv[1] + "/**/*.db", recursive=True), key=os.path.getmtime)
 c = sqlite3.connect(db)
 cols = [r[1] for r in c.execute("pragma table_info(top_kernels)")]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
