@@ -70,7 +70,7 @@ struct BinLayout {
 GeomLayout geom_layout(long long P) {
     Carver c;
     GeomLayout L;
-    L.totals = c.take(8 * (3 * gsr::TOTAL_SLOTS + 1));  // [slots][P_v, R, S] + error flag
+    L.totals = c.take(8 * gsr::TOTALS_U64);  // [slots][P_v, R, S, pad] + error flag
     L.radii = c.take(4 * P);
     L.tiles = c.take(4 * P);
     L.st_count = c.take(4 * P);
@@ -302,8 +302,8 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     if (!radii) radii = at<int>(geom, gl.radii);
 
     unsigned long long* totals = at<unsigned long long>(geom, gl.totals);
-    const size_t totals_bytes = 8 * (3 * gsr::TOTAL_SLOTS + 1);
-    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + 3 * gsr::TOTAL_SLOTS);
+    const size_t totals_bytes = 8 * gsr::TOTALS_U64;
+    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + gsr::TOTALS_U64 - 1);
     HIP_OK(hipMemsetAsync(totals, 0, totals_bytes, s));  // per-slot P_v, R, S (preprocess atomics) + error flag
 
     gsr::PreprocessArgs pa;
@@ -341,16 +341,16 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
     GSR_LAUNCH_CHECK();
 
     if (!g_pinned.p)
-        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * (3 * gsr::TOTAL_SLOTS + 1), hipHostMallocDefault));
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * gsr::TOTALS_U64, hipHostMallocDefault));
     HIP_OK(hipMemcpyAsync(g_pinned.p, totals, totals_bytes, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     unsigned long long Pv = 0, R64 = 0, S64 = 0;
     for (int k = 0; k < gsr::TOTAL_SLOTS; k++) {
-        Pv += g_pinned.p[3 * k];
-        R64 += g_pinned.p[3 * k + 1];
-        S64 += g_pinned.p[3 * k + 2];
+        Pv += g_pinned.p[gsr::TOTAL_STRIDE * k];
+        R64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 1];
+        S64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 2];
     }
-    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + 3 * gsr::TOTAL_SLOTS)[0];
+    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + gsr::TOTALS_U64 - 1)[0];
     if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
     if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
     const long long R = (long long)R64, S = (long long)S64;

@@ -34,9 +34,11 @@ struct PreprocessArgs {
     uint2* rect;
     Rec* rec;
     unsigned* err_flag;
-    unsigned long long* totals;  // [TOTAL_SLOTS][3] += P_v, R, S (zeroed by the caller; the host sums)
+    unsigned long long* totals;  // [TOTAL_SLOTS][TOTAL_STRIDE]: [0..2] += P_v, R, S (zeroed by the caller; the host sums)
 };
-constexpr int TOTAL_SLOTS = 64;  // spread of the totals' atomics (one slot per 1/64 of the blocks)
+constexpr int TOTAL_SLOTS = 128;  // spread of the totals' atomics (one slot per 1/128 of the blocks)
+constexpr int TOTAL_STRIDE = 16;  // u64 per slot: one 128-B line each, so slots do not share an L2 line
+constexpr int TOTALS_U64 = TOTAL_SLOTS * TOTAL_STRIDE + 1;  // + the error flag
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s);

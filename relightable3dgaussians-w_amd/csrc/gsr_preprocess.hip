@@ -14,7 +14,7 @@ namespace gsr {
 
 // One Gaussian; returns its tile and super-tile counts (0 when culled).
 __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, uint32_t& tiles,
-                                               uint32_t& stc) {
+                                               uint32_t& stc, const float* sh_row) {
     tiles = stc = 0;
     a.radii[idx] = 0;
     a.tiles[idx] = 0;
@@ -59,7 +59,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
     if (a.colors_precomp) {
         rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
     } else {
-        const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, a.shs + (size_t)idx * a.M * 3);
+        const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, sh_row);
         rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
     }
     const float opacity = a.opacities[idx];
@@ -81,11 +81,42 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
 // Preprocess + the frame totals (visible count P_v, instances R, super-tile entries S):
 // workgroup sums, one atomic per workgroup and total into one of TOTAL_SLOTS slots (a
 // single address per total serialises ~6k atomics; the host adds the slots).
+// The workgroup's SH rows (256 x M x 3 floats, contiguous) are first copied to LDS with
+// 16-B coalesced loads (row stride M*3+1 against bank conflicts); each thread then reads
+// its own row from LDS instead of 12 strided 16-B loads.
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     __shared__ unsigned long long sh[3][4];
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    extern __shared__ float s_sh[];
+    const int g0 = blockIdx.x * blockDim.x;
+    const int idx = g0 + threadIdx.x;
+    const int M3 = a.M * 3, stride = M3 + 1;
+    const bool staged = a.shs && !a.colors_precomp;
+    if (staged) {
+        const int rows = min((int)blockDim.x, a.P - g0);
+        const float* src = a.shs + (size_t)g0 * M3;
+        const int n = rows * M3;
+        if ((M3 & 3) == 0) {
+            const float4* s4 = reinterpret_cast<const float4*>(src);
+            for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
+                const float4 v = s4[f];
+                const int e0 = f * 4, r = e0 / M3;
+                float* d = s_sh + r * stride + (e0 - r * M3);
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
+            }
+        } else {
+            for (int f = threadIdx.x; f < n; f += blockDim.x) {
+                const int r = f / M3;
+                s_sh[r * stride + f - r * M3] = src[f];
+            }
+        }
+        __syncthreads();
+    }
     uint32_t tiles = 0, stc = 0;
-    if (idx < a.P) preprocess_one(a, idx, tiles, stc);
+    if (idx < a.P)
+        preprocess_one(a, idx, tiles, stc, staged ? s_sh + threadIdx.x * stride : nullptr);
     unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -98,7 +129,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     if (threadIdx.x < 3) {
         const int k = threadIdx.x;
         const unsigned long long t = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
-        if (t) atomicAdd(a.totals + 3 * (blockIdx.x % TOTAL_SLOTS) + k, t);
+        if (t) atomicAdd(a.totals + TOTAL_STRIDE * (blockIdx.x % TOTAL_SLOTS) + k, t);
     }
 }
 
@@ -135,7 +166,8 @@ void launch_recolor(int P, const int* radii_src, const Rec* src, const float* co
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P == 0) return;
-    hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
+    const size_t lds = (a.shs && !a.colors_precomp) ? sizeof(float) * 256 * (size_t)(3 * a.M + 1) : 0;
+    hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), lds, s, a);
 }
 
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s) {
