@@ -202,6 +202,10 @@ def main():
     ap.add_argument("--ply", default=None, help="a trained scene (GaussianModel.save_ply layout) instead of cfg2's "
                                                "synthetic cloud; camera looks at the foreground's median from "
                                                "2x its extent, 1920x1080, focal 1400")
+    ap.add_argument("--colmap", default=None, help="with --ply: a NeRF-OSR / COLMAP scene folder (sparse/0 model); "
+                                                  "renders from its training camera --view at the reference's "
+                                                  "default resolution rule")
+    ap.add_argument("--view", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -224,6 +228,11 @@ def main():
 
     if args.ply:
         cam, gs_cpu, cfg = scenes.ply_config(args.ply)
+        if args.colmap:
+            from gsr import colmap as gcm
+            train, _, _ = gcm.read_nerf_osr_info(args.colmap)
+            cam = gcm.render_camera(train[args.view % len(train)])
+            cfg = dict(cfg, W=cam.image_width, H=cam.image_height)
     else:
         cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
     W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
@@ -303,7 +312,9 @@ def main():
         "metric": METRIC, "value": round(world * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"{args.config}: {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view"
+        "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
+                                                                       else "") if args.ply else args.config)
+                               + f": {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view"
                    + (", RCCL grad all-reduce" if world > 1 else ""), "gaussians": P, "width": W, "height": H,
                    "sh_degree": deg, "num_rendered": R, "visible": Pv, "parallelism": f"views x{world}"},
         "roofline": roofline,
