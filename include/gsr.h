@@ -17,6 +17,10 @@
  *   gsr_forward_reuse  colours-only re-render over an earlier call's geometry (the 6-10
  *                      same-geometry calls of gaussian_renderer/__init__.py:160-264)
  *   gsr_knn_mean_dist  submodules/simple-knn/spatial.cu:14-26 distCUDA2
+ *   gsr_forward_channels / gsr_backward_channels
+ *                      the 6-10 same-geometry rasterizer calls of one render()
+ *                      (gaussian_renderer/__init__.py:160-264) as ONE composite of all
+ *                      their colour channels (multi-channel alternative)
  *
  * Error convention: every function returns 0 on success and a negative GSR_E* code on
  * failure; gsr_last_error() returns a thread-local message.  The reference's conditions
@@ -84,6 +88,32 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
                  void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
                  float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
                  float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream);
+
+/* Multi-channel forward: gsr_forward's geometry (preprocess, depth sort, binning) once,
+ * then one composite of nch per-Gaussian feature channels (16 per tile pass).  features is
+ * [P][feature_stride] floats, 16-B aligned, feature_stride >= nch and a multiple of 4;
+ * background [nch]; out [nch,H,W].  Channel c of out equals a gsr_forward call whose
+ * colors_precomp holds feature c (bit for bit; the blend decisions do not depend on the
+ * colours).  The buffers pair with gsr_backward_channels. */
+int gsr_forward_channels(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
+                         void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int nch,
+                         int feature_stride, const float* features, const float* background, int width, int height,
+                         const float* means3D, const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                         int prefiltered, float* out, int* radii, void* stream, int* num_rendered);
+
+/* Backward of gsr_forward_channels: dL_dout [nch,H,W] -> dL_dfeatures [P][feature_stride]
+ * (padding columns zero) and the geometric gradients of gsr_backward (their sum over the
+ * channels' separate calls). */
+int gsr_backward_channels(int P, int nch, int feature_stride, const float* features, int R, const float* background,
+                          int width, int height, const float* means3D, const float* scales, float scale_modifier,
+                          const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                          const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                          const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
+                          const float* dL_dout, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
+                          float* dL_dfeatures, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
+                          void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -211,6 +211,35 @@ struct StageTimer {
 
 }  // namespace
 
+namespace {
+// Multi-channel composite (gsr_render_mc.hip): nch feature channels per Gaussian, rows of
+// fstride floats (a multiple of 4); composited in groups of MC_GROUP channels.
+struct McSpec {
+    int nch, fstride;
+    const float* features;
+    const float* bg;     // [nch]
+    float* out;          // forward: [nch][H][W]
+    const float* dL_dout;  // backward: [nch][H][W]
+    float* dL_dfeat;       // backward: [P][fstride]
+};
+constexpr int MC_GROUP = 16;
+
+gsr::RenderMcArgs mc_args(int W, int H, unsigned gx, unsigned gy, const uint2* ranges, const uint32_t* point_list,
+                          const gsr::Rec* rec, const uint32_t* order, const uint32_t* nheavy, const McSpec& mc, int c0) {
+    gsr::RenderMcArgs m{};
+    m.W = W; m.H = H; m.grid_x = gx; m.grid_y = gy;
+    m.ranges = ranges; m.point_list = point_list; m.rec = rec;
+    m.feat = reinterpret_cast<const float4*>(mc.features + c0);
+    m.fstride4 = mc.fstride / 4;
+    m.fstride = mc.fstride;
+    m.nch = std::min(MC_GROUP, mc.nch - c0);
+    m.bg = mc.bg + c0;
+    m.order = order;
+    m.nheavy = nheavy;
+    return m;
+}
+}  // namespace
+
 extern "C" {
 
 const char* gsr_last_error(void) { return g_err.c_str(); }
@@ -268,18 +297,18 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     return GSR_OK;
 }
 
-int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer, void* binning_ctx,
-                gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M, const float* background, int width,
-                int height, const float* means3D, const float* shs, const float* colors_precomp,
-                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
-                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
-                float tan_fovx, float tan_fovy, int prefiltered, float* out_color, int* radii, void* stream_,
-                int* num_rendered) {
+static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
+                        void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M,
+                        const float* background, int width, int height, const float* means3D, const float* shs,
+                        const float* colors_precomp, const float* opacities, const float* scales, float scale_modifier,
+                        const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                        const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy, int prefiltered,
+                        float* out_color, int* radii, void* stream_, int* num_rendered, const McSpec* mc) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     if (num_rendered) *num_rendered = 0;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_forward: bad sizes P=%d W=%d H=%d", P, width, height);
     if (!geometry_buffer || !binning_buffer || !image_buffer) return fail(GSR_E_ARG, "gsr_forward: missing buffer callbacks");
-    if (!colors_precomp && !shs && P > 0)
+    if (!colors_precomp && !shs && P > 0 && !mc)
         return fail(GSR_E_ARG, "For non-RGB, provide precomputed Gaussian colors!");
     if (!cov3D_precomp && (!scales || !rotations) && P > 0)
         return fail(GSR_E_ARG, "gsr_forward: need scales+rotations or cov3D_precomp");
@@ -416,11 +445,70 @@ int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn
         gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), at<uint32_t>(img, il.nheavy),
                                gsr::FWD_HEAVY_BITS, s);
         HIP_OK(hipMemsetAsync(ra.tile_nmax, 0, 4 * (size_t)T, s));
-        gsr::launch_render_fwd(ra, s);
+        if (!mc) {
+            gsr::launch_render_fwd(ra, s);
+        } else {
+            for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
+                gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, ranges, point_list, pa.rec, ra.order, ra.nheavy, *mc, c0);
+                ma.out = mc->out + (size_t)c0 * width * height;
+                if (c0 == 0) {  // the other groups would write the same values
+                    ma.final_T = ra.final_T;
+                    ma.n_contrib = ra.n_contrib;
+                    ma.tile_nmax = ra.tile_nmax;
+                }
+                gsr::launch_render_fwd_mc(ma, s);
+            }
+        }
     }
     GSR_LAUNCH_CHECK();
     if (num_rendered) *num_rendered = (int)R;
     return GSR_OK;
+}
+
+int gsr_forward(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer, void* binning_ctx,
+                gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M, const float* background, int width,
+                int height, const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier, const float* rotations,
+                const float* cov3D_precomp, const float* viewmatrix, const float* projmatrix, const float* cam_pos,
+                float tan_fovx, float tan_fovy, int prefiltered, float* out_color, int* radii, void* stream_,
+                int* num_rendered) {
+    return forward_impl(geometry_buffer, geometry_ctx, binning_buffer, binning_ctx, image_buffer, image_ctx, P, D, M,
+                        background, width, height, means3D, shs, colors_precomp, opacities, scales, scale_modifier,
+                        rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                        out_color, radii, stream_, num_rendered, nullptr);
+}
+
+static int check_mc(const char* fn, int nch, int fstride, const float* features) {
+    if (nch <= 0 || fstride < nch || (fstride & 3) != 0)
+        return fail(GSR_E_ARG, "%s: need 0 < nch <= feature_stride, feature_stride a multiple of 4 (nch=%d stride=%d)",
+                    fn, nch, fstride);
+    if ((reinterpret_cast<uintptr_t>(features) & 15u) != 0) return fail(GSR_E_ARG, "%s: features must be 16-B aligned", fn);
+    return GSR_OK;
+}
+
+int gsr_forward_channels(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
+                         void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int nch,
+                         int feature_stride, const float* features, const float* background, int width, int height,
+                         const float* means3D, const float* opacities, const float* scales, float scale_modifier,
+                         const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                         const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                         int prefiltered, float* out, int* radii, void* stream_, int* num_rendered) {
+    if (num_rendered) *num_rendered = 0;
+    if (P > 0 || features) {
+        const int e = check_mc("gsr_forward_channels", nch, feature_stride, features);
+        if (e != GSR_OK) return e;
+    }
+    if (!background || !out) return fail(GSR_E_ARG, "gsr_forward_channels: missing background or output");
+    McSpec mc{nch, feature_stride, features, background, out, nullptr, nullptr};
+    if (P == 0) {  // background everywhere (the reference's P == 0 forward renders nothing)
+        hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+        HIP_OK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)nch * width * height, s));
+        return GSR_OK;
+    }
+    return forward_impl(geometry_buffer, geometry_ctx, binning_buffer, binning_ctx, image_buffer, image_ctx, P, 0, 0,
+                        background, width, height, means3D, nullptr, nullptr, opacities, scales, scale_modifier,
+                        rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                        nullptr, radii, stream_, num_rendered, &mc);
 }
 
 int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const void* src_geom_buffer,
@@ -465,13 +553,14 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     return GSR_OK;
 }
 
-int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
-                 const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
-                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
-                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
-                 void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
-                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
-                 float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream_) {
+static int backward_impl(int P, int D, int M, int R, const float* background, int width, int height,
+                         const float* means3D, const float* shs, const float* colors_precomp, const float* scales,
+                         float scale_modifier, const float* rotations, const float* cov3D_precomp,
+                         const float* viewmatrix, const float* projmatrix, const float* campos, float tan_fovx,
+                         float tan_fovy, const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
+                         const float* dL_dpix, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
+                         float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                         float* dL_drot, void* stream_, const McSpec* mc) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     if (P < 0 || R < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_backward: bad sizes");
     if (P == 0) return GSR_OK;
@@ -490,6 +579,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     {
         GSR_STAGE(ST_BWD_ZERO);
         HIP_OK(hipMemsetAsync(acc, 0, sizeof(float) * gsr::ACC_STRIDE * (size_t)P, s));
+        if (mc) HIP_OK(hipMemsetAsync(mc->dL_dfeat, 0, sizeof(float) * (size_t)mc->fstride * P, s));
     }
 
     if (R > 0) {
@@ -510,7 +600,20 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
             GSR_STAGE(ST_RENDER_BWD);
             gsr::launch_tile_order(gx * gy, ra.ranges, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8, gsr::BWD_HEAVY_BITS, s);
-            gsr::launch_render_bwd(ra, s);
+            if (!mc) {
+                gsr::launch_render_bwd(ra, s);
+            } else {
+                for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
+                    gsr::RenderMcArgs ma = mc_args(width, height, gx, gy, ra.ranges, ra.point_list, ra.rec, ra.order,
+                                                   ra.nheavy, *mc, c0);
+                    ma.final_T = const_cast<float*>(ra.final_T);
+                    ma.n_contrib = const_cast<uint32_t*>(ra.n_contrib);
+                    ma.dL_dout = mc->dL_dout + (size_t)c0 * width * height;
+                    ma.acc = acc;
+                    ma.dL_dfeat = mc->dL_dfeat + c0;
+                    gsr::launch_render_bwd_mc(ma, s);
+                }
+            }
         }
         GSR_LAUNCH_CHECK();
     }
@@ -531,6 +634,39 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     }
     GSR_LAUNCH_CHECK();
     return GSR_OK;
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
+                 const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy, const int* radii,
+                 void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
+                 float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream_) {
+    if (!dL_dcolor && P > 0) return fail(GSR_E_ARG, "gsr_backward: dL_dcolor required");
+    return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, scales, scale_modifier,
+                         rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                         geom_buffer, binning_buffer, img_buffer, dL_dpix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor,
+                         dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, stream_, nullptr);
+}
+
+int gsr_backward_channels(int P, int nch, int feature_stride, const float* features, int R, const float* background,
+                          int width, int height, const float* means3D, const float* scales, float scale_modifier,
+                          const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                          const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                          const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
+                          const float* dL_dout, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
+                          float* dL_dfeatures, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
+                          void* stream_) {
+    if (P == 0) return GSR_OK;
+    const int e = check_mc("gsr_backward_channels", nch, feature_stride, features);
+    if (e != GSR_OK) return e;
+    if (!background || !dL_dout || !dL_dfeatures) return fail(GSR_E_ARG, "gsr_backward_channels: missing buffers");
+    McSpec mc{nch, feature_stride, features, background, nullptr, dL_dout, dL_dfeatures};
+    return backward_impl(P, 0, 0, R, background, width, height, means3D, nullptr, nullptr, scales, scale_modifier,
+                         rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
+                         geom_buffer, binning_buffer, img_buffer, nullptr, dL_dmean2D, dL_dconic, dL_dopacity, nullptr,
+                         dL_dmean3D, dL_dcov3D, nullptr, dL_dscale, dL_drot, stream_, &mc);
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,

@@ -144,6 +144,30 @@ struct RenderBwdArgs {
 };
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 
+// Multi-channel tile passes (gsr_render_mc.hip): one group of <= 16 feature channels.
+struct RenderMcArgs {
+    int W, H;
+    unsigned grid_x, grid_y;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const Rec* rec;
+    const float4* feat;  // group's first channel; row stride fstride4 float4
+    int fstride4, fstride;
+    int nch;             // channels in this group
+    const float* bg;     // [nch]
+    float* out;          // forward: [nch][H][W]
+    float* final_T;      // forward: written when non-null
+    uint32_t* n_contrib;
+    uint32_t* tile_nmax;  // forward: atomicMax when non-null
+    const uint32_t* order;
+    const uint32_t* nheavy;
+    const float* dL_dout;  // backward: [nch][H][W]
+    float* acc;            // backward: [P][ACC_STRIDE], slots 0..5
+    float* dL_dfeat;       // backward: group's first channel, row stride fstride
+};
+void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
+void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);
+
 struct PreprocessBwdArgs {
     int P, D, M;
     const float* means3D;

@@ -58,9 +58,11 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
     float3 rgb;
     if (a.colors_precomp) {
         rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-    } else {
+    } else if (a.shs) {
         const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, sh_row);
         rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
+    } else {
+        rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record
     }
     const float opacity = a.opacities[idx];
     Rec r;

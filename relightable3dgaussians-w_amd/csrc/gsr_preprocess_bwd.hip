@@ -96,9 +96,11 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     a.dL_dmean2D[3 * idx + 2] = 0.f;
     *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
     a.dL_dopacity[idx] = dop;
-    a.dL_dcolor[3 * idx + 0] = dcol0;
-    a.dL_dcolor[3 * idx + 1] = dcol1;
-    a.dL_dcolor[3 * idx + 2] = dcol2;
+    if (a.dL_dcolor) {  // absent for the multi-channel composite (its features have their own gradient)
+        a.dL_dcolor[3 * idx + 0] = dcol0;
+        a.dL_dcolor[3 * idx + 1] = dcol1;
+        a.dL_dcolor[3 * idx + 2] = dcol2;
+    }
 
     float* dcov = a.dL_dcov3D + 6 * idx;
     float* dsh = a.dL_dsh ? s_sh + threadIdx.x * sh_stride : nullptr;  // LDS row, written back by the caller

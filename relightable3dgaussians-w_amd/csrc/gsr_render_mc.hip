@@ -1,0 +1,335 @@
+// gsr_render_mc.hip -- multi-channel tile passes: one forward / backward composite of up
+// to 16 per-Gaussian feature channels over one geometry.
+//
+// render() (gaussian_renderer/__init__.py:160-264) rasterizes the same Gaussians 6-10 times
+// with different colours (image, diffuse, specular, depth, normal, alpha, ...).  Every call
+// repeats the per-(pixel, Gaussian) alpha evaluation, the transmittance recurrence and the
+// backward's geometric gradient reduction; only the three colour FMAs differ.  Here all
+// channels are composited in one pass: alpha, T and the blend decisions are evaluated once
+// and applied to every channel.  The blend arithmetic per channel is the forward tile
+// pass's (gsr_render_fwd.hip), so each channel equals what a separate 3-channel call of the
+// same features produces, bit for bit; the backward's geometric gradients are the sum of
+// the separate calls' (the recurrence is carried as dot products over all channels).
+//
+// Layout: features [P][fstride] floats, fstride a multiple of 4; the pass handles one group
+// of <= 16 channels (NC4 float4 per Gaussian), the host loops over groups.  Per batch of 64
+// list entries the group's features go to LDS with the records and survivors read them by
+// broadcast ds_read_b128.  Backward: 6 geometric sums + 4 NC4 feature sums reduce with the
+// same permlane32 / permlane16 / DPP tree as the 3-channel pass; geometric sums go to the
+// Gaussian's accumulator line, feature sums to dL/dfeatures (one atomic per value per
+// (tile, Gaussian)).
+#include "gsr_kernels.hpp"
+#include "gsr_tile.hpp"
+
+namespace gsr {
+
+template <int NC4>
+__device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
+    constexpr int NCH = 4 * NC4;
+    WaveTile wt;
+    wt.init(tile, a.grid_x, a.W, a.H);
+    const int lane = threadIdx.x;
+    const uint2 range = a.ranges[tile];
+    const int n = (int)(range.y - range.x);
+
+    const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    __shared__ float4 s_a[64], s_b[64];
+    __shared__ float4 s_f[NC4][64];
+    __shared__ uint32_t s_q[64];
+    float T[4], Cc[4][NCH], lim[4];
+    uint32_t last[4];
+    uint32_t live = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        T[q] = 1.f;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) Cc[q][c] = 0.f;
+        last[q] = 0;
+        const bool in = wt.inside(q, a.W, a.H);
+        lim[q] = in ? 1.0f / 255.0f : __builtin_inff();
+        if (((qallow >> q) & 1u) && __ballot(in)) live |= 1u << q;
+    }
+    for (int b0 = 0; b0 < n && live; b0 += 64) {
+        const int j = b0 + lane;
+        uint32_t qm = 0;
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+        float4 f[NC4];
+#pragma unroll
+        for (int g = 0; g < NC4; g++) f[g] = ra;
+        if (j < n) {
+            const uint32_t id = a.point_list[range.x + j];
+            const Rec r = a.rec[id];
+            qm = wt.reach(r, (uint32_t)j, nullptr);
+            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
+            rb = make_float4(-0.5f * r.b.x, r.b.y, 0.f, 0.f);
+#pragma unroll
+            for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
+        }
+        wave_lds_sync();
+        s_a[lane] = ra;
+        s_b[lane] = rb;
+        s_q[lane] = qm;
+#pragma unroll
+        for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
+        wave_lds_sync();
+        uint64_t todo = __ballot((qm & live) != 0);
+        while (todo && live) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const float4 A = s_a[k], B = s_b[k];
+            float4 F[NC4];
+#pragma unroll
+            for (int g = 0; g < NC4; g++) F[g] = s_f[g][k];
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[k]) & live;
+            const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!((m >> q) & 1u)) continue;
+                const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
+                const float power = gauss_power(A.z, A.w, B.x, dx, dy);
+                const float alpha = fminf(0.99f, B.y * tile_exp(power));
+                const bool hit = !(power > 0.0f) && alpha >= lim[q];
+                const float test_T = T[q] * (1 - alpha);
+                const bool sat = hit && test_T < 0.0001f;
+                const bool blend = hit && !sat;
+                const float w = blend ? alpha * T[q] : 0.f;
+#pragma unroll
+                for (int g = 0; g < NC4; g++) {
+                    Cc[q][4 * g + 0] += F[g].x * w;
+                    Cc[q][4 * g + 1] += F[g].y * w;
+                    Cc[q][4 * g + 2] += F[g].z * w;
+                    Cc[q][4 * g + 3] += F[g].w * w;
+                }
+                T[q] = blend ? test_T : T[q];
+                last[q] = blend ? pos1 : last[q];
+                lim[q] = sat ? __builtin_inff() : lim[q];
+                if (__ballot(sat) && !__ballot(lim[q] < 1.f)) live &= ~(1u << q);
+            }
+        }
+    }
+    const int HW = a.H * a.W;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (((qallow >> q) & 1u) && wt.inside(q, a.W, a.H)) {
+            const int pix = wt.pixel(q, a.W);
+            if (a.final_T) {
+                a.final_T[pix] = T[q];
+                a.n_contrib[pix] = last[q];
+            }
+#pragma unroll
+            for (int c = 0; c < NCH; c++)
+                if (c < a.nch) a.out[c * HW + pix] = Cc[q][c] + T[q] * a.bg[c];
+        }
+    }
+    if (a.tile_nmax) {
+        uint32_t nm = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t mq = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
+            nm = mq > nm ? mq : nm;
+        }
+        if (lane == 0) atomicMax(&a.tile_nmax[tile], nm);
+    }
+}
+
+template <int NC4>
+__device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
+    constexpr int NCH = 4 * NC4;
+    constexpr int V = 6 + NCH;        // 6 geometric sums + the feature sums
+    constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
+    constexpr int NQ = (NP + 1) / 2;  // after the permlane16 stage: registers reduced by DPP rows
+    WaveTile wt;
+    wt.init(tile, a.grid_x, a.W, a.H);
+    const int lane = threadIdx.x;
+    const uint2 range = a.ranges[tile];
+    const int HW = a.H * a.W;
+
+    const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
+    __shared__ float4 s_a[64], s_b[64];
+    __shared__ float4 s_f[NC4][64];
+    __shared__ uint2 s_q[64];  // (quadrant mask, Gaussian id)
+    float T[4], Tb[4], dp[4][NCH], AD[4], LD[4], la[4];
+    uint32_t last[4], qlim[4];
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const bool in = wt.inside(q, a.W, a.H);
+        const int pix = in ? wt.pixel(q, a.W) : 0;
+        const float Tf = in ? a.final_T[pix] : 0.f;
+        last[q] = in ? a.n_contrib[pix] : 0u;
+        float bd = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            dp[q][c] = (in && c < a.nch) ? a.dL_dout[c * HW + pix] : 0.f;
+            bd = c < a.nch ? __builtin_fmaf(a.bg[c], dp[q][c], bd) : bd;
+        }
+        T[q] = Tf;
+        Tb[q] = -Tf * bd;
+        AD[q] = LD[q] = la[q] = 0.f;
+        qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
+        nmax = qlim[q] > nmax ? qlim[q] : nmax;
+    }
+    const int row = lane >> 4, col = lane & 15;
+    const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
+    const int vidx = (col < NQ && 4 * col + vrow < V) ? 4 * col + vrow : -1;
+    const float vscale = vidx == 0 ? 0.5f * a.W : vidx == 1 ? 0.5f * a.H : (vidx >= 2 && vidx <= 4) ? -0.5f : 1.f;
+    const bool vop = vidx >= 0 && vidx <= 4;
+    const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
+
+    for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
+        const uint32_t i = b0 + lane;
+        const uint32_t p = nmax - 1u - i;
+        uint32_t id = 0, qm = 0;
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
+        float4 f[NC4];
+#pragma unroll
+        for (int g = 0; g < NC4; g++) f[g] = ra;
+        if (i < nmax) {
+            id = a.point_list[range.x + p];
+            const Rec r = a.rec[id];
+            qm = wt.reach(r, p, qlim);
+            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
+            rb = make_float4(-0.5f * r.b.x, r.b.y, 0.f, 0.f);
+#pragma unroll
+            for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
+        }
+        wave_lds_sync();
+        s_a[lane] = ra;
+        s_b[lane] = rb;
+        s_q[lane] = make_uint2(qm, id);
+#pragma unroll
+        for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
+        wave_lds_sync();
+        uint64_t todo = __ballot(qm != 0);
+        while (todo) {
+            const int k = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            const float4 A = s_a[k], B = s_b[k];
+            const uint2 Q2 = s_q[k];
+            float F[NCH];
+#pragma unroll
+            for (int g = 0; g < NC4; g++) {
+                const float4 v = s_f[g][k];
+                F[4 * g] = v.x;
+                F[4 * g + 1] = v.y;
+                F[4 * g + 2] = v.z;
+                F[4 * g + 3] = v.w;
+            }
+            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)Q2.x);
+            const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
+            const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
+            float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f;
+            float SF[NCH];
+#pragma unroll
+            for (int c = 0; c < NCH; c++) SF[c] = 0.f;
+            bool any = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!((m >> q) & 1u)) continue;
+                const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
+                const float power = gauss_power(ka, kb, kc, dx, dy);
+                const float G = tile_exp(power);
+                const float alpha = fminf(0.99f, op * G);
+                const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();
+                if (act == 0ull) continue;
+                any = true;
+                const float ae = sel(act, alpha, 0.f);
+                const float Ge = sel(act, G, 0.f);
+                const float inv = __builtin_amdgcn_rcpf(1.f - ae);
+                const float Tn = T[q] * inv;
+                const float dch = ae * Tn;
+                float cdp = F[0] * dp[q][0];
+#pragma unroll
+                for (int c = 1; c < NCH; c++) cdp = __builtin_fmaf(F[c], dp[q][c], cdp);
+                const float nAD = __builtin_fmaf(la[q], LD[q] - AD[q], AD[q]);
+                const float dLda = __builtin_fmaf(Tn, cdp - nAD, inv * Tb[q]);
+                const float Gd = Ge * dLda;
+                S5 += Gd;
+                const float wdx = Gd * dx, wdy = Gd * dy;
+                M1 += wdx;
+                M2 += wdy;
+                S2 = __builtin_fmaf(wdx, dx, S2);
+                S3 = __builtin_fmaf(wdx, dy, S3);
+                S4 = __builtin_fmaf(wdy, dy, S4);
+#pragma unroll
+                for (int c = 0; c < NCH; c++) SF[c] = __builtin_fmaf(dch, dp[q][c], SF[c]);
+                T[q] = Tn;
+                AD[q] = sel(act, nAD, AD[q]);
+                LD[q] = sel(act, cdp, LD[q]);
+                la[q] = sel(act, alpha, la[q]);
+            }
+            if (any) {
+                float S[2 * NP];
+                S[0] = __builtin_fmaf(ka, M1 + M1, kb * M2);
+                S[1] = __builtin_fmaf(kc, M2 + M2, kb * M1);
+                S[2] = S2;
+                S[3] = S3;
+                S[4] = S4;
+                S[5] = S5;
+#pragma unroll
+                for (int c = 0; c < NCH; c++) S[6 + c] = SF[c];
+#pragma unroll
+                for (int c = V; c < 2 * NP; c++) S[c] = 0.f;
+                float Pp[2 * NQ];
+#pragma unroll
+                for (int t = 0; t < NP; t++) Pp[t] = swap32_sum(S[2 * t], S[2 * t + 1]);
+#pragma unroll
+                for (int t = NP; t < 2 * NQ; t++) Pp[t] = 0.f;
+                float v = 0.f;
+#pragma unroll
+                for (int t = 0; t < NQ; t++) {
+                    const float Qt = row_sum(swap16_sum(Pp[2 * t], Pp[2 * t + 1]));
+                    v = col == t ? Qt : v;
+                }
+                v *= vop ? op * vscale : vscale;
+                if (v != 0.f) {
+                    const uint32_t gid = Q2.y;
+                    if (vidx >= 0 && vidx < 6) atomicAdd(a.acc + (size_t)gid * ACC_STRIDE + vidx, v);
+                    else if (vfeat) atomicAdd(a.dL_dfeat + (size_t)gid * a.fstride + (vidx - 6), v);
+                }
+            }
+        }
+    }
+}
+
+template <int NC4>
+__global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
+    unsigned tile;
+    uint32_t qallow;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_fwd_mc_tile<NC4>(a, tile, qallow);
+}
+
+template <int NC4>
+__global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
+    unsigned tile;
+    uint32_t qallow;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_bwd_mc_tile<NC4>(a, tile, qallow);
+}
+
+void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
+    const unsigned ntile = a.grid_x * a.grid_y;
+    if (ntile == 0 || a.nch <= 0) return;
+    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    switch ((a.nch + 3) / 4) {
+        case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_render_fwd_mc<3>, grid, dim3(64), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_render_fwd_mc<4>, grid, dim3(64), 0, s, a); break;
+    }
+}
+
+void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
+    const unsigned ntile = a.grid_x * a.grid_y;
+    if (ntile == 0 || a.nch <= 0) return;
+    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    switch ((a.nch + 3) / 4) {
+        case 1: hipLaunchKernelGGL(k_render_bwd_mc<1>, grid, dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_render_bwd_mc<2>, grid, dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_render_bwd_mc<3>, grid, dim3(64), 0, s, a); break;
+        default: hipLaunchKernelGGL(k_render_bwd_mc<4>, grid, dim3(64), 0, s, a); break;
+    }
+}
+
+}  // namespace gsr

@@ -128,6 +128,90 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
 
 
+def pack_features(features):
+    """[P, nch] per-Gaussian channels -> contiguous [P, stride] float32, stride = nch rounded up
+    to a multiple of 4 (the multi-channel tile passes read 16-B rows)."""
+    P, nch = features.shape
+    stride = (nch + 3) // 4 * 4
+    if stride == nch and features.dtype == torch.float32 and features.is_contiguous() and \
+            features.data_ptr() % 16 == 0:
+        return features
+    out = torch.zeros((P, stride), dtype=torch.float32, device=features.device)
+    out[:, :nch] = features
+    return out
+
+
+def rasterize_gaussians_channels(background, means3D, features, opacity, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
+                                 campos, prefiltered):
+    """All channels of several same-geometry rasterizer calls in one composite
+    (gsr_forward_channels): background [nch], features [P, nch] ->
+    (num_rendered, out[nch,H,W], radii, geomBuffer, binningBuffer, imgBuffer, packed features)."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    _lib.require_gpu_tensor(means3D, "means3D")
+    dev = means3D.device
+    P, H, W = means3D.size(0), int(image_height), int(image_width)
+    nch = features.size(1)
+    if features.size(0) != P or background.numel() != nch:
+        raise ValueError(f"features must be [P, nch] and background [nch] (P={P}, features {tuple(features.shape)}, "
+                         f"background {tuple(background.shape)})")
+    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    bs = _lib.BufferSet(dev)
+    feat = pack_features(_f32(features))
+    out = torch.empty((nch, H, W), dtype=torch.float32, device=dev)
+    keep = [_f32(x) for x in (background, means3D, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                              campos)]
+    bg_, m_, op_, sc_, rot_, cov_, vm_, pm_, cp_ = keep
+    for name, t in (("background", bg_), ("features", feat), ("viewmatrix", vm_), ("projmatrix", pm_),
+                    ("campos", cp_)):
+        _lib.require_gpu_tensor(t, name)
+    rc = _lib.ResizeContexts(bs)
+    nr = C.c_int(0)
+    try:
+        ret = _lib.lib().gsr_forward_channels(
+            _lib.RESIZE, rc.ctx[0], _lib.RESIZE, rc.ctx[1], _lib.RESIZE, rc.ctx[2], P, nch, feat.size(1),
+            _lib.fptr(feat), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(op_), _lib.fptr(sc_),
+            float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
+            float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out.data_ptr(), radii.data_ptr(),
+            _lib.stream_of(dev), C.byref(nr))
+    finally:
+        rc.close()
+    _lib.check(ret, "rasterize_gaussians_channels")
+    return int(nr.value), out, radii, bs.bufs[0], bs.bufs[1], bs.bufs[2], feat
+
+
+def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch, scales, rotations, scale_modifier,
+                                          cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout, campos,
+                                          geomBuffer, R, binningBuffer, imageBuffer):
+    """Backward of rasterize_gaussians_channels (gsr_backward_channels) -> (dL_dmeans2D,
+    dL_dfeatures [P, nch], dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)."""
+    _lib.require_gpu_tensor(means3D, "means3D")
+    dev = means3D.device
+    P = means3D.size(0)
+    H, W = dL_dout.size(1), dL_dout.size(2)
+    alloc = torch.zeros if P == 0 else torch.empty
+    f = dict(dtype=torch.float32, device=dev)
+    dL_dmeans2D, dL_dconic, dL_dopacity = alloc((P, 3), **f), alloc((P, 2, 2), **f), alloc((P, 1), **f)
+    dL_dfeat = alloc((P, feat.size(1)), **f)
+    dL_dmeans3D, dL_dcov3D = alloc((P, 3), **f), alloc((P, 6), **f)
+    dL_dscales, dL_drotations = alloc((P, 3), **f), alloc((P, 4), **f)
+    if P != 0:
+        keep = [_f32(x) for x in (background, means3D, scales, rotations, cov3D_precomp, viewmatrix, projmatrix,
+                                  campos, dL_dout)]
+        bg_, m_, sc_, rot_, cov_, vm_, pm_, cp_, dout_ = keep
+        ptr = lambda t: t.data_ptr() if t.numel() else None
+        ret = _lib.lib().gsr_backward_channels(
+            P, int(nch), feat.size(1), _lib.fptr(feat), int(R), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(sc_),
+            float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
+            float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
+            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(), dL_dopacity.data_ptr(),
+            dL_dfeat.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), dL_dscales.data_ptr(),
+            dL_drotations.data_ptr(), _lib.stream_of(dev))
+        _lib.check(ret, "rasterize_gaussians_channels_backward")
+    return (dL_dmeans2D, dL_dfeat[:, :nch], dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)
+
+
 def mark_visible(means3D, viewmatrix, projmatrix):
     """rasterize_points.cu:194-213 markVisible -> bool[P]."""
     _lib.require_gpu_tensor(means3D, "means3D")

@@ -15,7 +15,7 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians", "_RasterizeGaussians",
-           "geometry_cache"]
+           "geometry_cache", "rasterize_channels"]
 
 
 class _GeometryCache:
@@ -142,6 +142,47 @@ class _RasterizeGaussians(torch.autograd.Function):
         return g_means3D, g_means2D, g_sh, g_colors, g_opacities, g_scales, g_rotations, g_cov3D, None
 
 
+def rasterize_channels(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
+                       raster_settings):
+    """Composite of all per-Gaussian channels `features` [P, nch] over one geometry
+    (gsr_forward_channels): returns (image [nch, H, W], radii).  Channel c equals the
+    reference rasterizer's output for colours holding channel c with background[c]."""
+    return _RasterizeChannels.apply(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp,
+                                    background, raster_settings)
+
+
+class _RasterizeChannels(torch.autograd.Function):
+    """Autograd node of the multi-channel composite.  Gradients: features, the geometry
+    inputs and means2D (summed over the channels, as autograd sums them over the separate
+    calls render() makes); none for background (the reference returns none for bg)."""
+
+    @staticmethod
+    def forward(ctx, means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
+                raster_settings):
+        s = raster_settings
+        num_rendered, out, radii, geom_buf, bin_buf, img_buf, feat = _C.rasterize_gaussians_channels(
+            background, means3D, features, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, s.campos, s.prefiltered)
+        ctx.raster_settings = s
+        ctx.num_rendered = num_rendered
+        ctx.nch = features.shape[1]
+        ctx.save_for_backward(background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf,
+                              img_buf)
+        return out, radii
+
+    @staticmethod
+    def backward(ctx, grad_out, _grad_radii):
+        s = ctx.raster_settings
+        background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf, img_buf = \
+            ctx.saved_tensors
+        (g_means2D, g_feat, g_opacities, g_means3D, g_cov3D, g_scales, g_rotations) = \
+            _C.rasterize_gaussians_channels_backward(background, means3D, radii, feat, ctx.nch, scales, rotations,
+                                                     s.scale_modifier, cov3Ds_precomp, s.viewmatrix, s.projmatrix,
+                                                     s.tanfovx, s.tanfovy, grad_out, s.campos, geom_buf,
+                                                     ctx.num_rendered, bin_buf, img_buf)
+        return g_means3D, g_means2D, g_feat, g_opacities, g_scales, g_rotations, g_cov3D, None, None
+
+
 class GaussianRasterizer(nn.Module):
     """reference __init__.py:146-195"""
 
@@ -165,3 +206,29 @@ class GaussianRasterizer(nn.Module):
         pick = lambda t: empty if t is None else t
         return rasterize_gaussians(means3D, means2D, pick(shs), pick(colors_precomp), opacities, pick(scales),
                                    pick(rotations), pick(cov3D_precomp), self.raster_settings)
+
+    def render_channels(self, means3D, means2D, opacities, colors, backgrounds=None, scales=None, rotations=None,
+                        cov3D_precomp=None):
+        """Several same-geometry rasterizations in one composite (the extension behind
+        render()'s 6-10 calls).  colors: list of [P, k_i] tensors;
+        backgrounds: list of [k_i] tensors (default: raster_settings.bg for 3-channel entries,
+        zeros otherwise).  Returns ([image_i [k_i, H, W]], radii); image_i equals
+        forward(colors_precomp=colors[i]) with that background, and gradients flow to every
+        colour tensor and the geometry as through separate calls."""
+        if ((scales is None or rotations is None) and cov3D_precomp is None) or \
+                ((scales is not None or rotations is not None) and cov3D_precomp is not None):
+            raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
+        s = self.raster_settings
+        ks = [int(c.shape[1]) for c in colors]
+        if backgrounds is None:
+            backgrounds = [None] * len(colors)
+        bgs = []
+        for k, b in zip(ks, backgrounds):
+            if b is None:
+                b = s.bg if (k == 3 and s.bg.numel() == 3) else torch.zeros(k, device=means3D.device)
+            bgs.append(b.reshape(-1).float())
+        empty = torch.Tensor([])
+        pick = lambda t: empty if t is None else t
+        out, radii = rasterize_channels(means3D, means2D, torch.cat([c.float() for c in colors], 1), opacities,
+                                        pick(scales), pick(rotations), pick(cov3D_precomp), torch.cat(bgs), s)
+        return list(torch.split(out, ks, 0)), radii
