@@ -114,8 +114,9 @@ def bench_relight(args, dev):
     """cfg3: the relightable render() step -- fused PBR shade of the foreground
     Gaussians, then render()'s six rasterizer calls over one geometry (main image, diffuse,
     specular, depth, normal, alpha; gaussian_renderer/__init__.py:160-264) and a training-
-    style loss backward through all of them.  value = views/s with the geometry cache on;
-    the same step with the cache off is reported beside it."""
+    style loss backward through all of them.  value = views/s with the six images from one
+    multi-channel composite (render_channels, 14 channels); the same step as six separate
+    drop-in calls, with and without the geometry cache, is reported beside it."""
     import diff_gaussian_rasterization as dgr
     import relit_shade
     from gsr import scenes
@@ -167,6 +168,44 @@ def bench_relight(args, dev):
             loss = loss + (img * w).sum()
         loss.backward()
 
+    def step_channels():
+        """The same six images from one multi-channel composite (render_channels): depth and
+        alpha are single channels expanded to 3 (the reference repeats one value x3)."""
+        means3D = g["means3D"].detach().requires_grad_(True)
+        opac = g["opacities"].detach().requires_grad_(True)
+        scales = g["scales"].detach().requires_grad_(True)
+        rots = g["rotations"].detach().requires_grad_(True)
+        albedo = mat["albedo"].detach().requires_grad_(True)
+        kr = mat["kr"].detach().requires_grad_(True)
+        km = mat["km"].detach().requires_grad_(True)
+        light.base = base.detach().clone().requires_grad_(True)
+        means2D = torch.zeros_like(means3D, requires_grad=True)
+        fg = means3D[:P_fg]
+        view_pos = cp.expand(P_fg, 3)
+        rgb, ex = light.shade(fg[None, None], mat["normal"][None, None], albedo[None, None], view_pos[None, None],
+                              kr[None, None], km[None, None])
+        rgb, dif, spe = rgb[0, 0], ex["diffuse"][0, 0], ex["specular"][0, 0]
+        cat = lambda x: torch.cat([x, sky_col], 0)
+        depth = (means3D @ vm[:3, :3] + vm[3, :3])[:, 2:3]
+        nrm = cat(0.5 * mat["normal"] + 0.5)
+        colours = [cat(rgb), cat(dif), cat(spe), depth, nrm, torch.ones(P, 1, device=dev)]
+        imgs, _ = dgr.GaussianRasterizer(settings).render_channels(
+            means3D=means3D, means2D=means2D, opacities=opac, colors=colours,
+            backgrounds=[zero3, zero3, zero3, zero3[:1], zero3, zero3[:1]], scales=scales, rotations=rots)
+        loss = 0.0
+        for img, w in zip(imgs, dweights):
+            loss = loss + (img.expand(3, H, W) * w).sum()
+        loss.backward()
+
+    for _ in range(args.warmup):
+        step_channels()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step_channels()
+    torch.cuda.synchronize()
+    ms_channels = (time.perf_counter() - t0) * 1e3 / args.steps
+
     res = {}
     for cached in (True, False):
         dgr.geometry_cache(cached)
@@ -179,15 +218,16 @@ def bench_relight(args, dev):
         torch.cuda.synchronize()
         res[cached] = (time.perf_counter() - t0) * 1e3 / args.steps
     dgr.geometry_cache(True)
-    ms = res[True]
+    ms = ms_channels
     print(json.dumps({
-        "metric": "relit render() views/s (shade + 6 rasterizer calls + backward)", "value": round(1e3 / ms, 3),
+        "metric": "relit render() views/s (shade + render()'s six images + backward)", "value": round(1e3 / ms, 3),
         "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"cfg3: {P_fg} foreground + {P - P_fg} sky Gaussians, {W}x{H}, env SH deg 4",
                    "gaussians": P, "width": W, "height": H},
-        "geometry_cache": {"on_ms": round(res[True], 4), "off_ms": round(res[False], 4),
-                           "speedup": round(res[False] / res[True], 3)}}), flush=True)
+        "implementation": "one multi-channel composite (render_channels) of the six images",
+        "six_calls": {"cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
+                      "composite_speedup_vs_cached": round(res[True] / ms_channels, 3)}}), flush=True)
 
 
 def main():

@@ -13,6 +13,7 @@
 // Templated on the SH degree so the basis and its gradient fully unroll.
 #include "gsr_block.hpp"
 #include "gsr_shade.hpp"
+#include "gsr_tile.hpp"
 
 namespace gsr {
 
@@ -106,6 +107,122 @@ __device__ __forceinline__ void sh_basis(float x, float y, float z, float* Y, fl
         }
     }
 }
+
+// sum_k w[k] * grad Y_k(x, y, z) with w[k] = s[k] * SHC[k] folded in: the gradient basis of
+// sh_basis<DEG, true> accumulated term by term instead of materialised as three K-arrays
+// (the shade backward needs only this dot product).
+template <int DEG>
+__device__ __forceinline__ void sh_grad_dot(float x, float y, float z, const float* s, float& gx, float& gy,
+                                            float& gz) {
+    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+    constexpr int K = (DEG + 1) * (DEG + 1);
+    float w[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) w[k] = s[k] * SHC[k];
+    gx = gy = gz = 0.f;
+    (void)xx; (void)yy; (void)zz; (void)xy; (void)yz; (void)xz;
+    if constexpr (DEG > 0) {
+        gy = __builtin_fmaf(w[1], -1.f, gy);
+        gz = __builtin_fmaf(w[2], 1.f, gz);
+        gx = __builtin_fmaf(w[3], -1.f, gx);
+    }
+    if constexpr (DEG > 1) {
+        gx = __builtin_fmaf(w[4], y, gx);
+        gy = __builtin_fmaf(w[4], x, gy);
+        gy = __builtin_fmaf(w[5], z, gy);
+        gz = __builtin_fmaf(w[5], y, gz);
+        gx = __builtin_fmaf(w[6], -2 * x, gx);
+        gy = __builtin_fmaf(w[6], -2 * y, gy);
+        gz = __builtin_fmaf(w[6], 4 * z, gz);
+        gx = __builtin_fmaf(w[7], z, gx);
+        gz = __builtin_fmaf(w[7], x, gz);
+        gx = __builtin_fmaf(w[8], 2 * x, gx);
+        gy = __builtin_fmaf(w[8], -2 * y, gy);
+    }
+    if constexpr (DEG > 2) {
+        gx = __builtin_fmaf(w[9], 6 * xy, gx);
+        gy = __builtin_fmaf(w[9], 3 * xx - 3 * yy, gy);
+        gx = __builtin_fmaf(w[10], yz, gx);
+        gy = __builtin_fmaf(w[10], xz, gy);
+        gz = __builtin_fmaf(w[10], xy, gz);
+        gx = __builtin_fmaf(w[11], -2 * xy, gx);
+        gy = __builtin_fmaf(w[11], 4 * zz - xx - 3 * yy, gy);
+        gz = __builtin_fmaf(w[11], 8 * yz, gz);
+        gx = __builtin_fmaf(w[12], -6 * xz, gx);
+        gy = __builtin_fmaf(w[12], -6 * yz, gy);
+        gz = __builtin_fmaf(w[12], 6 * zz - 3 * xx - 3 * yy, gz);
+        gx = __builtin_fmaf(w[13], 4 * zz - 3 * xx - yy, gx);
+        gy = __builtin_fmaf(w[13], -2 * xy, gy);
+        gz = __builtin_fmaf(w[13], 8 * xz, gz);
+        gx = __builtin_fmaf(w[14], 2 * xz, gx);
+        gy = __builtin_fmaf(w[14], -2 * yz, gy);
+        gz = __builtin_fmaf(w[14], xx - yy, gz);
+        gx = __builtin_fmaf(w[15], 3 * xx - 3 * yy, gx);
+        gy = __builtin_fmaf(w[15], -6 * xy, gy);
+    }
+    if constexpr (DEG > 3) {
+        gx = __builtin_fmaf(w[16], 3 * xx * y - yy * y, gx);
+        gy = __builtin_fmaf(w[16], xx * x - 3 * x * yy, gy);
+        gx = __builtin_fmaf(w[17], 6 * x * yz, gx);
+        gy = __builtin_fmaf(w[17], 3 * xx * z - 3 * yy * z, gy);
+        gz = __builtin_fmaf(w[17], 3 * xx * y - yy * y, gz);
+        gx = __builtin_fmaf(w[18], y * (7 * zz - 1), gx);
+        gy = __builtin_fmaf(w[18], x * (7 * zz - 1), gy);
+        gz = __builtin_fmaf(w[18], 14 * xy * z, gz);
+        gy = __builtin_fmaf(w[19], z * (7 * zz - 3), gy);
+        gz = __builtin_fmaf(w[19], 21 * y * zz - 3 * y, gz);
+        gz = __builtin_fmaf(w[20], 140 * zz * z - 60 * z, gz);
+        gx = __builtin_fmaf(w[21], z * (7 * zz - 3), gx);
+        gz = __builtin_fmaf(w[21], 21 * x * zz - 3 * x, gz);
+        gx = __builtin_fmaf(w[22], 2 * x * (7 * zz - 1), gx);
+        gy = __builtin_fmaf(w[22], -2 * y * (7 * zz - 1), gy);
+        gz = __builtin_fmaf(w[22], 14 * z * (xx - yy), gz);
+        gx = __builtin_fmaf(w[23], 3 * xx * z - 3 * yy * z, gx);
+        gy = __builtin_fmaf(w[23], -6 * xy * z, gy);
+        gz = __builtin_fmaf(w[23], xx * x - 3 * x * yy, gz);
+        gx = __builtin_fmaf(w[24], 4 * xx * x - 12 * x * yy, gx);
+        gy = __builtin_fmaf(w[24], -12 * xx * y + 4 * yy * y, gy);
+    }
+    if constexpr (DEG > 4) {
+        gx = __builtin_fmaf(w[25], 20 * xx * x - 20 * x * yy, gx);
+        gy = __builtin_fmaf(w[25], -20 * xx * y + 4 * yy * y, gy);
+        gx = __builtin_fmaf(w[26], 3 * xx * yz - yy * yz, gx);
+        gy = __builtin_fmaf(w[26], xx * xz - 3 * yy * xz, gy);
+        gz = __builtin_fmaf(w[26], xx * xy - xy * yy, gz);
+        {
+            const float A = 9 * zz - 1, B = 3 * xx - yy;
+            gx = __builtin_fmaf(w[27], y * A * 6 * x, gx);
+            gy = __builtin_fmaf(w[27], A * (B - 2 * yy), gy);
+            gz = __builtin_fmaf(w[27], y * B * 18 * z, gz);
+        }
+        gx = __builtin_fmaf(w[28], yz * (3 * zz - 1), gx);
+        gy = __builtin_fmaf(w[28], xz * (3 * zz - 1), gy);
+        gz = __builtin_fmaf(w[28], 9 * xy * zz - xy, gz);
+        gy = __builtin_fmaf(w[29], zz * (-14 + 21 * zz) + 1, gy);
+        gz = __builtin_fmaf(w[29], y * (84 * zz * z - 28 * z), gz);
+        gz = __builtin_fmaf(w[30], 315 * zz * zz - 210 * zz + 15, gz);
+        gx = __builtin_fmaf(w[31], zz * (21 * zz - 14) + 15, gx);
+        gz = __builtin_fmaf(w[31], x * (84 * zz * z - 28 * z), gz);
+        {
+            const float A = xx - yy, B = 3 * zz - 1;
+            gx = __builtin_fmaf(w[32], z * 2 * x * B, gx);
+            gy = __builtin_fmaf(w[32], -z * 2 * y * B, gy);
+            gz = __builtin_fmaf(w[32], A * (B + 6 * zz), gz);
+        }
+        {
+            const float A = xx - 3 * yy, B = 9 * zz - 1;
+            gx = __builtin_fmaf(w[33], B * (A + 2 * xx), gx);
+            gy = __builtin_fmaf(w[33], -6 * xy * B, gy);
+            gz = __builtin_fmaf(w[33], x * A * 18 * z, gz);
+        }
+        gx = __builtin_fmaf(w[34], z * (4 * xx * x - 12 * x * yy), gx);
+        gy = __builtin_fmaf(w[34], z * (-12 * xx * y + 4 * yy * y), gy);
+        gz = __builtin_fmaf(w[34], xx * (xx - 6 * yy) + yy * yy, gz);
+        gx = __builtin_fmaf(w[35], 5 * xx * xx - 30 * xx * yy + 5 * yy * yy, gx);
+        gy = __builtin_fmaf(w[35], -20 * xx * xy + 20 * xy * yy, gy);
+    }
+}
+
 
 // light.py:36-40 and the 2*C products evaluated in double by Python
 __device__ constexpr float LC1 = 0.429043f, LC2 = 0.511664f, LC3 = 0.743125f, LC4 = 0.886227f, LC5 = 0.247708f;
@@ -257,7 +374,7 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     float g_kr = 0.f, g_km = 0.f;
 #pragma unroll
     for (int c = 0; c < 3; c++) g_dh[c] = gdif[c] * gamma_d(dh[c]);
-    float Y[K], Yx[K], Yy[K], Yz[K], gw[DEG + 1];
+    float Y[K], gw[DEG + 1];
     if (!a.specular) {
 #pragma unroll
         for (int c = 0; c < 3; c++) g_dh[c] += grgb[c] * gamma_d(dh[c]);
@@ -287,7 +404,7 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         const float ndv = dwn < 1e-4f ? 1e-4f : dwn;
         float fg[2], fgu[2], fgv[2];
         lut_fetch<true>(a.lut, ndv, kr, fg, fgu, fgv);
-        sh_basis<DEG, true>(r[0], r[1], r[2], Y, Yx, Yy, Yz);
+        sh_basis<DEG, false>(r[0], r[1], r[2], Y, nullptr, nullptr, nullptr);
 #pragma unroll
         for (int l = 0; l <= DEG; l++) gw[l] = expf((float)(-l * (l + 1)) * (0.3f * kr));
         float g_fg0 = 0.f, g_fg1 = 0.f, g_r[3] = {0.f, 0.f, 0.f};
@@ -324,17 +441,19 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
                 g_a[c] += km * g_F0;
             }
         }
+        {
+            float sk[K];
 #pragma unroll
-        for (int l = 0, k = 0; l <= DEG; l++)
+            for (int l = 0, k = 0; l <= DEG; l++)
 #pragma unroll
-            for (int m = 0; m < 2 * l + 1; m++, k++) {
-                const float bs = sb[3 * k] * g_si[0] + sb[3 * k + 1] * g_si[1] + sb[3 * k + 2] * g_si[2];
-                g_gw[l] += Y[k] * bs;
-                const float s = gw[l] * bs;
-                g_r[0] += Yx[k] * s;
-                g_r[1] += Yy[k] * s;
-                g_r[2] += Yz[k] * s;
-            }
+                for (int m = 0; m < 2 * l + 1; m++, k++) {
+                    const float bs = sb[3 * k] * g_si[0] + sb[3 * k + 1] * g_si[1] + sb[3 * k + 2] * g_si[2];
+                    g_gw[l] += Y[k] * bs;
+                    sk[k] = gw[l] * bs;
+                }
+            // d si / d r through the basis gradients, accumulated term by term
+            sh_grad_dot<DEG>(r[0], r[1], r[2], sk, g_r[0], g_r[1], g_r[2]);
+        }
 #pragma unroll
         for (int l = 0; l <= DEG; l++) g_kr += g_gw[l] * gw[l] * ((float)(-l * (l + 1)) * 0.3f);
         const float g_ndv = g_fg0 * fgu[0] + g_fg1 * fgu[1];
@@ -381,18 +500,26 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     // d_base[k][c] = sum_i Y_k gw_l g_si[c] (+ diffuse coefficients for k < 9)
     const float dco[9] = {LC4, LC2x2 * y, LC2x2 * z, LC2x2 * x, LC1x2 * x * y, LC1x2 * y * z, LC3 * z * z - LC5,
                           LC1x2 * x * z, LC1 * (x * x - y * y)};
+    // the 3K wave sums in chunks of 12 values, each one transposed butterfly
+    // (gsr_tile.hpp wave_multi_sum; chunks keep the live registers small)
+    const int vi = wave_multi_sum_index(lane);
 #pragma unroll
-    for (int l = 0, k = 0; l <= DEG; l++)
+    for (int e0 = 0; e0 < 3 * K; e0 += 12) {
+        float vb[12];
 #pragma unroll
-        for (int m = 0; m < 2 * l + 1; m++, k++)
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                float v = Y[k] * gw[l] * g_si[c];
-                if (k < 9) v += gi[c] * dco[k];
-                v = valid ? v : 0.f;
-                v = wave_reduce_sum(v);
-                if (lane == 0) sred[wave][3 * k + c] = v;
+        for (int t = 0; t < 12; t++) {
+            const int e = e0 + t, k = e / 3, c = e - 3 * k;
+            float v = 0.f;
+            if (e < 3 * K) {
+                const int l = k < 1 ? 0 : k < 4 ? 1 : k < 9 ? 2 : k < 16 ? 3 : k < 25 ? 4 : 5;
+                v = Y[k] * gw[l] * g_si[c];
+                if (k < 9) v += gi[c] * dco[k < 9 ? k : 0];
             }
+            vb[t] = valid ? v : 0.f;
+        }
+        const float red = wave_multi_sum<12>(vb);
+        if ((lane & 15) < 3 && e0 + vi < 3 * K) sred[wave][e0 + vi] = red;
+    }
     __syncthreads();
     for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS)
         ws[(size_t)blockIdx.x * K * 3 + t] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];

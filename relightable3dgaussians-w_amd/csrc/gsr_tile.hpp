@@ -123,6 +123,31 @@ __device__ __forceinline__ float swap16_sum(float a, float b) {
     const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
     return __uint_as_float(s[0]) + __uint_as_float(s[1]);
 }
+// Wave sums of N per-lane values at once (transposed butterfly): N/2 permlane32 swaps, N/4
+// permlane16 swaps, then one 16-lane DPP row sum per 4 values -- ~1.75 N operations instead
+// of N full wave reductions.  On return, lane (row r, column c) with c < ceil(N/4) holds the
+// sum of value wave_multi_sum_index(lane) (if < N); `out` is that lane's value.
+__device__ __forceinline__ int wave_multi_sum_index(int lane) {
+    const int r = lane >> 4, c = lane & 15;
+    return 4 * c + (r == 0 ? 0 : r == 1 ? 2 : r == 2 ? 1 : 3);
+}
+template <int N>
+__device__ __forceinline__ float wave_multi_sum(const float (&v)[N]) {
+    constexpr int NP = (N + 1) / 2, NQ = (NP + 1) / 2;
+    float Pp[2 * NQ];
+#pragma unroll
+    for (int t = 0; t < NP; t++) Pp[t] = swap32_sum(v[2 * t], 2 * t + 1 < N ? v[2 * t + 1] : 0.f);
+#pragma unroll
+    for (int t = NP; t < 2 * NQ; t++) Pp[t] = 0.f;
+    const int col = threadIdx.x & 15;
+    float out = 0.f;
+#pragma unroll
+    for (int t = 0; t < NQ; t++) {
+        const float q = row_sum(swap16_sum(Pp[2 * t], Pp[2 * t + 1]));
+        out = col == t ? q : out;
+    }
+    return out;
+}
 __device__ __forceinline__ float wave_sum(float v) {
     v += dpp<0xB1>(v);   // quad_perm [1,0,3,2]
     v += dpp<0x4E>(v);   // quad_perm [2,3,0,1]
