@@ -17,6 +17,10 @@
  *   gsr_forward_reuse  colours-only re-render over an earlier call's geometry (the 6-10
  *                      same-geometry calls of gaussian_renderer/__init__.py:160-264)
  *   gsr_knn_mean_dist  submodules/simple-knn/spatial.cu:14-26 distCUDA2
+ *   gsr_relit_features / gsr_relit_features_backward
+ *                      render()'s per-Gaussian colour preparation (normals, shade, sky
+ *                      colour, depth; gaussian_renderer/__init__.py:120-200) fused into
+ *                      the composite's feature rows
  *   gsr_forward_channels / gsr_backward_channels
  *                      the 6-10 same-geometry rasterizer calls of one render()
  *                      (gaussian_renderer/__init__.py:160-264) as ONE composite of all
@@ -114,6 +118,34 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
                           const float* dL_dout, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
                           float* dL_dfeatures, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
                           void* stream);
+
+/* render()'s per-Gaussian channels in one pass (gaussian_renderer/__init__.py:120-200):
+ * features [P][16] = [rgb, diffuse, specular, depth, 0.5 n + 0.5, 1, 0, 0], with
+ *   n     = the minimum-scale axis of build_rotation(rotation), flipped towards the camera;
+ *   depth = view-space z (world_view_transform viewmatrix, row-major 4x4);
+ *   rgb/diffuse/specular = EnvironmentLight.shade of the foreground Gaussians (base
+ *           [(deg+1)^2,3], fg_lut [256,256,2], roughness/metalness [N_fg], metalness
+ *           nullable), and for sky Gaussians clamp_min(eval_sh(sky_deg, sky_sh, dir) + 0.5, 0)
+ *           (sky_deg = -1: 1, fix_sky) with diffuse = specular = 0.
+ * fg_rank [P] holds each Gaussian's rank among the foreground ones (-1: sky) and fg_rows
+ * [N_fg] the inverse map.  workspace: gsr_relit_workspace_bytes, kept from the forward to
+ * the backward (it holds the foreground normals). */
+size_t gsr_relit_workspace_bytes(int P, int N_fg, int deg, int sky_deg);
+int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
+                       const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
+                       const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
+                       int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
+                       float* features, void* workspace, void* stream);
+/* Backward: dL_dfeatures [P][16] -> d_xyz [P,3], d_rotation [P,4], d_albedo [N_fg,3],
+ * d_roughness / d_metalness [N_fg] (may be NULL), d_base, d_sky_sh (may be NULL).  The
+ * scaling gets no gradient (the axis is an argmin). */
+int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
+                                const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
+                                const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
+                                int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
+                                const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
+                                float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
+                                void* workspace, void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

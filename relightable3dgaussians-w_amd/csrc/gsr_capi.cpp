@@ -726,4 +726,103 @@ int gsr_shade_backward(int N, int deg, const float* pos, const float* normal, co
     return GSR_OK;
 }
 
+// ---- fused relit features ----------------------------------------------
+namespace {
+struct RelitWs {
+    size_t normal_fg, d_normal_fg, d_pos_fg, shade_ws, relit_ws, total;
+};
+RelitWs relit_ws_layout(int P, int N_fg, int deg, int sky_deg) {
+    RelitWs w{};
+    size_t t = 0;
+    auto take = [&](size_t b) { const size_t o = t; t += (b + 255) & ~(size_t)255; return o; };
+    w.normal_fg = take(12 * (size_t)N_fg);
+    w.d_normal_fg = take(12 * (size_t)N_fg);
+    w.d_pos_fg = take(12 * (size_t)N_fg);
+    w.shade_ws = take(gsr::shade_workspace_bytes(N_fg, deg));
+    w.relit_ws = take(gsr::relit_workspace_bytes(P, sky_deg));
+    w.total = t + 256;
+    return w;
+}
+}  // namespace
+
+size_t gsr_relit_workspace_bytes(int P, int N_fg, int deg, int sky_deg) {
+    return relit_ws_layout(P, N_fg, deg, sky_deg).total;
+}
+
+int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
+                       const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
+                       const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
+                       int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
+                       float* features, void* workspace, void* stream_) {
+    if (P < 0 || N_fg < 0 || N_fg > P || deg < 2 || deg > 5 || sky_deg < -1 || sky_deg > 3)
+        return fail(GSR_E_ARG, "gsr_relit_features: bad sizes P=%d N_fg=%d deg=%d sky_deg=%d", P, N_fg, deg, sky_deg);
+    if (P == 0) return GSR_OK;
+    if (!xyz || !rotation || !scaling || !fg_rank || !features || !workspace || !campos || !viewmatrix ||
+        (N_fg > 0 && (!fg_rows || !albedo || !base || !fg_lut || (specular && !roughness))) ||
+        (sky_deg >= 0 && !sky_sh))
+        return fail(GSR_E_ARG, "gsr_relit_features: missing inputs");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
+    char* ws = align_base(workspace);
+    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, features,
+                      at<float>(ws, wl.normal_fg)};
+    {
+        GSR_STAGE(ST_SHADE_FWD);
+        gsr::launch_relit_prep(ra, s);
+        if (N_fg > 0) {
+            gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
+                             fg_lut, specular};
+            a.rows = fg_rows;
+            a.io_stride = gsr::RELIT_STRIDE;
+            a.vp_stride = 0;
+            gsr::launch_shade_fwd(a, features, features + 3, features + 6, s);
+        }
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
+                                const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
+                                const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
+                                int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
+                                const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
+                                float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
+                                void* workspace, void* stream_) {
+    if (P < 0 || N_fg < 0 || N_fg > P || deg < 2 || deg > 5 || sky_deg < -1 || sky_deg > 3)
+        return fail(GSR_E_ARG, "gsr_relit_features_backward: bad sizes");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    if (P == 0) {
+        if (d_base) HIP_OK(hipMemsetAsync(d_base, 0, sizeof(float) * 3 * (deg + 1) * (deg + 1), s));
+        if (d_sky_sh && sky_deg >= 0) HIP_OK(hipMemsetAsync(d_sky_sh, 0, sizeof(float) * 3 * (sky_deg + 1) * (sky_deg + 1), s));
+        return GSR_OK;
+    }
+    if (!dL_dfeatures || !d_xyz || !d_rotation || !workspace) return fail(GSR_E_ARG, "gsr_relit_features_backward: missing buffers");
+    const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
+    char* ws = align_base(workspace);
+    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, nullptr,
+                      at<float>(ws, wl.normal_fg)};
+    {
+        GSR_STAGE(ST_SHADE_BWD);
+        if (N_fg > 0) {
+            gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
+                             fg_lut, specular};
+            a.rows = fg_rows;
+            a.io_stride = gsr::RELIT_STRIDE;
+            a.vp_stride = 0;
+            gsr::ShadeGrads g{dL_dfeatures, dL_dfeatures + 3, specular ? dL_dfeatures + 6 : nullptr,
+                              at<float>(ws, wl.d_pos_fg), at<float>(ws, wl.d_normal_fg), d_albedo, nullptr,
+                              specular ? d_roughness : nullptr, specular ? d_metalness : nullptr, d_base};
+            gsr::launch_shade_bwd(a, g, at<void>(ws, wl.shade_ws), s);
+        } else if (d_base) {
+            HIP_OK(hipMemsetAsync(d_base, 0, sizeof(float) * 3 * (deg + 1) * (deg + 1), s));
+        }
+        gsr::RelitGrads rg{dL_dfeatures, at<float>(ws, wl.d_normal_fg), at<float>(ws, wl.d_pos_fg), d_xyz, d_rotation,
+                           d_sky_sh, at<float>(ws, wl.relit_ws)};
+        gsr::launch_relit_prep_bwd(ra, rg, s);
+    }
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

@@ -264,6 +264,16 @@ __device__ __forceinline__ void lut_fetch(const float* lut, float u, float v, fl
 }
 
 __device__ __forceinline__ float3 ld3(const float* p, int i) { return make_float3(p[3 * i], p[3 * i + 1], p[3 * i + 2]); }
+__device__ __forceinline__ float3 ld3s(const float* p, size_t row, int stride) {
+    const float* q = p + row * (size_t)stride;
+    return make_float3(q[0], q[1], q[2]);
+}
+__device__ __forceinline__ void st3s(float* p, size_t row, int stride, float a, float b, float c) {
+    float* q = p + row * (size_t)stride;
+    q[0] = a;
+    q[1] = b;
+    q[2] = c;
+}
 __device__ __forceinline__ void st3(float* p, int i, float a, float b, float c) {
     p[3 * i] = a;
     p[3 * i + 1] = b;
@@ -292,14 +302,15 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         dh[c] = alc[c] * irr;
         dl[c] = gamma_f(dh[c]);
     }
-    st3(dif, i, dl[0], dl[1], dl[2]);
+    const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
+    st3s(dif, row, a.io_stride, dl[0], dl[1], dl[2]);
     if (!a.specular) {
-        st3(rgb, i, dl[0], dl[1], dl[2]);
-        st3(spe, i, 0.f, 0.f, 0.f);
+        st3s(rgb, row, a.io_stride, dl[0], dl[1], dl[2]);
+        st3s(spe, row, a.io_stride, 0.f, 0.f, 0.f);
         return;
     }
-    const float3 p = ld3(a.pos, i);
-    const float3 vp = ld3(a.view_pos, i);
+    const float3 p = ld3s(a.pos, row, 3);
+    const float3 vp = ld3s(a.view_pos, i, a.vp_stride);
     const float kr = a.kr[i];
     const float km = a.km ? a.km[i] : 0.f;
     float wo[3] = {vp.x - p.x, vp.y - p.y, vp.z - p.z};
@@ -334,8 +345,8 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         out_rgb[c] = gamma_f(shaded);
         out_spe[c] = gamma_f(sh_hdr);
     }
-    st3(rgb, i, out_rgb[0], out_rgb[1], out_rgb[2]);
-    st3(spe, i, out_spe[0], out_spe[1], out_spe[2]);
+    st3s(rgb, row, a.io_stride, out_rgb[0], out_rgb[1], out_rgb[2]);
+    st3s(spe, row, a.io_stride, out_spe[0], out_spe[1], out_spe[2]);
 }
 
 template <int DEG>
@@ -364,10 +375,17 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         dh[c] = alc[c] * irr[c];
     }
     float grgb[3] = {0.f, 0.f, 0.f}, gdif[3] = {0.f, 0.f, 0.f}, gspe[3] = {0.f, 0.f, 0.f};
+    const size_t row = a.rows ? (size_t)a.rows[ii] : (size_t)ii;
     if (valid) {
-        if (g.g_rgb) { const float3 t = ld3(g.g_rgb, ii); grgb[0] = t.x; grgb[1] = t.y; grgb[2] = t.z; }
-        if (g.g_diffuse) { const float3 t = ld3(g.g_diffuse, ii); gdif[0] = t.x; gdif[1] = t.y; gdif[2] = t.z; }
-        if (g.g_specular) { const float3 t = ld3(g.g_specular, ii); gspe[0] = t.x; gspe[1] = t.y; gspe[2] = t.z; }
+        if (g.g_rgb) { const float3 t = ld3s(g.g_rgb, row, a.io_stride); grgb[0] = t.x; grgb[1] = t.y; grgb[2] = t.z; }
+        if (g.g_diffuse) {
+            const float3 t = ld3s(g.g_diffuse, row, a.io_stride);
+            gdif[0] = t.x; gdif[1] = t.y; gdif[2] = t.z;
+        }
+        if (g.g_specular) {
+            const float3 t = ld3s(g.g_specular, row, a.io_stride);
+            gspe[0] = t.x; gspe[1] = t.y; gspe[2] = t.z;
+        }
     }
     float g_dh[3], g_a[3] = {0.f, 0.f, 0.f}, g_n[3] = {0.f, 0.f, 0.f}, g_p[3] = {0.f, 0.f, 0.f};
     float g_vp[3] = {0.f, 0.f, 0.f}, g_si[3] = {0.f, 0.f, 0.f};
@@ -383,8 +401,8 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
 #pragma unroll
         for (int l = 0; l <= DEG; l++) gw[l] = 0.f;
     } else {
-        const float3 p = ld3(a.pos, ii);
-        const float3 vp = ld3(a.view_pos, ii);
+        const float3 p = ld3s(a.pos, row, 3);
+        const float3 vp = ld3s(a.view_pos, ii, a.vp_stride);
         const float kr = a.kr[ii];
         const float km = a.km ? a.km[ii] : 0.f;
         const float wv[3] = {vp.x - p.x, vp.y - p.y, vp.z - p.z};
@@ -534,6 +552,234 @@ __global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
     if (threadIdx.x == 0) d_base[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// ---- fused relit features ------------------------------------------------
+// render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) in two
+// kernels around the shade, writing the multi-channel composite's feature rows directly:
+//   row i = [rgb 0-2, diffuse 3-5, specular 6-8, depth 9, 0.5 n + 0.5 10-12, alpha 13, 0, 0]
+// k_relit_prep: view direction (safe_normalize(xyz - campos), NVDIFFREC/util.py:27-31),
+// normal = minimum-scale axis of build_rotation(q) flipped towards the camera
+// (gaussian_model.py:115-122, general_utils.py:98-170), depth = view-space z
+// (gaussian_model.py:125-130), sky colour clamp_min(eval_sh(sky_deg, sky_sh, dir) + 0.5, 0)
+// or 1 with fix_sky (__init__.py:143-148); the foreground normals go to a compact array for
+// the shade kernel, which writes rows 0-8 of the foreground Gaussians (ShadeArgs.rows).
+template <int SDEG>
+__device__ __forceinline__ float3 sky_colour(float3 d, const float* sky) {
+    constexpr int K = (SDEG + 1) * (SDEG + 1);
+    float Y[K];
+    sh_basis<SDEG, false>(d.x, d.y, d.z, Y, nullptr, nullptr, nullptr);
+    float c[3];
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        float v = 0.f;
+#pragma unroll
+        for (int k = 0; k < K; k++) v = __builtin_fmaf(Y[k], sky[3 * k + ch], v);
+        c[ch] = v + 0.5f;
+    }
+    return make_float3(c[0], c[1], c[2]);
+}
+
+struct RelitGeom {
+    float3 dir;   // normalised view direction
+    float len;    // its length (clamped)
+    float4 q;     // normalised quaternion (r, x, y, z)
+    float qn;     // |rotation|
+    int axis;     // minimum-scale axis
+    bool keep;    // normal not flipped
+    float3 n;     // flipped normal
+};
+
+__device__ __forceinline__ RelitGeom relit_geom(const RelitArgs& a, int i, float3 xyz) {
+    RelitGeom g;
+    const float dx = xyz.x - a.campos[0], dy = xyz.y - a.campos[1], dz = xyz.z - a.campos[2];
+    const float l2 = dx * dx + dy * dy + dz * dz;
+    g.len = sqrtf(l2 < 1e-20f ? 1e-20f : l2);
+    g.dir = make_float3(dx / g.len, dy / g.len, dz / g.len);
+    const float4 r = *reinterpret_cast<const float4*>(a.rotation + 4 * (size_t)i);
+    g.qn = sqrtf(r.x * r.x + r.y * r.y + r.z * r.z + r.w * r.w);
+    g.q = make_float4(r.x / g.qn, r.y / g.qn, r.z / g.qn, r.w / g.qn);
+    const float s0 = a.scaling[3 * (size_t)i], s1 = a.scaling[3 * (size_t)i + 1], s2 = a.scaling[3 * (size_t)i + 2];
+    g.axis = (s1 < s0) ? ((s2 < s1) ? 2 : 1) : ((s2 < s0) ? 2 : 0);  // first minimum, as torch.min
+    const float qr = g.q.x, qx = g.q.y, qy = g.q.z, qz = g.q.w;
+    float3 ax;
+    if (g.axis == 0) ax = make_float3(1 - 2 * (qy * qy + qz * qz), 2 * (qx * qy + qr * qz), 2 * (qx * qz - qr * qy));
+    else if (g.axis == 1) ax = make_float3(2 * (qx * qy - qr * qz), 1 - 2 * (qx * qx + qz * qz), 2 * (qy * qz + qr * qx));
+    else ax = make_float3(2 * (qx * qz + qr * qy), 2 * (qy * qz - qr * qx), 1 - 2 * (qx * qx + qy * qy));
+    const float dp = ax.x * -g.dir.x + ax.y * -g.dir.y + ax.z * -g.dir.z;
+    g.keep = dp >= 0.f;
+    g.n = g.keep ? ax : make_float3(-ax.x, -ax.y, -ax.z);
+    return g;
+}
+
+template <int SDEG>
+__global__ void __launch_bounds__(256) k_relit_prep(RelitArgs a) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.P) return;
+    const float3 xyz = ld3(a.xyz, i);
+    const RelitGeom g = relit_geom(a, i, xyz);
+    float* f = a.features + (size_t)i * RELIT_STRIDE;
+    // depth: row 2 of W2V = column 2 of world_view_transform (gaussian_model.py:125-130)
+    const float* V = a.viewmatrix;
+    f[9] = xyz.x * V[2] + xyz.y * V[6] + xyz.z * V[10] + V[14];
+    f[10] = 0.5f * g.n.x + 0.5f;
+    f[11] = 0.5f * g.n.y + 0.5f;
+    f[12] = 0.5f * g.n.z + 0.5f;
+    f[13] = 1.f;
+    f[14] = 0.f;
+    f[15] = 0.f;
+    const int rank = a.fg_rank[i];
+    if (rank >= 0) {
+        st3(a.normal_fg, rank, g.n.x, g.n.y, g.n.z);
+    } else {
+        float3 c = make_float3(1.f, 1.f, 1.f);
+        if (SDEG >= 0) {
+            c = sky_colour<(SDEG < 0 ? 0 : SDEG)>(g.dir, a.sky_sh);
+            c = make_float3(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f));
+        }
+        f[0] = c.x; f[1] = c.y; f[2] = c.z;
+        f[3] = f[4] = f[5] = f[6] = f[7] = f[8] = 0.f;
+    }
+}
+
+// Backward of the preparation: dL/dxyz (depth, sky direction, + the shade's dL/dpos of the
+// foreground rows), dL/drotation (through the flipped minimum axis and build_rotation's
+// normalisation), per-workgroup partial dL/dsky_sh.  dL/dscaling is zero (the axis choice
+// is an argmin).
+template <int SDEG>
+__global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads gr) {
+    constexpr int KS = SDEG >= 0 ? (SDEG + 1) * (SDEG + 1) : 1;
+    __shared__ float sred[4][3 * KS];
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool valid = i < a.P;
+    const int ii = valid ? i : 0;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const float3 xyz = ld3(a.xyz, ii);
+    const RelitGeom g = relit_geom(a, ii, xyz);
+    const float* gf = gr.dL_dfeatures + (size_t)ii * RELIT_STRIDE;
+    const float* V = a.viewmatrix;
+    float gx = gf[9] * V[2], gy = gf[9] * V[6], gz = gf[9] * V[10];
+    float3 gn = make_float3(0.5f * gf[10], 0.5f * gf[11], 0.5f * gf[12]);
+    const int rank = a.fg_rank[ii];
+    float Yk[KS];
+    float gcol[3] = {0.f, 0.f, 0.f};
+    if (rank >= 0) {
+        const float3 dn = ld3(gr.d_normal_fg, rank), dpos = ld3(gr.d_pos_fg, rank);
+        gn.x += dn.x; gn.y += dn.y; gn.z += dn.z;
+        gx += dpos.x; gy += dpos.y; gz += dpos.z;
+#pragma unroll
+        for (int k = 0; k < KS; k++) Yk[k] = 0.f;
+    } else if (SDEG >= 0) {
+        constexpr int SD = SDEG < 0 ? 0 : SDEG;
+        sh_basis<SD, false>(g.dir.x, g.dir.y, g.dir.z, Yk, nullptr, nullptr, nullptr);
+        float raw[3];
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            float v = 0.f;
+#pragma unroll
+            for (int k = 0; k < KS; k++) v = __builtin_fmaf(Yk[k], a.sky_sh[3 * k + ch], v);
+            raw[ch] = v + 0.5f;
+            gcol[ch] = raw[ch] >= 0.f ? gf[ch] : 0.f;  // clamp_min backward passes at the bound
+        }
+        float s[KS];
+#pragma unroll
+        for (int k = 0; k < KS; k++)
+            s[k] = a.sky_sh[3 * k] * gcol[0] + a.sky_sh[3 * k + 1] * gcol[1] + a.sky_sh[3 * k + 2] * gcol[2];
+        float gd[3];
+        sh_grad_dot<SD>(g.dir.x, g.dir.y, g.dir.z, s, gd[0], gd[1], gd[2]);
+        // safe_normalize backward (x / sqrt(clamp(x.x, 1e-20)))
+        const float dg = g.dir.x * gd[0] + g.dir.y * gd[1] + g.dir.z * gd[2];
+        const bool clamped = g.len * g.len < 1e-20f;
+        gx += clamped ? gd[0] / g.len : (gd[0] - g.dir.x * dg) / g.len;
+        gy += clamped ? gd[1] / g.len : (gd[1] - g.dir.y * dg) / g.len;
+        gz += clamped ? gd[2] / g.len : (gd[2] - g.dir.z * dg) / g.len;
+    } else {
+#pragma unroll
+        for (int k = 0; k < KS; k++) Yk[k] = 0.f;
+    }
+    // normal -> axis (undo the flip) -> column of R -> q -> rotation
+    const float ga0 = g.keep ? gn.x : -gn.x, ga1 = g.keep ? gn.y : -gn.y, ga2 = g.keep ? gn.z : -gn.z;
+    const float qr = g.q.x, qx = g.q.y, qy = g.q.z, qz = g.q.w;
+    float gqr, gqx, gqy, gqz;
+    if (g.axis == 0) {  // (1 - 2(y^2 + z^2), 2(xy + rz), 2(xz - ry))
+        gqr = 2 * (qz * ga1 - qy * ga2);
+        gqx = 2 * (qy * ga1 + qz * ga2);
+        gqy = -4 * qy * ga0 + 2 * (qx * ga1 - qr * ga2);
+        gqz = -4 * qz * ga0 + 2 * (qr * ga1 + qx * ga2);
+    } else if (g.axis == 1) {  // (2(xy - rz), 1 - 2(x^2 + z^2), 2(yz + rx))
+        gqr = 2 * (-qz * ga0 + qx * ga2);
+        gqx = 2 * (qy * ga0 + qr * ga2) - 4 * qx * ga1;
+        gqy = 2 * (qx * ga0 + qz * ga2);
+        gqz = 2 * (-qr * ga0 + qy * ga2) - 4 * qz * ga1;
+    } else {  // (2(xz + ry), 2(yz - rx), 1 - 2(x^2 + y^2))
+        gqr = 2 * (qy * ga0 - qx * ga1);
+        gqx = 2 * (qz * ga0 - qr * ga1) - 4 * qx * ga2;
+        gqy = 2 * (qr * ga0 + qz * ga1) - 4 * qy * ga2;
+        gqz = 2 * (qx * ga0 + qy * ga1);
+    }
+    // q = r / |r|
+    const float qg = qr * gqr + qx * gqx + qy * gqy + qz * gqz;
+    if (valid) {
+        st3(gr.d_xyz, i, gx, gy, gz);
+        *reinterpret_cast<float4*>(gr.d_rotation + 4 * (size_t)i) =
+            make_float4((gqr - qr * qg) / g.qn, (gqx - qx * qg) / g.qn, (gqy - qy * qg) / g.qn, (gqz - qz * qg) / g.qn);
+    }
+    if (SDEG < 0 || !gr.d_sky_sh) return;
+    // dL/dsky_sh[k][c] = sum over sky Gaussians of Y_k(dir) gcol[c]: per-workgroup slab
+    const int vi = wave_multi_sum_index(lane);
+#pragma unroll
+    for (int e0 = 0; e0 < 3 * KS; e0 += 12) {
+        float vb[12];
+#pragma unroll
+        for (int t = 0; t < 12; t++) {
+            const int e = e0 + t, k = e / 3, c = e - 3 * k;
+            vb[t] = (valid && e < 3 * KS) ? Yk[k < KS ? k : 0] * gcol[c] : 0.f;
+        }
+        const float red = wave_multi_sum<12>(vb);
+        if ((lane & 15) < 3 && e0 + vi < 3 * KS) sred[wave][e0 + vi] = red;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < 3 * KS; t += 256)
+        gr.workspace[(size_t)blockIdx.x * 3 * KS + t] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+}
+
+size_t relit_workspace_bytes(int P, int sky_deg) {
+    const size_t nb = (size_t)((P + 255) / 256);
+    const int KS = sky_deg >= 0 ? (sky_deg + 1) * (sky_deg + 1) : 1;
+    return nb * 3 * KS * sizeof(float) + 256;
+}
+
+void launch_relit_prep(const RelitArgs& a, hipStream_t s) {
+    if (a.P == 0) return;
+    const dim3 grid((a.P + 255) / 256), blk(256);
+    switch (a.sky_deg) {
+        case 0: hipLaunchKernelGGL(k_relit_prep<0>, grid, blk, 0, s, a); break;
+        case 1: hipLaunchKernelGGL(k_relit_prep<1>, grid, blk, 0, s, a); break;
+        case 2: hipLaunchKernelGGL(k_relit_prep<2>, grid, blk, 0, s, a); break;
+        case 3: hipLaunchKernelGGL(k_relit_prep<3>, grid, blk, 0, s, a); break;
+        default: hipLaunchKernelGGL(k_relit_prep<-1>, grid, blk, 0, s, a); break;
+    }
+}
+
+void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s) {
+    if (a.P == 0) {
+        if (g.d_sky_sh && a.sky_deg >= 0)
+            (void)hipMemsetAsync(g.d_sky_sh, 0, sizeof(float) * 3 * (a.sky_deg + 1) * (a.sky_deg + 1), s);
+        return;
+    }
+    const int nb = (a.P + 255) / 256;
+    const dim3 grid(nb), blk(256);
+    switch (a.sky_deg) {
+        case 0: hipLaunchKernelGGL(k_relit_prep_bwd<0>, grid, blk, 0, s, a, g); break;
+        case 1: hipLaunchKernelGGL(k_relit_prep_bwd<1>, grid, blk, 0, s, a, g); break;
+        case 2: hipLaunchKernelGGL(k_relit_prep_bwd<2>, grid, blk, 0, s, a, g); break;
+        case 3: hipLaunchKernelGGL(k_relit_prep_bwd<3>, grid, blk, 0, s, a, g); break;
+        default: hipLaunchKernelGGL(k_relit_prep_bwd<-1>, grid, blk, 0, s, a, g); break;
+    }
+    if (g.d_sky_sh && a.sky_deg >= 0) {
+        const int KC = 3 * (a.sky_deg + 1) * (a.sky_deg + 1);
+        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, g.workspace, g.d_sky_sh);
+    }
 }
 
 size_t shade_workspace_bytes(int N, int deg) {

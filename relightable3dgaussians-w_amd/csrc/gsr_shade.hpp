@@ -16,6 +16,13 @@ struct ShadeArgs {
     const float* base;
     const float* lut;
     int specular;
+    // Row addressing (the fused relit features op, gsr_relit_features): Gaussian i of the
+    // shaded set is row rows[i] of pos and of the rgb/diffuse/specular outputs and their
+    // gradients (i when rows is null); those outputs/gradients have io_stride floats per
+    // row; view_pos advances vp_stride floats per Gaussian (0: one shared camera centre).
+    const int* rows = nullptr;
+    int io_stride = 3;
+    int vp_stride = 3;
 };
 
 struct ShadeGrads {
@@ -30,6 +37,34 @@ struct ShadeGrads {
     float* d_km;
     float* d_base;
 };
+
+// Fused relit features (gsr_shade.hip k_relit_prep / k_relit_prep_bwd).
+constexpr int RELIT_STRIDE = 16;  // feature row: rgb, diffuse, specular, depth, normal01, alpha, 0, 0
+struct RelitArgs {
+    int P;
+    const float* xyz;       // [P,3]
+    const float* rotation;  // [P,4]
+    const float* scaling;   // [P,3]
+    const int* fg_rank;     // [P]: rank among the foreground Gaussians, -1 for sky
+    int sky_deg;            // -1: fix_sky (sky colour 1)
+    const float* sky_sh;    // [(sky_deg+1)^2][3]
+    const float* campos;    // [3]
+    const float* viewmatrix;  // world_view_transform, row-major [4,4]
+    float* features;        // [P][RELIT_STRIDE]
+    float* normal_fg;       // [N_fg,3]
+};
+struct RelitGrads {
+    const float* dL_dfeatures;  // [P][RELIT_STRIDE]
+    const float* d_normal_fg;   // [N_fg,3] from the shade backward
+    const float* d_pos_fg;      // [N_fg,3] from the shade backward
+    float* d_xyz;               // [P,3]
+    float* d_rotation;          // [P,4]
+    float* d_sky_sh;            // [(sky_deg+1)^2][3] or null
+    float* workspace;           // relit_workspace_bytes
+};
+size_t relit_workspace_bytes(int P, int sky_deg);
+void launch_relit_prep(const RelitArgs& a, hipStream_t s);
+void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s);
 
 constexpr int SHADE_THREADS = 256;
 size_t shade_workspace_bytes(int N, int deg);

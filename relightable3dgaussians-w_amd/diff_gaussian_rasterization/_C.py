@@ -128,22 +128,25 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
 
 
-def pack_features(features):
-    """[P, nch] per-Gaussian channels -> contiguous [P, stride] float32, stride = nch rounded up
-    to a multiple of 4 (the multi-channel tile passes read 16-B rows)."""
-    P, nch = features.shape
-    stride = (nch + 3) // 4 * 4
-    if stride == nch and features.dtype == torch.float32 and features.is_contiguous() and \
+def pack_features(features, nch=None):
+    """[P, C] per-Gaussian channels -> contiguous 16-B aligned [P, stride] float32 whose first
+    nch (default C) columns are the channels, stride a multiple of 4 (the multi-channel tile
+    passes read 16-B rows).  A tensor that already has that layout (e.g. the [P, 16] rows of
+    relit_shade.relit_features with nch = 14) is used as is."""
+    P, C = features.shape
+    nch = C if nch is None else int(nch)
+    if features.dtype == torch.float32 and features.is_contiguous() and C % 4 == 0 and C >= nch and \
             features.data_ptr() % 16 == 0:
         return features
+    stride = (nch + 3) // 4 * 4
     out = torch.zeros((P, stride), dtype=torch.float32, device=features.device)
-    out[:, :nch] = features
+    out[:, :nch] = features[:, :nch]
     return out
 
 
 def rasterize_gaussians_channels(background, means3D, features, opacity, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width,
-                                 campos, prefiltered):
+                                 campos, prefiltered, nch=None):
     """All channels of several same-geometry rasterizer calls in one composite
     (gsr_forward_channels): background [nch], features [P, nch] ->
     (num_rendered, out[nch,H,W], radii, geomBuffer, binningBuffer, imgBuffer, packed features)."""
@@ -152,13 +155,13 @@ def rasterize_gaussians_channels(background, means3D, features, opacity, scales,
     _lib.require_gpu_tensor(means3D, "means3D")
     dev = means3D.device
     P, H, W = means3D.size(0), int(image_height), int(image_width)
-    nch = features.size(1)
-    if features.size(0) != P or background.numel() != nch:
+    nch = features.size(1) if nch is None else int(nch)
+    if features.size(0) != P or background.numel() != nch or features.size(1) < nch:
         raise ValueError(f"features must be [P, nch] and background [nch] (P={P}, features {tuple(features.shape)}, "
                          f"background {tuple(background.shape)})")
     radii = torch.zeros(P, dtype=torch.int32, device=dev)
     bs = _lib.BufferSet(dev)
-    feat = pack_features(_f32(features))
+    feat = pack_features(features if features.dtype == torch.float32 else features.float(), nch)
     out = torch.empty((nch, H, W), dtype=torch.float32, device=dev)
     keep = [_f32(x) for x in (background, means3D, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix,
                               campos)]
@@ -185,7 +188,8 @@ def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch,
                                           cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout, campos,
                                           geomBuffer, R, binningBuffer, imageBuffer):
     """Backward of rasterize_gaussians_channels (gsr_backward_channels) -> (dL_dmeans2D,
-    dL_dfeatures [P, nch], dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)."""
+    dL_dfeatures [P, stride] (columns >= nch zero), dL_dopacity, dL_dmeans3D, dL_dcov3D,
+    dL_dscales, dL_drotations)."""
     _lib.require_gpu_tensor(means3D, "means3D")
     dev = means3D.device
     P = means3D.size(0)
@@ -209,7 +213,7 @@ def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch,
             dL_dfeat.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), dL_dscales.data_ptr(),
             dL_drotations.data_ptr(), _lib.stream_of(dev))
         _lib.check(ret, "rasterize_gaussians_channels_backward")
-    return (dL_dmeans2D, dL_dfeat[:, :nch], dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)
+    return (dL_dmeans2D, dL_dfeat, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

@@ -143,12 +143,13 @@ class _RasterizeGaussians(torch.autograd.Function):
 
 
 def rasterize_channels(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
-                       raster_settings):
-    """Composite of all per-Gaussian channels `features` [P, nch] over one geometry
-    (gsr_forward_channels): returns (image [nch, H, W], radii).  Channel c equals the
-    reference rasterizer's output for colours holding channel c with background[c]."""
+                       raster_settings, nch=None):
+    """Composite of the first nch (default all) per-Gaussian channels of `features` [P, C]
+    over one geometry (gsr_forward_channels): returns (image [nch, H, W], radii).  Channel c
+    equals the reference rasterizer's output for colours holding channel c with
+    background[c]."""
     return _RasterizeChannels.apply(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp,
-                                    background, raster_settings)
+                                    background, raster_settings, nch)
 
 
 class _RasterizeChannels(torch.autograd.Function):
@@ -158,14 +159,16 @@ class _RasterizeChannels(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
-                raster_settings):
+                raster_settings, nch=None):
         s = raster_settings
         num_rendered, out, radii, geom_buf, bin_buf, img_buf, feat = _C.rasterize_gaussians_channels(
             background, means3D, features, opacities, scales, rotations, s.scale_modifier, cov3Ds_precomp,
-            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, s.campos, s.prefiltered)
+            s.viewmatrix, s.projmatrix, s.tanfovx, s.tanfovy, s.image_height, s.image_width, s.campos, s.prefiltered,
+            nch)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
-        ctx.nch = features.shape[1]
+        ctx.nch = features.shape[1] if nch is None else int(nch)
+        ctx.ncols = features.shape[1]
         ctx.save_for_backward(background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf,
                               img_buf)
         return out, radii
@@ -180,7 +183,13 @@ class _RasterizeChannels(torch.autograd.Function):
                                                      s.scale_modifier, cov3Ds_precomp, s.viewmatrix, s.projmatrix,
                                                      s.tanfovx, s.tanfovy, grad_out, s.campos, geom_buf,
                                                      ctx.num_rendered, bin_buf, img_buf)
-        return g_means3D, g_means2D, g_feat, g_opacities, g_scales, g_rotations, g_cov3D, None, None
+        if g_feat.shape[1] >= ctx.ncols:  # gradient for every input column (columns >= nch: 0)
+            g_feat = g_feat[:, :ctx.ncols]
+        else:
+            g_full = torch.zeros((g_feat.shape[0], ctx.ncols), dtype=g_feat.dtype, device=g_feat.device)
+            g_full[:, :g_feat.shape[1]] = g_feat
+            g_feat = g_full
+        return g_means3D, g_means2D, g_feat, g_opacities, g_scales, g_rotations, g_cov3D, None, None, None
 
 
 class GaussianRasterizer(nn.Module):

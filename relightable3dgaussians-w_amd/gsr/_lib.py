@@ -46,6 +46,11 @@ def _declare(lib):
                                          f, vp, vp, vp, vp, vp, f, f, i, vp, vp, vp, C.POINTER(C.c_int)]
     lib.gsr_backward_channels.argtypes = [i, i, i, vp, i, vp, i, i, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp, vp, vp,
                                           vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.gsr_relit_workspace_bytes.argtypes = [i, i, i, i]
+    lib.gsr_relit_workspace_bytes.restype = sz
+    lib.gsr_relit_features.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp]
+    lib.gsr_relit_features_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp,
+                                                vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
     lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                        vp, vp, vp]
@@ -61,6 +66,7 @@ def _declare(lib):
     lib.gsr_version.restype = C.c_char_p
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
+               "gsr_relit_features", "gsr_relit_features_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 

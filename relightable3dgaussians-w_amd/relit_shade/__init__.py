@@ -23,7 +23,7 @@ if _here not in sys.path:
 
 from gsr import _lib, assets  # noqa: E402
 
-__all__ = ["EnvironmentLight", "ShadeFunction", "shade", "install", "fg_lut"]
+__all__ = ["EnvironmentLight", "ShadeFunction", "shade", "install", "fg_lut", "relit_features", "RELIT_CHANNELS"]
 
 _LUT = {}
 
@@ -113,6 +113,88 @@ def shade(light, gb_pos, gb_normal, albedo, view_pos, kr=None, km=None, specular
     if not specular:
         return dif, {"diffuse": dif, "specular": torch.zeros_like(dif)}
     return rgb, {"diffuse": dif, "specular": spe.reshape(*lead, 3)}
+
+
+# column layout of relit_features rows (RELIT_STRIDE = 16 floats, the last two zero)
+RELIT_CHANNELS = {"render": (0, 3), "diffuse_color": (3, 6), "specular_color": (6, 9), "depth": (9, 10),
+                  "normal": (10, 13), "alpha": (13, 14)}
+
+
+class RelitFeaturesFunction(torch.autograd.Function):
+    """gsr_relit_features: render()'s per-Gaussian channels as [P, 16] feature rows."""
+
+    @staticmethod
+    def forward(ctx, xyz, rotation, scaling, albedo, roughness, metalness, base, sky_sh, fg_rank, fg_rows, campos,
+                viewmatrix, lut, deg, sky_deg, specular):
+        P, N = xyz.shape[0], fg_rows.shape[0]
+        dev = xyz.device
+        feat = torch.empty((P, 16), dtype=torch.float32, device=dev)
+        ws = torch.empty(int(_lib.lib().gsr_relit_workspace_bytes(P, N, deg, sky_deg)), dtype=torch.uint8, device=dev)
+        ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
+        if P:
+            _lib.check(_lib.lib().gsr_relit_features(
+                P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),
+                ptr(albedo), ptr(roughness), ptr(metalness), deg, base.data_ptr(), lut.data_ptr(), int(specular),
+                sky_deg, ptr(sky_sh), campos.data_ptr(), viewmatrix.data_ptr(), feat.data_ptr(), ws.data_ptr(),
+                _lib.stream_of(dev)), "gsr_relit_features")
+        ctx.deg, ctx.sky_deg, ctx.specular = deg, sky_deg, specular
+        ctx.has = (roughness is not None, metalness is not None, sky_sh is not None)
+        e = torch.empty(0, device=dev)
+        ctx.save_for_backward(xyz, rotation, scaling, albedo, roughness if roughness is not None else e,
+                              metalness if metalness is not None else e, base, sky_sh if sky_sh is not None else e,
+                              fg_rank, fg_rows, campos, viewmatrix, lut, ws)
+        return feat
+
+    @staticmethod
+    def backward(ctx, g_feat):
+        (xyz, rotation, scaling, albedo, roughness, metalness, base, sky_sh, fg_rank, fg_rows, campos, viewmatrix, lut,
+         ws) = ctx.saved_tensors
+        P, N = xyz.shape[0], fg_rows.shape[0]
+        dev = xyz.device
+        g_feat = g_feat.float().contiguous()
+        d_xyz = torch.zeros_like(xyz)
+        d_rot = torch.zeros_like(rotation)
+        d_alb = torch.zeros_like(albedo)
+        d_kr = torch.zeros_like(roughness) if ctx.has[0] else None
+        d_km = torch.zeros_like(metalness) if ctx.has[1] else None
+        d_base = torch.zeros_like(base)
+        d_sky = torch.zeros_like(sky_sh) if ctx.has[2] and ctx.sky_deg >= 0 else None
+        ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
+        _lib.check(_lib.lib().gsr_relit_features_backward(
+            P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),
+            ptr(albedo), ptr(roughness), ptr(metalness), ctx.deg, base.data_ptr(), lut.data_ptr(), int(ctx.specular),
+            ctx.sky_deg, ptr(sky_sh), campos.data_ptr(), viewmatrix.data_ptr(), g_feat.data_ptr(), d_xyz.data_ptr(),
+            d_rot.data_ptr(), ptr(d_alb), ptr(d_kr), ptr(d_km), d_base.data_ptr(), ptr(d_sky), ws.data_ptr(),
+            _lib.stream_of(dev)), "gsr_relit_features_backward")
+        return (d_xyz, d_rot, None, d_alb, d_kr, d_km, d_base, d_sky, None, None, None, None, None, None, None, None)
+
+
+def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness, light, campos, viewmatrix,
+                   sky_sh=None, sky_sh_degree=1, specular=True, fix_sky=False):
+    """render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) as
+    one fused op: returns features [P, 16] with the columns of RELIT_CHANNELS -- the shaded
+    colour (sky colour for sky Gaussians), diffuse and specular (0 for sky), view-space
+    depth, 0.5 normal + 0.5 and alpha = 1 -- ready for GaussianRasterizer.render_channels /
+    rasterize_channels(nch=14).  Inputs as render() takes them from the model: xyz [P,3]
+    (get_xyz), rotation [P,4] (get_rotation), scaling [P,3] (get_scaling), is_sky [P] or
+    [P,1] bool, albedo [N_fg,3], roughness / metalness [N_fg,1], sky_sh [1, K, 3] (the
+    sky SH; ignored with fix_sky), campos [3], viewmatrix = world_view_transform.
+    Differentiable w.r.t. xyz, rotation, albedo, roughness, metalness, light.base, sky_sh."""
+    _lib.require_gpu_tensor(xyz, "xyz")
+    dev = xyz.device
+    sky = is_sky.reshape(-1).bool()
+    fg = ~sky
+    fg_rows = torch.nonzero(fg).reshape(-1).int()
+    fg_rank = torch.full((xyz.shape[0],), -1, dtype=torch.int32, device=dev)
+    fg_rank[fg_rows.long()] = torch.arange(fg_rows.numel(), dtype=torch.int32, device=dev)
+    base = light.base.squeeze().reshape(-1, 3).float().contiguous()
+    deg = int(round(base.shape[0] ** 0.5)) - 1
+    sky_deg = -1 if (fix_sky or sky_sh is None) else int(sky_sh_degree)
+    sk = None if sky_deg < 0 else sky_sh.reshape(-1, 3)[:(sky_deg + 1) ** 2].float().contiguous()
+    f = lambda t: None if t is None else t.float().contiguous()
+    return RelitFeaturesFunction.apply(f(xyz), f(rotation), f(scaling), f(albedo), _flat1(roughness),
+                                       _flat1(metalness), base, sk, fg_rank, fg_rows, f(campos), f(viewmatrix),
+                                       fg_lut(dev), deg, sky_deg, bool(specular))
 
 
 class EnvironmentLight(torch.nn.Module):
