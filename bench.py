@@ -110,124 +110,86 @@ def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
                 seconds_estimated_full=est)
 
 
+class _RelitModel:
+    """The GaussianModel properties render() reads (scene/gaussian_model.py:74-180), as
+    plain tensors of a synthetic scene."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
 def bench_relight(args, dev):
-    """cfg3: the relightable render() step -- fused PBR shade of the foreground
-    Gaussians, then render()'s six rasterizer calls over one geometry (main image, diffuse,
-    specular, depth, normal, alpha; gaussian_renderer/__init__.py:160-264) and a training-
-    style loss backward through all of them.  value = views/s with the six images from one
-    multi-channel composite (render_channels, 14 channels); the same step as six separate
-    drop-in calls, with and without the geometry cache, is reported beside it."""
+    """cfg3: the relightable render() step (gaussian_renderer/__init__.py:69-280,
+    debug=False) and a training-style loss backward through all of its images (render,
+    diffuse, specular, depth, normal, alpha, normal_ref).  value = views/s of the fused path
+    (gsr.relit.render: relit features + one multi-channel composite); render()'s own call
+    sequence on the drop-in ops (gsr.relit.render_calls: PyTorch per-Gaussian steps + six
+    rasterizer calls), with and without the geometry cache, is reported beside it."""
+    import types
+
     import diff_gaussian_rasterization as dgr
     import relit_shade
-    from gsr import scenes
+    from gsr import relit, scenes
     P_fg = args.P or 1_000_000
     P = P_fg + P_fg // 10  # + 10 % sky Gaussians
     cam, gs, c = scenes.build_config("cfg2", device="cpu", seed=0, P=P)
     W, H = cam.image_width, cam.image_height
-    g = {k: v.to(dev) for k, v in gs.items()}
     gen = torch.Generator().manual_seed(7)
-    mat = {"albedo": torch.rand(P_fg, 3, generator=gen), "kr": torch.rand(P_fg, 1, generator=gen) * 0.9 + 0.05,
-           "km": torch.rand(P_fg, 1, generator=gen),
-           "normal": torch.nn.functional.normalize(torch.randn(P_fg, 3, generator=gen), dim=1)}
-    mat = {k: v.to(dev) for k, v in mat.items()}
+    is_sky = torch.zeros(P, dtype=torch.bool)
+    is_sky[P_fg:] = True
+    leaves = {"xyz": gs["means3D"], "rotation": gs["rotations"], "opacity": gs["opacities"],
+              "albedo": torch.rand(P_fg, 3, generator=gen), "roughness": torch.rand(P_fg, 1, generator=gen) * 0.9 + 0.05,
+              "metalness": torch.rand(P_fg, 1, generator=gen)}
+    leaves = {k: v.to(dev) for k, v in leaves.items()}
+    scaling = gs["scales"].to(dev)
     base = (torch.randn(25, 3, generator=gen) * 0.3).to(dev)
     base[0] = 1.0
-    sky_col = torch.rand(P - P_fg, 3, generator=gen).to(dev)
-    vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
-    light = relit_shade.EnvironmentLight(base.clone(), sh_degree=4)
-    zero3 = torch.zeros(3, device=dev)
-    settings = dgr.GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=cam.tanfovx,
-                                                 tanfovy=cam.tanfovy, bg=zero3, scale_modifier=1.0, viewmatrix=vm,
-                                                 projmatrix=pm, sh_degree=-1, campos=cp, prefiltered=False)
-    dweights = [torch.randn(3, H, W, generator=gen).to(dev) for _ in range(6)]
+    sky_sh = (torch.randn(1, 4, 3, generator=gen) * 0.3).to(dev)
+    view = types.SimpleNamespace(image_width=W, image_height=H, FoVx=cam.FoVx, FoVy=cam.FoVy,
+                                 world_view_transform=cam.world_view_transform.to(dev),
+                                 full_proj_transform=cam.full_proj_transform.to(dev),
+                                 camera_center=cam.camera_center.to(dev), sky_mask=torch.ones(1, H, W, device=dev))
+    pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    bg = torch.zeros(3, device=dev)
+    names = ("render", "diffuse_color", "specular_color", "depth", "normal", "alpha", "normal_ref")
+    dweights = {k: torch.randn(3, H, W, generator=gen).to(dev) for k in names}
 
-    def step():
-        means3D = g["means3D"].detach().requires_grad_(True)
-        opac = g["opacities"].detach().requires_grad_(True)
-        scales = g["scales"].detach().requires_grad_(True)
-        rots = g["rotations"].detach().requires_grad_(True)
-        albedo = mat["albedo"].detach().requires_grad_(True)
-        kr = mat["kr"].detach().requires_grad_(True)
-        km = mat["km"].detach().requires_grad_(True)
-        light.base = base.detach().clone().requires_grad_(True)
-        means2D = torch.zeros_like(means3D, requires_grad=True)
-        fg = means3D[:P_fg]
-        view_pos = cp.expand(P_fg, 3)
-        rgb, ex = light.shade(fg[None, None], mat["normal"][None, None], albedo[None, None], view_pos[None, None],
-                              kr[None, None], km[None, None])
-        rgb, dif, spe = rgb[0, 0], ex["diffuse"][0, 0], ex["specular"][0, 0]
-        cat = lambda x: torch.cat([x, sky_col], 0)
-        depth = (means3D @ vm[:3, :3] + vm[3, :3])[:, 2:3].expand(P, 3)
-        nrm = cat(0.5 * mat["normal"] + 0.5)
-        colours = [cat(rgb), cat(dif), cat(spe), depth, nrm, torch.ones(P, 3, device=dev)]
-        rast = dgr.GaussianRasterizer(settings)
-        loss = 0.0
-        for col, w in zip(colours, dweights):
-            img, _ = rast(means3D=means3D, means2D=means2D, opacities=opac, colors_precomp=col, scales=scales,
-                          rotations=rots)
-            loss = loss + (img * w).sum()
+    def step(fn):
+        t = {k: v.detach().requires_grad_(True) for k, v in leaves.items()}
+        light = relit_shade.EnvironmentLight(base.detach().clone().requires_grad_(True), sh_degree=4)
+        pc = _RelitModel(get_xyz=t["xyz"], get_rotation=t["rotation"], get_scaling=scaling, get_opacity=t["opacity"],
+                         get_is_sky=is_sky.to(dev)[:, None], get_albedo=t["albedo"], get_roughness=t["roughness"],
+                         get_metalness=t["metalness"])
+        out = fn(view, pc, light, sky_sh, 1, pipe, bg, debug=False)
+        loss = sum((out[k] * dweights[k]).sum() for k in names)
         loss.backward()
 
-    def step_channels():
-        """The same six images from one multi-channel composite (render_channels): depth and
-        alpha are single channels expanded to 3 (the reference repeats one value x3)."""
-        means3D = g["means3D"].detach().requires_grad_(True)
-        opac = g["opacities"].detach().requires_grad_(True)
-        scales = g["scales"].detach().requires_grad_(True)
-        rots = g["rotations"].detach().requires_grad_(True)
-        albedo = mat["albedo"].detach().requires_grad_(True)
-        kr = mat["kr"].detach().requires_grad_(True)
-        km = mat["km"].detach().requires_grad_(True)
-        light.base = base.detach().clone().requires_grad_(True)
-        means2D = torch.zeros_like(means3D, requires_grad=True)
-        fg = means3D[:P_fg]
-        view_pos = cp.expand(P_fg, 3)
-        rgb, ex = light.shade(fg[None, None], mat["normal"][None, None], albedo[None, None], view_pos[None, None],
-                              kr[None, None], km[None, None])
-        rgb, dif, spe = rgb[0, 0], ex["diffuse"][0, 0], ex["specular"][0, 0]
-        cat = lambda x: torch.cat([x, sky_col], 0)
-        depth = (means3D @ vm[:3, :3] + vm[3, :3])[:, 2:3]
-        nrm = cat(0.5 * mat["normal"] + 0.5)
-        colours = [cat(rgb), cat(dif), cat(spe), depth, nrm, torch.ones(P, 1, device=dev)]
-        imgs, _ = dgr.GaussianRasterizer(settings).render_channels(
-            means3D=means3D, means2D=means2D, opacities=opac, colors=colours,
-            backgrounds=[zero3, zero3, zero3, zero3[:1], zero3, zero3[:1]], scales=scales, rotations=rots)
-        loss = 0.0
-        for img, w in zip(imgs, dweights):
-            loss = loss + (img.expand(3, H, W) * w).sum()
-        loss.backward()
-
-    for _ in range(args.warmup):
-        step_channels()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step_channels()
-    torch.cuda.synchronize()
-    ms_channels = (time.perf_counter() - t0) * 1e3 / args.steps
-
-    res = {}
-    for cached in (True, False):
-        dgr.geometry_cache(cached)
+    def timed(fn):
         for _ in range(args.warmup):
-            step()
+            step(fn)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
-            step()
+            step(fn)
         torch.cuda.synchronize()
-        res[cached] = (time.perf_counter() - t0) * 1e3 / args.steps
-    dgr.geometry_cache(True)
-    ms = ms_channels
+        return (time.perf_counter() - t0) * 1e3 / args.steps
+
+    ms = timed(relit.render)
+    res = {True: float("nan"), False: float("nan")}
+    if not args.fused_only:
+        for cached in (True, False):
+            dgr.geometry_cache(cached)
+            res[cached] = timed(relit.render_calls)
+        dgr.geometry_cache(True)
     print(json.dumps({
-        "metric": "relit render() views/s (shade + render()'s six images + backward)", "value": round(1e3 / ms, 3),
+        "metric": "relit render() views/s (render()'s images + training loss backward)", "value": round(1e3 / ms, 3),
         "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"cfg3: {P_fg} foreground + {P - P_fg} sky Gaussians, {W}x{H}, env SH deg 4",
-                   "gaussians": P, "width": W, "height": H},
-        "implementation": "one multi-channel composite (render_channels) of the six images",
-        "six_calls": {"cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
-                      "composite_speedup_vs_cached": round(res[True] / ms_channels, 3)}}), flush=True)
+        "config": {"workload": f"cfg3: {P_fg} foreground + {P - P_fg} sky Gaussians, {W}x{H}, env SH deg 4, "
+                               "sky SH deg 1, debug=False", "gaussians": P, "width": W, "height": H},
+        "implementation": "gsr.relit.render: fused relit features + one 14-channel composite",
+        "render_calls": {"cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
+                         "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
 
 
 def main():
@@ -246,6 +208,7 @@ def main():
                                                   "renders from its training camera --view at the reference's "
                                                   "default resolution rule")
     ap.add_argument("--view", type=int, default=0)
+    ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

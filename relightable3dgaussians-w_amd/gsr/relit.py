@@ -132,3 +132,129 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     extras["normal_ref"] = nref + torch.ones_like(nref) * (1 - sky_mask)
     out.update(extras)
     return out
+
+
+_C0, _C1 = 0.28209479177387814, 0.4886025119029199
+_C2 = (1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396)
+_C3 = (-0.5900435899266435, 2.890611442640554, -0.4570457994644658, 0.3731763325901154, -0.4570457994644658,
+       1.445305721320277, -0.5900435899266435)
+
+
+def eval_sh(deg, sh, dirs):
+    """Real SH of degree <= 3 at unit directions (utils/sh_utils.py:81-125, same polynomial
+    order): sh [..., C, K], dirs [..., 3] -> [..., C]."""
+    assert 0 <= deg <= 3
+    res = _C0 * sh[..., 0]
+    if deg > 0:
+        x, y, z = dirs[..., 0:1], dirs[..., 1:2], dirs[..., 2:3]
+        res = res - _C1 * y * sh[..., 1] + _C1 * z * sh[..., 2] - _C1 * x * sh[..., 3]
+        if deg > 1:
+            xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+            res = (res + _C2[0] * xy * sh[..., 4] + _C2[1] * yz * sh[..., 5] +
+                   _C2[2] * (2.0 * zz - xx - yy) * sh[..., 6] + _C2[3] * xz * sh[..., 7] +
+                   _C2[4] * (xx - yy) * sh[..., 8])
+            if deg > 2:
+                res = (res + _C3[0] * y * (3 * xx - yy) * sh[..., 9] + _C3[1] * xy * z * sh[..., 10] +
+                       _C3[2] * y * (4 * zz - xx - yy) * sh[..., 11] +
+                       _C3[3] * z * (2 * zz - 3 * xx - 3 * yy) * sh[..., 12] +
+                       _C3[4] * x * (4 * zz - xx - yy) * sh[..., 13] + _C3[5] * z * (xx - yy) * sh[..., 14] +
+                       _C3[6] * x * (xx - 3 * yy) * sh[..., 15])
+    return res
+
+
+def _prep_torch(pc, light, campos, wvt, sky_sh, sky_sh_degree, specular, fix_sky):
+    """render()'s per-Gaussian steps as the reference writes them in PyTorch
+    (gaussian_renderer/__init__.py:120-200; get_normal gaussian_model.py:115-122,
+    build_rotation / get_minimum_axis / flip_align_view general_utils.py:98-170, get_depth
+    gaussian_model.py:125-130), around the drop-in shade.  Returns [P, 14] rows in the
+    column layout of relit_shade.relit_features."""
+    import relit_shade
+    xyz = pc.get_xyz
+    d = xyz - campos[None]
+    dirn = d / torch.sqrt(torch.clamp((d * d).sum(-1, keepdim=True), min=1e-20))
+    q = pc.get_rotation
+    q = q / torch.sqrt((q * q).sum(1, keepdim=True))
+    r, x, y, z = q.unbind(1)
+    R = torch.stack([torch.stack([1 - 2 * (y * y + z * z), 2 * (x * y - r * z), 2 * (x * z + r * y)], -1),
+                     torch.stack([2 * (x * y + r * z), 1 - 2 * (x * x + z * z), 2 * (y * z - r * x)], -1),
+                     torch.stack([2 * (x * z - r * y), 2 * (y * z + r * x), 1 - 2 * (x * x + y * y)], -1)], 1)
+    axis = R.gather(2, pc.get_scaling.min(dim=-1)[1][..., None, None].expand(-1, 3, -1)).squeeze(2)
+    n = axis * torch.where((axis * -dirn).sum(-1, keepdim=True) >= 0, 1, -1)
+    is_sky = pc.get_is_sky.squeeze()
+    fg = ~is_sky
+    P = xyz.shape[0]
+    rgb, ex = relit_shade.shade(light, xyz[fg][None, None], n[fg][None, None], pc.get_albedo[None, None],
+                                campos.expand(int(fg.sum()), 3)[None, None], pc.get_roughness[None, None],
+                                pc.get_metalness[None, None], specular=specular)
+    cols = torch.zeros(P, 3, device=xyz.device)
+    cols[fg] = rgb[0, 0]
+    if fix_sky or sky_sh is None:
+        cols[is_sky] = 1.0
+    else:
+        sh = sky_sh.transpose(1, 2)  # [1, 3, K] (coefficients last, as eval_sh takes them)
+        cols[is_sky] = torch.clamp_min(eval_sh(sky_sh_degree, sh, dirn[is_sky]) + 0.5, 0.0)
+    dif = torch.zeros(P, 3, device=xyz.device)
+    dif[fg] = ex["diffuse"][0, 0]
+    spe = torch.zeros(P, 3, device=xyz.device)
+    spe[fg] = ex["specular"][0, 0]
+    depth = torch.matmul(wvt.transpose(0, 1), torch.cat([xyz, torch.ones_like(xyz[:, :1])], -1).unsqueeze(-1))[:, 2]
+    return torch.cat([cols, dif, spe, depth, 0.5 * n + 0.5, torch.ones(P, 1, device=xyz.device)], 1), is_sky
+
+
+def render_calls(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color, scaling_modifier=1.0,
+                 debug=True, specular=True, fix_sky=False, normal_view=False):
+    """render() as the reference sequences it: the per-Gaussian steps in PyTorch (around the
+    drop-in shade) and one drop-in rasterizer call per image (the geometry cache makes the
+    repeated calls colour-only).  Same arguments and outputs as `render`; the unfused
+    baseline it is measured against (bench.py --config cfg3)."""
+    import diff_gaussian_rasterization as dgr
+    xyz = pc.get_xyz
+    dev = xyz.device
+    sp = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True) + 0
+    try:
+        sp.retain_grad()
+    except Exception:
+        pass
+    st = dgr.GaussianRasterizationSettings(
+        image_height=int(viewpoint_camera.image_height), image_width=int(viewpoint_camera.image_width),
+        tanfovx=math.tan(viewpoint_camera.FoVx * 0.5), tanfovy=math.tan(viewpoint_camera.FoVy * 0.5), bg=bg_color,
+        scale_modifier=scaling_modifier, viewmatrix=viewpoint_camera.world_view_transform,
+        projmatrix=viewpoint_camera.full_proj_transform, sh_degree=-1, campos=viewpoint_camera.camera_center,
+        prefiltered=False)
+    kw = dict(cov3D_precomp=pc.get_covariance(scaling_modifier)) if pipe.compute_cov3D_python else \
+        dict(scales=pc.get_scaling, rotations=pc.get_rotation)
+    f, is_sky = _prep_torch(pc, envlight, viewpoint_camera.camera_center, viewpoint_camera.world_view_transform,
+                            sky_sh, sky_sh_degree, specular, fix_sky)
+    rast = dgr.GaussianRasterizer(st)
+    call = lambda col, r=rast: r(means3D=xyz, means2D=sp, shs=None, colors_precomp=col.contiguous(),
+                                 opacities=pc.get_opacity, **kw)
+    img, radii = call(f[:, 0:3])
+    out = {"render": img, "viewspace_points": sp, "visibility_filter": radii > 0, "radii": radii}
+    extras = {"diffuse_color": f[:, 3:6], "specular_color": f[:, 6:9], "depth": f[:, 9:10].repeat(1, 3),
+              "normal": f[:, 10:13]}
+    if debug:
+        P = xyz.shape[0]
+        fg = ~is_sky
+        r_all = torch.zeros((P, 1), device=dev)
+        r_all[fg] = pc.get_roughness
+        m_all = torch.zeros((P, 1), device=dev)
+        m_all[fg] = pc.get_metalness
+        a_all = torch.ones_like(xyz)
+        a_all[fg] = pc.get_albedo
+        extras.update({"sky_color": f[:, 0:3] * is_sky[:, None].float(), "roughness": r_all.repeat(1, 3),
+                       "metalness": m_all.repeat(1, 3), "albedo": a_all})
+    sky_mask = viewpoint_camera.sky_mask.to(dev).squeeze()
+    for k, v in extras.items():
+        im = call(v)[0]
+        if k == "normal":
+            im = (im - 0.5) * 2.
+            if normal_view:
+                im = -im.clone()
+            im = im * sky_mask + torch.ones_like(im) * (1 - sky_mask)
+        out[k] = im
+    ra = dgr.GaussianRasterizer(st._replace(bg=torch.zeros(3, device=dev)))
+    out["alpha"] = call(torch.ones_like(xyz), ra)[0]
+    nr = depth_to_normal(viewpoint_camera, (out["depth"][0] * sky_mask).unsqueeze(0)).permute(2, 0, 1)
+    nr = nr * out["alpha"].detach()
+    out["normal_ref"] = nr + torch.ones_like(nr) * (1 - sky_mask)
+    return out
