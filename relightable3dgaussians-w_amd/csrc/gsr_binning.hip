@@ -255,8 +255,10 @@ bool st_bin_supported(int NS) { return 12 * ST_W * NS <= 65536; }
 
 void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
                    uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
-    (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
-    if (Pv <= 0) return;
+    if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
+        (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
+        return;
+    }
     const int nb = (Pv + ST_G - 1) / ST_G;
     char* t = reinterpret_cast<char*>(temp);
     auto take = [&](size_t bytes) {
@@ -352,7 +354,8 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
                                                     const uint32_t* seg_e0, const uint2* st_ranges,
                                                     const uint32_t* st_keys, const uint32_t* st_vals, unsigned gx,
                                                     unsigned gy, unsigned gsx, uint32_t* seg_cnt,
-                                                    const uint32_t* seg_base, uint32_t* point_list) {
+                                                    const uint32_t* seg_base, const uint32_t* tile_start,
+                                                    uint32_t* point_list) {
     __shared__ uint32_t s_wc[4][ST_TILES];
     const uint32_t gseg = blockIdx.x;
     if (gseg >= *nseg_total) return;
@@ -360,8 +363,15 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t e0 = seg_e0[gseg];
     const uint32_t e1 = min(e0 + SEG, st_ranges[st].y);
-    // lane t < 32: running output position of tile t (block-uniform across waves)
-    uint32_t run = (WRITE && lane < ST_TILES) ? seg_base[(size_t)gseg * ST_TILES + lane] : 0u;
+    // lane t < 32: running output position of tile t (block-uniform across waves): the
+    // segment's base within the tile's list + the tile's list start
+    uint32_t run = 0;
+    if (WRITE && lane < ST_TILES) {
+        run = seg_base[(size_t)gseg * ST_TILES + lane];
+        const StGeom g = st_geom(st, gsx, gx, gy);
+        const unsigned lx = lane % GSR_ST_W, ly = lane / GSR_ST_W;
+        if (lx < g.nx && ly < g.ny) run += tile_start[(g.ty0 + ly) * gx + g.tx0 + lx];
+    }
     for (uint32_t b = e0; b < e1; b += 256) {
         const uint32_t e = b + tid;
         uint32_t id = 0, mask = 0;
@@ -421,25 +431,65 @@ __global__ void __launch_bounds__(256) k_seg_prefix(int nst, const uint32_t* st_
     if (lx < g.nx && ly < g.ny) tile_cnt[(g.ty0 + ly) * gx + g.tx0 + lx] = run;
 }
 
-// segment bases become absolute: += tile_start of the tile
-__global__ void __launch_bounds__(256) k_seg_absolute(const uint32_t* nseg_total, const uint32_t* seg_st, unsigned gx,
-                                                       unsigned gy, unsigned gsx, const uint32_t* tile_start,
-                                                       uint32_t* seg_base, long long max_items) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= max_items || i >= (long long)(*nseg_total) * ST_TILES) return;
-    const uint32_t gseg = (uint32_t)(i / ST_TILES), t = (uint32_t)(i % ST_TILES);
-    const StGeom g = st_geom(seg_st[gseg], gsx, gx, gy);
-    const unsigned lx = t % GSR_ST_W, ly = t / GSR_ST_W;
-    if (lx < g.nx && ly < g.ny) seg_base[i] += tile_start[(g.ty0 + ly) * gx + g.tx0 + lx];
-}
 
-// ranges[t] = [start, start + cnt), (0, 0) for empty tiles (rasterizer_impl.cu:310-318)
-__global__ void __launch_bounds__(256) k_tile_ranges(int T, const uint32_t* tile_cnt, const uint32_t* tile_start,
-                                                      uint2* ranges) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= T) return;
-    const uint32_t c = tile_cnt[t];
-    ranges[t] = c ? make_uint2(tile_start[t], tile_start[t] + c) : make_uint2(0u, 0u);
+
+// One 1024-thread workgroup: tile_start = exclusive scan of the tile counts, ranges =
+// [start, start + count) (empty tiles (0, 0)), and tile_nmax zeroed for the forward's
+// atomicMax.  The counts are staged in LDS (up to TS_LDS tiles; larger grids read them
+// from HBM).  (The dispatch order stays its own 8-workgroup launch: its LDS atomics
+// serialise when all eight bands share one CU.)
+constexpr int TS_LDS = 12288;
+__global__ void __launch_bounds__(1024) k_tile_scan(int T, const uint32_t* cnt, uint32_t* start, uint2* ranges,
+                                                     uint32_t* tile_nmax) {
+    __shared__ uint32_t s_cnt[TS_LDS];
+    __shared__ uint32_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const bool in_lds = T <= TS_LDS;
+    if (in_lds) {  // coalesced; all loads issued before the first LDS store
+        uint32_t tmp[TS_LDS / 1024];
+#pragma unroll
+        for (int k = 0; k < TS_LDS / 1024; k++) tmp[k] = tid + 1024 * k < T ? cnt[tid + 1024 * k] : 0u;
+#pragma unroll
+        for (int k = 0; k < TS_LDS / 1024; k++)
+            if (tid + 1024 * k < T) s_cnt[tid + 1024 * k] = tmp[k];
+    }
+    __syncthreads();
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < T; c0 += 8192) {
+        const int base = c0 + tid * 8;
+        uint32_t v[8], tot = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            v[k] = base + k < T ? (in_lds ? s_cnt[base + k] : cnt[base + k]) : 0u;
+            tot += v[k];
+        }
+        uint32_t inc = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += t;
+        }
+        if (lane == 63) wsum[wave] = inc;
+        __syncthreads();
+        uint32_t wpre = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < 16; w++) {
+            wpre += w < wave ? wsum[w] : 0u;
+            all += wsum[w];
+        }
+        uint32_t run = carry + wpre + inc - tot;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            if (base + k < T) {
+                start[base + k] = run;
+                ranges[base + k] = v[k] ? make_uint2(run, run + v[k]) : make_uint2(0u, 0u);
+            }
+            run += v[k];
+        }
+        carry += all;
+        __syncthreads();
+    }
+    for (int t = tid; t < T; t += 1024) tile_nmax[t] = 0;
 }
 
 // ---- host launchers ---------------------------------------------------------------------
@@ -463,7 +513,8 @@ size_t tile_lists_temp_bytes(long long S, int nst) {
 
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
-                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s) {
+                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
+                       int heavy_bits, uint32_t* tile_nmax, hipStream_t s) {
     const int T = (int)(gx * gy);
     const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
     uint32_t* seg_st = reinterpret_cast<uint32_t*>(temp);
@@ -475,20 +526,19 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
                            st_ranges, st_keys, st_vals, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
-                           (uint32_t*)nullptr);
+                           (const uint32_t*)nullptr, (uint32_t*)nullptr);
     }
-    (void)hipMemsetAsync(tile_cnt, 0, sizeof(uint32_t) * (size_t)T, s);
+    // k_seg_prefix writes every tile's count (the super-tiles partition the grid)
     const int np = nst * (int)ST_TILES;
     hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, st_seg0, gx, gy, gsx, seg_cnt,
                        tile_cnt);
-    launch_exclusive_scan_u32(T, tile_cnt, nullptr, tile_start, scan_tmp, nullptr, s);
-    hipLaunchKernelGGL(k_tile_ranges, dim3((T + 255) / 256), dim3(256), 0, s, T, tile_cnt, tile_start, ranges);
+    (void)scan_tmp;
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, tile_nmax);
+    launch_tile_order((unsigned)T, ranges, nullptr, order, nheavy, heavy_bits, s);
     if (G > 0) {
-        const long long items = (long long)G * ST_TILES;
-        hipLaunchKernelGGL(k_seg_absolute, dim3((unsigned)((items + 255) / 256)), dim3(256), 0, s, nseg_total, seg_st,
-                           gx, gy, gsx, tile_start, seg_cnt, items);
         hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
-                           st_ranges, st_keys, st_vals, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, point_list);
+                           st_ranges, st_keys, st_vals, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, tile_start,
+                           point_list);
     }
 }
 

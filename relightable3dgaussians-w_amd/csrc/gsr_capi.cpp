@@ -429,7 +429,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         GSR_STAGE(ST_RANGES);
         gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
                                at<uint32_t>(bin, bl.tile_start), ranges, at<uint32_t>(bin, bl.scan_tmp),
-                               at<void>(bin, bl.lists_tmp), point_list, s);
+                               at<void>(bin, bl.lists_tmp), point_list, at<uint32_t>(img, il.order_fwd),
+                               at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS, at<uint32_t>(img, il.tile_nmax), s);
     }
     GSR_LAUNCH_CHECK();
 
@@ -442,9 +443,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     {
         GSR_STAGE(ST_RENDER_FWD);
-        gsr::launch_tile_order((unsigned)T, ranges, nullptr, at<uint32_t>(img, il.order_fwd), at<uint32_t>(img, il.nheavy),
-                               gsr::FWD_HEAVY_BITS, s);
-        HIP_OK(hipMemsetAsync(ra.tile_nmax, 0, 4 * (size_t)T, s));
+        // dispatch order, nheavy and the zeroed tile_nmax come from launch_tile_lists' tile scan
         if (!mc) {
             gsr::launch_render_fwd(ra, s);
         } else {

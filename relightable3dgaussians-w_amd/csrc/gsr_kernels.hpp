@@ -99,7 +99,8 @@ void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2
 size_t tile_lists_temp_bytes(long long S, int nst);
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
-                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, hipStream_t s);
+                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
+                       int heavy_bits, uint32_t* tile_nmax, hipStream_t s);
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of

@@ -12,72 +12,98 @@
 
 namespace gsr {
 
-// One Gaussian; returns its tile and super-tile counts (0 when culled).
-__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, uint32_t& tiles,
-                                               uint32_t& stc, const float* sh_row) {
-    tiles = stc = 0;
-    a.radii[idx] = 0;
-    a.tiles[idx] = 0;
-    a.st_count[idx] = 0;
-    a.depth_key[idx] = 0xFFFFFFFFu;  // culled Gaussians sort after every visible depth
-    const float3 p_orig = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
-    // in_frustum (auxiliary.h:139-164): near cull only
-    const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
-    if (p_view.z <= 0.2f) {
-        if (a.prefiltered) atomicOr(a.err_flag, 1u);
-        return;
-    }
-    const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
-    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
-    const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
+// One Gaussian's inputs, loaded up front (all of them unconditionally, so that a wave has
+// every global load in flight at once instead of one dependent round trip per stage).
+struct GaussIn {
+    float3 p;
+    float4 rot;
+    float3 scale;
+    float opacity;
+    float3 col;
+    float cov[6];
+};
 
-    float cov3[6];
+__device__ __forceinline__ void load_gauss(const PreprocessArgs& a, const int idx, GaussIn& g) {
+    g.p = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    g.opacity = a.opacities[idx];
     if (a.cov3D_precomp) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
+        for (int i = 0; i < 6; i++) g.cov[i] = a.cov3D_precomp[6 * idx + i];
     } else {
-        const float4 rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
-        cov3d_from(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2], a.scale_modifier, rot, cov3);
+        g.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        g.scale = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
     }
-    const float3 cov = cov2d_from(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3, a.viewmatrix);
-    const float det = (cov.x * cov.z - cov.y * cov.y);
-    if (det == 0.0f) return;
-    const float det_inv = 1.f / det;
-    const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
-    const float mid = 0.5f * (cov.x + cov.z);
-    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
-    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
-    const float2 point_image = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
-    uint2 rmin, rmax;
-    const int irad = f2i(my_radius);
-    get_rect(point_image, irad, a.grid_x, a.grid_y, rmin, rmax);
-    const unsigned area = (rmax.x - rmin.x) * (rmax.y - rmin.y);
-    if (area == 0) return;
+    if (a.colors_precomp)
+        g.col = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
+}
 
-    float3 rgb;
-    if (a.colors_precomp) {
-        rgb = make_float3(a.colors_precomp[3 * idx], a.colors_precomp[3 * idx + 1], a.colors_precomp[3 * idx + 2]);
-    } else if (a.shs) {
-        const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, sh_row);
-        rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
-    } else {
-        rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record
-    }
-    const float opacity = a.opacities[idx];
-    Rec r;
-    r.a = make_float4(point_image.x, point_image.y, conic.x, conic.y);
-    r.b = make_float4(conic.z, opacity, rgb.x, rgb.y);
-    r.c = make_float4(rgb.z, __logf(255.0f * opacity), 0.f, 0.f);
-    a.rec[idx] = r;
-    a.depth_key[idx] = __float_as_uint(p_view.z);
-    a.rect[idx] = make_uint2(rmin.x | (rmax.x << 16), rmin.y | (rmax.y << 16));
+// One Gaussian (forward.cu:155-256).  Every output is stored once; returns the tile and
+// super-tile counts (0 when culled).
+__device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, const GaussIn& g,
+                                               uint32_t& tiles, uint32_t& stc, const float* sh_row) {
+    tiles = stc = 0;
+    int irad = 0;
+    uint32_t key = 0xFFFFFFFFu;  // culled Gaussians sort after every visible depth
+    do {
+        const float3 p_orig = g.p;
+        // in_frustum (auxiliary.h:139-164): near cull only
+        const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
+        if (p_view.z <= 0.2f) {
+            if (a.prefiltered) atomicOr(a.err_flag, 1u);
+            break;
+        }
+        const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
+        const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+        const float3 p_proj = make_float3(p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w);
+
+        float cov3[6];
+        if (a.cov3D_precomp) {
+#pragma unroll
+            for (int i = 0; i < 6; i++) cov3[i] = g.cov[i];
+        } else {
+            cov3d_from(g.scale.x, g.scale.y, g.scale.z, a.scale_modifier, g.rot, cov3);
+        }
+        const float3 cov = cov2d_from(p_orig, a.focal_x, a.focal_y, a.tan_fovx, a.tan_fovy, cov3, a.viewmatrix);
+        const float det = (cov.x * cov.z - cov.y * cov.y);
+        if (det == 0.0f) break;
+        const float det_inv = 1.f / det;
+        const float3 conic = make_float3(cov.z * det_inv, -cov.y * det_inv, cov.x * det_inv);
+        const float mid = 0.5f * (cov.x + cov.z);
+        const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+        const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+        const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+        const float2 point_image = make_float2(ndc2pix(p_proj.x, a.W), ndc2pix(p_proj.y, a.H));
+        uint2 rmin, rmax;
+        const int r_ = f2i(my_radius);
+        get_rect(point_image, r_, a.grid_x, a.grid_y, rmin, rmax);
+        const unsigned area = (rmax.x - rmin.x) * (rmax.y - rmin.y);
+        if (area == 0) break;
+
+        float3 rgb;
+        if (a.colors_precomp) {
+            rgb = g.col;
+        } else if (a.shs) {
+            const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, sh_row);
+            rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
+        } else {
+            rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record
+        }
+        Rec r;
+        r.a = make_float4(point_image.x, point_image.y, conic.x, conic.y);
+        r.b = make_float4(conic.z, g.opacity, rgb.x, rgb.y);
+        r.c = make_float4(rgb.z, __logf(255.0f * g.opacity), 0.f, 0.f);
+        a.rec[idx] = r;
+        a.rect[idx] = make_uint2(rmin.x | (rmax.x << 16), rmin.y | (rmax.y << 16));
+        key = __float_as_uint(p_view.z);
+        irad = r_;
+        tiles = area;
+        stc = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
+              ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
+    } while (false);
+    a.depth_key[idx] = key;
     a.radii[idx] = irad;
-    a.tiles[idx] = area;
-    stc = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
-          ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
+    a.tiles[idx] = tiles;
     a.st_count[idx] = stc;
-    tiles = area;
 }
 
 // Preprocess + the frame totals (visible count P_v, instances R, super-tile entries S):
@@ -93,6 +119,8 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     const int idx = g0 + threadIdx.x;
     const int M3 = a.M * 3, stride = M3 + 1;
     const bool staged = a.shs && !a.colors_precomp;
+    GaussIn gin;
+    if (idx < a.P) load_gauss(a, idx, gin);  // issued before the SH staging: one wait for all
     if (staged) {
         const int rows = min((int)blockDim.x, a.P - g0);
         const float* src = a.shs + (size_t)g0 * M3;
@@ -118,7 +146,7 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     }
     uint32_t tiles = 0, stc = 0;
     if (idx < a.P)
-        preprocess_one(a, idx, tiles, stc, staged ? s_sh + threadIdx.x * stride : nullptr);
+        preprocess_one(a, idx, gin, tiles, stc, staged ? s_sh + threadIdx.x * stride : nullptr);
     unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll

@@ -35,7 +35,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     _lib.require_gpu_tensor(means3D, "means3D")
     dev = means3D.device
     P, H, W = means3D.size(0), int(image_height), int(image_width)
-    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)  # preprocess writes every entry (0 when culled)
     bs = _lib.BufferSet(dev)
     if P == 0:
         return 0, torch.zeros((NUM_CHANNELS, H, W), dtype=torch.float32, device=dev), radii, *bs.bufs
@@ -159,7 +159,7 @@ def rasterize_gaussians_channels(background, means3D, features, opacity, scales,
     if features.size(0) != P or background.numel() != nch or features.size(1) < nch:
         raise ValueError(f"features must be [P, nch] and background [nch] (P={P}, features {tuple(features.shape)}, "
                          f"background {tuple(background.shape)})")
-    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)  # preprocess writes every entry (0 when culled)
     bs = _lib.BufferSet(dev)
     feat = pack_features(features if features.dtype == torch.float32 else features.float(), nch)
     out = torch.empty((nch, H, W), dtype=torch.float32, device=dev)
