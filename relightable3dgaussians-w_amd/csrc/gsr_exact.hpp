@@ -98,6 +98,9 @@ __device__ __forceinline__ float3 cov2d_from(float3 mean, float fx, float fy, fl
 }
 
 // forward.cu:20-71: SH (deg <= 3) -> RGB before clamping.  sh: this Gaussian's [M][3].
+// MAXD: the largest degree the row can hold (register rows of fewer than 16 coefficients
+// prune the higher blocks at compile time); deg must not exceed it.
+template <int MAXD = 3>
 __device__ __forceinline__ float3 sh_to_rgb_raw(int deg, float3 pos, const float* campos, const float* sh) {
     float3 dir = make_float3(pos.x - campos[0], pos.y - campos[1], pos.z - campos[2]);
     const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
@@ -107,12 +110,12 @@ __device__ __forceinline__ float3 sh_to_rgb_raw(int deg, float3 pos, const float
     float res[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) res[c] = SH_C0 * sh[c];
-    if (deg > 0) {
+    if (MAXD > 0 && deg > 0) {
         const float x = dir.x, y = dir.y, z = dir.z;
 #pragma unroll
         for (int c = 0; c < 3; c++)
             res[c] = res[c] - SH_C1 * y * sh[3 + c] + SH_C1 * z * sh[6 + c] - SH_C1 * x * sh[9 + c];
-        if (deg > 1) {
+        if (MAXD > 1 && deg > 1) {
             const float xx = x * x, yy = y * y, zz = z * z;
             const float xy = x * y, yz = y * z, xz = x * z;
 #pragma unroll
@@ -120,7 +123,7 @@ __device__ __forceinline__ float3 sh_to_rgb_raw(int deg, float3 pos, const float
                 res[c] = res[c] + SH_C2_0 * xy * sh[12 + c] + SH_C2_1 * yz * sh[15 + c] +
                          SH_C2_2 * (2.0f * zz - xx - yy) * sh[18 + c] + SH_C2_3 * xz * sh[21 + c] +
                          SH_C2_4 * (xx - yy) * sh[24 + c];
-            if (deg > 2) {
+            if (MAXD > 2 && deg > 2) {
 #pragma unroll
                 for (int c = 0; c < 3; c++)
                     res[c] = res[c] + SH_C3_0 * y * (3.0f * xx - yy) * sh[27 + c] + SH_C3_1 * xy * z * sh[30 + c] +

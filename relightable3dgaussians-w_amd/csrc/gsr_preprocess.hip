@@ -39,6 +39,7 @@ __device__ __forceinline__ void load_gauss(const PreprocessArgs& a, const int id
 
 // One Gaussian (forward.cu:155-256).  Every output is stored once; returns the tile and
 // super-tile counts (0 when culled).
+template <int MAXD = 3>
 __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, const GaussIn& g,
                                                uint32_t& tiles, uint32_t& stc, const float* sh_row) {
     tiles = stc = 0;
@@ -83,7 +84,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
         if (a.colors_precomp) {
             rgb = g.col;
         } else if (a.shs) {
-            const float3 raw = sh_to_rgb_raw(a.D, p_orig, a.campos, sh_row);
+            const float3 raw = sh_to_rgb_raw<MAXD>(a.D, p_orig, a.campos, sh_row);
             rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
         } else {
             rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record
@@ -163,6 +164,52 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     }
 }
 
+// SH path with M in {1, 4, 9, 16}: each thread loads its own SH row into registers with
+// the other inputs (16-B loads when 3M is a multiple of 4) -- no LDS, so occupancy is
+// bounded by registers only (16 coefficients: 102 vs 130 us at cfg2 against the
+// LDS-staged k_preprocess, which serves any other M).
+template <int M>
+__global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
+    __shared__ unsigned long long sh[3][4];
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    GaussIn gin;
+    float shr[3 * M];
+    if (idx < a.P) {
+        load_gauss(a, idx, gin);
+        if constexpr ((3 * M) % 4 == 0) {
+            const float4* s4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 3 * M);
+#pragma unroll
+            for (int k = 0; k < 3 * M / 4; k++) {
+                const float4 v = s4[k];
+                shr[4 * k] = v.x;
+                shr[4 * k + 1] = v.y;
+                shr[4 * k + 2] = v.z;
+                shr[4 * k + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 3 * M; k++) shr[k] = a.shs[(size_t)idx * 3 * M + k];
+        }
+    }
+    uint32_t tiles = 0, stc = 0;
+    if (idx < a.P) preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr);
+    unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+        if (lane == 0) sh[k][wave] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int k = threadIdx.x;
+        const unsigned long long t = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
+        if (t) atomicAdd(a.totals + TOTAL_STRIDE * (blockIdx.x % TOTAL_SLOTS) + k, t);
+    }
+}
+
+
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,
                                                        bool* present) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -196,6 +243,18 @@ void launch_recolor(int P, const int* radii_src, const Rec* src, const float* co
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
     if (a.P == 0) return;
+    const int maxd = a.M >= 16 ? 3 : a.M >= 9 ? 2 : a.M >= 4 ? 1 : 0;
+    if (a.shs && !a.colors_precomp && a.D <= maxd) {
+        const dim3 grid((a.P + 255) / 256), blk(256);
+        const bool al16 = (reinterpret_cast<uintptr_t>(a.shs) & 15u) == 0;
+        switch (a.M) {
+            case 1: hipLaunchKernelGGL(k_preprocess_regsh<1>, grid, blk, 0, s, a); return;
+            case 4: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<4>, grid, blk, 0, s, a); return; } break;
+            case 9: hipLaunchKernelGGL(k_preprocess_regsh<9>, grid, blk, 0, s, a); return;
+            case 16: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<16>, grid, blk, 0, s, a); return; } break;
+            default: break;
+        }
+    }
     const size_t lds = (a.shs && !a.colors_precomp) ? sizeof(float) * 256 * (size_t)(3 * a.M + 1) : 0;
     hipLaunchKernelGGL(k_preprocess, dim3((a.P + 255) / 256), dim3(256), lds, s, a);
 }
