@@ -21,6 +21,10 @@
  *                      render()'s per-Gaussian colour preparation (normals, shade, sky
  *                      colour, depth; gaussian_renderer/__init__.py:120-200) fused into
  *                      the composite's feature rows
+ *   gsr_relit_epilogue / gsr_relit_epilogue_backward
+ *                      render()'s image-space tail: normal remap + sky mask and normal_ref
+ *                      from the depth image (gaussian_renderer/__init__.py:226-276,
+ *                      utils/graphics_utils.py:141-169)
  *   gsr_forward_channels / gsr_backward_channels
  *                      the 6-10 same-geometry rasterizer calls of one render()
  *                      (gaussian_renderer/__init__.py:160-264) as ONE composite of all
@@ -146,6 +150,20 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
                                 const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
                                 float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
                                 void* workspace, void* stream);
+
+/* render()'s image-space tail over the composite's images ([H,W] planes, [3,H,W] for n01):
+ *   normal     = ((n01 - 0.5) * 2 * (normal_view ? -1 : 1)) * sky + (1 - sky)
+ *   normal_ref = normalize(cross(p[y+1] - p[y-1], p[x+1] - p[x-1])) * alpha + (1 - sky),
+ *                zero normals on the one-pixel border, p = (depth * sky) * rays + centre.
+ * cam12 (host memory): rows M0, M1, M2 of K^-1^T R^T (rays = x M0 + y M1 + M2) and the
+ * camera centre.  The backward gives dL/dn01 and dL/ddepth (alpha gets none: the
+ * reference detaches it). */
+int gsr_relit_epilogue(int width, int height, const float* cam12, const float* n01, const float* depth,
+                       const float* alpha, const float* sky_mask, int normal_view, float* normal, float* normal_ref,
+                       void* stream);
+int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const float* depth, const float* alpha,
+                                const float* sky_mask, int normal_view, const float* g_normal,
+                                const float* g_normal_ref, float* d_n01, float* d_depth, void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -824,4 +824,27 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
     return GSR_OK;
 }
 
+int gsr_relit_epilogue(int width, int height, const float* cam12, const float* n01, const float* depth,
+                       const float* alpha, const float* sky_mask, int normal_view, float* normal, float* normal_ref,
+                       void* stream_) {
+    if (width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_relit_epilogue: bad size");
+    if (!cam12 || !n01 || !depth || !alpha || !sky_mask || !normal || !normal_ref)
+        return fail(GSR_E_ARG, "gsr_relit_epilogue: missing buffers");
+    gsr::launch_epilogue_fwd(width, height, cam12, n01, depth, alpha, sky_mask, normal_view, normal, normal_ref,
+                             reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const float* depth, const float* alpha,
+                                const float* sky_mask, int normal_view, const float* g_normal,
+                                const float* g_normal_ref, float* d_n01, float* d_depth, void* stream_) {
+    if (width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_relit_epilogue_backward: bad size");
+    if (!cam12 || !depth || !alpha || !sky_mask) return fail(GSR_E_ARG, "gsr_relit_epilogue_backward: missing buffers");
+    gsr::launch_epilogue_bwd(width, height, cam12, depth, alpha, sky_mask, normal_view, g_normal, g_normal_ref, d_n01,
+                             d_depth, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

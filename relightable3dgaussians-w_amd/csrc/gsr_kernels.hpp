@@ -169,6 +169,13 @@ struct RenderMcArgs {
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);
 
+// render()'s image-space tail (gsr_epilogue.hip): cam12 = rows of K^-1^T R^T, then the centre
+void launch_epilogue_fwd(int W, int H, const float* cam12, const float* n01, const float* depth, const float* alpha,
+                         const float* sky, int normal_view, float* normal, float* normal_ref, hipStream_t s);
+void launch_epilogue_bwd(int W, int H, const float* cam12, const float* depth, const float* alpha, const float* sky,
+                         int normal_view, const float* g_normal, const float* g_normal_ref, float* d_n01,
+                         float* d_depth, hipStream_t s);
+
 struct PreprocessBwdArgs {
     int P, D, M;
     const float* means3D;

@@ -51,6 +51,8 @@ def _declare(lib):
     lib.gsr_relit_features.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp]
     lib.gsr_relit_features_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp,
                                                 vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.gsr_relit_epilogue.argtypes = [i, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
+    lib.gsr_relit_epilogue_backward.argtypes = [i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
     lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
     lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                        vp, vp, vp]
@@ -66,7 +68,8 @@ def _declare(lib):
     lib.gsr_version.restype = C.c_char_p
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
-               "gsr_relit_features", "gsr_relit_features_backward",
+               "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
+               "gsr_relit_epilogue_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 

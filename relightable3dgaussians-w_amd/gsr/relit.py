@@ -22,16 +22,19 @@ import torch
 
 
 def depths_to_points(view, depthmap):
-    """graphics_utils.py:141-156: back-project a depth map through the camera."""
+    """graphics_utils.py:141-156: back-project a depth map through the camera.  The
+    reference's `pixels @ K^-1^T @ R^T` is written as three broadcast multiply-adds per
+    pixel (two [H*W,3] @ [3,3] GEMMs cost ~130 us each on hipBLASLt at 1080p)."""
     c2w = view.world_view_transform.T.inverse()
     W, H = view.image_width, view.image_height
     fx = W / (2 * math.tan(view.FoVx / 2.))
     fy = H / (2 * math.tan(view.FoVy / 2.))
     dev = depthmap.device
     intrins = torch.tensor([[fx, 0., W / 2.], [0., fy, H / 2.], [0., 0., 1.0]], device=dev).float()
-    gx, gy = torch.meshgrid(torch.arange(W, device=dev).float(), torch.arange(H, device=dev).float(), indexing="xy")
-    pts = torch.stack([gx, gy, torch.ones_like(gx)], dim=-1).reshape(-1, 3)
-    rays_d = pts @ intrins.inverse().T @ c2w[:3, :3].T
+    M = intrins.inverse().T @ c2w[:3, :3].T  # [3, 3]: rays_d = [x, y, 1] @ M
+    gx = torch.arange(W, device=dev).float()
+    gy = torch.arange(H, device=dev).float()
+    rays_d = (gx[None, :, None] * M[0] + gy[:, None, None] * M[1] + M[2]).reshape(-1, 3)
     return depthmap.reshape(-1, 1) * rays_d + c2w[:3, 3]
 
 
@@ -43,6 +46,55 @@ def depth_to_normal(view, depth):
     dy = points[1:-1, 2:] - points[1:-1, :-2]
     out[1:-1, 1:-1, :] = torch.nn.functional.normalize(torch.cross(dx, dy, dim=-1), dim=-1)
     return out
+
+
+def _epilogue_camera(view):
+    """cam12 for gsr_relit_epilogue: rows of K^-1^T R^T (rays = x M0 + y M1 + M2) and the
+    camera centre, as depths_to_points builds them."""
+    c2w = view.world_view_transform.T.inverse().double()
+    W, H = view.image_width, view.image_height
+    fx = W / (2 * math.tan(view.FoVx / 2.))
+    fy = H / (2 * math.tan(view.FoVy / 2.))
+    K = torch.tensor([[fx, 0., W / 2.], [0., fy, H / 2.], [0., 0., 1.0]], dtype=torch.float64, device=c2w.device)
+    M = K.inverse().T @ c2w[:3, :3].T
+    return torch.cat([M.reshape(-1), c2w[:3, 3]]).float().cpu().contiguous()
+
+
+class _Epilogue(torch.autograd.Function):
+    """render()'s image-space tail on the GPU (gsr_relit_epilogue): (n01 [3,H,W], depth
+    [H,W], alpha [H,W] (detached), sky [H,W]) -> (normal, normal_ref), both [3,H,W]."""
+
+    @staticmethod
+    def forward(ctx, n01, depth, alpha, sky, cam12, normal_view):
+        from . import _lib
+        H, W = depth.shape
+        n01, depth, alpha, sky = (t.float().contiguous() for t in (n01, depth, alpha, sky))
+        normal = torch.empty((3, H, W), dtype=torch.float32, device=depth.device)
+        nref = torch.empty_like(normal)
+        _lib.check(_lib.lib().gsr_relit_epilogue(W, H, cam12.data_ptr(), n01.data_ptr(), depth.data_ptr(),
+                                                 alpha.data_ptr(), sky.data_ptr(), int(normal_view),
+                                                 normal.data_ptr(), nref.data_ptr(), _lib.stream_of(depth.device)),
+                   "gsr_relit_epilogue")
+        ctx.save_for_backward(depth, alpha, sky, cam12)
+        ctx.normal_view = normal_view
+        return normal, nref
+
+    @staticmethod
+    def backward(ctx, g_normal, g_nref):
+        from . import _lib
+        depth, alpha, sky, cam12 = ctx.saved_tensors
+        H, W = depth.shape
+        c = lambda t: None if t is None else t.float().contiguous()
+        g_normal, g_nref = c(g_normal), c(g_nref)
+        d_n01 = torch.empty((3, H, W), dtype=torch.float32, device=depth.device) if ctx.needs_input_grad[0] else None
+        d_depth = torch.empty_like(depth) if ctx.needs_input_grad[1] else None
+        ptr = lambda t: None if t is None else t.data_ptr()
+        if d_n01 is not None or d_depth is not None:
+            _lib.check(_lib.lib().gsr_relit_epilogue_backward(
+                W, H, cam12.data_ptr(), depth.data_ptr(), alpha.data_ptr(), sky.data_ptr(), int(ctx.normal_view),
+                ptr(g_normal), ptr(g_nref), ptr(d_n01), ptr(d_depth), _lib.stream_of(depth.device)),
+                "gsr_relit_epilogue_backward")
+        return d_n01, d_depth, None, None, None, None
 
 
 def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color, scaling_modifier=1.0, debug=True,
@@ -123,13 +175,10 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     out = {"render": imgs["render"], "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
            "radii": radii}
     extras = {k: v for k, v in imgs.items() if k != "render"}
-    nrm = (extras["normal"] - 0.5) * 2.
-    if normal_view:
-        nrm = -nrm.clone()
-    extras["normal"] = nrm * sky_mask + torch.ones_like(nrm) * (1 - sky_mask)
-    nref = depth_to_normal(viewpoint_camera, (extras["depth"][0] * sky_mask).unsqueeze(0)).permute(2, 0, 1)
-    nref = nref * extras["alpha"].detach()
-    extras["normal_ref"] = nref + torch.ones_like(nref) * (1 - sky_mask)
+    # normal remap + sky mask and normal_ref from the depth image in one kernel each way
+    extras["normal"], extras["normal_ref"] = _Epilogue.apply(
+        extras["normal"], extras["depth"][0], extras["alpha"][0].detach(), sky_mask.float(),
+        _epilogue_camera(viewpoint_camera), bool(normal_view))
     out.update(extras)
     return out
 

@@ -152,13 +152,15 @@ class RelitFeaturesFunction(torch.autograd.Function):
         P, N = xyz.shape[0], fg_rows.shape[0]
         dev = xyz.device
         g_feat = g_feat.float().contiguous()
-        d_xyz = torch.zeros_like(xyz)
-        d_rot = torch.zeros_like(rotation)
-        d_alb = torch.zeros_like(albedo)
-        d_kr = torch.zeros_like(roughness) if ctx.has[0] else None
-        d_km = torch.zeros_like(metalness) if ctx.has[1] else None
-        d_base = torch.zeros_like(base)
-        d_sky = torch.zeros_like(sky_sh) if ctx.has[2] and ctx.sky_deg >= 0 else None
+        # every entry is written by the kernels (d_kr / d_km only with specular)
+        d_xyz = torch.empty_like(xyz)
+        d_rot = torch.empty_like(rotation)
+        d_alb = torch.empty_like(albedo)
+        zk = torch.empty_like if ctx.specular else torch.zeros_like
+        d_kr = zk(roughness) if ctx.has[0] else None
+        d_km = zk(metalness) if ctx.has[1] else None
+        d_base = torch.empty_like(base)
+        d_sky = torch.empty_like(sky_sh) if ctx.has[2] and ctx.sky_deg >= 0 else None
         ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
         _lib.check(_lib.lib().gsr_relit_features_backward(
             P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),

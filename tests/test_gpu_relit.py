@@ -242,3 +242,41 @@ def test_fused_render_matches_reference_calls(bg, debug):
         assert _rel(o_f[k], o_r[k]) < 1e-5, (k, _rel(o_f[k], o_r[k]))
     for name, a, b in zip(["xyz", "rotation", "albedo", "base", "opacity", "means2D"], g_f, g_r):
         assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+
+
+@pytest.mark.parametrize("normal_view", [False, True])
+def test_epilogue_matches_torch_restatement(normal_view):
+    """gsr_relit_epilogue (normal remap + sky mask + normal_ref) against render()'s PyTorch
+    tail (gaussian_renderer/__init__.py:226-276 with depth_to_normal), forward and backward."""
+    from gsr import relit
+    from gsr import scenes
+    H, W = 70, 96
+    R, T = scenes.look_at_rotation([0.4, -0.3, -1.0], [0.0, 0.0, 5.0])
+    cam = scenes.make_camera(W, H, 1.1, 0.85, R=R, T=T)
+    view = types.SimpleNamespace(world_view_transform=cam.world_view_transform.cuda(), image_width=W, image_height=H,
+                                 FoVx=cam.FoVx, FoVy=cam.FoVy)
+    g = torch.Generator().manual_seed(3)
+    n01 = torch.rand(3, H, W, generator=g).cuda()
+    depth = (torch.rand(H, W, generator=g) * 0.5 + 4.0).cuda()
+    alpha = torch.rand(H, W, generator=g).cuda()
+    sky = (torch.rand(H, W, generator=g) > 0.15).float().cuda()
+    w1, w2 = torch.randn(3, H, W, generator=g).cuda(), torch.randn(3, H, W, generator=g).cuda()
+
+    def torch_tail(n, d):
+        nrm = (n - 0.5) * 2.
+        if normal_view:
+            nrm = -nrm.clone()
+        nrm = nrm * sky + torch.ones_like(nrm) * (1 - sky)
+        nr = relit.depth_to_normal(view, (d * sky).unsqueeze(0)).permute(2, 0, 1) * alpha
+        return nrm, nr + torch.ones_like(nr) * (1 - sky)
+
+    def run(fn):
+        n, d = n01.clone().requires_grad_(True), depth.clone().requires_grad_(True)
+        a, b = fn(n, d)
+        ((a * w1).sum() + (b * w2).sum()).backward()
+        return a.detach(), b.detach(), n.grad, d.grad
+
+    got = run(lambda n, d: relit._Epilogue.apply(n, d, alpha, sky, relit._epilogue_camera(view), normal_view))
+    want = run(torch_tail)
+    for name, a, b in zip(("normal", "normal_ref", "d_n01", "d_depth"), got, want):
+        assert _rel(a, b) < 1e-5, (name, _rel(a, b))

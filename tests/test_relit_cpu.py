@@ -31,3 +31,23 @@ def test_depth_to_normal_plane():
     assert n.shape == (24, 32, 3)
     np.testing.assert_allclose(n[1:-1, 1:-1].numpy(), np.broadcast_to([0.0, 0.0, -1.0], (22, 30, 3)), atol=1e-6)
     assert not n[0].any() and not n[:, 0].any()
+
+
+def test_depths_to_points_matches_reference_formula():
+    """The broadcast form of graphics_utils.py:141-156 equals the reference's matrix form
+    (pixels @ K^-1^T @ R^T) to float rounding on a rotated, translated camera."""
+    import math
+    import types
+    from gsr import scenes
+    R, T = scenes.look_at_rotation([0.5, 0.2, -1.0], [0.0, 0.0, 5.0])
+    cam = scenes.make_camera(64, 48, 1.0, 0.8, R=R, T=T)
+    view = types.SimpleNamespace(world_view_transform=cam.world_view_transform, image_width=64, image_height=48,
+                                 FoVx=cam.FoVx, FoVy=cam.FoVy)
+    d = torch.rand(1, 48, 64, generator=torch.Generator().manual_seed(0)) + 1
+    c2w = view.world_view_transform.T.inverse()
+    fx, fy = 64 / (2 * math.tan(view.FoVx / 2.)), 48 / (2 * math.tan(view.FoVy / 2.))
+    K = torch.tensor([[fx, 0., 32.], [0., fy, 24.], [0., 0., 1.0]]).float()
+    gx, gy = torch.meshgrid(torch.arange(64).float(), torch.arange(48).float(), indexing="xy")
+    pts = torch.stack([gx, gy, torch.ones_like(gx)], dim=-1).reshape(-1, 3)
+    ref = d.reshape(-1, 1) * (pts @ K.inverse().T @ c2w[:3, :3].T) + c2w[:3, 3]
+    np.testing.assert_allclose(relit.depths_to_points(view, d).numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
