@@ -14,7 +14,7 @@
 
 namespace gsr {
 
-template <int MC>
+template <int MC, bool DO_SH = true>
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* row);
 
 // auxiliary.h:107-117
@@ -86,11 +86,115 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     }
 }
 
+// backward.cu:20-139 for one Gaussian: reads the SH coefficients from `row`, overwrites
+// them with dL/dsh (each degree block reads its coefficients before overwriting them) and
+// returns the view-direction part of dL/dmean3D.  MC as preprocess_bwd_one.
+template <int MC>
+__device__ __forceinline__ float3 sh_bwd_row(const PreprocessBwdArgs& a, float3 mean, float* row, float dcol0,
+                                             float dcol1, float dcol2) {
+    // backward.cu:20-139 on this Gaussian's LDS row (coalesced in/out, see below);
+    // each degree block reads its coefficients before overwriting them with dL/dsh.
+    float* sh = row;
+    constexpr int MAXD = MC == 0 ? 3 : (MC >= 16 ? 3 : MC >= 9 ? 2 : MC >= 4 ? 1 : 0);
+    const float3 raw = sh_to_rgb_raw<MAXD>(a.D, mean, a.campos, sh);  // clamp flags, as the forward
+    const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
+    const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+    float g[3] = {dcol0 * (raw.x < 0 ? 0 : 1), dcol1 * (raw.y < 0 ? 0 : 1), dcol2 * (raw.z < 0 ? 0 : 1)};
+    float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
+    const int deg = a.D;
+    float* dsh = sh;
+#define SHC(k, c) sh[3 * (k) + (c)]
+#pragma unroll
+    for (int c = 0; c < 3; c++) dsh[c] = SH_C0 * g[c];
+    if ((MC == 0 || MC >= 4) && deg > 0) {
+        const float b1 = -SH_C1 * y, b2 = SH_C1 * z, b3 = -SH_C1 * x;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            ddx[c] = -SH_C1 * SHC(3, c);
+            ddy[c] = -SH_C1 * SHC(1, c);
+            ddz[c] = SH_C1 * SHC(2, c);
+            dsh[3 + c] = b1 * g[c];
+            dsh[6 + c] = b2 * g[c];
+            dsh[9 + c] = b3 * g[c];
+        }
+        if ((MC == 0 || MC >= 9) && deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            const float b4 = SH_C2_0 * xy, b5 = SH_C2_1 * yz, b6 = SH_C2_2 * (2.f * zz - xx - yy);
+            const float b7 = SH_C2_3 * xz, b8 = SH_C2_4 * (xx - yy);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
+                          SH_C2_4 * 2.f * x * SHC(8, c);
+                ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
+                          SH_C2_4 * 2.f * -y * SHC(8, c);
+                ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
+                dsh[12 + c] = b4 * g[c];
+                dsh[15 + c] = b5 * g[c];
+                dsh[18 + c] = b6 * g[c];
+                dsh[21 + c] = b7 * g[c];
+                dsh[24 + c] = b8 * g[c];
+            }
+            if ((MC == 0 || MC >= 16) && deg > 2) {
+                const float b9 = SH_C3_0 * y * (3.f * xx - yy);
+                const float b10 = SH_C3_1 * xy * z;
+                const float b11 = SH_C3_2 * y * (4.f * zz - xx - yy);
+                const float b12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                const float b13 = SH_C3_4 * x * (4.f * zz - xx - yy);
+                const float b14 = SH_C3_5 * z * (xx - yy);
+                const float b15 = SH_C3_6 * x * (xx - 3.f * yy);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
+                               SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
+                               SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
+                               SH_C3_5 * SHC(14, c) * 2.f * xz + SH_C3_6 * SHC(15, c) * 3.f * (xx - yy));
+                    ddy[c] += (SH_C3_0 * SHC(9, c) * 3.f * (xx - yy) + SH_C3_1 * SHC(10, c) * xz +
+                               SH_C3_2 * SHC(11, c) * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3_3 * SHC(12, c) * -3.f * 2.f * yz + SH_C3_4 * SHC(13, c) * -2.f * xy +
+                               SH_C3_5 * SHC(14, c) * -2.f * yz + SH_C3_6 * SHC(15, c) * -3.f * 2.f * xy);
+                    ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
+                               SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
+                               SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
+                    dsh[27 + c] = b9 * g[c];
+                    dsh[30 + c] = b10 * g[c];
+                    dsh[33 + c] = b11 * g[c];
+                    dsh[36 + c] = b12 * g[c];
+                    dsh[39 + c] = b13 * g[c];
+                    dsh[42 + c] = b14 * g[c];
+                    dsh[45 + c] = b15 * g[c];
+                }
+            }
+        }
+    }
+#undef SHC
+    // coefficients above the evaluated degree get zero gradient (torch::zeros in the reference)
+    const int kmin = deg < 0 ? 0 : (deg > 3 ? 16 : (deg + 1) * (deg + 1));
+    if constexpr (MC > 0) {
+#pragma unroll
+        for (int k = 0; k < MC; k++)
+            if (k >= kmin) dsh[3 * k] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
+    } else {
+        for (int k = kmin; k < a.M; k++) {
+            dsh[3 * k] = 0.f;
+            dsh[3 * k + 1] = 0.f;
+            dsh[3 * k + 2] = 0.f;
+        }
+    }
+    const float3 dL_ddir = make_float3(ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2],
+                                       ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2],
+                                       ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2]);
+    return dnormvdv3(dir_orig, dL_ddir);
+}
+
 // `row` holds the Gaussian's SH coefficients (MC > 0: a register array of 3 MC floats; MC
 // == 0: an LDS row of a.M * 3 floats, k_preprocess_bwd).  The SH backward reads the
-// coefficients from the row and overwrites them with dL/dsh.  (Register rows measured
-// slower here, 242 vs 199 us at cfg2: 182 VGPRs leave 2 waves per SIMD.)
-template <int MC>
+// coefficients from the row and overwrites them with dL/dsh.  (Measured slower at cfg2:
+// register rows, 242 vs 199 us -- 182 VGPRs leave 2 waves per SIMD; and a split into a
+// geometry kernel + a register-row SH kernel, 63 + 196 us -- its strided 16-B row stores
+// write partial lines, where the LDS-staged rows leave the workgroup as whole lines.)
+template <int MC, bool DO_SH>
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* row) {
     // ---- unpack the render-backward accumulator line ------------------------------
     const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
@@ -111,7 +215,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 
     float* dcov = a.dL_dcov3D + 6 * idx;
     float* dsh = row;  // written back by the caller when dL_dsh is requested
-    const bool want_dsh = a.dL_dsh != nullptr;
+    const bool want_dsh = DO_SH && a.dL_dsh != nullptr;
     if (!(a.radii[idx] > 0)) {
         a.dL_dmean3D[3 * idx + 0] = 0.f;
         a.dL_dmean3D[3 * idx + 1] = 0.f;
@@ -230,101 +334,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     dm.y += (proj[4] * m_w - proj[7] * mul1) * dm2x + (proj[5] * m_w - proj[7] * mul2) * dm2y;
     dm.z += (proj[8] * m_w - proj[11] * mul1) * dm2x + (proj[9] * m_w - proj[11] * mul2) * dm2y;
 
-    if (a.shs) {
-        // backward.cu:20-139 on this Gaussian's LDS row (coalesced in/out, see below);
-        // each degree block reads its coefficients before overwriting them with dL/dsh.
-        float* sh = row;
-        constexpr int MAXD = MC == 0 ? 3 : (MC >= 16 ? 3 : MC >= 9 ? 2 : MC >= 4 ? 1 : 0);
-        const float3 raw = sh_to_rgb_raw<MAXD>(a.D, mean, a.campos, sh);  // clamp flags, as the forward
-        const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
-        const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-        const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-        float g[3] = {dcol0 * (raw.x < 0 ? 0 : 1), dcol1 * (raw.y < 0 ? 0 : 1), dcol2 * (raw.z < 0 ? 0 : 1)};
-        float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
-        const int deg = a.D;
-        float* dsh = sh;
-#define SHC(k, c) sh[3 * (k) + (c)]
-#pragma unroll
-        for (int c = 0; c < 3; c++) dsh[c] = SH_C0 * g[c];
-        if ((MC == 0 || MC >= 4) && deg > 0) {
-            const float b1 = -SH_C1 * y, b2 = SH_C1 * z, b3 = -SH_C1 * x;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                ddx[c] = -SH_C1 * SHC(3, c);
-                ddy[c] = -SH_C1 * SHC(1, c);
-                ddz[c] = SH_C1 * SHC(2, c);
-                dsh[3 + c] = b1 * g[c];
-                dsh[6 + c] = b2 * g[c];
-                dsh[9 + c] = b3 * g[c];
-            }
-            if ((MC == 0 || MC >= 9) && deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z;
-                const float xy = x * y, yz = y * z, xz = x * z;
-                const float b4 = SH_C2_0 * xy, b5 = SH_C2_1 * yz, b6 = SH_C2_2 * (2.f * zz - xx - yy);
-                const float b7 = SH_C2_3 * xz, b8 = SH_C2_4 * (xx - yy);
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
-                              SH_C2_4 * 2.f * x * SHC(8, c);
-                    ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
-                              SH_C2_4 * 2.f * -y * SHC(8, c);
-                    ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
-                    dsh[12 + c] = b4 * g[c];
-                    dsh[15 + c] = b5 * g[c];
-                    dsh[18 + c] = b6 * g[c];
-                    dsh[21 + c] = b7 * g[c];
-                    dsh[24 + c] = b8 * g[c];
-                }
-                if ((MC == 0 || MC >= 16) && deg > 2) {
-                    const float b9 = SH_C3_0 * y * (3.f * xx - yy);
-                    const float b10 = SH_C3_1 * xy * z;
-                    const float b11 = SH_C3_2 * y * (4.f * zz - xx - yy);
-                    const float b12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                    const float b13 = SH_C3_4 * x * (4.f * zz - xx - yy);
-                    const float b14 = SH_C3_5 * z * (xx - yy);
-                    const float b15 = SH_C3_6 * x * (xx - 3.f * yy);
-#pragma unroll
-                    for (int c = 0; c < 3; c++) {
-                        ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
-                                   SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
-                                   SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
-                                   SH_C3_5 * SHC(14, c) * 2.f * xz + SH_C3_6 * SHC(15, c) * 3.f * (xx - yy));
-                        ddy[c] += (SH_C3_0 * SHC(9, c) * 3.f * (xx - yy) + SH_C3_1 * SHC(10, c) * xz +
-                                   SH_C3_2 * SHC(11, c) * (-3.f * yy + 4.f * zz - xx) +
-                                   SH_C3_3 * SHC(12, c) * -3.f * 2.f * yz + SH_C3_4 * SHC(13, c) * -2.f * xy +
-                                   SH_C3_5 * SHC(14, c) * -2.f * yz + SH_C3_6 * SHC(15, c) * -3.f * 2.f * xy);
-                        ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
-                                   SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
-                                   SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
-                        dsh[27 + c] = b9 * g[c];
-                        dsh[30 + c] = b10 * g[c];
-                        dsh[33 + c] = b11 * g[c];
-                        dsh[36 + c] = b12 * g[c];
-                        dsh[39 + c] = b13 * g[c];
-                        dsh[42 + c] = b14 * g[c];
-                        dsh[45 + c] = b15 * g[c];
-                    }
-                }
-            }
-        }
-#undef SHC
-        // coefficients above the evaluated degree get zero gradient (torch::zeros in the reference)
-        const int kmin = deg < 0 ? 0 : (deg > 3 ? 16 : (deg + 1) * (deg + 1));
-        if constexpr (MC > 0) {
-#pragma unroll
-            for (int k = 0; k < MC; k++)
-                if (k >= kmin) dsh[3 * k] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
-        } else {
-            for (int k = kmin; k < a.M; k++) {
-                dsh[3 * k] = 0.f;
-                dsh[3 * k + 1] = 0.f;
-                dsh[3 * k + 2] = 0.f;
-            }
-        }
-        const float3 dL_ddir = make_float3(ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2],
-                                           ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2],
-                                           ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2]);
-        const float3 d = dnormvdv3(dir_orig, dL_ddir);
+    if (DO_SH && a.shs) {
+        const float3 d = sh_bwd_row<MC>(a, mean, row, dcol0, dcol1, dcol2);
         dm.x += d.x;
         dm.y += d.y;
         dm.z += d.z;
