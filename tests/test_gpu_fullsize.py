@@ -180,3 +180,22 @@ def test_forward_is_deterministic(cfg2):
     assert torch.equal(st["color"], st2["color"])
     np.testing.assert_array_equal(st["point_list"], st2["point_list"])
     np.testing.assert_array_equal(st["n_contrib"], st2["n_contrib"])
+
+
+def test_4k_frame_binning_exact():
+    """3840x2160 (cfg5's frame): 30 x 34 = 1020 super-tiles exceed the fused
+    super-tile binning's LDS budget, so this runs the emit + offsets scan + one-pass sort
+    path.  Its point_list and tile ranges must equal the oracle's (tile, depth, index)
+    order bit for bit."""
+    from gsr import scenes
+    cam, gs, c = scenes.build_config("cfg5", device="cpu", seed=1, P=100_000)
+    W, H = cam.image_width, cam.image_height
+    st = run_gpu(cam, gs, mode="sh", sh_degree=c["sh_degree"])
+    ref = orc.preprocess(np32(gs["means3D"]), np32(gs["scales"]), np32(gs["rotations"]),
+                         np32(gs["opacities"]).reshape(-1), np32(gs["shs"]), None, None, np32(cam.world_view_transform),
+                         np32(cam.full_proj_transform), np32(cam.camera_center), W, H, cam.tanfovx, cam.tanfovy, 1.0,
+                         c["sh_degree"])
+    R, keys, vals, ranges = orc.binning(ref, W, H)
+    assert st["R"] == R and R > 1_000_000
+    np.testing.assert_array_equal(st["point_list"].astype(np.int64), vals.astype(np.int64))
+    np.testing.assert_array_equal(st["ranges"].astype(np.int64), ranges.astype(np.int64))
