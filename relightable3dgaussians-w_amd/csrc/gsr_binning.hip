@@ -104,8 +104,8 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
 constexpr int ST_G = 1024;  // Gaussians per block
-constexpr int ST_W = 8;     // waves per block in k_st_hist / k_st_scatter (ST_G / ST_W Gaussians each)
-constexpr int ST_T = 64 * ST_W;
+// waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
+// per-wave LDS state of 8 waves would not fit (st_waves)
 
 __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
@@ -113,11 +113,12 @@ __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
 }
 
-__global__ void __launch_bounds__(ST_T) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
+template <int ST_W>
+__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
                                                   int NS, int nb, uint32_t* table, uint32_t* wcounts,
                                                   uint2* rect_sorted) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
-    for (int i = threadIdx.x; i < ST_W * NS; i += ST_T) hist[i] = 0;
+    for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -133,8 +134,8 @@ __global__ void __launch_bounds__(ST_T) k_st_hist(int Pv, const uint32_t* sorted
     }
     __syncthreads();
     uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
-    for (int i = threadIdx.x; i < ST_W * NS; i += ST_T) wc[i] = hist[i];
-    for (int i = threadIdx.x; i < NS; i += ST_T) {
+    for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) wc[i] = hist[i];
+    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
         uint32_t t = 0;
 #pragma unroll
         for (int w = 0; w < ST_W; w++) t += hist[w * NS + i];
@@ -218,7 +219,8 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
     }
 }
 
-__global__ void __launch_bounds__(ST_T) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
+template <int ST_W>
+__global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
                                                      unsigned gsx, int NS, int nb, const uint32_t* table,
                                                      const uint32_t* wcounts, const uint32_t* bases,
                                                      uint32_t* st_keys, uint32_t* st_vals) {
@@ -232,7 +234,7 @@ __global__ void __launch_bounds__(ST_T) k_st_scatter(int Pv, const uint32_t* sor
     // each wave's run of super-tile s starts after the block's earlier waves (k_st_hist's
     // per-wave counts)
     const uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
-    for (int i = threadIdx.x; i < NS; i += ST_T) {
+    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
         uint32_t run = bases[i] + table[(size_t)i * nb + blk];
         for (int w = 0; w < ST_W; w++) {
             wmask_all[w * NS + i] = 0ull;
@@ -245,13 +247,15 @@ __global__ void __launch_bounds__(ST_T) k_st_scatter(int Pv, const uint32_t* sor
                   st_vals);
 }
 
+static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
+
 size_t st_bin_temp_bytes(long long Pv, int NS) {
     const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
-    return (4 + 4 * ST_W) * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 5 * 256 + 1024;
+    return (4 + 4 * (size_t)st_waves(NS)) * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 5 * 256 + 1024;
 }
 
-// per-wave LDS masks + counters: 12 B x ST_W x NS within a 64 KiB workgroup allocation
-bool st_bin_supported(int NS) { return 12 * ST_W * NS <= 65536; }
+// per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
+bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
 void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
                    uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
@@ -260,6 +264,7 @@ void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsign
         return;
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
+    const int W = st_waves(NS);
     char* t = reinterpret_cast<char*>(temp);
     auto take = [&](size_t bytes) {
         char* p = t;
@@ -270,13 +275,21 @@ void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsign
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint2* rect_sorted = reinterpret_cast<uint2*>(take(8 * (size_t)Pv));
-    uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * ST_W * (size_t)NS * nb));
-    hipLaunchKernelGGL(k_st_hist, dim3(nb), dim3(ST_T), 4 * ST_W * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
-                       wcounts, rect_sorted);
+    uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
+    if (W == 8)
+        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
+                           wcounts, rect_sorted);
+    else
+        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
+                           wcounts, rect_sorted);
     launch_digit_scan(NS, table, nb, tot, s);
     hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
-    hipLaunchKernelGGL(k_st_scatter, dim3(nb), dim3(ST_T), 12 * ST_W * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS, nb,
-                       table, wcounts, bases, st_keys, st_vals);
+    if (W == 8)
+        hipLaunchKernelGGL(k_st_scatter<8>, dim3(nb), dim3(512), 12 * 8 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS,
+                           nb, table, wcounts, bases, st_keys, st_vals);
+    else
+        hipLaunchKernelGGL(k_st_scatter<4>, dim3(nb), dim3(256), 12 * 4 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS,
+                           nb, table, wcounts, bases, st_keys, st_vals);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)

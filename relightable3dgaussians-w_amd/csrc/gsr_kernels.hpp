@@ -79,7 +79,7 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
 // Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
-// order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1024.
+// order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1365.
 size_t st_bin_temp_bytes(long long Pv, int NS);
 bool st_bin_supported(int NS);
 void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,

@@ -182,20 +182,21 @@ def test_forward_is_deterministic(cfg2):
     np.testing.assert_array_equal(st["n_contrib"], st2["n_contrib"])
 
 
-def test_4k_frame_binning_exact():
-    """3840x2160 (cfg5's frame): 30 x 34 = 1020 super-tiles exceed the fused
-    super-tile binning's LDS budget, so this runs the emit + offsets scan + one-pass sort
-    path.  Its point_list and tile ranges must equal the oracle's (tile, depth, index)
-    order bit for bit."""
+@pytest.mark.parametrize("W,H,P", [(3840, 2160, 100_000), (5120, 2880, 60_000)])
+def test_large_frame_binning_exact(W, H, P):
+    """cfg5's 3840x2160 frame: 30 x 34 = 1020 super-tiles run the fused
+    super-tile binning with four waves per workgroup (eight would exceed its LDS budget);
+    5120x2880 (1800 super-tiles) exceeds that too and runs the emit + offsets scan +
+    one-pass sort path.  Both must reproduce the oracle's (tile, depth, index) lists and
+    tile ranges bit for bit."""
     from gsr import scenes
-    cam, gs, c = scenes.build_config("cfg5", device="cpu", seed=1, P=100_000)
-    W, H = cam.image_width, cam.image_height
+    cam, gs, c = scenes.build_config("cfg5", device="cpu", seed=1, P=P, W=W, H=H)
     st = run_gpu(cam, gs, mode="sh", sh_degree=c["sh_degree"])
     ref = orc.preprocess(np32(gs["means3D"]), np32(gs["scales"]), np32(gs["rotations"]),
                          np32(gs["opacities"]).reshape(-1), np32(gs["shs"]), None, None, np32(cam.world_view_transform),
                          np32(cam.full_proj_transform), np32(cam.camera_center), W, H, cam.tanfovx, cam.tanfovy, 1.0,
                          c["sh_degree"])
     R, keys, vals, ranges = orc.binning(ref, W, H)
-    assert st["R"] == R and R > 1_000_000
+    assert st["R"] == R and R > 500_000
     np.testing.assert_array_equal(st["point_list"].astype(np.int64), vals.astype(np.int64))
     np.testing.assert_array_equal(st["ranges"].astype(np.int64), ranges.astype(np.int64))
