@@ -192,6 +192,38 @@ def bench_relight(args, dev):
                          "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
 
 
+def refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_ours):
+    """The reference rasterizer's stage structure in plain HIP on the same GPU and inputs
+    (baseline/refalgo.hip: 64-bit duplicate keys + hipcub radix sort, one thread per pixel,
+    9 global atomics per (pixel, Gaussian) in the backward).  Timed after, not inside, the
+    timed region; `speedup` = its step time / libgsr's."""
+    from baseline.refalgo import RefAlgoRasterizer
+    ras = RefAlgoRasterizer()
+
+    def step():
+        R, color, radii = ras.forward(bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm,
+                                      pm, cam.tanfovx, cam.tanfovy, H, W, g["shs"], deg, cp)
+        ras.backward(bg, g["means3D"], radii, g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy,
+                     dout, g["shs"], deg, cp)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize()
+    n = max(1, min(args.steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / n
+    return {"value": round(W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "ms_per_step": round(ms, 4),
+            "steps": n, "speedup": round(ms / ms_ours, 3),
+            "what": "reference stage structure in plain HIP on this MI355X (baseline/refalgo.hip): per-Gaussian "
+                    "preprocess, hipcub inclusive scan + D2H num_rendered, duplicateWithKeys (64-bit tile|depth "
+                    "keys), hipcub radix sort on 32+msb(T) bits, tile ranges, 16x16-thread per-pixel render with "
+                    "256-Gaussian shared-memory rounds, per-pixel backward with 9 global atomics per pair; shares "
+                    "libgsr's per-Gaussian preprocess kernels (so it is an upper bound on the reference's speed)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -209,6 +241,7 @@ def main():
                                                   "default resolution rule")
     ap.add_argument("--view", type=int, default=0)
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
+    ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -323,6 +356,8 @@ def main():
         "roofline": roofline,
         "stage_ms": per_stage,
     }
+    if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
+        out["gpu_reference_algorithm"] = refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(cam, gs_cpu, M, deg, dout_cpu.numpy(), ntiles=args.cpu_tiles)
         out["cpu_baseline"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cb.items()

@@ -51,3 +51,11 @@ def test_cpu_tensors_are_rejected():
     assert dgr.GaussianRasterizationSettings._fields == (
         "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix", "projmatrix",
         "sh_degree", "campos", "prefiltered")
+
+
+def test_refalgo_baseline_loads_and_exports():
+    """The reference-structure GPU baseline bench.py times (baseline/) is built and loadable."""
+    from baseline import refalgo
+    L = refalgo.lib()
+    for s in refalgo.SYMBOLS:
+        assert hasattr(L, s), s
