@@ -192,6 +192,69 @@ def bench_relight(args, dev):
                          "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
 
 
+def bench_train(args, dev, dist, rank, world):
+    """cfg4: the data-parallel relightable training iteration.  Every rank
+    holds the whole scene (1.5M Gaussians: 1.36M foreground + 10 % sky, cfg2 distribution,
+    1920x1080) and renders its own 4 views per iteration through the fused render(), with
+    the reference's reconstruction (L1 + D-SSIM), sky-BRDF and normal losses and backward;
+    then one RCCL all-reduce of the flat gradient buffer, the densification statistics'
+    SUM/MAX, and one fused Adam launch (gsr/train.py).  value = iterations/s (whole job;
+    weak scaling: 4 views per rank per iteration)."""
+    from gsr import train
+    vpr = 4
+    P_fg = args.P or 1_363_637
+    W, H, focal = 1920, 1080, 1400.0
+    scene, views, gts = train.synthetic_relit_scene(P_fg, vpr * world, W, H, focal, dev, seed=0)
+    mine = list(range(rank * vpr, (rank + 1) * vpr))
+    my_views, my_gts = [views[i] for i in mine], [gts[i] for i in mine]
+    group = None
+
+    def step():
+        return train.train_step(scene, my_views, mine, my_gts, group=group, world=world)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    ar_ms = None
+    if dist is not None:
+        t = torch.tensor([ms], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+        # the exchange step alone: the flat-gradient all-reduce
+        for _ in range(3):
+            dist.all_reduce(scene.fp.grad)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(10):
+            dist.all_reduce(scene.fp.grad)
+        torch.cuda.synchronize()
+        ar_ms = (time.perf_counter() - t1) * 1e3 / 10
+    if rank == 0:
+        print(json.dumps({
+            "metric": "train iters/s (relit render + losses + backward + grad all-reduce + Adam, 4 views per GPU)",
+            "value": round(1e3 / ms, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"cfg4: {scene.P} Gaussians ({P_fg} fg + {scene.P - P_fg} sky), {W}x{H}, "
+                                   f"{vpr} views per GPU per iteration, env SH deg 4, sky SH deg 1",
+                       "gaussians": scene.P, "width": W, "height": H, "views_per_iter": vpr * world,
+                       "parallelism": f"views x{world}", "flat_params": scene.fp.n},
+            "views_per_s": round(vpr * world * 1e3 / ms, 3),
+            "grad_all_reduce_ms": None if ar_ms is None else round(ar_ms, 4),
+            "grad_bucket_mb": round(scene.fp.n * 4 / 1e6, 2),
+            "final_loss_rank0": round(float(loss) / vpr, 6)}), flush=True)
+
+
 def refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_ours):
     """The reference rasterizer's stage structure in plain HIP on the same GPU and inputs
     (baseline/refalgo.hip: 64-bit duplicate keys + hipcub radix sort, one thread per pixel,
@@ -256,6 +319,11 @@ def main():
     torch.cuda.set_device(dev)
     if args.config == "cfg3":
         bench_relight(args, dev)
+        return
+    if args.config == "cfg4":
+        bench_train(args, dev, dist, rank, world)
+        if dist is not None:
+            dist.destroy_process_group()
         return
 
     from diff_gaussian_rasterization import _C

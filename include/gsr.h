@@ -21,6 +21,9 @@
  *                      render()'s per-Gaussian colour preparation (normals, shade, sky
  *                      colour, depth; gaussian_renderer/__init__.py:120-200) fused into
  *                      the composite's feature rows
+ *   gsr_adam_step      torch.optim.Adam.step over the per-Gaussian param groups
+ *                      (train.py:191, relit3DGW_model.py:149) as one fused launch over a
+ *                      flat parameter buffer (the data-parallel training step)
  *   gsr_relit_epilogue / gsr_relit_epilogue_backward
  *                      render()'s image-space tail: normal remap + sky mask and normal_ref
  *                      from the depth image (gaussian_renderer/__init__.py:226-276,
@@ -164,6 +167,16 @@ int gsr_relit_epilogue(int width, int height, const float* cam12, const float* n
 int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const float* depth, const float* alpha,
                                 const float* sky_mask, int normal_view, const float* g_normal,
                                 const float* g_normal_ref, float* d_n01, float* d_depth, void* stream);
+
+/* One Adam step (torch.optim.Adam semantics, relit3DGW_model.py:149 / gaussian_model.py:264-274)
+ * over a flat fp32 parameter buffer whose param groups are consecutive segments:
+ * segment k = [seg_end[k-1], seg_end[k]) with learning rate seg_lr[k] (host arrays, nseg <= 16,
+ * seg_end[nseg-1] == n).  grad is scaled by grad_scale first (1/views after a SUM all-reduce).
+ * step is the 1-based step count after this update.  param, grad, exp_avg, exp_avg_sq: n floats
+ * on the device, 16-B aligned. */
+int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double* seg_lr, double beta1, double beta2,
+                  double eps, int step, float grad_scale, float* param, const float* grad, float* exp_avg,
+                  float* exp_avg_sq, void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

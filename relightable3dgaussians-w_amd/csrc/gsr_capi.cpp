@@ -847,4 +847,40 @@ int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const
     return GSR_OK;
 }
 
+int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double* seg_lr, double beta1, double beta2,
+                  double eps, int step, float grad_scale, float* param, const float* grad, float* exp_avg,
+                  float* exp_avg_sq, void* stream_) {
+    if (n < 0 || nseg < 1 || nseg > gsr::ADAM_MAX_SEGS || step < 1)
+        return fail(GSR_E_ARG, "gsr_adam_step: bad sizes n=%lld nseg=%d step=%d", n, nseg, step);
+    if (n == 0) return GSR_OK;
+    if (!seg_end || !seg_lr || !param || !grad || !exp_avg || !exp_avg_sq)
+        return fail(GSR_E_ARG, "gsr_adam_step: missing buffers");
+    for (const void* q : {(const void*)param, (const void*)grad, (const void*)exp_avg, (const void*)exp_avg_sq})
+        if (reinterpret_cast<uintptr_t>(q) & 15u) return fail(GSR_E_ARG, "gsr_adam_step: buffers must be 16-B aligned");
+    if (seg_end[nseg - 1] != n) return fail(GSR_E_ARG, "gsr_adam_step: last segment must end at n");
+    gsr::AdamSegs s;
+    memset(&s, 0, sizeof(s));
+    s.n = nseg;
+    // torch: bias_correction1 = 1 - beta1 ** step, step_size = lr / bias_correction1,
+    // bias_correction2_sqrt = (1 - beta2 ** step) ** 0.5 (Python floats, i.e. double)
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    long long prev = 0;
+    for (int k = 0; k < nseg; k++) {
+        if (seg_end[k] < prev) return fail(GSR_E_ARG, "gsr_adam_step: segment ends must ascend");
+        prev = s.end[k] = seg_end[k];
+        s.step_size[k] = (float)(seg_lr[k] / bc1);
+    }
+    s.bc2_sqrt = (float)sqrt(bc2);
+    // the scalars as torch passes them (Python floats, cast to the fp32 op math)
+    s.one_minus_b1 = (float)(1.0 - beta1);
+    s.b2 = (float)beta2;
+    s.one_minus_b2 = (float)(1.0 - beta2);
+    s.eps = (float)eps;
+    s.grad_scale = grad_scale;
+    gsr::launch_adam(n, s, param, grad, exp_avg, exp_avg_sq, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

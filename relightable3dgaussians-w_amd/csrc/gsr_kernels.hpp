@@ -169,6 +169,16 @@ struct RenderMcArgs {
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);
 
+// ---- fused Adam over a flat parameter buffer (gsr_adam.hip) ---------------------------
+constexpr int ADAM_MAX_SEGS = 16;
+struct AdamSegs {
+    int n;                               // segments (param groups), <= ADAM_MAX_SEGS
+    long long end[ADAM_MAX_SEGS];        // exclusive end element of each segment (ascending)
+    float step_size[ADAM_MAX_SEGS];      // lr / (1 - b1^t) per segment
+    float bc2_sqrt, one_minus_b1, b2, one_minus_b2, eps, grad_scale;
+};
+void launch_adam(long long n, const AdamSegs& s, float* p, const float* g, float* m, float* v, hipStream_t st);
+
 // render()'s image-space tail (gsr_epilogue.hip): cam12 = rows of K^-1^T R^T, then the centre
 void launch_epilogue_fwd(int W, int H, const float* cam12, const float* n01, const float* depth, const float* alpha,
                          const float* sky, int normal_view, float* normal, float* normal_ref, hipStream_t s);

@@ -50,7 +50,22 @@ def depth_to_normal(view, depth):
 
 def _epilogue_camera(view):
     """cam12 for gsr_relit_epilogue: rows of K^-1^T R^T (rays = x M0 + y M1 + M2) and the
-    camera centre, as depths_to_points builds them."""
+    camera centre, as depths_to_points builds them.  Cached on the view object (keyed on the
+    matrix object and its version), so a training loop pays its host round trip once."""
+    wvt = view.world_view_transform
+    key = (wvt._version, view.image_width, view.image_height, view.FoVx, view.FoVy)
+    hit = getattr(view, "_gsr_cam12", None)
+    if hit is not None and hit[0] is wvt and hit[1] == key:
+        return hit[2]
+    cam12 = _epilogue_camera_uncached(view)
+    try:
+        view._gsr_cam12 = (wvt, key, cam12)
+    except AttributeError:
+        pass
+    return cam12
+
+
+def _epilogue_camera_uncached(view):
     c2w = view.world_view_transform.T.inverse().double()
     W, H = view.image_width, view.image_height
     fx = W / (2 * math.tan(view.FoVx / 2.))

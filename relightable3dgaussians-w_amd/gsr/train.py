@@ -1,0 +1,272 @@
+"""The data-parallel relightable training step (BASELINE cfg 4).
+
+The reference trains on one view per iteration (train.py:56-194): environment SH from the
+view's embedding, render(), the reconstruction / sky-BRDF / normal losses, backward,
+densification statistics, one torch.optim.Adam step over nine param groups
+(gaussian_model.py:259-274, relit3DGW_model.py:149).  The MI355X design:
+
+  * every per-Gaussian attribute and the per-view lighting live in ONE flat fp32 buffer
+    (FlatParams); each attribute is a leaf view of it, and each leaf's ``.grad`` is set to
+    the matching view of ONE flat gradient buffer, so autograd accumulates in place and the
+    gradient bucket needs no pack/unpack copies;
+  * each rank renders its own views through the fused path (gsr.relit.render: relit
+    features + one multi-channel composite + the image-space tail), ``views_per_rank`` of
+    them per iteration, accumulating gradients;
+  * one RCCL all-reduce (SUM) of the flat gradient buffer, one SUM/MAX of the
+    densification statistics (gsr.dp) -- the path's only exchange steps;
+  * one fused Adam launch over the flat buffer (gsr_adam_step): the per-group learning rates
+    come from a segment table, and the all-reduced sum is turned into the mean over the
+    step's views by the kernel's grad scale.
+
+Out of scope (the caller's, unchanged): the embedding MLP (here a per-view environment/sky
+SH table stands in for its output), the envlight / min-scale / sky-depth regularisers,
+densify_and_prune's tensor surgery and sky Gaussians' radius/angle parameterisation (sky
+Gaussians share the xyz group here).
+"""
+from __future__ import annotations
+
+import math
+import types
+from typing import Dict, List, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+
+# (name, columns, lr) -- configs/optimizer/*.yaml defaults, gaussian_model.py:264-274
+# (xyz and scaling lrs carry the scene's spatial_lr_scale, applied by the caller)
+GAUSSIAN_GROUPS = (("xyz", 3, 0.00016), ("albedo", 3, 0.0025), ("opacity", 1, 0.05), ("scaling", 3, 0.001),
+                   ("rotation", 4, 0.001), ("roughness", 1, 0.0002), ("metalness", 1, 0.0002))
+LIGHT_LR = 0.0002  # mlp_lr: the per-view lighting table stands in for the embedding MLP's output
+
+
+class FlatParams:
+    """Named fp32 parameters packed back to back (16-B aligned segments) in one buffer.
+
+    ``params[name]`` is a leaf view of ``flat`` with ``.grad`` preset to the matching view
+    of ``grad``; ``step()`` is one fused Adam launch (torch.optim.Adam semantics, eps as the
+    reference's 1e-15)."""
+
+    def __init__(self, spec: Sequence[Tuple[str, Tuple[int, ...], float]], device, betas=(0.9, 0.999), eps=1e-15):
+        self.names, self.shapes, self.lrs, self.offsets, ends = [], [], [], [], []
+        o = 0
+        for name, shape, lr in spec:
+            n = int(math.prod(shape))
+            self.names.append(name)
+            self.shapes.append(tuple(shape))
+            self.lrs.append(float(lr))
+            self.offsets.append(o)
+            o += (n + 3) // 4 * 4  # padding belongs to this segment (zero grads: no update)
+            ends.append(o)
+        self.n = o
+        self.ends = ends
+        self.device = torch.device(device)
+        self.flat = torch.zeros(self.n, device=self.device)
+        self.grad = torch.zeros(self.n, device=self.device)
+        self.exp_avg = torch.zeros(self.n, device=self.device)
+        self.exp_avg_sq = torch.zeros(self.n, device=self.device)
+        self.betas, self.eps, self.t = betas, eps, 0
+        self.params: Dict[str, torch.Tensor] = {}
+        for name, shape, off in zip(self.names, self.shapes, self.offsets):
+            n = int(math.prod(shape))
+            p = self.flat[off:off + n].view(shape)
+            p.requires_grad_(True)
+            p.grad = self.grad[off:off + n].view(shape)
+            self.params[name] = p
+
+    def load(self, name: str, value: torch.Tensor) -> None:
+        with torch.no_grad():
+            self.params[name].copy_(value.reshape(self.params[name].shape))
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    def check_grads_in_place(self) -> None:
+        """Autograd accumulated into the preset views (not into fresh tensors)."""
+        for name, off in zip(self.names, self.offsets):
+            g = self.params[name].grad
+            if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * off:
+                raise RuntimeError(f"gradient of {name} left the flat buffer")
+
+    def set_lr(self, name: str, lr: float) -> None:
+        self.lrs[self.names.index(name)] = float(lr)
+
+    def step(self, grad_scale: float = 1.0) -> None:
+        import ctypes as C
+        if self.device.type != "cuda":
+            raise RuntimeError("FlatParams.step runs the HIP Adam kernel; parameters must be on the GPU")
+        self.t += 1
+        nseg = len(self.names)
+        ends = (C.c_longlong * nseg)(*self.ends)
+        lrs = (C.c_double * nseg)(*self.lrs)
+        _lib.check(_lib.lib().gsr_adam_step(self.n, nseg, ends, lrs, self.betas[0], self.betas[1], self.eps, self.t,
+                                            float(grad_scale), self.flat.data_ptr(), self.grad.data_ptr(),
+                                            self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                            _lib.stream_of(self.device)), "gsr_adam_step")
+
+
+# ---- losses (utils/loss_utils.py; the caller's code, restated for the step) ---------------
+
+def l1_loss(out, gt, mask=None):
+    """utils/loss_utils.py:27-35 (masked: sum |out*m - gt*m| / #(m == 1))."""
+    if mask is None:
+        return (out - gt).abs().mean()
+    return (out * mask - gt * mask).abs().sum() / (mask == 1).sum()
+
+
+_WINDOWS: Dict[Tuple, torch.Tensor] = {}
+
+
+def _window(size, channel, device):
+    key = (size, channel, str(device))
+    if key not in _WINDOWS:
+        g = torch.tensor([math.exp(-(x - size // 2) ** 2 / (2 * 1.5 ** 2)) for x in range(size)])
+        g = (g / g.sum()).unsqueeze(1)
+        _WINDOWS[key] = (g @ g.t()).float().expand(channel, 1, size, size).contiguous().to(device)
+    return _WINDOWS[key]
+
+
+def ssim(img1, img2, mask=None, window_size=11):
+    """utils/loss_utils.py:53-96 (masked mean of the SSIM map)."""
+    c = img1.shape[-3]
+    w = _window(window_size, c, img1.device)
+    a, b = img1[None], img2[None]
+    pad = window_size // 2
+    mu1 = F.conv2d(a, w, padding=pad, groups=c)
+    mu2 = F.conv2d(b, w, padding=pad, groups=c)
+    mu1_sq, mu2_sq, mu12 = mu1 * mu1, mu2 * mu2, mu1 * mu2
+    s1 = F.conv2d(a * a, w, padding=pad, groups=c) - mu1_sq
+    s2 = F.conv2d(b * b, w, padding=pad, groups=c) - mu2_sq
+    s12 = F.conv2d(a * b, w, padding=pad, groups=c) - mu12
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    m = ((2 * mu12 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
+    if mask is None:
+        return m.mean()
+    return (m * mask[None]).sum() / (mask == 1).sum()
+
+
+def view_loss(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):
+    """train.py:77-99: reconstruction (L1 + D-SSIM), sky-BRDF and normal-consistency terms."""
+    img = out["render"]
+    rec = l1_loss(img, gt, occ_mask) * (1 - lambda_dssim) + lambda_dssim * (1.0 - ssim(img, gt, occ_mask))
+    nsky = 1 - sky_mask
+    loss = rec + lambda_sky_brdf * (l1_loss(out["diffuse_color"], torch.zeros_like(img), nsky) +
+                                    l1_loss(out["specular_color"], torch.zeros_like(img), nsky))
+    n = out["normal"] * occ_mask * sky_mask
+    nr = out["normal_ref"] * occ_mask * sky_mask
+    loss = loss + lambda_normal * (1 - (n * nr).sum(dim=0))[None].mean()
+    return loss
+
+
+# ---- the model view render() reads and the step ------------------------------------------
+
+class RelitScene:
+    """A relightable scene on one rank: FlatParams with the Gaussian groups plus a per-view
+    environment SH (deg 4, [V,25,3]) and sky SH (deg 1, [V,4,3]) table, and the constant
+    sky flags.  ``model()`` gives the activated attributes as render() reads them
+    (gaussian_model.py:74-180: exp scaling, normalised rotation, sigmoid opacity and
+    materials)."""
+
+    def __init__(self, xyz, scaling_raw, rotation_raw, opacity_raw, albedo_raw, rough_raw, metal_raw, is_sky,
+                 n_views, device, spatial_lr_scale=1.0, seed=0):
+        P, N_fg = xyz.shape[0], albedo_raw.shape[0]
+        spec = []
+        for name, cols, lr in GAUSSIAN_GROUPS:
+            rows = N_fg if name in ("albedo", "roughness", "metalness") else P
+            if name in ("xyz", "scaling"):
+                lr *= spatial_lr_scale
+            spec.append((name, (rows, cols), lr))
+        spec += [("env_sh", (n_views, 25, 3), LIGHT_LR), ("sky_sh", (n_views, 4, 3), LIGHT_LR)]
+        self.fp = FlatParams(spec, device)
+        for name, v in (("xyz", xyz), ("scaling", scaling_raw), ("rotation", rotation_raw), ("opacity", opacity_raw),
+                        ("albedo", albedo_raw), ("roughness", rough_raw), ("metalness", metal_raw)):
+            self.fp.load(name, v)
+        g = torch.Generator().manual_seed(seed)
+        env = torch.randn(n_views, 25, 3, generator=g) * 0.3
+        env[:, 0] = 1.0
+        self.fp.load("env_sh", env)
+        self.fp.load("sky_sh", torch.randn(n_views, 4, 3, generator=g) * 0.3)
+        self.is_sky = is_sky.to(device).reshape(-1, 1).bool()
+        self.P = P
+        self.stats = {"xyz_gradient_accum": torch.zeros(P, 1, device=device),
+                      "denom": torch.zeros(P, 1, device=device),
+                      "max_radii2D": torch.zeros(P, device=device)}
+
+    def model(self):
+        p = self.fp.params
+        return types.SimpleNamespace(get_xyz=p["xyz"], get_scaling=torch.exp(p["scaling"]),
+                                     get_rotation=F.normalize(p["rotation"]), get_opacity=torch.sigmoid(p["opacity"]),
+                                     get_albedo=torch.sigmoid(p["albedo"]), get_roughness=torch.sigmoid(p["roughness"]),
+                                     get_metalness=torch.sigmoid(p["metalness"]), get_is_sky=self.is_sky)
+
+
+def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
+               world: int = 1, bg=None) -> torch.Tensor:
+    """One data-parallel iteration: this rank's views rendered and back-propagated, one
+    all-reduce of the flat gradient, the densification statistics reduced, one fused Adam
+    step with the mean gradient over all ranks' views.  Returns this rank's summed loss as a
+    device scalar (no host synchronisation inside the step)."""
+    import relit_shade
+
+    from . import relit
+    from . import dp as gdp
+    fp = scene.fp
+    fp.zero_grad()
+    dev = fp.device
+    bg = torch.zeros(3, device=dev) if bg is None else bg
+    pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    total = torch.zeros((), device=dev)
+    for view, vid, gt in zip(views, view_ids, gts):
+        pc = scene.model()
+        light = relit_shade.EnvironmentLight(fp.params["env_sh"][vid], sh_degree=4)
+        out = relit.render(view, pc, light, fp.params["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
+        sky = view.sky_mask.expand_as(gt)
+        loss = view_loss(out, gt, sky, view.occluders_mask.expand_as(gt))
+        loss.backward()
+        total = total + loss.detach()
+        gdp.accumulate_view_stats(scene.stats, out["viewspace_points"].grad, out["radii"])
+    fp.check_grads_in_place()
+    n_views = len(views)
+    if world > 1:
+        import torch.distributed as dist
+        dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=group)
+        gdp.reduce_densification_stats(scene.stats["xyz_gradient_accum"], scene.stats["denom"],
+                                       scene.stats["max_radii2D"], group=group)
+        n_views *= world
+    fp.step(grad_scale=1.0 / n_views)
+    return total
+
+
+def synthetic_relit_scene(P_fg, n_views, W, H, focal, device, seed=0, sky_frac=0.1):
+    """A cfg2-distributed relightable scene (z ~ logU(1, 30), screen radius
+    ~10-20 px) with ``P_fg`` foreground + ``sky_frac * P_fg`` sky Gaussians, materials
+    ~ U(0, 1), and ``n_views`` cameras jittered around the origin looking down +z (each with
+    a sky mask over the top fifth of the frame, no occluders, and a fixed random target
+    image).  Returns (RelitScene, views, gts)."""
+    from . import scenes
+    P = P_fg + int(P_fg * sky_frac)
+    cam0 = scenes.focal_camera(W, H, focal)
+    gs = scenes.synthetic_gaussians(P, W, H, cam0.tanfovx, cam0.tanfovy, 0, seed=seed, zrange=(1.0, 30.0),
+                                    log_z=True, scale_mode="cfg2")
+    g = torch.Generator().manual_seed(seed + 1)
+    is_sky = torch.zeros(P, dtype=torch.bool)
+    is_sky[P_fg:] = True
+    logit = lambda x: torch.log(x / (1 - x))
+    scene = RelitScene(gs["means3D"], torch.log(gs["scales"]), gs["rotations"], logit(gs["opacities"]),
+                       logit(torch.rand(P_fg, 3, generator=g) * 0.9 + 0.05),
+                       logit(torch.rand(P_fg, 1, generator=g) * 0.9 + 0.05),
+                       logit(torch.rand(P_fg, 1, generator=g) * 0.9 + 0.05), is_sky, n_views, device, seed=seed)
+    views, gts = [], []
+    for v in range(n_views):
+        pos = (torch.rand(3, generator=g) - 0.5).numpy() * 0.4
+        R, T = scenes.look_at_rotation(pos, [0.0, 0.0, 10.0])
+        cam = scenes.focal_camera(W, H, focal, R=R, T=T, device=device)
+        sky = torch.ones(1, H, W, device=device)
+        sky[:, : H // 5] = 0.0
+        views.append(types.SimpleNamespace(
+            image_width=W, image_height=H, FoVx=cam.FoVx, FoVy=cam.FoVy,
+            world_view_transform=cam.world_view_transform, full_proj_transform=cam.full_proj_transform,
+            camera_center=cam.camera_center, sky_mask=sky, occluders_mask=torch.ones(1, H, W, device=device)))
+        gts.append(torch.rand(3, H, W, generator=g).to(device))
+    return scene, views, gts
