@@ -24,6 +24,9 @@
  *   gsr_adam_step      torch.optim.Adam.step over the per-Gaussian param groups
  *                      (train.py:191, relit3DGW_model.py:149) as one fused launch over a
  *                      flat parameter buffer (the data-parallel training step)
+ *   gsr_ssim_forward / gsr_ssim_backward
+ *                      the training loss's SSIM (utils/loss_utils.py:53-96, train.py:78)
+ *                      as one fused stencil kernel each way
  *   gsr_relit_epilogue / gsr_relit_epilogue_backward
  *                      render()'s image-space tail: normal remap + sky mask and normal_ref
  *                      from the depth image (gaussian_renderer/__init__.py:226-276,
@@ -177,6 +180,19 @@ int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const
 int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double* seg_lr, double beta1, double beta2,
                   double eps, int step, float grad_scale, float* param, const float* grad, float* exp_avg,
                   float* exp_avg_sq, void* stream);
+
+/* SSIM of the training loss (utils/loss_utils.py:53-96: 11x11 Gaussian window, sigma 1.5,
+ * zero padding, C1 = 0.01^2, C2 = 0.03^2) over img1, img2 [C,H,W].  window: the 11 normalised
+ * 1-D weights (host).  mask: null or [C,H,W] / [1,H,W] (mask_cstride = H*W or 0).
+ * block_sums: gsr_ssim_partials(C,H,W) floats, each a fixed-order partial of sum(map * mask)
+ * (the caller adds them).  dmaps: null (no backward) or 3*C*H*W floats kept for the backward.
+ * The backward writes dL/dimg1 = gscale[0] * (window^T applied to dmaps) (img2 gets none:
+ * it is the ground truth); gscale is a device scalar, dL/dloss / #mask. */
+long long gsr_ssim_partials(int C, int height, int width);
+int gsr_ssim_forward(int C, int height, int width, const float* img1, const float* img2, const float* mask,
+                     long long mask_cstride, const float* window, float* block_sums, float* dmaps, void* stream);
+int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
+                      const float* gscale, const float* window, float* dimg1, void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

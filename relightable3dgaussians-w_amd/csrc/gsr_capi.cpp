@@ -883,4 +883,38 @@ int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double*
     return GSR_OK;
 }
 
+long long gsr_ssim_partials(int C, int height, int width) {
+    if (C <= 0 || height <= 0 || width <= 0) return 0;
+    const dim3 g = gsr::ssim_grid(C, height, width);
+    return (long long)g.x * g.y * g.z;
+}
+
+static bool ssim_window(const float* window, gsr::SsimWindow& w) {
+    if (!window) return false;
+    for (int k = 0; k < 11; k++) w.w[k] = window[k];
+    return true;
+}
+
+int gsr_ssim_forward(int C, int height, int width, const float* img1, const float* img2, const float* mask,
+                     long long mask_cstride, const float* window, float* block_sums, float* dmaps, void* stream_) {
+    if (C <= 0 || C > 65535 || height <= 0 || width <= 0) return fail(GSR_E_ARG, "gsr_ssim_forward: bad sizes");
+    gsr::SsimWindow w;
+    if (!img1 || !img2 || !block_sums || !ssim_window(window, w)) return fail(GSR_E_ARG, "gsr_ssim_forward: missing buffers");
+    gsr::launch_ssim_fwd(C, height, width, img1, img2, mask, mask_cstride, w, 0.01f * 0.01f, 0.03f * 0.03f, block_sums,
+                         dmaps, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
+                      const float* gscale, const float* window, float* dimg1, void* stream_) {
+    if (C <= 0 || C > 65535 || height <= 0 || width <= 0) return fail(GSR_E_ARG, "gsr_ssim_backward: bad sizes");
+    gsr::SsimWindow w;
+    if (!img1 || !img2 || !dmaps || !gscale || !dimg1 || !ssim_window(window, w))
+        return fail(GSR_E_ARG, "gsr_ssim_backward: missing buffers");
+    gsr::launch_ssim_bwd(C, height, width, img1, img2, dmaps, gscale, w, dimg1, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

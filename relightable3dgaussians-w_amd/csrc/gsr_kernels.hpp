@@ -179,6 +179,17 @@ struct AdamSegs {
 };
 void launch_adam(long long n, const AdamSegs& s, float* p, const float* g, float* m, float* v, hipStream_t st);
 
+// ---- fused SSIM loss (gsr_ssim.hip) ---------------------------------------------------
+struct SsimWindow {
+    float w[11];  // normalised 1-D Gaussian (window 11, sigma 1.5)
+};
+dim3 ssim_grid(int C, int H, int W);
+void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, const float* mask,
+                     long long mask_cstride, const SsimWindow& win, float C1, float C2, float* block_sums,
+                     float* dmaps, hipStream_t s);
+void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
+                     const float* gscale, const SsimWindow& win, float* dimg1, hipStream_t s);
+
 // render()'s image-space tail (gsr_epilogue.hip): cam12 = rows of K^-1^T R^T, then the centre
 void launch_epilogue_fwd(int W, int H, const float* cam12, const float* n01, const float* depth, const float* alpha,
                          const float* sky, int normal_view, float* normal, float* normal_ref, hipStream_t s);

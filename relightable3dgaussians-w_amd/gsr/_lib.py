@@ -58,6 +58,10 @@ def _declare(lib):
                                        vp, vp, vp]
     lib.gsr_adam_step.argtypes = [C.c_longlong, i, C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.c_double, C.c_double,
                                   C.c_double, i, f, vp, vp, vp, vp, vp]
+    lib.gsr_ssim_partials.argtypes = [i, i, i]
+    lib.gsr_ssim_partials.restype = C.c_longlong
+    lib.gsr_ssim_forward.argtypes = [i, i, i, vp, vp, vp, C.c_longlong, C.POINTER(C.c_float), vp, vp, vp]
+    lib.gsr_ssim_backward.argtypes = [i, i, i, vp, vp, vp, vp, C.POINTER(C.c_float), vp, vp]
     lib.gsr_shade_workspace_bytes.argtypes = [i, i]
     lib.gsr_shade_workspace_bytes.restype = sz
     lib.gsr_get_layout.argtypes = [i, C.c_longlong, i, i, C.POINTER(Layout)]
@@ -71,7 +75,7 @@ def _declare(lib):
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
-               "gsr_relit_epilogue_backward", "gsr_adam_step",
+               "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 

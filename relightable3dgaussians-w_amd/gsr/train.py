@@ -118,32 +118,87 @@ def l1_loss(out, gt, mask=None):
 _WINDOWS: Dict[Tuple, torch.Tensor] = {}
 
 
+def gaussian_1d(size=11, sigma=1.5):
+    """utils/loss_utils.py:45-47: the fp32 window weights exp(-(x - 5)^2 / 4.5), normalised in fp32."""
+    g = torch.tensor([math.exp(-(x - size // 2) ** 2 / float(2 * sigma ** 2)) for x in range(size)],
+                     dtype=torch.float32)
+    return g / g.sum()
+
+
 def _window(size, channel, device):
+    """utils/loss_utils.py:50-54: the 2-D depthwise window (outer product of gaussian_1d)."""
     key = (size, channel, str(device))
     if key not in _WINDOWS:
-        g = torch.tensor([math.exp(-(x - size // 2) ** 2 / (2 * 1.5 ** 2)) for x in range(size)])
-        g = (g / g.sum()).unsqueeze(1)
+        g = gaussian_1d(size).unsqueeze(1)
         _WINDOWS[key] = (g @ g.t()).float().expand(channel, 1, size, size).contiguous().to(device)
     return _WINDOWS[key]
 
 
+_WIN11 = None
+
+
+class _FusedSSIM(torch.autograd.Function):
+    """sum(ssim_map * mask) over the image (gsr_ssim_forward / gsr_ssim_backward); the
+    gradient goes to img1 only (img2 is the ground truth)."""
+
+    @staticmethod
+    def forward(ctx, img1, img2, mask):
+        import ctypes as C
+        global _WIN11
+        if _WIN11 is None:
+            _WIN11 = (C.c_float * 11)(*gaussian_1d(11).tolist())
+        Cn, H, W = img1.shape
+        img1, img2 = img1.contiguous(), img2.contiguous()
+        cstride = 0
+        if mask is not None:
+            mask = mask.float().contiguous()
+            if mask.shape[0] == Cn and Cn > 1:
+                cstride = H * W
+        L = _lib.lib()
+        parts = torch.empty(L.gsr_ssim_partials(Cn, H, W), device=img1.device)
+        dmaps = torch.empty((3, Cn, H, W), device=img1.device) if ctx.needs_input_grad[0] else None
+        _lib.check(L.gsr_ssim_forward(Cn, H, W, img1.data_ptr(), img2.data_ptr(),
+                                      None if mask is None else mask.data_ptr(), cstride, _WIN11, parts.data_ptr(),
+                                      None if dmaps is None else dmaps.data_ptr(), _lib.stream_of(img1.device)),
+                   "gsr_ssim_forward")
+        ctx.save_for_backward(img1, img2, dmaps)
+        return parts.sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        img1, img2, dmaps = ctx.saved_tensors
+        Cn, H, W = img1.shape
+        gs = g.reshape(1).float().contiguous()
+        d = torch.empty_like(img1)
+        _lib.check(_lib.lib().gsr_ssim_backward(Cn, H, W, img1.data_ptr(), img2.data_ptr(), dmaps.data_ptr(),
+                                                gs.data_ptr(), _WIN11, d.data_ptr(), _lib.stream_of(img1.device)),
+                   "gsr_ssim_backward")
+        return d, None, None
+
+
 def ssim(img1, img2, mask=None, window_size=11):
-    """utils/loss_utils.py:53-96 (masked mean of the SSIM map)."""
-    c = img1.shape[-3]
-    w = _window(window_size, c, img1.device)
-    a, b = img1[None], img2[None]
-    pad = window_size // 2
-    mu1 = F.conv2d(a, w, padding=pad, groups=c)
-    mu2 = F.conv2d(b, w, padding=pad, groups=c)
-    mu1_sq, mu2_sq, mu12 = mu1 * mu1, mu2 * mu2, mu1 * mu2
-    s1 = F.conv2d(a * a, w, padding=pad, groups=c) - mu1_sq
-    s2 = F.conv2d(b * b, w, padding=pad, groups=c) - mu2_sq
-    s12 = F.conv2d(a * b, w, padding=pad, groups=c) - mu12
-    C1, C2 = 0.01 ** 2, 0.03 ** 2
-    m = ((2 * mu12 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
+    """utils/loss_utils.py:53-96 (window 11, size_average): the masked mean of the SSIM map,
+    on the fused HIP kernels.  Shapes [C,H,W] (a leading batch of 1 is squeezed, as the
+    reference does); mask [C,H,W] or [1,H,W].  No host synchronisation: an empty mask gives
+    1, as the reference's early return."""
+    if window_size != 11:
+        raise NotImplementedError("the fused SSIM implements the reference's 11x11 window")
+    img1, img2 = img1.squeeze(0) if img1.dim() == 4 else img1, img2.squeeze(0) if img2.dim() == 4 else img2
+    _lib.require_gpu_tensor(img1, "img1")
+    _lib.require_gpu_tensor(img2, "img2")
+    if img1.dim() != 3 or img1.shape != img2.shape:
+        raise ValueError(f"ssim: images must both be [C,H,W], got {tuple(img1.shape)} and {tuple(img2.shape)}")
+    if mask is not None:
+        mask = mask.squeeze(0) if mask.dim() == 4 else mask
+        C, H, W = img1.shape
+        if mask.dim() != 3 or tuple(mask.shape[1:]) != (H, W) or mask.shape[0] not in (1, C):
+            raise ValueError(f"ssim: mask must be [C,H,W] or [1,H,W], got {tuple(mask.shape)}")
+        _lib.require_gpu_tensor(mask, "mask")
+    s = _FusedSSIM.apply(img1.float(), img2.float().detach(), None if mask is None else mask.detach())
     if mask is None:
-        return m.mean()
-    return (m * mask[None]).sum() / (mask == 1).sum()
+        return s / img1.numel()
+    count = (mask == 1).sum()
+    return torch.where(count > 0, s / count.clamp(min=1), torch.ones_like(s))
 
 
 def view_loss(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):

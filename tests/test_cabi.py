@@ -59,3 +59,17 @@ def test_refalgo_baseline_loads_and_exports():
     L = refalgo.lib()
     for s in refalgo.SYMBOLS:
         assert hasattr(L, s), s
+
+
+def test_every_entry_point_with_parameters_has_ctypes_argtypes():
+    """A pointer passed without argtypes is truncated to a C int: every header function that
+    takes parameters must be declared in gsr._lib."""
+    import re
+
+    from gsr import _lib
+    L = _lib.lib()
+    hdr = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "gsr.h")).read(), flags=re.S)
+    for name, params in re.findall(r"\b(gsr_[a-z_0-9]+)\(([^)]*)\)\s*;", hdr):
+        if params.strip() in ("", "void"):
+            continue
+        assert getattr(L, name).argtypes is not None, name

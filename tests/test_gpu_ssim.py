@@ -1,0 +1,44 @@
+"""GPU: the fused SSIM (gsr_ssim.hip) against the reference's conv2d formulation
+(utils/loss_utils.py:53-96, restated in test_train_cpu.ssim_conv2d) -- value and dL/dimg1,
+with and without masks, ragged sizes, 1080p.  fp32: relative tolerance 1e-5 on the value,
+1e-4 (relative L2) on the gradient (different summation orders)."""
+import pytest
+import torch
+
+from helpers import rel_l2
+from test_train_cpu import ssim_conv2d
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("shape,mask_kind", [((3, 97, 131), None), ((3, 64, 64), "one"), ((3, 75, 200), "full"),
+                                             ((1, 40, 33), "one"), ((3, 1080, 1920), "one")])
+def test_fused_ssim_matches_conv2d(shape, mask_kind):
+    from gsr import train
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(5)
+    C, H, W = shape
+    base = torch.rand(shape, generator=g)
+    a = (base + 0.1 * torch.randn(shape, generator=g)).to(dev)
+    b = base.to(dev)
+    if mask_kind is None:
+        mask = None
+    else:
+        m = (torch.rand((1, H, W), generator=g) > 0.2).float()
+        mask = m.expand(C, H, W).to(dev) if mask_kind == "one" else (torch.rand(shape, generator=g) > 0.3).float().to(dev)
+    a1 = a.clone().requires_grad_(True)
+    a2 = a.clone().requires_grad_(True)
+    v1 = train.ssim(a1, b, mask)
+    v2 = ssim_conv2d(a2, b, mask)
+    (3.0 * v1).backward()
+    (3.0 * v2).backward()
+    torch.cuda.synchronize()
+    assert abs(float(v1) - float(v2)) <= 1e-5 * abs(float(v2)) + 1e-7, (float(v1), float(v2))
+    e = rel_l2(a1.grad.cpu().numpy(), a2.grad.cpu().numpy())
+    assert e < 1e-4, e
+
+
+def test_fused_ssim_empty_mask_is_one():
+    from gsr import train
+    a = torch.rand(3, 20, 20, device="cuda")
+    assert float(train.ssim(a, a * 0.5, torch.zeros(3, 20, 20, device="cuda"))) == 1.0

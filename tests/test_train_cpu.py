@@ -34,6 +34,25 @@ def test_step_requires_gpu():
         fp.step()
 
 
+def ssim_conv2d(img1, img2, mask=None):
+    """utils/loss_utils.py:53-96 restated with torch conv2d (test reference for gsr_ssim)."""
+    import torch.nn.functional as F
+    c = img1.shape[-3]
+    w = train._window(11, c, img1.device)
+    a, b = img1[None], img2[None]
+    mu1 = F.conv2d(a, w, padding=5, groups=c)
+    mu2 = F.conv2d(b, w, padding=5, groups=c)
+    mu1_sq, mu2_sq, mu12 = mu1.pow(2), mu2.pow(2), mu1 * mu2
+    s1 = F.conv2d(a * a, w, padding=5, groups=c) - mu1_sq
+    s2 = F.conv2d(b * b, w, padding=5, groups=c) - mu2_sq
+    s12 = F.conv2d(a * b, w, padding=5, groups=c) - mu12
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    m = ((2 * mu12 + C1) * (2 * s12 + C2)) / ((mu1_sq + mu2_sq + C1) * (s1 + s2 + C2))
+    if mask is None:
+        return m.mean()
+    return (m * mask[None]).sum() / (mask == 1).sum()
+
+
 def test_losses_match_reference_formulas():
     g = torch.Generator().manual_seed(0)
     a, b = torch.rand(3, 20, 24, generator=g), torch.rand(3, 20, 24, generator=g)
@@ -42,9 +61,11 @@ def test_losses_match_reference_formulas():
     # utils/loss_utils.py:27-35
     assert torch.allclose(train.l1_loss(a, b, m), (a * m - b * m).abs().sum() / (m == 1).sum())
     assert torch.allclose(train.l1_loss(a, b), (a - b).abs().mean())
-    # SSIM of an image with itself is 1; with noise it drops
-    assert abs(float(train.ssim(a, a, m)) - 1.0) < 1e-5
-    assert float(train.ssim(a, b, m)) < 0.5
+    # the torch restatement the fused GPU SSIM is tested against: 1 for an image with itself
+    assert abs(float(ssim_conv2d(a, a, m)) - 1.0) < 1e-5
+    assert float(ssim_conv2d(a, b, m)) < 0.5
+    with pytest.raises(RuntimeError):  # the product SSIM is the HIP kernel: no CPU path
+        train.ssim(a, b, m)
     # the window is the reference's normalised 11-tap Gaussian (sigma 1.5) outer product
     w = train._window(11, 3, "cpu")
     assert w.shape == (3, 1, 11, 11) and abs(float(w[0].sum()) - 1.0) < 1e-6
