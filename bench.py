@@ -304,6 +304,8 @@ def main():
                                                   "default resolution rule")
     ap.add_argument("--view", type=int, default=0)
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
+    ap.add_argument("--views-per-sync", type=int, default=4,
+                    help="N > 1: views each rank renders per gradient all-reduce (the mini-batch per GPU)")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     args = ap.parse_args()
 
@@ -313,8 +315,15 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
+        # one process per GPU over RCCL ("nccl"); GSR_DIST_BACKEND=gloo rehearses the N > 1 path
+        # with several ranks on one GPU (ranks wrap around the visible devices)
+        backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.config == "cfg3":
@@ -359,14 +368,32 @@ def main():
                                                 pm, cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb,
                                                 img)
         if dist is not None:
-            # one bucket: dL/d(means3D, sh, opacity, scales, rotations) summed over the view-parallel ranks
+            # dL/d(means3D, sh, opacity, scales, rotations) accumulated over this rank's views of
+            # one mini-batch in one flat bucket, then summed over the view-parallel ranks with
+            # one RCCL all-reduce per mini-batch (cfg4's 4 views per GPU per iteration)
             ts = [grads[3], grads[5], grads[2], grads[6], grads[7]]
-            state["bucket"] = gdp.all_reduce_grads(ts, bucket=state.get("bucket"))
+            if "bucket" not in state:
+                state["bucket"], state["k"] = gdp.GradBucket(ts), 0
+            b = state["bucket"]
+            if state["k"] == 0:
+                b.pack(ts)
+            else:
+                for v, t in zip(b.views(), ts):
+                    v.add_(t)
+            state["k"] += 1
+            if state["k"] == args.views_per_sync:
+                sync()
         state["R"], state["radii"] = R, radii
         return grads
 
+    def sync():
+        if dist is not None and state.get("k", 0) > 0:
+            state["bucket"].all_reduce()
+            state["k"] = 0
+
     for _ in range(args.warmup):
         step()
+    sync()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -376,6 +403,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    sync()  # a partial mini-batch is reduced inside the timed region too
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -388,6 +416,16 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
 
+    ar_ms = None
+    if dist is not None:
+        for _ in range(2):
+            state["bucket"].all_reduce()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(5):
+            state["bucket"].all_reduce()
+        torch.cuda.synchronize()
+        ar_ms = (time.perf_counter() - ta) * 1e3 / 5
     R = int(state["R"])
     Pv = int((state["radii"] > 0).sum().item())
     T = ((W + 15) // 16) * ((H + 15) // 16)
@@ -419,11 +457,14 @@ def main():
         "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
                                                                        else "") if args.ply else args.config)
                                + f": {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view"
-                   + (", RCCL grad all-reduce" if world > 1 else ""), "gaussians": P, "width": W, "height": H,
+                   + (f", RCCL grad all-reduce per {args.views_per_sync} views" if world > 1 else ""), "gaussians": P, "width": W, "height": H,
                    "sh_degree": deg, "num_rendered": R, "visible": Pv, "parallelism": f"views x{world}"},
         "roofline": roofline,
         "stage_ms": per_stage,
     }
+    if dist is not None:
+        out["data_parallel"] = {"views_per_sync": args.views_per_sync, "grad_all_reduce_ms": round(ar_ms, 4),
+                                "grad_bucket_mb": round(state["bucket"].flat.numel() * 4 / 1e6, 2)}
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
         out["gpu_reference_algorithm"] = refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -106,7 +106,10 @@ def reduce_densification_stats(xyz_gradient_accum: torch.Tensor, denom: torch.Te
 
 def accumulate_view_stats(stats: Dict[str, torch.Tensor], mean2D_grad: torch.Tensor, radii: torch.Tensor) -> None:
     """Per-rank, per-view densification update (train.py:130, gaussian_model.py:627-629)."""
+    # dense masked updates (no boolean indexing: that is a nonzero + host sync per array)
     vis = radii > 0
-    stats["max_radii2D"][vis] = torch.max(stats["max_radii2D"][vis], radii[vis].to(stats["max_radii2D"].dtype))
-    stats["xyz_gradient_accum"][vis] += torch.norm(mean2D_grad[vis, :2], dim=-1, keepdim=True)
-    stats["denom"][vis] += 1
+    mr = stats["max_radii2D"]
+    torch.where(vis, torch.maximum(mr, radii.to(mr.dtype)), mr, out=mr)
+    v1 = vis[:, None]
+    stats["xyz_gradient_accum"].add_(torch.where(v1, torch.norm(mean2D_grad[:, :2], dim=-1, keepdim=True), 0.0))
+    stats["denom"].add_(v1.to(stats["denom"].dtype))

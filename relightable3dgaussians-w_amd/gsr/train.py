@@ -271,16 +271,20 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     dev = fp.device
     bg = torch.zeros(3, device=dev) if bg is None else bg
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    # the activations are computed once per iteration and the views' losses share one
+    # backward (autograd sums the views' gradients exactly as sequential backwards would)
+    pc = scene.model()
     total = torch.zeros((), device=dev)
+    outs = []
     for view, vid, gt in zip(views, view_ids, gts):
-        pc = scene.model()
         light = relit_shade.EnvironmentLight(fp.params["env_sh"][vid], sh_degree=4)
         out = relit.render(view, pc, light, fp.params["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
-        sky = view.sky_mask.expand_as(gt)
-        loss = view_loss(out, gt, sky, view.occluders_mask.expand_as(gt))
-        loss.backward()
-        total = total + loss.detach()
+        total = total + view_loss(out, gt, view.sky_mask.expand_as(gt), view.occluders_mask.expand_as(gt))
+        outs.append(out)
+    total.backward()
+    for out in outs:
         gdp.accumulate_view_stats(scene.stats, out["viewspace_points"].grad, out["radii"])
+    del outs
     fp.check_grads_in_place()
     n_views = len(views)
     if world > 1:
@@ -290,7 +294,7 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
                                        scene.stats["max_radii2D"], group=group)
         n_views *= world
     fp.step(grad_scale=1.0 / n_views)
-    return total
+    return total.detach()
 
 
 def synthetic_relit_scene(P_fg, n_views, W, H, focal, device, seed=0, sky_frac=0.1):

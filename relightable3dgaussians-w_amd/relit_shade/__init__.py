@@ -171,6 +171,26 @@ class RelitFeaturesFunction(torch.autograd.Function):
         return (d_xyz, d_rot, None, d_alb, d_kr, d_km, d_base, d_sky, None, None, None, None, None, None, None, None)
 
 
+_FG_CACHE = {}
+
+
+def _fg_index(is_sky, P, dev):
+    """(fg_rows, fg_rank) of the foreground Gaussians.  The sky flags change only when the
+    model is densified, so the index (a nonzero: one host synchronisation) is cached on the
+    flag tensor's identity and version counter and rebuilt when either changes."""
+    hit = _FG_CACHE.get(id(is_sky))
+    if hit is not None and hit[0] is is_sky and hit[1] == (is_sky._version, P, str(dev)):
+        return hit[2], hit[3]
+    fg = ~is_sky.reshape(-1).bool()
+    fg_rows = torch.nonzero(fg).reshape(-1).int()
+    fg_rank = torch.full((P,), -1, dtype=torch.int32, device=dev)
+    fg_rank[fg_rows.long()] = torch.arange(fg_rows.numel(), dtype=torch.int32, device=dev)
+    if len(_FG_CACHE) > 8:
+        _FG_CACHE.clear()
+    _FG_CACHE[id(is_sky)] = (is_sky, (is_sky._version, P, str(dev)), fg_rows, fg_rank)
+    return fg_rows, fg_rank
+
+
 def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness, light, campos, viewmatrix,
                    sky_sh=None, sky_sh_degree=1, specular=True, fix_sky=False):
     """render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) as
@@ -184,11 +204,7 @@ def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness,
     Differentiable w.r.t. xyz, rotation, albedo, roughness, metalness, light.base, sky_sh."""
     _lib.require_gpu_tensor(xyz, "xyz")
     dev = xyz.device
-    sky = is_sky.reshape(-1).bool()
-    fg = ~sky
-    fg_rows = torch.nonzero(fg).reshape(-1).int()
-    fg_rank = torch.full((xyz.shape[0],), -1, dtype=torch.int32, device=dev)
-    fg_rank[fg_rows.long()] = torch.arange(fg_rows.numel(), dtype=torch.int32, device=dev)
+    fg_rows, fg_rank = _fg_index(is_sky, xyz.shape[0], dev)
     base = light.base.squeeze().reshape(-1, 3).float().contiguous()
     deg = int(round(base.shape[0] ** 0.5)) - 1
     sky_deg = -1 if (fix_sky or sky_sh is None) else int(sky_sh_degree)
