@@ -52,28 +52,39 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "ren
 VALU_NS_PER_INST = 1.16  # wave64 v_fma_f32 issue cost per SIMD at 8 waves/SIMD (tools/micro/pk_fma.hip, vops.hip)
 
 
-def pmc_kernel(stage):
-    """The newest committed rocprofv3 record (profiles/r*_hbm_traffic.json) of the stage's kernel."""
+def _pmc_record(stage, workload):
+    """The newest committed rocprofv3 record (profiles/r*_hbm_traffic.json, tools/profile_summary.py)
+    of the stage's kernel whose profiled bench line ran the same workload; ({}, None) if none."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
-    if not files:
-        return {}, None
-    d = json.load(open(files[-1]))
-    return d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {}), os.path.relpath(files[-1], ROOT)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        b = d.get("bench_under_profiler") or {}
+        if (b.get("config") or {}).get("workload", "").split(",")[0] != workload.split(",")[0]:
+            continue
+        return d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {}), os.path.relpath(f, ROOT)
+    return {}, None
 
 
-def pmc_traffic(stage):
+def pmc_kernel(stage, workload):
+    return _pmc_record(stage, workload)
+
+
+def pmc_traffic(stage, workload):
     """HBM bytes per launch of the stage's kernel from the newest committed rocprofv3 PMC pass
-    (profiles/<tag>_hbm_traffic.json, written by tools/profile_summary.py from separate
-    --pmc FETCH_SIZE / WRITE_SIZE runs of this same bench command, corrected as
+    of this same workload (profiles/<tag>_hbm_traffic.json, written by tools/profile_summary.py
+    from separate --pmc FETCH_SIZE / WRITE_SIZE runs of this bench command, corrected as
     MI355X_MICROARCH.md prescribes).  None when no such profile exists."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")))
-    if not files:
-        return None, None
-    d = json.load(open(files[-1]))
-    k = d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {})
-    return k.get("traffic_bytes"), os.path.relpath(files[-1], ROOT)
+    k, src = _pmc_record(stage, workload)
+    return k.get("traffic_bytes"), src
+
+
+def unique_bytes(stage, P, Pv, R, T, Npix, M):
+    """Compulsory HBM bytes of the tile passes if every array were read once: the point list
+    (R ids), each visible Gaussian's 48-B record once, the image state, the gradient lines.
+    SURVEY §8d's figure counts one 40-B record read per instance (R x 40) instead; the
+    records are re-read from L2 across the tiles a Gaussian touches."""
+    return {"render_fwd": T * 8 + R * 4 + Pv * 48 + Npix * 20,
+            "render_bwd": T * 8 + R * 4 + Pv * 48 + Npix * 20 + Pv * 44}.get(stage)
 
 
 def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
@@ -130,9 +141,10 @@ def bench_relight(args, dev):
     import diff_gaussian_rasterization as dgr
     import relit_shade
     from gsr import relit, scenes
-    P_fg = args.P or 1_000_000
+    stress = args.config == "cfg5-relit"  # cfg5: 5M Gaussians at 3840x2160, relit render with backward
+    P_fg = args.P or (4_545_455 if stress else 1_000_000)
     P = P_fg + P_fg // 10  # + 10 % sky Gaussians
-    cam, gs, c = scenes.build_config("cfg2", device="cpu", seed=0, P=P)
+    cam, gs, c = scenes.build_config("cfg5" if stress else "cfg2", device="cpu", seed=0, P=P)
     W, H = cam.image_width, cam.image_height
     gen = torch.Generator().manual_seed(7)
     is_sky = torch.zeros(P, dtype=torch.bool)
@@ -176,7 +188,7 @@ def bench_relight(args, dev):
 
     ms = timed(relit.render)
     res = {True: float("nan"), False: float("nan")}
-    if not args.fused_only:
+    if not args.fused_only and not stress:
         for cached in (True, False):
             dgr.geometry_cache(cached)
             res[cached] = timed(relit.render_calls)
@@ -185,11 +197,14 @@ def bench_relight(args, dev):
         "metric": "relit render() views/s (render()'s images + training loss backward)", "value": round(1e3 / ms, 3),
         "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"cfg3: {P_fg} foreground + {P - P_fg} sky Gaussians, {W}x{H}, env SH deg 4, "
-                               "sky SH deg 1, debug=False", "gaussians": P, "width": W, "height": H},
+        "config": {"workload": f"{'cfg5 (relit stress)' if stress else 'cfg3'}: {P_fg} foreground + {P - P_fg} sky "
+                               f"Gaussians, {W}x{H}, env SH deg 4, sky SH deg 1, debug=False", "gaussians": P,
+                   "width": W, "height": H},
+        "mpix_per_s": round(W * H / (ms * 1e-3) / 1e6, 3),
         "implementation": "gsr.relit.render: fused relit features + one 14-channel composite",
-        "render_calls": {"cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
-                         "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
+        "render_calls": None if res[True] != res[True] else {
+            "cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
+            "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
 
 
 def bench_train(args, dev, dist, rank, world):
@@ -326,7 +341,7 @@ def main():
             dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if args.config == "cfg3":
+    if args.config in ("cfg3", "cfg5-relit"):
         bench_relight(args, dev)
         return
     if args.config == "cfg4":
@@ -434,13 +449,18 @@ def main():
                algorithmic_bytes(k, P, Pv, R, T, W * H, M) is not None), key=lambda kv: kv[1])
     dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
     achieved = dom_bytes / (dom[1] * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(dom[0])
+    workload = (f"ply {os.path.basename(args.ply)}" if args.ply else args.config) + f": {P} Gaussians SH{deg}, {W}x{H}"
+    traffic, traffic_src = pmc_traffic(dom[0], workload)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
                 "kernel": dom[0],
                 "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom[1], 4)}
-    kinfo, ksrc = pmc_kernel(dom[0])
+    ub = unique_bytes(dom[0], P, Pv, R, T, W * H, M)
+    if ub is not None:
+        roofline["unique_bytes_per_launch"] = int(ub)
+        roofline["unique_frac"] = round(ub / (dom[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    kinfo, ksrc = pmc_kernel(dom[0], workload)
     if kinfo.get("valu_insts"):
         # the tile passes are VALU-issue-bound: instruction throughput against the measured
         # wave64 VALU issue rate of the chip
