@@ -24,6 +24,9 @@
  *   gsr_adam_step      torch.optim.Adam.step over the per-Gaussian param groups
  *                      (train.py:191, relit3DGW_model.py:149) as one fused launch over a
  *                      flat parameter buffer (the data-parallel training step)
+ *   gsr_view_loss_forward / gsr_view_loss_backward
+ *                      the pointwise loss terms of train.py:77-99 (masked L1, sky-BRDF,
+ *                      normal consistency) fused into one kernel each way
  *   gsr_ssim_forward / gsr_ssim_backward
  *                      the training loss's SSIM (utils/loss_utils.py:53-96, train.py:78)
  *                      as one fused stencil kernel each way
@@ -193,6 +196,19 @@ int gsr_ssim_forward(int C, int height, int width, const float* img1, const floa
                      long long mask_cstride, const float* window, float* block_sums, float* dmaps, void* stream);
 int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
                       const float* gscale, const float* window, float* dimg1, void* stream);
+
+/* The pointwise terms of the training loss (train.py:77-99) over one view: images img, gt,
+ * diff, spec, nrm, nref are [3,H,W] (npix = H*W), the sky and occluder masks [H,W].
+ * Forward: gsr_view_loss_partials(npix) x 5 partial sums (see csrc/gsr_loss.hip) that the
+ * caller adds.  Backward: coef (device) = (k_img, k_brdf, k_normal); any gradient pointer
+ * may be null. */
+int gsr_view_loss_partials(int npix);
+int gsr_view_loss_forward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                          const float* nrm, const float* nref, const float* sky, const float* occ, float* partials,
+                          void* stream);
+int gsr_view_loss_backward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                           const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
+                           float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -917,4 +917,30 @@ int gsr_ssim_backward(int C, int height, int width, const float* img1, const flo
     return GSR_OK;
 }
 
+int gsr_view_loss_partials(int npix) { return npix > 0 ? gsr::view_loss_blocks(npix) : 0; }
+
+int gsr_view_loss_forward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                          const float* nrm, const float* nref, const float* sky, const float* occ, float* partials,
+                          void* stream_) {
+    if (npix <= 0) return fail(GSR_E_ARG, "gsr_view_loss_forward: bad size");
+    if (!img || !gt || !diff || !spec || !nrm || !nref || !sky || !occ || !partials)
+        return fail(GSR_E_ARG, "gsr_view_loss_forward: missing buffers");
+    gsr::launch_view_loss_fwd(npix, img, gt, diff, spec, nrm, nref, sky, occ, partials,
+                              reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_view_loss_backward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                           const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
+                           float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, void* stream_) {
+    if (npix <= 0) return fail(GSR_E_ARG, "gsr_view_loss_backward: bad size");
+    if (!img || !gt || !diff || !spec || !nrm || !nref || !sky || !occ || !coef)
+        return fail(GSR_E_ARG, "gsr_view_loss_backward: missing buffers");
+    gsr::launch_view_loss_bwd(npix, img, gt, diff, spec, nrm, nref, sky, occ, coef, d_img, d_diff, d_spec, d_nrm,
+                              d_nref, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

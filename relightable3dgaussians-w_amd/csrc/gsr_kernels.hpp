@@ -190,6 +190,15 @@ void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, 
 void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
                      const float* gscale, const SsimWindow& win, float* dimg1, hipStream_t s);
 
+// ---- fused pointwise training-loss terms (gsr_loss.hip) ---------------------------------
+int view_loss_blocks(int npix);
+void launch_view_loss_fwd(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                          const float* nrm, const float* nref, const float* sky, const float* occ, float* partials,
+                          hipStream_t s);
+void launch_view_loss_bwd(int npix, const float* img, const float* gt, const float* diff, const float* spec,
+                          const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
+                          float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, hipStream_t s);
+
 // render()'s image-space tail (gsr_epilogue.hip): cam12 = rows of K^-1^T R^T, then the centre
 void launch_epilogue_fwd(int W, int H, const float* cam12, const float* n01, const float* depth, const float* alpha,
                          const float* sky, int normal_view, float* normal, float* normal_ref, hipStream_t s);

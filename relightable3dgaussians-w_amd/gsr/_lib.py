@@ -58,6 +58,9 @@ def _declare(lib):
                                        vp, vp, vp]
     lib.gsr_adam_step.argtypes = [C.c_longlong, i, C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.c_double, C.c_double,
                                   C.c_double, i, f, vp, vp, vp, vp, vp]
+    lib.gsr_view_loss_partials.argtypes = [i]
+    lib.gsr_view_loss_forward.argtypes = [i] + [vp] * 9 + [vp]
+    lib.gsr_view_loss_backward.argtypes = [i] + [vp] * 9 + [vp] * 5 + [vp]
     lib.gsr_ssim_partials.argtypes = [i, i, i]
     lib.gsr_ssim_partials.restype = C.c_longlong
     lib.gsr_ssim_forward.argtypes = [i, i, i, vp, vp, vp, C.c_longlong, C.POINTER(C.c_float), vp, vp, vp]
@@ -76,6 +79,7 @@ def _declare(lib):
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
+               "gsr_view_loss_forward", "gsr_view_loss_backward",
                "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 

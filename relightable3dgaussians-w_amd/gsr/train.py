@@ -109,10 +109,13 @@ class FlatParams:
 # ---- losses (utils/loss_utils.py; the caller's code, restated for the step) ---------------
 
 def l1_loss(out, gt, mask=None):
-    """utils/loss_utils.py:27-35 (masked: sum |out*m - gt*m| / #(m == 1))."""
+    """utils/loss_utils.py:27-35 (masked: sum |out*m - gt*m| / #(m == 1); 0 for an empty mask,
+    as the reference's early return, without its host synchronisation)."""
     if mask is None:
         return (out - gt).abs().mean()
-    return (out * mask - gt * mask).abs().sum() / (mask == 1).sum()
+    n = (mask == 1).sum()
+    s = (out * mask - gt * mask).abs().sum()
+    return torch.where(n > 0, s / n.clamp(min=1), torch.zeros_like(s))
 
 
 _WINDOWS: Dict[Tuple, torch.Tensor] = {}
@@ -198,11 +201,75 @@ def ssim(img1, img2, mask=None, window_size=11):
     if mask is None:
         return s / img1.numel()
     count = (mask == 1).sum()
+    if mask.shape[0] == 1 and img1.shape[0] > 1:  # a [1,H,W] mask stands for its expansion over C
+        count = count * img1.shape[0]
     return torch.where(count > 0, s / count.clamp(min=1), torch.ones_like(s))
 
 
+class _FusedViewLoss(torch.autograd.Function):
+    """(1 - l_dssim) L1(img, gt; occ) + l_sky (L1(diff, 0; 1 - sky) + L1(spec, 0; 1 - sky))
+    + l_normal mean(1 - sum_c (n o s)(nr o s)) on gsr_view_loss_forward/backward; masks [H,W]."""
+
+    @staticmethod
+    def forward(ctx, img, diff, spec, nrm, nref, gt, sky, occ, lam):
+        H, W = sky.shape
+        npix = H * W
+        ts = [t.float().contiguous() for t in (img, gt, diff, spec, nrm, nref, sky, occ)]
+        L = _lib.lib()
+        parts = torch.empty((L.gsr_view_loss_partials(npix), 5), device=img.device)
+        _lib.check(L.gsr_view_loss_forward(npix, *[t.data_ptr() for t in ts], parts.data_ptr(),
+                                           _lib.stream_of(img.device)), "gsr_view_loss_forward")
+        S = parts.double().sum(0)  # counts stay exact in double
+        l_dssim, l_sky, l_normal = lam
+        zero = torch.zeros((), dtype=torch.float64, device=img.device)
+        k0 = torch.where(S[1] > 0, (1.0 - l_dssim) / S[1].clamp(min=1), zero)
+        k2 = torch.where(S[3] > 0, l_sky / S[3].clamp(min=1), zero)
+        loss = k0 * S[0] + k2 * S[2] + l_normal * (1.0 - S[4] / npix)
+        ctx.coef = torch.stack([k0, k2, zero - l_normal / npix]).float()
+        ctx.save_for_backward(*ts)
+        return loss.float()
+
+    @staticmethod
+    def backward(ctx, g):
+        ts = ctx.saved_tensors
+        H, W = ts[6].shape
+        coef = (ctx.coef * g.float()).contiguous()
+        need = ctx.needs_input_grad
+        outs = [torch.empty_like(ts[0]) if need[k] else None for k in range(5)]
+        ptr = lambda t: None if t is None else t.data_ptr()
+        _lib.check(_lib.lib().gsr_view_loss_backward(H * W, *[t.data_ptr() for t in ts], coef.data_ptr(),
+                                                     *[ptr(t) for t in outs], _lib.stream_of(ts[0].device)),
+                   "gsr_view_loss_backward")
+        return (*outs, None, None, None, None)
+
+
+def _plane(mask, H, W):
+    """A [H,W] plane of a [H,W], [1,H,W] or channel-expanded [C,H,W] mask (channels equal)."""
+    m = mask.detach()
+    while m.dim() > 2:
+        m = m[0]
+    if tuple(m.shape) != (H, W):
+        raise ValueError(f"mask shape {tuple(mask.shape)} does not match the image {H}x{W}")
+    return m
+
+
 def view_loss(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):
-    """train.py:77-99: reconstruction (L1 + D-SSIM), sky-BRDF and normal-consistency terms."""
+    """train.py:77-99: reconstruction (L1 + D-SSIM), sky-BRDF and normal-consistency terms.
+    The pointwise terms run as one fused kernel each way (gsr_view_loss_*), the SSIM on
+    gsr_ssim_*.  Masks: [H,W], [1,H,W] or their channel expansion."""
+    img = out["render"]
+    H, W = img.shape[-2:]
+    sky, occ = _plane(sky_mask, H, W), _plane(occ_mask, H, W)
+    _lib.require_gpu_tensor(img, "render")
+    pw = _FusedViewLoss.apply(img, out["diffuse_color"], out["specular_color"], out["normal"], out["normal_ref"],
+                              gt.detach(), sky, occ, (float(lambda_dssim), float(lambda_sky_brdf),
+                                                      float(lambda_normal)))
+    return pw + lambda_dssim * (1.0 - ssim(img, gt, occ[None]))
+
+
+def view_loss_torch(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):
+    """The same loss composed from PyTorch ops as train.py writes it (test reference for the
+    fused kernels; its SSIM is the fused one)."""
     img = out["render"]
     rec = l1_loss(img, gt, occ_mask) * (1 - lambda_dssim) + lambda_dssim * (1.0 - ssim(img, gt, occ_mask))
     nsky = 1 - sky_mask
@@ -210,8 +277,7 @@ def view_loss(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5
                                     l1_loss(out["specular_color"], torch.zeros_like(img), nsky))
     n = out["normal"] * occ_mask * sky_mask
     nr = out["normal_ref"] * occ_mask * sky_mask
-    loss = loss + lambda_normal * (1 - (n * nr).sum(dim=0))[None].mean()
-    return loss
+    return loss + lambda_normal * (1 - (n * nr).sum(dim=0))[None].mean()
 
 
 # ---- the model view render() reads and the step ------------------------------------------

@@ -42,3 +42,32 @@ def test_fused_ssim_empty_mask_is_one():
     from gsr import train
     a = torch.rand(3, 20, 20, device="cuda")
     assert float(train.ssim(a, a * 0.5, torch.zeros(3, 20, 20, device="cuda"))) == 1.0
+
+
+@pytest.mark.parametrize("H,W,empty_sky", [(64, 96, False), (1080, 1920, False), (40, 40, True)])
+def test_fused_view_loss_matches_torch(H, W, empty_sky):
+    """train.py:77-99's loss: the fused pointwise kernels + fused SSIM against the same
+    terms composed from PyTorch ops (train.view_loss_torch), value and the five gradients."""
+    from gsr import train
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(9)
+    names = ["render", "diffuse_color", "specular_color", "normal", "normal_ref"]
+    base = {k: torch.rand(3, H, W, generator=g) for k in names}
+    base["normal"] = base["normal"] * 2 - 1
+    gt = torch.rand(3, H, W, generator=g).to(dev)
+    sky = (torch.rand(1, H, W, generator=g) > 0.3).float()
+    if empty_sky:
+        sky.fill_(1.0)  # no non-sky pixel: the sky-BRDF L1s are 0 (the reference's early return)
+    occ = (torch.rand(1, H, W, generator=g) > 0.1).float()
+    sky3, occ3 = sky.expand(3, H, W).to(dev), occ.expand(3, H, W).to(dev)
+    a = {k: v.to(dev).requires_grad_(True) for k, v in base.items()}
+    b = {k: v.to(dev).requires_grad_(True) for k, v in base.items()}
+    la = train.view_loss(a, gt, sky3, occ3)
+    lb = train.view_loss_torch(b, gt, sky3, occ3)
+    (2.0 * la).backward()
+    (2.0 * lb).backward()
+    torch.cuda.synchronize()
+    assert abs(float(la) - float(lb)) <= 1e-5 * abs(float(lb)) + 1e-7, (float(la), float(lb))
+    for k in names:
+        e = rel_l2(a[k].grad.cpu().numpy(), b[k].grad.cpu().numpy())
+        assert e < 1e-5 or (b[k].grad.abs().max() == 0 and a[k].grad.abs().max() == 0), (k, e)
