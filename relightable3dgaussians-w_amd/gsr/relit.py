@@ -112,6 +112,58 @@ class _Epilogue(torch.autograd.Function):
         return d_n01, d_depth, None, None, None, None
 
 
+_GREY = {}
+
+
+def _is_grey(bg_color):
+    """Whether every background channel is equal (one composite channel then serves a value
+    render() repeats over three).  Cached on the tensor's identity and version: the check
+    reads the device tensor, i.e. it is a host synchronisation, and the background of a
+    training run never changes."""
+    hit = _GREY.get(id(bg_color))
+    if hit is not None and hit[0] is bg_color and hit[1] == bg_color._version:
+        return hit[2]
+    bg = bg_color.reshape(-1).float()
+    grey = bool((bg == bg[0]).all())
+    if len(_GREY) > 16:
+        _GREY.clear()
+    _GREY[id(bg_color)] = (bg_color, bg_color._version, grey)
+    return grey
+
+
+class _SplitChannels(torch.autograd.Function):
+    """The composite image [C,H,W] split into consecutive channel groups (views).  The
+    backward writes each group's gradient into one [C,H,W] tensor (zeros only where a group
+    has none) instead of autograd's full-size zero tensor + add per slice."""
+
+    @staticmethod
+    def forward(ctx, image, widths):
+        ctx.widths = widths
+        ctx.shape = image.shape
+        out, c = [], 0
+        for k in widths:
+            out.append(image[c:c + k])
+            c += k
+        return tuple(out)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        g = torch.empty(ctx.shape, dtype=torch.float32, device=next(t for t in grads if t is not None).device) \
+            if any(t is not None for t in grads) else None
+        if g is None:
+            return None, None
+        c = 0
+        for k, t in zip(ctx.widths, grads):
+            if t is None:
+                g[c:c + k].zero_()
+            else:
+                g[c:c + k].copy_(t)
+            c += k
+        if c < g.shape[0]:
+            g[c:].zero_()
+        return g, None
+
+
 def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color, scaling_modifier=1.0, debug=True,
            specular=True, fix_sky=False, normal_view=False):
     """gaussian_renderer/__init__.py:69-280 on the fused path (same arguments, same output
@@ -153,7 +205,7 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     bg = bg_color.reshape(-1).float()
     # A value repeated over three channels (depth, alpha, roughness, metalness) is one
     # composite channel when the background is grey; otherwise three.
-    grey = bool((bg == bg[0]).all())
+    grey = _is_grey(bg_color)
     zero3 = torch.zeros(3, device=dev)
     # (name, columns [P, k], background [k]); alpha is rendered with a black background
     chans = [("render", feat[:, 0:3], bg), ("diffuse_color", feat[:, 3:6], bg), ("specular_color", feat[:, 6:9], bg),
@@ -183,10 +235,8 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     image, radii = dgr.rasterize_channels(means3D, screenspace_points, features, opacity, scales, rotations,
                                           cov3D_precomp, torch.cat(bgs), settings, nch=nch)
     H, W = settings.image_height, settings.image_width
-    imgs, c = {}, 0
-    for (name, _, _), k in zip(chans, widths):
-        imgs[name] = image[c:c + 1].expand(3, H, W) if k == 1 else image[c:c + 3]
-        c += k
+    parts = _SplitChannels.apply(image, tuple(widths))
+    imgs = {name: (v.expand(3, H, W) if k == 1 else v) for (name, _, _), k, v in zip(chans, widths, parts)}
     out = {"render": imgs["render"], "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
            "radii": radii}
     extras = {k: v for k, v in imgs.items() if k != "render"}
