@@ -223,9 +223,11 @@ def bench_train(args, dev, dist, rank, world):
     mine = list(range(rank * vpr, (rank + 1) * vpr))
     my_views, my_gts = [views[i] for i in mine], [gts[i] for i in mine]
     group = None
+    ns = max(1, min(args.streams, vpr))
+    streams = None if ns == 1 else [torch.cuda.Stream(dev) for _ in range(ns)]
 
     def step():
-        return train.train_step(scene, my_views, mine, my_gts, group=group, world=world)
+        return train.train_step(scene, my_views, mine, my_gts, group=group, world=world, streams=streams)
 
     for _ in range(args.warmup):
         step()
@@ -263,7 +265,7 @@ def bench_train(args, dev, dist, rank, world):
             "config": {"workload": f"cfg4: {scene.P} Gaussians ({P_fg} fg + {scene.P - P_fg} sky), {W}x{H}, "
                                    f"{vpr} views per GPU per iteration, env SH deg 4, sky SH deg 1",
                        "gaussians": scene.P, "width": W, "height": H, "views_per_iter": vpr * world,
-                       "parallelism": f"views x{world}", "flat_params": scene.fp.n},
+                       "parallelism": f"views x{world}", "flat_params": scene.fp.n, "streams": ns},
             "views_per_s": round(vpr * world * 1e3 / ms, 3),
             "grad_all_reduce_ms": None if ar_ms is None else round(ar_ms, 4),
             "grad_bucket_mb": round(scene.fp.n * 4 / 1e6, 2),
@@ -319,8 +321,10 @@ def main():
                                                   "default resolution rule")
     ap.add_argument("--view", type=int, default=0)
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
-    ap.add_argument("--views-per-sync", type=int, default=4,
-                    help="N > 1: views each rank renders per gradient all-reduce (the mini-batch per GPU)")
+    ap.add_argument("--views-per-step", "--views-per-sync", dest="views_per_step", type=int, default=4,
+                    help="views per step (the per-GPU mini-batch; N > 1: one gradient all-reduce per step)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the views of a step (cfg2) or a training iteration (cfg4) alternate over")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     args = ap.parse_args()
 
@@ -373,58 +377,88 @@ def main():
     gen = torch.Generator().manual_seed(1)
     dout_cpu = torch.randn(3, H, W, generator=gen)
     dout = dout_cpu.to(dev)
+    V = max(1, args.views_per_step)
+    NS = max(1, min(args.streams, V))
+    main_s = torch.cuda.current_stream(dev)
+    vstreams = [main_s] if NS == 1 else [torch.cuda.Stream(dev) for _ in range(NS)]
     state = {}
 
-    def step():
+    def view():
+        """One rasterizer forward + backward through the drop-in _C (the reference's call pair)."""
         R, color, radii, geom, binb, img = _C.rasterize_gaussians(
             bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx,
             cam.tanfovy, H, W, g["shs"], deg, cp, False)
         grads = _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm,
                                                 pm, cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb,
                                                 img)
-        if dist is not None:
-            # dL/d(means3D, sh, opacity, scales, rotations) accumulated over this rank's views of
-            # one mini-batch in one flat bucket, then summed over the view-parallel ranks with
-            # one RCCL all-reduce per mini-batch (cfg4's 4 views per GPU per iteration)
-            ts = [grads[3], grads[5], grads[2], grads[6], grads[7]]
-            if "bucket" not in state:
-                state["bucket"], state["k"] = gdp.GradBucket(ts), 0
-            b = state["bucket"]
-            if state["k"] == 0:
-                b.pack(ts)
-            else:
-                for v, t in zip(b.views(), ts):
-                    v.add_(t)
-            state["k"] += 1
-            if state["k"] == args.views_per_sync:
-                sync()
         state["R"], state["radii"] = R, radii
         return grads
 
-    def sync():
-        if dist is not None and state.get("k", 0) > 0:
+    def step():
+        """One mini-batch of V independent views (cfg4's per-GPU mini-batch), alternating over NS
+        HIP streams so that one view's latency-bound geometry passes overlap another's tile
+        passes.  At N > 1 the views' dL/d(means3D, sh, opacity, scales, rotations) are summed
+        into one flat bucket on the main stream and over the ranks with one RCCL all-reduce."""
+        for s in vstreams:
+            if s is not main_s:
+                s.wait_stream(main_s)  # the previous mini-batch's exchange comes first
+        for i in range(V):
+            s = vstreams[i % NS]
+            with torch.cuda.stream(s):
+                grads = view()
+            if dist is not None:
+                ts = [grads[3], grads[5], grads[2], grads[6], grads[7]]
+                if s is not main_s:
+                    main_s.wait_stream(s)
+                    for t in ts:
+                        t.record_stream(main_s)
+                if "bucket" not in state:
+                    state["bucket"] = gdp.GradBucket(ts)
+                b = state["bucket"]
+                if i == 0:
+                    b.pack(ts)
+                else:
+                    for v, t in zip(b.views(), ts):
+                        v.add_(t)
+        for s in vstreams:
+            if s is not main_s:
+                main_s.wait_stream(s)
+        if dist is not None:
             state["bucket"].all_reduce()
-            state["k"] = 0
 
     for _ in range(args.warmup):
         step()
-    sync()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    # Stage breakdown: three profiled views, one at a time on one stream (every stage
+    # bracketed by HIP events), before the timed region.  Inside it only the dominant stage
+    # keeps its events, so the step time carries two events per view instead of sixteen.
     _lib.profile_read(reset=True)
+    _lib.profile_stages(None)
+    _lib.profile_enable(True)
+    for _ in range(3):
+        view()
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    stages = _lib.profile_read(reset=True)
+    dom_name = max(((k, v[0] / v[1]) for k, v in stages.items() if v[1] > 0 and k in STAGE_KERNEL),
+                   key=lambda kv: kv[1])[0]
+    _lib.profile_stages([dom_name])
     _lib.profile_enable(True)
     torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    sync()  # a partial mini-batch is reduced inside the timed region too
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     t1 = time.perf_counter()
     _lib.profile_enable(False)
-    stages = _lib.profile_read(reset=True)
+    live = _lib.profile_read(reset=True).get(dom_name, (0.0, 0))
+    _lib.profile_stages(None)
     ms = (t1 - t0) * 1e3 / args.steps
     if dist is not None:
         t = torch.tensor([ms], device=dev)
@@ -445,8 +479,21 @@ def main():
     Pv = int((state["radii"] > 0).sum().item())
     T = ((W + 15) // 16) * ((H + 15) // 16)
     per_stage = {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1] > 0}
-    dom = max(((k, v[0] / max(v[1], 1)) for k, v in stages.items() if v[1] > 0 and
-               algorithmic_bytes(k, P, Pv, R, T, W * H, M) is not None), key=lambda kv: kv[1])
+    # the dominant stage's average launch time, from its events over the timed region
+    dom = (dom_name, live[0] / max(live[1], 1))
+    single = None
+    if world == 1 and (V > 1 or NS > 1):
+        # the reference's call pattern for comparison: one view at a time on one stream
+        for _ in range(3):
+            view()
+        torch.cuda.synchronize()
+        ts0 = time.perf_counter()
+        for _ in range(10):
+            view()
+        torch.cuda.synchronize()
+        sv = (time.perf_counter() - ts0) * 1e3 / 10
+        single = {"ms_per_view": round(sv, 4), "value": round(W * H / (sv * 1e-3) / 1e6, 3), "unit": "MPix/s",
+                  "what": "one view at a time on one stream (the reference's call pattern)"}
     dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
     achieved = dom_bytes / (dom[1] * 1e-3) / 1e9
     workload = (f"ply {os.path.basename(args.ply)}" if args.ply else args.config) + f": {P} Gaussians SH{deg}, {W}x{H}"
@@ -471,22 +518,29 @@ def main():
                             "peak_ginst_s": round(peak, 1), "frac": round(ach / peak, 4), "source": ksrc,
                             "peak_basis": f"{n_simd} SIMDs x 1 wave64 v_fma_f32 per {VALU_NS_PER_INST} ns"}
     out = {
-        "metric": METRIC, "value": round(world * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "metric": METRIC, "value": round(world * V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
                                                                        else "") if args.ply else args.config)
-                               + f": {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view"
-                   + (f", RCCL grad all-reduce per {args.views_per_sync} views" if world > 1 else ""), "gaussians": P, "width": W, "height": H,
-                   "sh_degree": deg, "num_rendered": R, "visible": Pv, "parallelism": f"views x{world}"},
+                               + f": {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view, {V} views per "
+                                 f"step on {NS} HIP streams"
+                   + (", one RCCL grad all-reduce per step" if world > 1 else ""), "gaussians": P, "width": W,
+                   "height": H, "sh_degree": deg, "num_rendered": R, "visible": Pv, "views_per_step": V,
+                   "streams": NS, "parallelism": f"views x{world}"},
         "roofline": roofline,
         "stage_ms": per_stage,
+        "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
+                           "stage); roofline.avg_launch_ms is the dominant stage's events inside the timed region",
     }
+    if single is not None:
+        out["single_view"] = single
     if dist is not None:
-        out["data_parallel"] = {"views_per_sync": args.views_per_sync, "grad_all_reduce_ms": round(ar_ms, 4),
+        out["data_parallel"] = {"views_per_step": V, "grad_all_reduce_ms": round(ar_ms, 4),
                                 "grad_bucket_mb": round(state["bucket"].flat.numel() * 4 / 1e6, 2)}
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
-        out["gpu_reference_algorithm"] = refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms)
+        ms_view = single["ms_per_view"] if single is not None else ms / V
+        out["gpu_reference_algorithm"] = refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_view)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(cam, gs_cpu, M, deg, dout_cpu.numpy(), ntiles=args.cpu_tiles)
         out["cpu_baseline"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cb.items()

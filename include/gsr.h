@@ -256,6 +256,9 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
  * shade_bwd) is bracketed by hipEvents on the call's stream.  gsr_profile_read() waits for
  * the recorded events and returns accumulated milliseconds and launch counts per stage. */
 int gsr_profile_enable(int on);
+/* Restrict the timed stages to the set bits of mask (bit i = stage i; default all), so a
+ * timed loop can bracket only the kernel it reports with events. */
+int gsr_profile_stages(unsigned mask);
 int gsr_profile_stage_count(void);
 const char* gsr_profile_stage_name(int i);
 int gsr_profile_read(double* ms, long long* counts, int n, int reset);

@@ -178,6 +178,7 @@ const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort"
                                      "preprocess_bwd", "shade_fwd", "shade_bwd"};
 struct Prof {
     bool on = false;
+    unsigned mask = ~0u;  // stages timed while on (gsr_profile_stages)
     std::vector<hipEvent_t> pool;
     struct Rec { hipEvent_t a, b; int stage; };
     std::vector<Rec> pending;
@@ -197,7 +198,7 @@ struct StageTimer {
     int stage;
     hipStream_t s;
     StageTimer(int st, hipStream_t ss) : stage(st), s(ss) {
-        if (g_prof.on) { a = g_prof.get(); (void)hipEventRecord(a, s); }
+        if (g_prof.on && ((g_prof.mask >> st) & 1u)) { a = g_prof.get(); (void)hipEventRecord(a, s); }
     }
     ~StageTimer() {
         if (a) {
@@ -248,6 +249,11 @@ const char* gsr_version(void) { return "gsr 0.1 gfx950"; }
 
 int gsr_profile_enable(int on) {
     g_prof.on = on != 0;
+    return GSR_OK;
+}
+
+int gsr_profile_stages(unsigned mask) {
+    g_prof.mask = mask;
     return GSR_OK;
 }
 

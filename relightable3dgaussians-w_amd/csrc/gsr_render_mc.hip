@@ -23,9 +23,10 @@
 
 namespace gsr {
 
-template <int NC4>
+// NCH: channels composited (<= 4 NC4; render()'s layout has 14, so its group skips the two
+// padding channels' FMAs and reduction slots)
+template <int NC4, int NCH = 4 * NC4>
 __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
-    constexpr int NCH = 4 * NC4;
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -93,13 +94,16 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 const bool sat = hit && test_T < 0.0001f;
                 const bool blend = hit && !sat;
                 const float w = blend ? alpha * T[q] : 0.f;
+                float Fs[4 * NC4];
 #pragma unroll
                 for (int g = 0; g < NC4; g++) {
-                    Cc[q][4 * g + 0] += F[g].x * w;
-                    Cc[q][4 * g + 1] += F[g].y * w;
-                    Cc[q][4 * g + 2] += F[g].z * w;
-                    Cc[q][4 * g + 3] += F[g].w * w;
+                    Fs[4 * g + 0] = F[g].x;
+                    Fs[4 * g + 1] = F[g].y;
+                    Fs[4 * g + 2] = F[g].z;
+                    Fs[4 * g + 3] = F[g].w;
                 }
+#pragma unroll
+                for (int c = 0; c < NCH; c++) Cc[q][c] += Fs[c] * w;
                 T[q] = blend ? test_T : T[q];
                 last[q] = blend ? pos1 : last[q];
                 lim[q] = sat ? __builtin_inff() : lim[q];
@@ -132,10 +136,9 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     }
 }
 
-template <int NC4>
+template <int NC4, int NCH = 4 * NC4>
 __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
-    constexpr int NCH = 4 * NC4;
-    constexpr int V = 6 + NCH;        // 6 geometric sums + the feature sums
+    constexpr int V = 6 + NCH;       // 6 geometric sums + the feature sums
     constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
     constexpr int NQ = (NP + 1) / 2;  // after the permlane16 stage: registers reduced by DPP rows
     WaveTile wt;
@@ -206,7 +209,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             todo &= todo - 1;
             const float4 A = s_a[k], B = s_b[k];
             const uint2 Q2 = s_q[k];
-            float F[NCH];
+            float F[4 * NC4];
 #pragma unroll
             for (int g = 0; g < NC4; g++) {
                 const float4 v = s_f[g][k];
@@ -292,20 +295,20 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     }
 }
 
-template <int NC4>
+template <int NC4, int NCH = 4 * NC4>
 __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_fwd_mc_tile<NC4>(a, tile, qallow);
+    render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
-template <int NC4>
+template <int NC4, int NCH = 4 * NC4>
 __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_bwd_mc_tile<NC4>(a, tile, qallow);
+    render_bwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
@@ -316,7 +319,10 @@ void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
         case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;
         case 3: hipLaunchKernelGGL(k_render_fwd_mc<3>, grid, dim3(64), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_render_fwd_mc<4>, grid, dim3(64), 0, s, a); break;
+        default:
+            if (a.nch == 14) hipLaunchKernelGGL((k_render_fwd_mc<4, 14>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL(k_render_fwd_mc<4>, grid, dim3(64), 0, s, a);
+            break;
     }
 }
 
@@ -328,7 +334,10 @@ void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
         case 1: hipLaunchKernelGGL(k_render_bwd_mc<1>, grid, dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_render_bwd_mc<2>, grid, dim3(64), 0, s, a); break;
         case 3: hipLaunchKernelGGL(k_render_bwd_mc<3>, grid, dim3(64), 0, s, a); break;
-        default: hipLaunchKernelGGL(k_render_bwd_mc<4>, grid, dim3(64), 0, s, a); break;
+        default:
+            if (a.nch == 14) hipLaunchKernelGGL((k_render_bwd_mc<4, 14>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL(k_render_bwd_mc<4>, grid, dim3(64), 0, s, a);
+            break;
     }
 }
 

@@ -69,6 +69,7 @@ def _declare(lib):
     lib.gsr_shade_workspace_bytes.restype = sz
     lib.gsr_get_layout.argtypes = [i, C.c_longlong, i, i, C.POINTER(Layout)]
     lib.gsr_profile_enable.argtypes = [i]
+    lib.gsr_profile_stages.argtypes = [C.c_uint]
     lib.gsr_profile_stage_count.restype = i
     lib.gsr_profile_stage_name.argtypes = [i]
     lib.gsr_profile_stage_name.restype = C.c_char_p
@@ -128,6 +129,19 @@ def stream_of(device):
 
 def profile_enable(on=True):
     lib().gsr_profile_enable(int(bool(on)))
+
+
+def profile_stages(names=None):
+    """Time only the named stages while profiling is on (None: all)."""
+    L = lib()
+    if names is None:
+        mask = 0xFFFFFFFF
+    else:
+        all_names = [L.gsr_profile_stage_name(k).decode() for k in range(L.gsr_profile_stage_count())]
+        mask = 0
+        for n in names:
+            mask |= 1 << all_names.index(n)
+    check(L.gsr_profile_stages(mask), "gsr_profile_stages")
 
 
 def profile_read(reset=True):

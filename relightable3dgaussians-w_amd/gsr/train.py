@@ -323,11 +323,14 @@ class RelitScene:
 
 
 def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
-               world: int = 1, bg=None) -> torch.Tensor:
+               world: int = 1, bg=None, streams=None) -> torch.Tensor:
     """One data-parallel iteration: this rank's views rendered and back-propagated, one
     all-reduce of the flat gradient, the densification statistics reduced, one fused Adam
-    step with the mean gradient over all ranks' views.  Returns this rank's summed loss as a
-    device scalar (no host synchronisation inside the step)."""
+    step with the mean gradient over all ranks' views.  ``streams``: HIP streams the views
+    alternate over (None: the current stream).  The views are independent until the
+    optimizer step, so one view's latency-bound geometry passes overlap another's tile
+    passes; autograd runs each view's backward on its forward's stream.  Returns this
+    rank's summed loss as a device scalar (no host synchronisation inside the step)."""
     import relit_shade
 
     from . import relit
@@ -337,19 +340,33 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     dev = fp.device
     bg = torch.zeros(3, device=dev) if bg is None else bg
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    main = torch.cuda.current_stream(dev)
+    streams = [main] if not streams else list(streams)
     # the activations are computed once per iteration and the views' losses share one
     # backward (autograd sums the views' gradients exactly as sequential backwards would)
     pc = scene.model()
-    total = torch.zeros((), device=dev)
-    outs = []
-    for view, vid, gt in zip(views, view_ids, gts):
-        light = relit_shade.EnvironmentLight(fp.params["env_sh"][vid], sh_degree=4)
-        out = relit.render(view, pc, light, fp.params["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
-        total = total + view_loss(out, gt, view.sky_mask.expand_as(gt), view.occluders_mask.expand_as(gt))
+    losses, outs = [], []
+    for i, (view, vid, gt) in enumerate(zip(views, view_ids, gts)):
+        s = streams[i % len(streams)]
+        s.wait_stream(main)
+        with torch.cuda.stream(s):
+            light = relit_shade.EnvironmentLight(fp.params["env_sh"][vid], sh_degree=4)
+            out = relit.render(view, pc, light, fp.params["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
+            losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask))
         outs.append(out)
+    for s in streams:
+        main.wait_stream(s)
+    for t in losses:
+        t.record_stream(main)
+    total = torch.stack(losses).sum()
     total.backward()
+    for s in streams:
+        main.wait_stream(s)
     for out in outs:
-        gdp.accumulate_view_stats(scene.stats, out["viewspace_points"].grad, out["radii"])
+        g, r = out["viewspace_points"].grad, out["radii"]
+        g.record_stream(main)
+        r.record_stream(main)
+        gdp.accumulate_view_stats(scene.stats, g, r)
     del outs
     fp.check_grads_in_place()
     n_views = len(views)

@@ -185,6 +185,8 @@ def _fg_index(is_sky, P, dev):
     fg_rows = torch.nonzero(fg).reshape(-1).int()
     fg_rank = torch.full((P,), -1, dtype=torch.int32, device=dev)
     fg_rank[fg_rows.long()] = torch.arange(fg_rows.numel(), dtype=torch.int32, device=dev)
+    if fg_rank.is_cuda:  # complete before another stream reads the cached index
+        torch.cuda.current_stream(dev).synchronize()
     if len(_FG_CACHE) > 8:
         _FG_CACHE.clear()
     _FG_CACHE[id(is_sky)] = (is_sky, (is_sky._version, P, str(dev)), fg_rows, fg_rank)

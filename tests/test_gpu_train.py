@@ -56,7 +56,9 @@ def test_adam_rejects_bad_arguments():
                            x.data_ptr(), None) != 0
 
 
-def test_train_step_matches_plain_autograd_and_adam():
+@pytest.mark.parametrize("nstreams", [1, 2])
+def test_train_step_matches_plain_autograd_and_adam(nstreams):
+    """... with the views on one stream or alternating over two (the bench's cfg4 layout)."""
     import types
 
     import torch.nn.functional as F
@@ -64,6 +66,7 @@ def test_train_step_matches_plain_autograd_and_adam():
     import relit_shade
     from gsr import relit, train
     dev = torch.device("cuda")
+    streams = None if nstreams == 1 else [torch.cuda.Stream() for _ in range(nstreams)]
     scene, views, gts = train.synthetic_relit_scene(3000, 2, 160, 96, 120.0, dev, seed=3)
     fp = scene.fp
     # the reference-style step: separate leaves, autograd, torch.optim.Adam over the groups
@@ -87,7 +90,7 @@ def test_train_step_matches_plain_autograd_and_adam():
         for p in leaves.values():
             p.grad /= len(views)
         opt.step()
-        loss_flat = train.train_step(scene, views, [0, 1], gts)
+        loss_flat = train.train_step(scene, views, [0, 1], gts, streams=streams)
     torch.cuda.synchronize()
     assert torch.isfinite(loss_flat)
     for n in fp.names:
