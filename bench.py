@@ -223,7 +223,7 @@ def bench_train(args, dev, dist, rank, world):
     mine = list(range(rank * vpr, (rank + 1) * vpr))
     my_views, my_gts = [views[i] for i in mine], [gts[i] for i in mine]
     group = None
-    ns = max(1, min(args.streams, vpr))
+    ns = max(1, min(2 if args.streams is None else args.streams, vpr))
     streams = None if ns == 1 else [torch.cuda.Stream(dev) for _ in range(ns)]
 
     def step():
@@ -323,8 +323,9 @@ def main():
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
     ap.add_argument("--views-per-step", "--views-per-sync", dest="views_per_step", type=int, default=4,
                     help="views per step (the per-GPU mini-batch; N > 1: one gradient all-reduce per step)")
-    ap.add_argument("--streams", type=int, default=2,
-                    help="HIP streams the views of a step (cfg2) or a training iteration (cfg4) alternate over")
+    ap.add_argument("--streams", type=int, default=None,
+                    help="HIP streams the views of a step (cfg2, default 3) or a training iteration (cfg4, "
+                         "default 2) alternate over")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     args = ap.parse_args()
 
@@ -378,7 +379,7 @@ def main():
     dout_cpu = torch.randn(3, H, W, generator=gen)
     dout = dout_cpu.to(dev)
     V = max(1, args.views_per_step)
-    NS = max(1, min(args.streams, V))
+    NS = max(1, min(3 if args.streams is None else args.streams, V))
     main_s = torch.cuda.current_stream(dev)
     vstreams = [main_s] if NS == 1 else [torch.cuda.Stream(dev) for _ in range(NS)]
     state = {}
