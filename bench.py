@@ -2,13 +2,15 @@
 """bench.py -- MPix/s fwd+bwd of the MI355X rasterizer on BASELINE.json's headline config.
 
 Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): 1.5M synthetic Gaussians, SH degree 3,
-1920x1080, one rasterizer forward + backward per step through the drop-in
-diff_gaussian_rasterization._C (libgsr.so, hand-written gfx950 HIP).  With --gpus N > 1 (one
-process per GPU, launched by torch.distributed.run) every rank renders its own view of its own
-scene shard-seed (weak scaling: view-parallel data parallelism) and the per-Gaussian
-gradients of the step are summed over ranks with one RCCL all-reduce.
+1920x1080.  A step is one mini-batch of 4 views (cfg4's per-GPU mini-batch), each one
+rasterizer forward + backward through the drop-in diff_gaussian_rasterization._C (libgsr.so,
+hand-written gfx950 HIP); the views alternate over 3 HIP streams.  With --gpus N > 1 (one
+process per GPU, launched by torch.distributed.run) every rank renders its own views of its
+own scene shard-seed (weak scaling: view-parallel data parallelism) and the
+per-Gaussian gradients of the step are summed over ranks with one RCCL all-reduce.
+`single_view` reports one view at a time on one stream beside it.
 
-Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * W * H / step time (max over
+Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * 4 * W * H / step time (max over
 ranks).  roofline: the dominant kernel (stage) by HIP-event time inside the timed region, with
 its algorithmic bytes per launch / its average duration.  cpu_baseline: the C
 oracle (oracle/, a scalar port of the reference algorithm) timed on this host on a bounded
