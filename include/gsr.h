@@ -187,8 +187,8 @@ int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double*
 /* SSIM of the training loss (utils/loss_utils.py:53-96: 11x11 Gaussian window, sigma 1.5,
  * zero padding, C1 = 0.01^2, C2 = 0.03^2) over img1, img2 [C,H,W].  window: the 11 normalised
  * 1-D weights (host).  mask: null or [C,H,W] / [1,H,W] (mask_cstride = H*W or 0).
- * block_sums: gsr_ssim_partials(C,H,W) floats, each a fixed-order partial of sum(map * mask)
- * (the caller adds them).  dmaps: null (no backward) or 3*C*H*W floats kept for the backward.
+ * block_sums: 2 * gsr_ssim_partials(C,H,W) floats, per workgroup a fixed-order partial of
+ * sum(map * mask) and of #(mask == 1) (the caller adds them).  dmaps: null (no backward) or 3*C*H*W floats kept for the backward.
  * The backward writes dL/dimg1 = gscale[0] * (window^T applied to dmaps) (img2 gets none:
  * it is the ground truth); gscale is a device scalar, dL/dloss / #mask. */
 long long gsr_ssim_partials(int C, int height, int width);

@@ -5,7 +5,7 @@
 // E[y^2], E[xy]) plus ~15 elementwise kernels, and autograd replays the convolutions
 // backward: at 1080p that is the largest cost of a training iteration (8 MIOpen
 // convolutions per view).  Here:
-//   forward   one 32x16 output tile per workgroup, both images staged with a 5-pixel zero
+//   forward   one 32x32 output tile per workgroup, both images staged with a 5-pixel zero
 //             halo in LDS, the separable Gaussian window (11 taps, sigma 1.5, the
 //             reference's normalised fp32 weights) applied as a horizontal then a
 //             vertical pass over the five moments; per pixel the SSIM value is
@@ -24,8 +24,14 @@
 
 namespace gsr {
 
-constexpr int SS_TW = 32, SS_TH = 16, SS_R = 5, SS_K = 2 * SS_R + 1;
-constexpr int SS_LW = SS_TW + 2 * SS_R, SS_LH = SS_TH + 2 * SS_R;  // 42 x 26 staged pixels
+// One 32x32 output tile per workgroup.  The window passes slide in registers: a horizontal
+// task produces 4 consecutive columns of one staged row from 14 loaded pixels, a vertical
+// task 4 consecutive rows of one column from 14 loaded row values (about a third of the LDS
+// reads of one output per task).  The summation order per output is the plain 11-tap order.
+constexpr int SS_TW = 32, SS_TH = 32, SS_R = 5, SS_K = 2 * SS_R + 1, SS_HX = 4, SS_VY = 4;
+constexpr int SS_LW = SS_TW + 2 * SS_R, SS_LH = SS_TH + 2 * SS_R;  // 42 x 42 staged pixels
+constexpr int SS_HTASKS = SS_LH * (SS_TW / SS_HX);                 // 336 horizontal tasks
+static_assert((SS_TW / 1) * (SS_TH / SS_VY) == 256, "one vertical task per thread");
 
 __device__ __forceinline__ float ld_zero(const float* p, int x, int y, int W, int H) {
     return (x >= 0 && x < W && y >= 0 && y < H) ? p[(size_t)y * W + x] : 0.f;
@@ -37,7 +43,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
                                                   float* __restrict__ block_sums, float* __restrict__ dmaps) {
     __shared__ float s1[SS_LH][SS_LW], s2[SS_LH][SS_LW];
     __shared__ float hm[5][SS_LH][SS_TW + 1];
-    __shared__ float red[4];
+    __shared__ float red[8];
     const int c = blockIdx.z;
     const size_t plane = (size_t)H * W;
     const float* a = img1 + c * plane;
@@ -49,70 +55,101 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
         s2[ly][lx] = ld_zero(b, x0 + lx, y0 + ly, W, H);
     }
     __syncthreads();
-    // horizontal pass: the five moments over 11 columns, for every staged row
-    for (int i = threadIdx.x; i < SS_LH * SS_TW; i += 256) {
-        const int ly = i / SS_TW, lx = i - ly * SS_TW;
-        float m1 = 0.f, m2 = 0.f, m11 = 0.f, m22 = 0.f, m12 = 0.f;
+    // horizontal pass: the five moments over 11 columns, 4 outputs per task
+    for (int t = threadIdx.x; t < SS_HTASKS; t += 256) {
+        const int ly = t / (SS_TW / SS_HX), lx = (t - ly * (SS_TW / SS_HX)) * SS_HX;
+        float u[SS_K + SS_HX - 1], v[SS_K + SS_HX - 1];
 #pragma unroll
-        for (int k = 0; k < SS_K; k++) {
-            const float u = s1[ly][lx + k], v = s2[ly][lx + k], g = win.w[k];
-            m1 += g * u;
-            m2 += g * v;
-            m11 += g * (u * u);
-            m22 += g * (v * v);
-            m12 += g * (u * v);
+        for (int k = 0; k < SS_K + SS_HX - 1; k++) {
+            u[k] = s1[ly][lx + k];
+            v[k] = s2[ly][lx + k];
         }
-        hm[0][ly][lx] = m1;
-        hm[1][ly][lx] = m2;
-        hm[2][ly][lx] = m11;
-        hm[3][ly][lx] = m22;
-        hm[4][ly][lx] = m12;
+#pragma unroll
+        for (int o = 0; o < SS_HX; o++) {
+            float m1 = 0.f, m2 = 0.f, m11 = 0.f, m22 = 0.f, m12 = 0.f;
+#pragma unroll
+            for (int k = 0; k < SS_K; k++) {
+                const float uu = u[o + k], vv = v[o + k], g = win.w[k];
+                m1 += g * uu;
+                m2 += g * vv;
+                m11 += g * (uu * uu);
+                m22 += g * (vv * vv);
+                m12 += g * (uu * vv);
+            }
+            hm[0][ly][lx + o] = m1;
+            hm[1][ly][lx + o] = m2;
+            hm[2][ly][lx + o] = m11;
+            hm[3][ly][lx + o] = m22;
+            hm[4][ly][lx + o] = m12;
+        }
     }
     __syncthreads();
-    float acc = 0.f;
+    float acc = 0.f, cnt = 0.f;  // sum(map * mask) and #(mask == 1) over the tile
     const float* mk = mask ? mask + c * mask_cstride : nullptr;
-    for (int i = threadIdx.x; i < SS_TH * SS_TW; i += 256) {
-        const int ty = i / SS_TW, tx = i - ty * SS_TW;
-        const int x = blockIdx.x * SS_TW + tx, y = blockIdx.y * SS_TH + ty;
-        if (x >= W || y >= H) continue;
-        float mu1 = 0.f, mu2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+    {
+        const int tx = threadIdx.x % SS_TW, ty0 = (threadIdx.x / SS_TW) * SS_VY;
+        float col[5][SS_K + SS_VY - 1];
 #pragma unroll
-        for (int k = 0; k < SS_K; k++) {
-            const float g = win.w[k];
-            mu1 += g * hm[0][ty + k][tx];
-            mu2 += g * hm[1][ty + k][tx];
-            e11 += g * hm[2][ty + k][tx];
-            e22 += g * hm[3][ty + k][tx];
-            e12 += g * hm[4][ty + k][tx];
+        for (int k = 0; k < SS_K + SS_VY - 1; k++) {
+#pragma unroll
+            for (int q = 0; q < 5; q++) col[q][k] = hm[q][ty0 + k][tx];
         }
-        const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu12 = mu1 * mu2;
-        const float s11 = e11 - mu1_sq, s22 = e22 - mu2_sq, s12 = e12 - mu12;
-        const float A = 2.f * mu12 + C1, B = 2.f * s12 + C2;
-        const float Cc = mu1_sq + mu2_sq + C1, D = s11 + s22 + C2;
-        const float inv = 1.f / (Cc * D);
-        const float map = (A * B) * inv;
-        const size_t pix = (size_t)y * W + x;
-        const float m = mk ? mk[pix] : 1.f;
-        acc += map * m;
-        if (dmaps) {
-            // d map / d mu1 (through A, B, Cc, D), d map / d E[x^2], d map / d E[xy]
-            const float d_mu1 = 2.f * mu2 * (B - A) * inv - 2.f * mu1 * map * (1.f / Cc - 1.f / D);
-            const float d_xx = -map / D;
-            const float d_xy = 2.f * A * inv;
-            const size_t o = c * plane + pix;  // maps are [3][C][H][W]
-            dmaps[o] = m * d_mu1;
-            dmaps[(size_t)gridDim.z * plane + o] = m * d_xx;
-            dmaps[(size_t)2 * gridDim.z * plane + o] = m * d_xy;
+        const int x = blockIdx.x * SS_TW + tx;
+#pragma unroll
+        for (int o = 0; o < SS_VY; o++) {
+            const int y = blockIdx.y * SS_TH + ty0 + o;
+            if (x >= W || y >= H) continue;
+            float mu1 = 0.f, mu2 = 0.f, e11 = 0.f, e22 = 0.f, e12 = 0.f;
+#pragma unroll
+            for (int k = 0; k < SS_K; k++) {
+                const float g = win.w[k];
+                mu1 += g * col[0][o + k];
+                mu2 += g * col[1][o + k];
+                e11 += g * col[2][o + k];
+                e22 += g * col[3][o + k];
+                e12 += g * col[4][o + k];
+            }
+            const float mu1_sq = mu1 * mu1, mu2_sq = mu2 * mu2, mu12 = mu1 * mu2;
+            const float s11 = e11 - mu1_sq, s22 = e22 - mu2_sq, s12 = e12 - mu12;
+            const float A = 2.f * mu12 + C1, B = 2.f * s12 + C2;
+            const float Cc = mu1_sq + mu2_sq + C1, D = s11 + s22 + C2;
+            // v_rcp_f32 (1 ulp) instead of four IEEE divisions: the loss value and its
+            // gradient stay within the tests' 1e-5 of the conv2d formulation
+            const float rC = __builtin_amdgcn_rcpf(Cc), rD = __builtin_amdgcn_rcpf(D);
+            const float inv = rC * rD;
+            const float map = (A * B) * inv;
+            const size_t pix = (size_t)y * W + x;
+            const float m = mk ? mk[pix] : 1.f;
+            acc += map * m;
+            cnt += m == 1.f ? 1.f : 0.f;
+            if (dmaps) {
+                // d map / d mu1 (through A, B, Cc, D), d map / d E[x^2], d map / d E[xy]
+                const float d_mu1 = 2.f * mu2 * (B - A) * inv - 2.f * mu1 * map * (rC - rD);
+                const float d_xx = -map * rD;
+                const float d_xy = 2.f * A * inv;
+                const size_t oo = c * plane + pix;  // maps are [3][C][H][W]
+                dmaps[oo] = m * d_mu1;
+                dmaps[(size_t)gridDim.z * plane + oo] = m * d_xx;
+                dmaps[(size_t)2 * gridDim.z * plane + oo] = m * d_xy;
+            }
         }
     }
-    // fixed-order workgroup sum (deterministic)
+    // fixed-order workgroup sums (deterministic); the count is exact (< 2^24 per tile)
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    for (int o = 32; o > 0; o >>= 1) {
+        acc += __shfl_xor(acc, o, 64);
+        cnt += __shfl_xor(cnt, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[threadIdx.x >> 6] = acc;
+        red[4 + (threadIdx.x >> 6)] = cnt;
+    }
     __syncthreads();
-    if (threadIdx.x == 0)
-        block_sums[((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x] =
-            (red[0] + red[1]) + (red[2] + red[3]);
+    if (threadIdx.x == 0) {
+        const size_t bid = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+        block_sums[2 * bid] = (red[0] + red[1]) + (red[2] + red[3]);
+        block_sums[2 * bid + 1] = (red[4] + red[5]) + (red[6] + red[7]);
+    }
 }
 
 __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
@@ -131,36 +168,53 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
         for (int k = 0; k < 3; k++) s[k][ly][lx] = ld_zero(dmaps + k * cs + c * plane, x0 + lx, y0 + ly, W, H);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < SS_LH * SS_TW; i += 256) {
-        const int ly = i / SS_TW, lx = i - ly * SS_TW;
-        float q0 = 0.f, q1 = 0.f, q2 = 0.f;
+    for (int t = threadIdx.x; t < SS_HTASKS; t += 256) {
+        const int ly = t / (SS_TW / SS_HX), lx = (t - ly * (SS_TW / SS_HX)) * SS_HX;
+        float r[3][SS_K + SS_HX - 1];
 #pragma unroll
-        for (int k = 0; k < SS_K; k++) {
-            const float g = win.w[k];
-            q0 += g * s[0][ly][lx + k];
-            q1 += g * s[1][ly][lx + k];
-            q2 += g * s[2][ly][lx + k];
+        for (int k = 0; k < SS_K + SS_HX - 1; k++) {
+#pragma unroll
+            for (int q = 0; q < 3; q++) r[q][k] = s[q][ly][lx + k];
         }
-        hm[0][ly][lx] = q0;
-        hm[1][ly][lx] = q1;
-        hm[2][ly][lx] = q2;
+#pragma unroll
+        for (int o = 0; o < SS_HX; o++) {
+            float q0 = 0.f, q1 = 0.f, q2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < SS_K; k++) {
+                const float g = win.w[k];
+                q0 += g * r[0][o + k];
+                q1 += g * r[1][o + k];
+                q2 += g * r[2][o + k];
+            }
+            hm[0][ly][lx + o] = q0;
+            hm[1][ly][lx + o] = q1;
+            hm[2][ly][lx + o] = q2;
+        }
     }
     __syncthreads();
     const float sc = *gscale;
-    for (int i = threadIdx.x; i < SS_TH * SS_TW; i += 256) {
-        const int ty = i / SS_TW, tx = i - ty * SS_TW;
-        const int x = blockIdx.x * SS_TW + tx, y = blockIdx.y * SS_TH + ty;
+    const int tx = threadIdx.x % SS_TW, ty0 = (threadIdx.x / SS_TW) * SS_VY;
+    float col[3][SS_K + SS_VY - 1];
+#pragma unroll
+    for (int k = 0; k < SS_K + SS_VY - 1; k++) {
+#pragma unroll
+        for (int q = 0; q < 3; q++) col[q][k] = hm[q][ty0 + k][tx];
+    }
+    const int x = blockIdx.x * SS_TW + tx;
+#pragma unroll
+    for (int o = 0; o < SS_VY; o++) {
+        const int y = blockIdx.y * SS_TH + ty0 + o;
         if (x >= W || y >= H) continue;
         float q0 = 0.f, q1 = 0.f, q2 = 0.f;
 #pragma unroll
         for (int k = 0; k < SS_K; k++) {
             const float g = win.w[k];
-            q0 += g * hm[0][ty + k][tx];
-            q1 += g * hm[1][ty + k][tx];
-            q2 += g * hm[2][ty + k][tx];
+            q0 += g * col[0][o + k];
+            q1 += g * col[1][o + k];
+            q2 += g * col[2][o + k];
         }
-        const size_t o = c * plane + (size_t)y * W + x;
-        dimg1[o] = sc * (q0 + 2.f * img1[o] * q1 + img2[o] * q2);
+        const size_t oo = c * plane + (size_t)y * W + x;
+        dimg1[oo] = sc * (q0 + 2.f * img1[oo] * q1 + img2[oo] * q2);
     }
 }
 

@@ -158,17 +158,22 @@ class _FusedSSIM(torch.autograd.Function):
             if mask.shape[0] == Cn and Cn > 1:
                 cstride = H * W
         L = _lib.lib()
-        parts = torch.empty(L.gsr_ssim_partials(Cn, H, W), device=img1.device)
+        parts = torch.empty((L.gsr_ssim_partials(Cn, H, W), 2), device=img1.device)
         dmaps = torch.empty((3, Cn, H, W), device=img1.device) if ctx.needs_input_grad[0] else None
         _lib.check(L.gsr_ssim_forward(Cn, H, W, img1.data_ptr(), img2.data_ptr(),
                                       None if mask is None else mask.data_ptr(), cstride, _WIN11, parts.data_ptr(),
                                       None if dmaps is None else dmaps.data_ptr(), _lib.stream_of(img1.device)),
                    "gsr_ssim_forward")
         ctx.save_for_backward(img1, img2, dmaps)
-        return parts.sum()
+        # sum(map * mask) and #(mask == 1) over the C planes the kernel read; double keeps the
+        # count exact past 2^24 elements (4K frames)
+        sums = parts.double().sum(0)
+        value, count = sums[0].float(), sums[1].clone()
+        ctx.mark_non_differentiable(count)
+        return value, count
 
     @staticmethod
-    def backward(ctx, g):
+    def backward(ctx, g, _g_count):
         img1, img2, dmaps = ctx.saved_tensors
         Cn, H, W = img1.shape
         gs = g.reshape(1).float().contiguous()
@@ -197,13 +202,12 @@ def ssim(img1, img2, mask=None, window_size=11):
         if mask.dim() != 3 or tuple(mask.shape[1:]) != (H, W) or mask.shape[0] not in (1, C):
             raise ValueError(f"ssim: mask must be [C,H,W] or [1,H,W], got {tuple(mask.shape)}")
         _lib.require_gpu_tensor(mask, "mask")
-    s = _FusedSSIM.apply(img1.float(), img2.float().detach(), None if mask is None else mask.detach())
+    # the kernel also counts #(mask == 1) over every plane it reads (a [1,H,W] mask stands
+    # for its expansion over C, as the reference expands it)
+    s, count = _FusedSSIM.apply(img1.float(), img2.float().detach(), None if mask is None else mask.detach())
     if mask is None:
         return s / img1.numel()
-    count = (mask == 1).sum()
-    if mask.shape[0] == 1 and img1.shape[0] > 1:  # a [1,H,W] mask stands for its expansion over C
-        count = count * img1.shape[0]
-    return torch.where(count > 0, s / count.clamp(min=1), torch.ones_like(s))
+    return torch.where(count > 0, s / count.clamp(min=1), torch.ones_like(s)).to(s.dtype)
 
 
 class _FusedViewLoss(torch.autograd.Function):
