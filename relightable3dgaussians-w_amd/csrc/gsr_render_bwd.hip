@@ -37,9 +37,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64], s_c[64];
     // per quadrant pixel state: T, dL/dpix, the background term, and the recurrence of
-    // backward.cu:514-537 carried as dot products with dL/dpix (accum_rec . dL/dpix and
-    // last_color . dL/dpix) plus last_alpha
-    float T[4], Tb[4], dp0[4], dp1[4], dp2[4], AD[4], LD[4], la[4];
+    // backward.cu:514-537 carried as one dot product with dL/dpix: Sr = accum_rec . dL/dpix
+    // of the Gaussians behind the current one.  The reference updates accum_rec one step
+    // late from (last_alpha, last_color); Sr is updated right after each Gaussian,
+    // Sr = alpha cd + (1 - alpha) Sr = Sr + alpha (cd - Sr) -- the same recurrence, and a no-op
+    // for a lane whose alpha is 0, so no per-lane selects are needed.
+    float T[4], Tb[4], dp0[4], dp1[4], dp2[4], Sr[4];
     uint32_t last[4], qlim[4];
     uint32_t nmax = 0;
 #pragma unroll
@@ -54,7 +57,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         T[q] = Tf;
         // -T_final * bg . dL/dpix, the background term of dL/dalpha (backward.cu:533-537)
         Tb[q] = -Tf * (a.bg[0] * dp0[q] + a.bg[1] * dp1[q] + a.bg[2] * dp2[q]);
-        AD[q] = LD[q] = la[q] = 0.f;
+        Sr[q] = 0.f;
         qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;  // other quadrants: another wave
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
@@ -137,8 +140,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 const float Tn = T[q] * inv;
                 const float dch = ae * Tn;
                 const float cdp = __builtin_fmaf(c2, dp2[q], __builtin_fmaf(c1, dp1[q], c0 * dp0[q]));
-                const float nAD = __builtin_fmaf(la[q], LD[q] - AD[q], AD[q]);
-                const float dLda = __builtin_fmaf(Tn, cdp - nAD, inv * Tb[q]);
+                const float dcs = cdp - Sr[q];
+                const float dLda = __builtin_fmaf(Tn, dcs, inv * Tb[q]);
+                Sr[q] = __builtin_fmaf(ae, dcs, Sr[q]);
                 const float Gd = Ge * dLda;
                 S5 += Gd;
                 const float wdx = Gd * dx, wdy = Gd * dy;
@@ -151,9 +155,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 S7 = __builtin_fmaf(dch, dp1[q], S7);
                 S8 = __builtin_fmaf(dch, dp2[q], S8);
                 T[q] = Tn;
-                AD[q] = sel(act, nAD, AD[q]);
-                LD[q] = sel(act, cdp, LD[q]);
-                la[q] = sel(act, alpha, la[q]);
             }
             if (any) {
             BWD_STAT(5, 1);

@@ -151,7 +151,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
     __shared__ uint2 s_q[64];  // (quadrant mask, Gaussian id)
-    float T[4], Tb[4], dp[4][NCH], AD[4], LD[4], la[4];
+    float T[4], Tb[4], dp[4][NCH], Sr[4];  // Sr: the recurrence as in gsr_render_bwd.hip
     uint32_t last[4], qlim[4];
     uint32_t nmax = 0;
 #pragma unroll
@@ -168,7 +168,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         }
         T[q] = Tf;
         Tb[q] = -Tf * bd;
-        AD[q] = LD[q] = la[q] = 0.f;
+        Sr[q] = 0.f;
         qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
@@ -244,8 +244,9 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 float cdp = F[0] * dp[q][0];
 #pragma unroll
                 for (int c = 1; c < NCH; c++) cdp = __builtin_fmaf(F[c], dp[q][c], cdp);
-                const float nAD = __builtin_fmaf(la[q], LD[q] - AD[q], AD[q]);
-                const float dLda = __builtin_fmaf(Tn, cdp - nAD, inv * Tb[q]);
+                const float dcs = cdp - Sr[q];
+                const float dLda = __builtin_fmaf(Tn, dcs, inv * Tb[q]);
+                Sr[q] = __builtin_fmaf(ae, dcs, Sr[q]);
                 const float Gd = Ge * dLda;
                 S5 += Gd;
                 const float wdx = Gd * dx, wdy = Gd * dy;
@@ -257,9 +258,6 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
 #pragma unroll
                 for (int c = 0; c < NCH; c++) SF[c] = __builtin_fmaf(dch, dp[q][c], SF[c]);
                 T[q] = Tn;
-                AD[q] = sel(act, nAD, AD[q]);
-                LD[q] = sel(act, cdp, LD[q]);
-                la[q] = sel(act, alpha, la[q]);
             }
             if (any) {
                 float S[2 * NP];
