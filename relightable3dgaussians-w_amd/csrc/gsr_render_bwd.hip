@@ -68,7 +68,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                      : col == 1 ? (row == 0 ? 4 : row == 1 ? 6 : row == 2 ? 5 : 7)
                      : (col == 2 && row == 0) ? 8 : -1;
     // per-value scale: dL/dmean2D gets op * (W/2, H/2), dL/dconic -op/2, the rest 1
-    const float vscale = vidx == 0 ? 0.5f * a.W : vidx == 1 ? 0.5f * a.H : vidx <= 4 ? -0.5f : 1.f;
+    const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : vidx <= 4 ? -0.5f : 1.f;
     const bool vop = vidx >= 0 && vidx <= 4;
 
 #ifdef GSR_RENDER_STATS
@@ -85,9 +85,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             id = a.point_list[range.x + p];
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
-            // conic as gauss_power takes it: (-a/2, -b, -c/2)
-            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
-            rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
+            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
+            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // records to LDS; survivors are read back with broadcast LDS loads (LDS pipe)
@@ -124,7 +124,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 BWD_STAT(2, 1);
                 const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
                 const float power = gauss_power(ka, kb, kc, dx, dy);
-                const float G = tile_exp(power);
+                const float G = tile_exp2(power);
                 const float alpha = fminf(0.99f, op * G);
                 // active: pos < last && !(power > 0) && !(alpha < 1/255)
                 const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();

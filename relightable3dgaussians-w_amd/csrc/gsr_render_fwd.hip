@@ -59,9 +59,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         if (j < n) {
             const Rec r = a.rec[a.point_list[range.x + j]];
             qm = wt.reach(r, (uint32_t)j, nullptr);
-            // conic as gauss_power takes it: (-a/2, -b, -c/2)
-            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
-            rb = make_float4(-0.5f * r.b.x, r.b.y, r.b.z, r.b.w);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
+            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
+            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // the batch's records go to LDS; the walk below reads each survivor's record with
@@ -93,7 +93,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 if (!((m >> q) & 1u)) continue;
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
-                const float alpha = fminf(0.99f, B.y * tile_exp(power));
+                const float alpha = fminf(0.99f, B.y * tile_exp2(power));
                 const bool hit = !(power > 0.0f) && alpha >= lim[q];
                 FWD_STAT(2, 1);
                 FWD_STAT(3, __ballot(hit) != 0ull);

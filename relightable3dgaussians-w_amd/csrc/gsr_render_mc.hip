@@ -61,8 +61,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
             const uint32_t id = a.point_list[range.x + j];
             const Rec r = a.rec[id];
             qm = wt.reach(r, (uint32_t)j, nullptr);
-            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
-            rb = make_float4(-0.5f * r.b.x, r.b.y, 0.f, 0.f);
+            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
+            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
@@ -88,7 +88,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 if (!((m >> q) & 1u)) continue;
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
-                const float alpha = fminf(0.99f, B.y * tile_exp(power));
+                const float alpha = fminf(0.99f, B.y * tile_exp2(power));
                 const bool hit = !(power > 0.0f) && alpha >= lim[q];
                 const float test_T = T[q] * (1 - alpha);
                 const bool sat = hit && test_T < 0.0001f;
@@ -175,7 +175,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     const int row = lane >> 4, col = lane & 15;
     const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
     const int vidx = (col < NQ && 4 * col + vrow < V) ? 4 * col + vrow : -1;
-    const float vscale = vidx == 0 ? 0.5f * a.W : vidx == 1 ? 0.5f * a.H : (vidx >= 2 && vidx <= 4) ? -0.5f : 1.f;
+    const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : (vidx >= 2 && vidx <= 4) ? -0.5f : 1.f;
     const bool vop = vidx >= 0 && vidx <= 4;
     const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
 
@@ -191,8 +191,8 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             id = a.point_list[range.x + p];
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
-            ra = make_float4(r.a.x, r.a.y, -0.5f * r.a.z, -r.a.w);
-            rb = make_float4(-0.5f * r.b.x, r.b.y, 0.f, 0.f);
+            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
+            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
@@ -231,7 +231,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 if (!((m >> q) & 1u)) continue;
                 const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
                 const float power = gauss_power(ka, kb, kc, dx, dy);
-                const float G = tile_exp(power);
+                const float G = tile_exp2(power);
                 const float alpha = fminf(0.99f, op * G);
                 const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();
                 if (act == 0ull) continue;

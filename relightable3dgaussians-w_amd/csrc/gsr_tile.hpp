@@ -51,9 +51,16 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// exp as the tile loops evaluate it, identical in forward and backward so that the
-// backward replays exactly the forward's blend decisions (v_exp_f32 on x*log2(e)).
-__device__ __forceinline__ float tile_exp(float x) { return __expf(x); }
+// The tile passes evaluate Gaussians in log2 units: the conic is pre-scaled by log2(e) when
+// a record is staged (once per record and batch), so exp(power) is one v_exp_f32 (exp2) per
+// evaluation with no multiply.  Forward and backward stage and evaluate identically, so the
+// backward replays exactly the forward's blend decisions.  The backward's conic-weighted
+// position gradients come out scaled by log2(e) and are rescaled by ln 2 once per Gaussian.
+constexpr float TILE_LOG2E = 1.44269504088896340736f;
+constexpr float TILE_LN2 = 0.69314718055994530942f;
+constexpr float TILE_HALF_LOG2E = -0.5f * TILE_LOG2E;  // factor of conic.a and conic.c
+constexpr float TILE_NEG_LOG2E = -TILE_LOG2E;          // factor of conic.b
+__device__ __forceinline__ float tile_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // Minimum over the pixel box [dx0,dx1]x[dy0,dy1] (offsets from the Gaussian centre) of
 // q(d) = a dx^2 + 2 b dx dy + c dy^2, for a positive-definite conic (a, b, c).
@@ -204,7 +211,7 @@ struct WaveTile {
 };
 
 // Exponent of the Gaussian at offset (dx, dy) from its centre, with the conic prepared as
-// (na, nb, nc) = (-a/2, -b, -c/2): power = -(a dx^2 + c dy^2)/2 - b dx dy.  The forward and
+// (na, nb, nc) = (-a/2, -b, -c/2) log2(e): power = (-(a dx^2 + c dy^2)/2 - b dx dy) log2(e).  The forward and
 // backward tile passes evaluate it with this exact operation sequence, so the backward
 // replays the forward's blend decisions bit for bit.
 __device__ __forceinline__ float gauss_power(float na, float nb, float nc, float dx, float dy) {
