@@ -96,8 +96,8 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
 
 // ---- 2+3 fused: super-tile entries emitted straight into super-tile order ----------------
 // The depth-sorted visible Gaussians are cut into blocks of ST_G.  k_st_hist counts each
-// block's entries per super-tile (digit-major table [NS][nb]) and stores the block's rects
-// in sorted order; k_digit_scan (gsr_sort.hip) turns every super-tile's row into
+// block's entries per super-tile (digit-major table [NS][nb]) from the rects in depth order
+// (carried through the depth sort, so nothing is gathered at random); k_digit_scan (gsr_sort.hip) turns every super-tile's row into
 // block offsets + a total; k_st_bases scans the totals into super-tile bases and ranges;
 // k_st_scatter re-enumerates each block's entries in (Gaussian, super-tile) order and
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
@@ -114,9 +114,8 @@ __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
 }
 
 template <int ST_W>
-__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx,
-                                                  int NS, int nb, uint32_t* table, uint32_t* wcounts,
-                                                  uint2* rect_sorted) {
+__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const uint2* rect_sorted, unsigned gsx, int NS, int nb,
+                                                  uint32_t* table, uint32_t* wcounts) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
     __syncthreads();
@@ -126,9 +125,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const uint32_t* s
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
     uint32_t* wh = hist + wave * NS;
     for (int p = p0 + lane; p < p1; p += 64) {
-        const uint2 r = rect[sorted_ids[p]];
-        rect_sorted[p] = r;
-        const uint2 sr = st_rect_of(r);
+        const uint2 sr = st_rect_of(rect_sorted[p]);
         for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
             for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
     }
@@ -251,13 +248,13 @@ static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
 
 size_t st_bin_temp_bytes(long long Pv, int NS) {
     const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
-    return (4 + 4 * (size_t)st_waves(NS)) * (size_t)NS * nb + 8 * (size_t)NS + 8 * (size_t)Pv + 5 * 256 + 1024;
+    return (4 + 4 * (size_t)st_waves(NS)) * (size_t)NS * nb + 8 * (size_t)NS + 4 * 256 + 1024;
 }
 
 // per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
 bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
-void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
+void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted, unsigned gsx, int NS, void* temp,
                    uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
     if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
         (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
@@ -274,14 +271,13 @@ void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsign
     uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
-    uint2* rect_sorted = reinterpret_cast<uint2*>(take(8 * (size_t)Pv));
     uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
     if (W == 8)
-        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
-                           wcounts, rect_sorted);
+        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, rect_sorted, gsx, NS, nb, table,
+                           wcounts);
     else
-        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, sorted_ids, rect, gsx, NS, nb, table,
-                           wcounts, rect_sorted);
+        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, rect_sorted, gsx, NS, nb, table,
+                           wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
     hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
     if (W == 8)

@@ -55,7 +55,7 @@ struct Carver {
 };
 
 struct GeomLayout {
-    size_t totals, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt,
+    size_t totals, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, rect_s, rect_s_alt,
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
@@ -82,6 +82,8 @@ GeomLayout geom_layout(long long P) {
     L.vis_val = c.take(4 * P);
     L.vis_key_alt = c.take(4 * P);
     L.vis_val_alt = c.take(4 * P);
+    L.rect_s = c.take(8 * P);
+    L.rect_s_alt = c.take(8 * P);
     L.offsets = c.take(4 * P);
     L.scan_tmp = c.take(24 * (size_t)gsr::scan_blocks(P) + 16);
     L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(P));
@@ -371,7 +373,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     {
         GSR_STAGE(ST_DEPTH_SORT);
         flip = gsr::radix_sort_pairs_from(P, pa.depth_key, nullptr, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
-                                          at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s);
+                                          at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s,
+                                          pa.rect, at<uint2>(geom, gl.rect_s), at<uint2>(geom, gl.rect_s_alt));
     }
     GSR_LAUNCH_CHECK();
 
@@ -405,7 +408,9 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     const uint32_t* st_sorted_vals = stv;
     if (gsr::st_bin_supported(NS)) {
         GSR_STAGE(ST_DUPLICATE);
-        gsr::launch_st_bin((int)Pv, sorted_ids, pa.rect, gsx, NS, at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, s);
+        const uint2* rect_sorted = flip ? at<uint2>(geom, gl.rect_s_alt) : at<uint2>(geom, gl.rect_s);
+        gsr::launch_st_bin((int)Pv, sorted_ids, rect_sorted, gsx, NS, at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges,
+                           s);
     } else {
         uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
         {

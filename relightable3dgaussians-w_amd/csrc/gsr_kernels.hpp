@@ -58,8 +58,11 @@ void launch_exclusive_scan_u32(long long n, const uint32_t* in, const uint32_t* 
 
 // ---- radix sort (gsr_sort.hip) ---------------------------------------------------------
 constexpr int SORT_THREADS = 256;
-constexpr int SORT_ITEMS = 16;
-constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 4096 keys per block
+#ifndef GSR_SORT_ITEMS
+#define GSR_SORT_ITEMS 8
+#endif
+constexpr int SORT_ITEMS = GSR_SORT_ITEMS;
+constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 2048 keys per block
 inline int sort_blocks(long long n) { return (int)((n + SORT_TILE - 1) / SORT_TILE); }
 // scratch bytes for sort of n items
 size_t radix_sort_temp_bytes(long long n);
@@ -70,9 +73,12 @@ int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys
                      int end_bit, void* temp, hipStream_t s);
 // The same with a separate, untouched input (keys_in, vals_in; vals_in == nullptr means
 // the values 0..n-1); the result lands in (keys, vals) or, when 1 is returned, the alt pair.
+// A non-null aux_in (8 B per pair, input order) moves with the pairs and lands in aux or,
+// when 1 is returned, aux_alt.
 int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
                           uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int end_bit, void* temp,
-                          hipStream_t s);
+                          hipStream_t s, const uint2* aux_in = nullptr, uint2* aux = nullptr,
+                          uint2* aux_alt = nullptr);
 
 // table[d][0..nb) -> exclusive prefix within each of ndigits rows; digit_tot[d] = row total
 void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot, hipStream_t s);
@@ -80,9 +86,10 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
 // Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
 // order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1365.
+// rect_sorted: the rects already in depth order (the depth sort's side payload).
 size_t st_bin_temp_bytes(long long Pv, int NS);
 bool st_bin_supported(int NS);
-void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect, unsigned gsx, int NS, void* temp,
+void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted, unsigned gsx, int NS, void* temp,
                    uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s);
 // In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
 // super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).

@@ -77,12 +77,17 @@ __global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int
     if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
 }
 
+// AUX: an 8-byte side payload (the Gaussians' tile rects) moves with every pair, so that the
+// depth-sorted order never has to gather it at random afterwards
+template <bool AUX>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
                                                                   const uint32_t* offsets, const uint32_t* digit_tot,
-                                                                  int nb, uint32_t* keys_out, uint32_t* vals_out) {
+                                                                  int nb, uint32_t* keys_out, uint32_t* vals_out,
+                                                                  const uint2* aux_in, uint2* aux_out) {
     __shared__ uint32_t s_keys[SORT_TILE];
     __shared__ uint32_t s_vals[SORT_TILE];
+    __shared__ uint2 s_aux[AUX ? SORT_TILE : 1];
     __shared__ uint32_t wh[4][256];
     __shared__ uint32_t dstart[256];
     __shared__ uint32_t goff[256];
@@ -94,6 +99,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     const long long tile_base = (long long)blk * SORT_TILE;
     const long long base = tile_base + wave * WAVE_ITEMS;
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
+    uint2 aux[AUX ? SORT_ITEMS : 1];
     volatile uint32_t* wc = wh[wave];
     const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     // all loads first (32 per lane in flight), then the ranking
@@ -102,6 +108,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         const long long i = base + k * 64 + lane;
         key[k] = i < n ? keys_in[i] : 0u;
         val[k] = i < n ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
+        if constexpr (AUX) aux[k] = i < n ? aux_in[i] : make_uint2(0u, 0u);
     }
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
@@ -140,6 +147,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
             const uint32_t p = wh[wave][d] + rank[k];
             s_keys[p] = key[k];
             s_vals[p] = val[k];
+            if constexpr (AUX) s_aux[p] = aux[k];
         }
     }
     __syncthreads();
@@ -153,6 +161,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
             const uint32_t g = goff[d] + (uint32_t)(p - dstart[d]);
             keys_out[g] = kk;
             vals_out[g] = s_vals[p];
+            if constexpr (AUX) aux_out[g] = s_aux[p];
         }
     }
 }
@@ -169,7 +178,7 @@ size_t radix_sort_temp_bytes(long long n) {
 
 int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys,
                           uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, int end_bit, void* temp,
-                          hipStream_t s) {
+                          hipStream_t s, const uint2* aux_in, uint2* aux, uint2* aux_alt) {
     if (n <= 0 || end_bit <= 0) return -1;
     const int nb = sort_blocks(n);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
@@ -178,14 +187,22 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
     const uint32_t* vin = vals_in;
     uint32_t* out_k[2] = {keys, keys_alt};
     uint32_t* out_v[2] = {vals, vals_alt};
+    const uint2* ain = aux_in;
+    uint2* out_a[2] = {aux, aux_alt};
     int cur = 0;
     for (int shift = 0; shift < end_bit; shift += 8) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
         const uint32_t mask = (1u << nbits) - 1u;
         hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
         hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask, hist,
-                           digit_tot, nb, out_k[cur], out_v[cur]);
+        if (ain) {
+            hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask,
+                               hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur]);
+            ain = out_a[cur];
+        } else {
+            hipLaunchKernelGGL(k_radix_scatter<false>, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask,
+                               hist, digit_tot, nb, out_k[cur], out_v[cur], nullptr, nullptr);
+        }
         kin = out_k[cur];
         vin = out_v[cur];
         cur ^= 1;
