@@ -94,21 +94,24 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
                 const float alpha = fminf(0.99f, B.y * tile_exp2(power));
-                const bool hit = !(power > 0.0f) && alpha >= lim[q];
+                // hit: !(power > 0) && alpha >= lim (masks and selects in SGPR pairs, see m_ge)
+                const lmask hit = ~m_gt0(power) & m_ge(alpha, lim[q]) & exec_mask();
                 FWD_STAT(2, 1);
-                FWD_STAT(3, __ballot(hit) != 0ull);
-                FWD_STAT(4, __popcll(__ballot(hit)));
+                FWD_STAT(3, hit != 0ull);
+                FWD_STAT(4, __popcll(hit));
                 const float test_T = T[q] * (1 - alpha);
-                const bool sat = hit && test_T < 0.0001f;  // saturating Gaussian is not blended
-                const bool blend = hit && !sat;
-                const float w = blend ? alpha * T[q] : 0.f;
+                const lmask sat = hit & m_lt(test_T, 0.0001f);  // saturating Gaussian is not blended
+                const lmask blend = hit & ~sat;
+                const float w = sel(blend, alpha * T[q], 0.f);
                 C0[q] += B.z * w;
                 C1[q] += B.w * w;
                 C2[q] += Cq.x * w;
-                T[q] = blend ? test_T : T[q];
-                last[q] = blend ? pos1 : last[q];
-                lim[q] = sat ? __builtin_inff() : lim[q];
-                if (__ballot(sat) && !__ballot(lim[q] < 1.f)) live &= ~(1u << q);
+                T[q] = sel(blend, test_T, T[q]);
+                last[q] = sel(blend, pos1, last[q]);
+                if (sat) {  // rare: pixels finish
+                    lim[q] = sel(sat, __builtin_inff(), lim[q]);
+                    if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
+                }
             }
             if (!live || !more) break;
             k = kn;

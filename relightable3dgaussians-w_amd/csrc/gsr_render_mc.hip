@@ -89,11 +89,11 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
                 const float alpha = fminf(0.99f, B.y * tile_exp2(power));
-                const bool hit = !(power > 0.0f) && alpha >= lim[q];
+                const lmask hit = ~m_gt0(power) & m_ge(alpha, lim[q]) & exec_mask();
                 const float test_T = T[q] * (1 - alpha);
-                const bool sat = hit && test_T < 0.0001f;
-                const bool blend = hit && !sat;
-                const float w = blend ? alpha * T[q] : 0.f;
+                const lmask sat = hit & m_lt(test_T, 0.0001f);
+                const lmask blend = hit & ~sat;
+                const float w = sel(blend, alpha * T[q], 0.f);
                 float Fs[4 * NC4];
 #pragma unroll
                 for (int g = 0; g < NC4; g++) {
@@ -104,10 +104,12 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 }
 #pragma unroll
                 for (int c = 0; c < NCH; c++) Cc[q][c] += Fs[c] * w;
-                T[q] = blend ? test_T : T[q];
-                last[q] = blend ? pos1 : last[q];
-                lim[q] = sat ? __builtin_inff() : lim[q];
-                if (__ballot(sat) && !__ballot(lim[q] < 1.f)) live &= ~(1u << q);
+                T[q] = sel(blend, test_T, T[q]);
+                last[q] = sel(blend, pos1, last[q]);
+                if (sat) {  // rare: pixels finish
+                    lim[q] = sel(sat, __builtin_inff(), lim[q]);
+                    if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
+                }
             }
         }
     }
