@@ -101,14 +101,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
         BWD_STAT(1, __popcll(todo));
         if (!todo) continue;
-        int k = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
-        for (;;) {
-            const bool more = todo != 0ull;
-            const int kn = more ? __builtin_ctzll(todo) : k;
-            todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
+        // one survivor (record A, B, Cq at batch slot k), back to front
+        auto grad_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
             const float c0 = B.z, c1 = B.w, c2 = Cq.x;
@@ -174,11 +168,27 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             v *= vop ? op * vscale : vscale;
             if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
             }
+        };
+        // survivors in pairs over two register sets (the next survivor's record is read
+        // while the current one runs, and no register copies between them)
+        int k = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
+        for (;;) {
+            bool more = todo != 0ull;
+            const int kn = more ? __builtin_ctzll(todo) : k;
+            todo &= todo - 1;
+            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
+            grad_one(A, B, Cq, k);
             if (!more) break;
-            k = kn;
-            A = An;
-            B = Bn;
-            Cq = Cn;
+            more = todo != 0ull;
+            k = more ? __builtin_ctzll(todo) : kn;
+            todo &= todo - 1;
+            A = s_a[k];
+            B = s_b[k];
+            Cq = s_c[k];
+            grad_one(An, Bn, Cn, kn);
+            if (!more) break;
         }
     }
 #ifdef GSR_RENDER_STATS

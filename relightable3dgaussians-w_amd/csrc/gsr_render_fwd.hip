@@ -76,16 +76,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
         FWD_STAT(1, __popcll(todo));
         if (!todo) continue;
-        int k = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        float4 A = s_a[k], B = s_b[k];
-        float2 Cq = s_c[k];
-        for (;;) {
-            const bool more = todo != 0ull;
-            const int kn = more ? __builtin_ctzll(todo) : k;
-            todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn];
-            const float2 Cn = s_c[kn];
+        // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
+        auto blend_one = [&](const float4& A, const float4& B, const float2& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
             const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
 #pragma unroll
@@ -113,11 +105,29 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
                 }
             }
+        };
+        // survivors in pairs over two register sets (the next survivor's record is read
+        // while the current one blends, and no register copies between them)
+        int k = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        float4 A = s_a[k], B = s_b[k];
+        float2 Cq = s_c[k];
+        for (;;) {
+            bool more = todo != 0ull;
+            const int kn = more ? __builtin_ctzll(todo) : k;
+            todo &= todo - 1;
+            const float4 An = s_a[kn], Bn = s_b[kn];
+            const float2 Cn = s_c[kn];
+            blend_one(A, B, Cq, k);
             if (!live || !more) break;
-            k = kn;
-            A = An;
-            B = Bn;
-            Cq = Cn;
+            more = todo != 0ull;
+            k = more ? __builtin_ctzll(todo) : kn;
+            todo &= todo - 1;
+            A = s_a[k];
+            B = s_b[k];
+            Cq = s_c[k];
+            blend_one(An, Bn, Cn, kn);
+            if (!live || !more) break;
         }
     }
 #ifdef GSR_RENDER_STATS
