@@ -177,9 +177,12 @@ _FG_CACHE = {}
 def _fg_index(is_sky, P, dev):
     """(fg_rows, fg_rank) of the foreground Gaussians.  The sky flags change only when the
     model is densified, so the index (a nonzero: one host synchronisation) is cached on the
-    flag tensor's identity and version counter and rebuilt when either changes."""
-    hit = _FG_CACHE.get(id(is_sky))
-    if hit is not None and hit[0] is is_sky and hit[1] == (is_sky._version, P, str(dev)):
+    flags' storage (address, shape, strides -- render() passes a fresh squeeze() view of the
+    model's tensor every call) and version counter, and rebuilt when either changes.  The
+    cache holds the flag tensor, so its storage cannot be freed and the address reused."""
+    key = (is_sky.data_ptr(), tuple(is_sky.shape), tuple(is_sky.stride()), P, str(dev))
+    hit = _FG_CACHE.get(key)
+    if hit is not None and hit[1] == is_sky._version:
         return hit[2], hit[3]
     fg = ~is_sky.reshape(-1).bool()
     fg_rows = torch.nonzero(fg).reshape(-1).int()
@@ -189,7 +192,7 @@ def _fg_index(is_sky, P, dev):
         torch.cuda.current_stream(dev).synchronize()
     if len(_FG_CACHE) > 8:
         _FG_CACHE.clear()
-    _FG_CACHE[id(is_sky)] = (is_sky, (is_sky._version, P, str(dev)), fg_rows, fg_rank)
+    _FG_CACHE[key] = (is_sky, is_sky._version, fg_rows, fg_rank)
     return fg_rows, fg_rank
 
 

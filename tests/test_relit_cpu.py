@@ -51,3 +51,20 @@ def test_depths_to_points_matches_reference_formula():
     pts = torch.stack([gx, gy, torch.ones_like(gx)], dim=-1).reshape(-1, 3)
     ref = d.reshape(-1, 1) * (pts @ K.inverse().T @ c2w[:3, :3].T) + c2w[:3, 3]
     np.testing.assert_allclose(relit.depths_to_points(view, d).numpy(), ref.numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_fg_index_cache_across_views():
+    """relit_features' foreground index is rebuilt only when the sky flags change: render()
+    hands it a fresh squeeze() view of the model's flags every call (a cache miss there is a
+    nonzero + host synchronisation per view)."""
+    import relit_shade as rs
+    flags = torch.zeros(10, 1, dtype=torch.bool)
+    flags[7:] = True
+    cpu = torch.device("cpu")
+    rows, rank = rs._fg_index(flags.squeeze(), 10, cpu)
+    assert rows.tolist() == list(range(7)) and rank.tolist() == list(range(7)) + [-1] * 3
+    again = rs._fg_index(flags.squeeze(), 10, cpu)
+    assert again[0] is rows and again[1] is rank
+    flags[0] = True  # in-place change (densification): version bump -> rebuilt
+    rows2, rank2 = rs._fg_index(flags.squeeze(), 10, cpu)
+    assert rows2.tolist() == list(range(1, 7)) and rank2.tolist() == [-1, 0, 1, 2, 3, 4, 5, -1, -1, -1]

@@ -1,0 +1,37 @@
+#!/usr/bin/env python
+"""Where the cfg4 training iteration spends GPU time outside the HIP kernels: runs a few
+train_step()s under torch.profiler and prints the device-time table grouped by Python
+call site (tools only; run on the GPU box).
+
+    python tools/train_glue.py [P_fg] [rows]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "relightable3dgaussians-w_amd")]
+
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+
+def main():
+    from gsr import train
+    P_fg = int(sys.argv[1]) if len(sys.argv) > 1 else 1_363_637
+    rows = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    dev = torch.device("cuda", 0)
+    scene, views, gts = train.synthetic_relit_scene(P_fg, 4, 1920, 1080, 1400.0, dev, seed=0)
+    ids = list(range(4))
+    for _ in range(3):
+        train.train_step(scene, views, ids, gts)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        for _ in range(3):
+            train.train_step(scene, views, ids, gts)
+        torch.cuda.synchronize()
+    print(prof.key_averages(group_by_stack_n=4).table(sort_by="device_time_total", row_limit=rows,
+                                                      max_name_column_width=40, max_src_column_width=90))
+
+
+if __name__ == "__main__":
+    main()
