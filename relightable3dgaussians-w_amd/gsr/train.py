@@ -326,6 +326,9 @@ class RelitScene:
                                      get_metalness=torch.sigmoid(p["metalness"]), get_is_sky=self.is_sky)
 
 
+_BLACK = {}
+
+
 def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
                world: int = 1, bg=None, streams=None) -> torch.Tensor:
     """One data-parallel iteration: this rank's views rendered and back-propagated, one
@@ -342,7 +345,10 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     fp = scene.fp
     fp.zero_grad()
     dev = fp.device
-    bg = torch.zeros(3, device=dev) if bg is None else bg
+    if bg is None:  # one tensor per device: render()'s grey-background check is cached on it
+        bg = _BLACK.get(str(dev))
+        if bg is None:
+            bg = _BLACK[str(dev)] = torch.zeros(3, device=dev)
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
     main = torch.cuda.current_stream(dev)
     streams = [main] if not streams else list(streams)
