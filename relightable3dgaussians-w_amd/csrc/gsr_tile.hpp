@@ -255,6 +255,19 @@ __device__ __forceinline__ uint32_t sel(lmask m, uint32_t t, uint32_t f) {
 }
 __device__ __forceinline__ lmask exec_mask() { return __builtin_amdgcn_read_exec(); }
 
+// Row sums of three registers' 16-lane rows at once, transposed: row_mirror and
+// row_half_mirror steps pair two registers per add (lane bit 3, then bit 2, selects which
+// register a lane carries), then two quad_perm steps -- 5 DPP adds + 4 selects instead of
+// 3 x 4 DPP adds.  On return the lanes of column 0 hold a's row sums, column 8 b's and
+// column 4 c's.  mb3 / mb2: lane masks of column bit 3 / bit 2.
+__device__ __forceinline__ float row_sum3(float a, float b, float c, lmask mb3, lmask mb2) {
+    const float w = sel(mb3, b, a) + dpp<0x140>(sel(mb3, a, b));  // row_mirror: l <-> 15 - l
+    const float v = c + dpp<0x140>(c);
+    float x = sel(mb2, v, w) + dpp<0x141>(sel(mb2, w, v));        // row_half_mirror: l <-> 7 - l
+    x += dpp<0x4E>(x);
+    return x + dpp<0xB1>(x);
+}
+
 __device__ __forceinline__ float bcast(float v, int k) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
 }
