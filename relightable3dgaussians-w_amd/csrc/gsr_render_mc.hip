@@ -176,7 +176,9 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     }
     const int row = lane >> 4, col = lane & 15;
     const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
-    const int vidx = (col < NQ && 4 * col + vrow < V) ? 4 * col + vrow : -1;
+    const int vreg = row_sums_t_reg<NQ>(col);  // the register whose row sums this lane ends with
+    const int vidx = (vreg >= 0 && 4 * vreg + vrow < V) ? 4 * vreg + vrow : -1;
+    const lmask mb3 = __ballot((col & 8) != 0), mb2 = __ballot((col & 4) != 0);
     const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : (vidx >= 2 && vidx <= 4) ? -0.5f : 1.f;
     const bool vop = vidx >= 0 && vidx <= 4;
     const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
@@ -278,12 +280,10 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 for (int t = 0; t < NP; t++) Pp[t] = swap32_sum(S[2 * t], S[2 * t + 1]);
 #pragma unroll
                 for (int t = NP; t < 2 * NQ; t++) Pp[t] = 0.f;
-                float v = 0.f;
+                float Qr[NQ];
 #pragma unroll
-                for (int t = 0; t < NQ; t++) {
-                    const float Qt = row_sum(swap16_sum(Pp[2 * t], Pp[2 * t + 1]));
-                    v = col == t ? Qt : v;
-                }
+                for (int t = 0; t < NQ; t++) Qr[t] = swap16_sum(Pp[2 * t], Pp[2 * t + 1]);
+                float v = row_sums_t<NQ>(Qr, mb3, mb2, col);
                 v *= vop ? op * vscale : vscale;
                 if (v != 0.f) {
                     const uint32_t gid = Q2.y;

@@ -255,6 +255,40 @@ __device__ __forceinline__ uint32_t sel(lmask m, uint32_t t, uint32_t f) {
 }
 __device__ __forceinline__ lmask exec_mask() { return __builtin_amdgcn_read_exec(); }
 
+// Row sums of NQ registers' 16-lane rows at once, transposed as row_sum3 (mirror steps pair
+// registers, lone ones add to themselves), then quad_perm steps; lane column c returns
+// register row_sums_t_reg<NQ>(c)'s row sum (-1: a duplicate or unused lane).
+template <int NQ>
+__device__ __forceinline__ int row_sums_t_reg(int col) {
+    constexpr int NW = (NQ + 1) / 2, NX = (NW + 1) / 2;
+    const int j = col & 3, b2 = (col >> 2) & 1, b3 = (col >> 3) & 1;
+    if (j >= NX) return -1;
+    const int w = 2 * j + 1 < NW ? 2 * j + b2 : (b2 ? -1 : 2 * j);
+    if (w < 0) return -1;
+    return 2 * w + 1 < NQ ? 2 * w + b3 : (b3 ? -1 : 2 * w);
+}
+template <int NQ>
+__device__ __forceinline__ float row_sums_t(const float (&Q)[NQ], lmask mb3, lmask mb2, int col) {
+    constexpr int NW = (NQ + 1) / 2, NX = (NW + 1) / 2;
+    static_assert(NX <= 4, "at most 16 registers");
+    float W[NW], X[NX];
+#pragma unroll
+    for (int i = 0; i < NW; i++)
+        W[i] = 2 * i + 1 < NQ ? sel(mb3, Q[2 * i + 1], Q[2 * i]) + dpp<0x140>(sel(mb3, Q[2 * i], Q[2 * i + 1]))
+                              : Q[2 * i] + dpp<0x140>(Q[2 * i]);
+#pragma unroll
+    for (int j = 0; j < NX; j++) {
+        X[j] = 2 * j + 1 < NW ? sel(mb2, W[2 * j + 1], W[2 * j]) + dpp<0x141>(sel(mb2, W[2 * j], W[2 * j + 1]))
+                              : W[2 * j] + dpp<0x141>(W[2 * j]);
+        X[j] += dpp<0x4E>(X[j]);
+        X[j] += dpp<0xB1>(X[j]);
+    }
+    float out = X[0];
+#pragma unroll
+    for (int j = 1; j < NX; j++) out = (col & 3) == j ? X[j] : out;
+    return out;
+}
+
 // Row sums of three registers' 16-lane rows at once, transposed: row_mirror and
 // row_half_mirror steps pair two registers per add (lane bit 3, then bit 2, selects which
 // register a lane carries), then two quad_perm steps -- 5 DPP adds + 4 selects instead of
