@@ -62,11 +62,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
     // Reduction layout (see the end of the loop): lane 16 r + 8 j, j < 2, ends up holding
-    // value 4 j + {0,2,1,3}[r] of the Gaussian's 9 gradient sums; lanes 4 and 20 hold the
-    // two halves of value 8.
+    // value 4 j + {0,2,1,3}[r] of the Gaussian's 9 gradient sums; lanes 4 + 16 r hold four
+    // partial sums of value 8.
     const int row = lane >> 4, col = lane & 15;
     const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
-    const int vidx = col == 0 ? vrow : col == 8 ? 4 + vrow : (col == 4 && row < 2) ? 8 : -1;
+    const int vidx = col == 0 ? vrow : col == 8 ? 4 + vrow : col == 4 ? 8 : -1;
     const lmask mb3 = __ballot((col & 8) != 0), mb2 = __ballot((col & 4) != 0);
     // per-value scale: dL/dmean2D gets op * (W/2, H/2), dL/dconic -op/2, the rest 1
     const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : vidx <= 4 ? -0.5f : 1.f;
@@ -156,14 +156,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             // conic part of dL/dmean2D (backward.cu:540-545): -(a M1 + b M2), -(b M1 + c M2)
             const float S0 = __builtin_fmaf(ka, M1 + M1, kb * M2);
             const float S1 = __builtin_fmaf(kc, M2 + M2, kb * M1);
-            // wave reduction: permlane32 swaps pair (S0,S1),(S2,S3),(S4,S5),(S6,S7),(S8,-)
+            // wave reduction: permlane32 swaps pair (S0,S1),(S2,S3),(S4,S5),(S6,S7)
             // into half-wave sums, permlane16 swaps pair those into row sums of four values
             // per register, then the three registers' 16-lane rows sum transposed (row_sum3)
             float P0 = swap32_sum(S0, S1), P1 = swap32_sum(S2, S3), P2 = swap32_sum(S4, S5);
-            float P3 = swap32_sum(S6, S7), P4 = swap32_sum(S8, S8);
-            // S8 skips the permlane16 stage: rows 0 and 1 of P4 carry two partial sums, and
-            // both go to the atomic (lanes 4 and 20)
-            const float Q0 = swap16_sum(P0, P1), Q1 = swap16_sum(P2, P3), Q2 = P4;
+            float P3 = swap32_sum(S6, S7);
+            // S8 skips both swap stages: its four row sums go to the atomic as partial sums
+            // (lanes 4, 20, 36, 52)
+            const float Q0 = swap16_sum(P0, P1), Q1 = swap16_sum(P2, P3), Q2 = S8;
             float v = row_sum3(Q0, Q1, Q2, mb3, mb2);
             v *= vop ? op * vscale : vscale;
             if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
