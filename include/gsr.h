@@ -34,6 +34,10 @@
  *                      render()'s image-space tail: normal remap + sky mask and normal_ref
  *                      from the depth image (gaussian_renderer/__init__.py:226-276,
  *                      utils/graphics_utils.py:141-169)
+ *   gsr_texture2d_forward / gsr_texture2d_backward
+ *                      nvdiffrast's dr.texture (2D, linear/nearest, wrap/clamp/zero) as
+ *                      the reference calls it (scene/NVDIFFREC/light.py:170, util.py:117);
+ *                      backs the drop-in `nvdiffrast.torch.texture`
  *   gsr_forward_channels / gsr_backward_channels
  *                      the 6-10 same-geometry rasterizer calls of one render()
  *                      (gaussian_renderer/__init__.py:160-264) as ONE composite of all
@@ -209,6 +213,17 @@ int gsr_view_loss_forward(int npix, const float* img, const float* gt, const flo
 int gsr_view_loss_backward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
                            const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
                            float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, void* stream);
+
+/* 2D texture lookups with nvdiffrast.torch.texture semantics (csrc/gsr_texture.hip).
+ * tex [tex_nb][tex_h][tex_w][C] (tex_nb == 1 broadcasts over the minibatch, else == nb);
+ * uv [nb][npix][2]; out [nb][npix][C].  filter: 0 nearest, 1 linear; boundary: 0 wrap,
+ * 1 clamp, 2 zero.  Backward: dout [nb][npix][C] -> d_uv [nb][npix][2] (may be NULL) and
+ * d_tex (may be NULL; ACCUMULATED into, the caller zero-fills it). */
+int gsr_texture2d_forward(int nb, int npix, int tex_nb, int tex_h, int tex_w, int C, const float* tex,
+                          const float* uv, int filter, int boundary, float* out, void* stream);
+int gsr_texture2d_backward(int nb, int npix, int tex_nb, int tex_h, int tex_w, int C, const float* tex,
+                           const float* uv, int filter, int boundary, const float* dout, float* d_uv, float* d_tex,
+                           void* stream);
 
 /* present[i] = (view * means3D[i]).z > 0.2 (uint8 0/1). */
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

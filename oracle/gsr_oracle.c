@@ -848,6 +848,109 @@ void orc_eval_sh(int deg, int N, const REAL* sh /* N x K x 3, K >= (deg+1)^2 */,
     }
 }
 
+/* nvdiffrast dr.texture, 2D (third-party, not vendored; called at light.py:170 with
+ * filter 'linear' / boundary 'clamp' and at util.py:117 with the default 'wrap').
+ * Restated from nvdiffrast's published 2D semantics -- parity unpinned beyond its call
+ * sites: texel space u*w - 0.5 (wrap first takes u - floor(u)); clamp clamps the texel
+ * coordinate to [0, w-1] before the floor and then uses the same texel twice on the edge
+ * (zero uv gradient); wrap takes indices modulo the size; zero drops taps outside;
+ * nearest reads texel floor(u*w).  tex [tnb][th][tw][C], uv [nb][npix][2].
+ * filter: 0 nearest, 1 linear; boundary: 0 wrap, 1 clamp, 2 zero. */
+static int tex_nearest(REAL u, REAL v, int w, int h, int boundary) {
+    if (boundary == 0) { u = u - FLOOR(u); v = v - FLOOR(v); }
+    int iu = (int)FLOOR(u * (REAL)w), iv = (int)FLOOR(v * (REAL)h);
+    if (boundary != 2) {
+        iu = iu < 0 ? 0 : (iu > w - 1 ? w - 1 : iu);
+        iv = iv < 0 ? 0 : (iv > h - 1 ? h - 1 : iv);
+    }
+    return (iu < 0 || iu >= w || iv < 0 || iv >= h) ? -1 : iv * w + iu;
+}
+
+static void tex_linear(REAL u, REAL v, int w, int h, int boundary, int* idx, REAL* fu, REAL* fv) {
+    if (boundary == 0) { u = u - FLOOR(u); v = v - FLOOR(v); }
+    u = u * (REAL)w - F(0.5);
+    v = v * (REAL)h - F(0.5);
+    int cu = 0, cv = 0;
+    if (boundary == 1) {
+        u = FMIN(FMAX(u, F(0.0)), (REAL)(w - 1));
+        v = FMIN(FMAX(v, F(0.0)), (REAL)(h - 1));
+        cu = (u == F(0.0) || u == (REAL)(w - 1));
+        cv = (v == F(0.0) || v == (REAL)(h - 1));
+    }
+    int iu0 = (int)FLOOR(u), iv0 = (int)FLOOR(v);
+    int iu1 = iu0 + (cu ? 0 : 1), iv1 = iv0 + (cv ? 0 : 1);
+    *fu = u - (REAL)iu0;
+    *fv = v - (REAL)iv0;
+    if (boundary == 0) {
+        if (iu0 < 0) iu0 += w;
+        if (iv0 < 0) iv0 += h;
+        if (iu1 >= w) iu1 -= w;
+        if (iv1 >= h) iv1 -= h;
+    }
+    int us[2] = {iu0, iu1}, vs[2] = {iv0, iv1};
+    for (int k = 0; k < 4; k++) {
+        int a = us[k & 1], b = vs[k >> 1];
+        idx[k] = (a < 0 || a >= w || b < 0 || b >= h) ? -1 : b * w + a;
+    }
+}
+
+void orc_texture2d_fwd(int nb, int npix, int tnb, int th, int tw, int C, const REAL* tex, const REAL* uv, int filter,
+                       int boundary, REAL* out) {
+    for (int i = 0; i < nb * npix; i++) {
+        const REAL* t = tex + (size_t)(tnb == 1 ? 0 : i / npix) * th * tw * C;
+        REAL u = uv[2 * i], v = uv[2 * i + 1];
+        if (filter == 0) {
+            int k = tex_nearest(u, v, tw, th, boundary);
+            for (int c = 0; c < C; c++) out[(size_t)i * C + c] = k < 0 ? F(0.0) : t[(size_t)k * C + c];
+            continue;
+        }
+        int idx[4];
+        REAL fu, fv;
+        tex_linear(u, v, tw, th, boundary, idx, &fu, &fv);
+        for (int c = 0; c < C; c++) {
+            REAL a[4];
+            for (int k = 0; k < 4; k++) a[k] = idx[k] < 0 ? F(0.0) : t[(size_t)idx[k] * C + c];
+            REAL x0 = a[0] + fu * (a[1] - a[0]), x1 = a[2] + fu * (a[3] - a[2]);
+            out[(size_t)i * C + c] = x0 + fv * (x1 - x0);
+        }
+    }
+}
+
+/* d_uv [nb][npix][2] (written), d_tex (accumulated; may be NULL) */
+void orc_texture2d_bwd(int nb, int npix, int tnb, int th, int tw, int C, const REAL* tex, const REAL* uv, int filter,
+                       int boundary, const REAL* dout, REAL* d_uv, REAL* d_tex) {
+    for (int i = 0; i < nb * npix; i++) {
+        size_t layer = (size_t)(tnb == 1 ? 0 : i / npix) * th * tw * C;
+        const REAL* t = tex + layer;
+        const REAL* g = dout + (size_t)i * C;
+        REAL u = uv[2 * i], v = uv[2 * i + 1];
+        if (filter == 0) {
+            int k = tex_nearest(u, v, tw, th, boundary);
+            if (d_tex && k >= 0)
+                for (int c = 0; c < C; c++) d_tex[layer + (size_t)k * C + c] += g[c];
+            d_uv[2 * i] = d_uv[2 * i + 1] = F(0.0);
+            continue;
+        }
+        int idx[4];
+        REAL fu, fv;
+        tex_linear(u, v, tw, th, boundary, idx, &fu, &fv);
+        REAL gu = F(0.0), gv = F(0.0);
+        for (int c = 0; c < C; c++) {
+            REAL a[4];
+            for (int k = 0; k < 4; k++) a[k] = idx[k] < 0 ? F(0.0) : t[(size_t)idx[k] * C + c];
+            gu += g[c] * ((a[1] - a[0]) * (1 - fv) + (a[3] - a[2]) * fv);
+            gv += g[c] * ((a[2] - a[0]) * (1 - fu) + (a[3] - a[1]) * fu);
+            if (d_tex) {
+                REAL wt[4] = {(1 - fu) * (1 - fv), fu * (1 - fv), (1 - fu) * fv, fu * fv};
+                for (int k = 0; k < 4; k++)
+                    if (idx[k] >= 0) d_tex[layer + (size_t)idx[k] * C + c] += g[c] * wt[k];
+            }
+        }
+        d_uv[2 * i] = gu * (REAL)tw;
+        d_uv[2 * i + 1] = gv * (REAL)th;
+    }
+}
+
 /* util.py:523-526 gamma_correction and its derivative (clamp mask inclusive, as torch) */
 static REAL gamma_f(REAL x) { REAL c = x < 0 ? 0 : (x > 1 ? 1 : x); return POW(c + F(1e-4), (REAL)(1.0 / 2.2)); }
 static REAL gamma_d(REAL x) {

@@ -251,6 +251,29 @@ def shade_bwd(pos, nrm, albedo, view_pos, kr, km, base, lut, g_rgb, g_diff, g_sp
     return d
 
 
+def texture2d(tex, uv, filter_mode="linear", boundary_mode="clamp", dout=None, f64=False):
+    """nvdiffrast dr.texture, 2D (orc_texture2d_fwd/bwd): tex [tnb,th,tw,C], uv [nb,h,w,2]
+    -> out [nb,h,w,C]; with dout also (d_uv, d_tex)."""
+    dt, _ = _real(f64)
+    L = _lib(f64)
+    tex = _arr(tex, dt)
+    uv = _arr(uv, dt)
+    tnb, th, tw, Cc = tex.shape
+    nb, h, w, _ = uv.shape
+    fm = {"nearest": 0, "linear": 1}[filter_mode]
+    bm = {"wrap": 0, "clamp": 1, "zero": 2}[boundary_mode]
+    args = [C.c_int(nb), C.c_int(h * w), C.c_int(tnb), C.c_int(th), C.c_int(tw), C.c_int(Cc), _p(tex), _p(uv),
+            C.c_int(fm), C.c_int(bm)]
+    out = np.zeros((nb, h, w, Cc), dt)
+    L.orc_texture2d_fwd(*args, _p(out))
+    if dout is None:
+        return out
+    d_uv = np.zeros_like(uv)
+    d_tex = np.zeros_like(tex)
+    L.orc_texture2d_bwd(*args, _p(_arr(dout, dt)), _p(d_uv), _p(d_tex))
+    return out, d_uv, d_tex
+
+
 def knn(points):
     """submodules/simple-knn distCUDA2: mean squared distance to the 3 nearest other points
     (orc_knn, the reference's Morton/box algorithm, float arithmetic)."""

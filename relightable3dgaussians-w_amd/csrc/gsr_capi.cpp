@@ -14,6 +14,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -178,7 +179,10 @@ enum Stage {
 const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "st_emit",
                                      "st_sort",     "tile_lists",       "render_fwd",     "bwd_zero",     "render_bwd",
                                      "preprocess_bwd", "shade_fwd", "shade_bwd"};
+// Forward calls run on the Python thread and backward calls on autograd's device thread,
+// so the pending list and the event pool are guarded by one mutex.
 struct Prof {
+    std::mutex mu;
     bool on = false;
     unsigned mask = ~0u;  // stages timed while on (gsr_profile_stages)
     std::vector<hipEvent_t> pool;
@@ -187,6 +191,7 @@ struct Prof {
     double ms[ST_COUNT] = {0};
     long long n[ST_COUNT] = {0};
     hipEvent_t get() {
+        std::lock_guard<std::mutex> lk(mu);
         if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
         hipEvent_t e;
         (void)hipEventCreate(&e);
@@ -206,6 +211,7 @@ struct StageTimer {
         if (a) {
             hipEvent_t b = g_prof.get();
             (void)hipEventRecord(b, s);
+            std::lock_guard<std::mutex> lk(g_prof.mu);
             g_prof.pending.push_back({a, b, stage});
         }
     }
@@ -264,6 +270,7 @@ int gsr_profile_stage_count(void) { return ST_COUNT; }
 const char* gsr_profile_stage_name(int i) { return (i >= 0 && i < ST_COUNT) ? kStageNames[i] : ""; }
 
 int gsr_profile_read(double* ms, long long* counts, int n, int reset) {
+    std::lock_guard<std::mutex> lk(g_prof.mu);
     for (auto& r : g_prof.pending) {
         HIP_OK(hipEventSynchronize(r.b));
         float t = 0.f;
@@ -854,6 +861,35 @@ int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const
     if (!cam12 || !depth || !alpha || !sky_mask) return fail(GSR_E_ARG, "gsr_relit_epilogue_backward: missing buffers");
     gsr::launch_epilogue_bwd(width, height, cam12, depth, alpha, sky_mask, normal_view, g_normal, g_normal_ref, d_n01,
                              d_depth, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_texture2d_forward(int nb, int npix, int tex_nb, int tex_h, int tex_w, int C, const float* tex,
+                          const float* uv, int filter, int boundary, float* out, void* stream_) {
+    if (nb < 0 || npix < 0 || tex_h <= 0 || tex_w <= 0 || C <= 0 || (tex_nb != 1 && tex_nb != nb))
+        return fail(GSR_E_ARG, "gsr_texture2d_forward: bad sizes");
+    if (filter < 0 || filter > 1 || boundary < 0 || boundary > 2)
+        return fail(GSR_E_ARG, "gsr_texture2d_forward: bad filter/boundary mode");
+    if ((long long)nb * npix > 0x7fffffffLL) return fail(GSR_E_OVERFLOW, "gsr_texture2d_forward: too many lookups");
+    if (nb * npix > 0 && (!tex || !uv || !out)) return fail(GSR_E_ARG, "gsr_texture2d_forward: missing buffers");
+    gsr::launch_texture_fwd(nb, npix, tex_nb, tex_h, tex_w, C, tex, uv, filter, boundary, out,
+                            reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_texture2d_backward(int nb, int npix, int tex_nb, int tex_h, int tex_w, int C, const float* tex,
+                           const float* uv, int filter, int boundary, const float* dout, float* d_uv, float* d_tex,
+                           void* stream_) {
+    if (nb < 0 || npix < 0 || tex_h <= 0 || tex_w <= 0 || C <= 0 || (tex_nb != 1 && tex_nb != nb))
+        return fail(GSR_E_ARG, "gsr_texture2d_backward: bad sizes");
+    if (filter < 0 || filter > 1 || boundary < 0 || boundary > 2)
+        return fail(GSR_E_ARG, "gsr_texture2d_backward: bad filter/boundary mode");
+    if ((long long)nb * npix > 0x7fffffffLL) return fail(GSR_E_OVERFLOW, "gsr_texture2d_backward: too many lookups");
+    if (nb * npix > 0 && (!tex || !uv || !dout)) return fail(GSR_E_ARG, "gsr_texture2d_backward: missing buffers");
+    gsr::launch_texture_bwd(nb, npix, tex_nb, tex_h, tex_w, C, tex, uv, filter, boundary, dout, d_uv, d_tex,
+                            reinterpret_cast<hipStream_t>(stream_));
     GSR_LAUNCH_CHECK();
     return GSR_OK;
 }

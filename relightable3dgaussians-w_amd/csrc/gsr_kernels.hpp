@@ -244,4 +244,10 @@ void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 size_t knn_workspace_bytes(int P);
 void launch_knn(int P, const float* pts, float* dists, void* ws, hipStream_t s);
 
+// ---- 2D texture sampling, nvdiffrast dr.texture semantics (gsr_texture.hip) -------------
+void launch_texture_fwd(int nb, int npix, int tex_nb, int h, int w, int C, const float* tex, const float* uv,
+                        int filter, int boundary, float* out, hipStream_t s);
+void launch_texture_bwd(int nb, int npix, int tex_nb, int h, int w, int C, const float* tex, const float* uv,
+                        int filter, int boundary, const float* dout, float* d_uv, float* d_tex, hipStream_t s);
+
 }  // namespace gsr

@@ -26,7 +26,7 @@ class _GeometryCache:
     with different colors_precomp and background.  Preprocess, depth sort, binning and the
     tile ranges depend only on the geometry, so a call whose geometry inputs are the same
     tensors, unmodified (data pointer, version counter, shape, strides), with the same camera
-    and image settings, re-renders colours over the previous call's binning
+    and image settings, on the same HIP stream, re-renders colours over the previous call's binning
     (gsr_forward_reuse).  The outputs are bit-identical to a full call.  The cache holds
     references to the keyed tensors, so their memory cannot be recycled into a false hit
     while it lives.  Only the colors_precomp path is cached (SH colours depend on campos).
@@ -50,10 +50,14 @@ class _GeometryCache:
         return (t.data_ptr(), t._version, tuple(t.shape), t.stride(), t.dtype, str(t.device))
 
     def key_of(self, s, means3D, opacities, scales, rotations, cov3Ds_precomp):
+        """The key includes the current HIP stream: a hit reuses the miss call's binning and
+        image buffers (and rewrites parts of the image buffer), which is ordered only on the
+        stream that produced them.  A call on another stream misses."""
         tensors = (means3D, opacities, scales, rotations, cov3Ds_precomp, s.viewmatrix, s.projmatrix)
+        stream = torch.cuda.current_stream(means3D.device).cuda_stream
         return (tuple(self._tkey(t) for t in tensors),
                 (int(s.image_height), int(s.image_width), float(s.tanfovx), float(s.tanfovy),
-                 float(s.scale_modifier), bool(s.prefiltered))), tensors
+                 float(s.scale_modifier), bool(s.prefiltered)), stream), tensors
 
 
 _geometry_cache = _GeometryCache()

@@ -53,6 +53,8 @@ def _declare(lib):
                                                 vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.gsr_relit_epilogue.argtypes = [i, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
     lib.gsr_relit_epilogue_backward.argtypes = [i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
+    lib.gsr_texture2d_forward.argtypes = [i, i, i, i, i, i, vp, vp, i, i, vp, vp]
+    lib.gsr_texture2d_backward.argtypes = [i, i, i, i, i, i, vp, vp, i, i, vp, vp, vp, vp]
     lib.gsr_shade_forward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp]
     lib.gsr_shade_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                        vp, vp, vp]
@@ -81,7 +83,7 @@ def _declare(lib):
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward",
-               "gsr_get_layout"):
+               "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout"):
         getattr(lib, fn).restype = C.c_int
 
 

@@ -13,8 +13,16 @@ exactly one exchange step per iteration:
     at cfg2 the bucket is 1.5M x 59 floats = 354 MB, which amortises ring latency.
   * the densification statistics: ``xyz_gradient_accum`` and ``denom``
     (gaussian_model.py:627-629) are SUMmed, ``max_radii2D`` (train.py:130) is MAXed.  Each
-    rank accumulates its own views' norms first, so the reduced statistics equal the
-    sequential reference's after the same set of views.
+    rank accumulates ONE STEP's views into zeroed per-step buffers (StepStats); only those
+    deltas are reduced and then folded into the running statistics, so after any number of
+    steps the running statistics equal the sequential reference's over the same views
+    (reducing the running totals instead would re-multiply every earlier step by the world
+    size).
+  * densification (gaussian_model.py:610-625) stays rank-consistent: the statistics and
+    parameters are identical on every rank by construction, and the only random draw (the
+    split's torch.normal, :560) comes from a generator seeded with a value broadcast from
+    rank 0 (``shared_generator`` / ``consistent_rng``), so every rank clones, splits and
+    prunes the same Gaussians and draws the same samples.
 
 No collective touches the rasterizer itself: every rank calls the same libgsr.so on its own
 view.  The helpers take any process group, so the gloo world_size-2 tests in
@@ -22,6 +30,7 @@ tests/test_dp_gloo.py exercise the same code the nccl bench path runs.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -113,3 +122,81 @@ def accumulate_view_stats(stats: Dict[str, torch.Tensor], mean2D_grad: torch.Ten
     v1 = vis[:, None]
     stats["xyz_gradient_accum"].add_(torch.where(v1, torch.norm(mean2D_grad[:, :2], dim=-1, keepdim=True), 0.0))
     stats["denom"].add_(v1.to(stats["denom"].dtype))
+
+
+class StepStats:
+    """One step's densification deltas on this rank (train.py:130, gaussian_model.py:627-629).
+
+    ``zero()`` at the start of a step, ``add_view`` per rendered view, ``commit`` once per
+    step: the deltas are reduced across ranks (SUM for the norm accumulator and the view
+    counter, MAX for the radii) and then added to / maxed into the running statistics.
+    Preallocated; a step allocates nothing."""
+
+    def __init__(self, P: int, device):
+        self.d = {"xyz_gradient_accum": torch.zeros(P, 1, device=device), "denom": torch.zeros(P, 1, device=device),
+                  "max_radii2D": torch.zeros(P, device=device)}
+
+    def zero(self) -> None:
+        for t in self.d.values():
+            t.zero_()
+
+    def add_view(self, mean2D_grad: torch.Tensor, radii: torch.Tensor) -> None:
+        accumulate_view_stats(self.d, mean2D_grad, radii)
+
+    def commit(self, running: Dict[str, torch.Tensor], group=None, world: int = 1) -> None:
+        d = self.d
+        if world > 1:
+            reduce_densification_stats(d["xyz_gradient_accum"], d["denom"], d["max_radii2D"], group=group)
+        running["xyz_gradient_accum"].add_(d["xyz_gradient_accum"])
+        running["denom"].add_(d["denom"])
+        torch.maximum(running["max_radii2D"], d["max_radii2D"], out=running["max_radii2D"])
+
+
+def shared_seed(group=None, device="cpu") -> int:
+    """A fresh 63-bit seed drawn on rank 0 and broadcast to every rank."""
+    seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)
+    if dist.is_available() and dist.is_initialized():
+        t = seed.to(device)
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        seed = t.cpu()
+    return int(seed.item())
+
+
+def shared_generator(device, group=None) -> torch.Generator:
+    """A generator on ``device`` seeded identically on every rank (the split's samples,
+    gaussian_model.py:560)."""
+    dev = torch.device(device)
+    return torch.Generator(device=dev).manual_seed(shared_seed(group, dev if dev.type == "cuda" else "cpu"))
+
+
+@contextlib.contextmanager
+def consistent_rng(device, group=None):
+    """Run the reference's own GaussianModel.densify_and_prune (which draws from the global
+    RNG through torch.normal) with the global generators seeded identically on every rank,
+    restoring them afterwards::
+
+        with dp.consistent_rng("cuda", group):
+            gaussians.densify_and_prune(...)
+    """
+    dev = torch.device(device)
+    seed = shared_seed(group, dev if dev.type == "cuda" else "cpu")
+    devices = [dev.index or 0] if dev.type == "cuda" else []
+    with torch.random.fork_rng(devices=devices):
+        torch.manual_seed(seed)
+        yield seed
+
+
+def replica_checksums(tensors: Sequence[torch.Tensor], group=None) -> List[List[float]]:
+    """Per-rank float64 checksums (sum and sum of squares of the bit patterns' values) of
+    ``tensors``, all-gathered: identical rows mean identical replicas (a debug check after
+    densification)."""
+    sums = []
+    for t in tensors:
+        x = t.detach().reshape(-1).double()
+        sums += [float(x.numel()), float(x.sum()), float((x * x).sum())]
+    mine = torch.tensor(sums, dtype=torch.float64)
+    if not (dist.is_available() and dist.is_initialized()):
+        return [sums]
+    out = [torch.zeros_like(mine) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, mine, group=group)
+    return [o.tolist() for o in out]

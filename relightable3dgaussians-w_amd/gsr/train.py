@@ -104,6 +104,9 @@ class FlatParams:
                                             float(grad_scale), self.flat.data_ptr(), self.grad.data_ptr(),
                                             self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
                                             _lib.stream_of(self.device)), "gsr_adam_step")
+        # the kernel wrote through a raw pointer: advance the version counter (shared by every
+        # view of the flat buffer) so saved-tensor checks and version-keyed caches see it
+        torch.autograd.graph.increment_version(self.flat)
 
 
 # ---- losses (utils/loss_utils.py; the caller's code, restated for the step) ---------------
@@ -317,10 +320,18 @@ class RelitScene:
         self.stats = {"xyz_gradient_accum": torch.zeros(P, 1, device=device),
                       "denom": torch.zeros(P, 1, device=device),
                       "max_radii2D": torch.zeros(P, device=device)}
+        self.step_stats = None
+        # the sky shell split samples are projected onto (gaussian_model.py:566-568)
+        sky_xyz = xyz[is_sky.reshape(-1).bool()].float()
+        self.sky_center = torch.zeros(3, device=device)
+        self.sky_radius = float(sky_xyz.norm(dim=1).median()) if sky_xyz.shape[0] else 1.0
 
     def model(self):
         p = self.fp.params
-        return types.SimpleNamespace(get_xyz=p["xyz"], get_scaling=torch.exp(p["scaling"]),
+        # xyz goes through a view made on the current (main) stream: the views render on side
+        # streams, and a leaf consumed there would accumulate its gradient off the stream it
+        # lives on (autograd's AccumulateGrad stream-mismatch warning)
+        return types.SimpleNamespace(get_xyz=p["xyz"].view(p["xyz"].shape), get_scaling=torch.exp(p["scaling"]),
                                      get_rotation=F.normalize(p["rotation"]), get_opacity=torch.sigmoid(p["opacity"]),
                                      get_albedo=torch.sigmoid(p["albedo"]), get_roughness=torch.sigmoid(p["roughness"]),
                                      get_metalness=torch.sigmoid(p["metalness"]), get_is_sky=self.is_sky)
@@ -355,13 +366,16 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     # the activations are computed once per iteration and the views' losses share one
     # backward (autograd sums the views' gradients exactly as sequential backwards would)
     pc = scene.model()
+    # per-view lighting slices are taken on the main stream too (their leaves live there)
+    env = [fp.params["env_sh"][vid] for vid in view_ids]
+    sky = [fp.params["sky_sh"][vid:vid + 1] for vid in view_ids]
     losses, outs = [], []
-    for i, (view, vid, gt) in enumerate(zip(views, view_ids, gts)):
+    for i, (view, gt) in enumerate(zip(views, gts)):
         s = streams[i % len(streams)]
         s.wait_stream(main)
         with torch.cuda.stream(s):
-            light = relit_shade.EnvironmentLight(fp.params["env_sh"][vid], sh_degree=4)
-            out = relit.render(view, pc, light, fp.params["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
+            light = relit_shade.EnvironmentLight(env[i], sh_degree=4)
+            out = relit.render(view, pc, light, sky[i], 1, pipe, bg, debug=False)
             losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask))
         outs.append(out)
     for s in streams:
@@ -372,20 +386,23 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     total.backward()
     for s in streams:
         main.wait_stream(s)
+    # this step's densification deltas (zeroed per step; only they cross ranks)
+    if scene.step_stats is None or scene.step_stats.d["denom"].shape[0] != scene.P:
+        scene.step_stats = gdp.StepStats(scene.P, dev)
+    scene.step_stats.zero()
     for out in outs:
         g, r = out["viewspace_points"].grad, out["radii"]
         g.record_stream(main)
         r.record_stream(main)
-        gdp.accumulate_view_stats(scene.stats, g, r)
+        scene.step_stats.add_view(g, r)
     del outs
     fp.check_grads_in_place()
     n_views = len(views)
     if world > 1:
         import torch.distributed as dist
         dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=group)
-        gdp.reduce_densification_stats(scene.stats["xyz_gradient_accum"], scene.stats["denom"],
-                                       scene.stats["max_radii2D"], group=group)
         n_views *= world
+    scene.step_stats.commit(scene.stats, group=group, world=world)
     fp.step(grad_scale=1.0 / n_views)
     return total.detach()
 

@@ -287,33 +287,3 @@ def install(light_cls):
     light_cls.shade = _shade
     return prev
 
-
-def smoke_check(device):
-    """Tiny shade forward + backward on `device`, checked against the CPU oracle (used by
-    __graft_entry__.smoke; imports the oracle lazily, test-only)."""
-    from oracle import oracle as orc
-    g = torch.Generator().manual_seed(7)
-    N = 1000
-    pos = torch.randn(N, 3, generator=g) * 2
-    vp = torch.tensor([[0.3, -0.2, -4.0]]).repeat(N, 1)
-    n = torch.nn.functional.normalize(torch.randn(N, 3, generator=g), dim=1)
-    alb = torch.rand(N, 3, generator=g)
-    kr = torch.rand(N, 1, generator=g) * 0.9 + 0.05
-    km = torch.rand(N, 1, generator=g)
-    base = torch.randn(25, 3, generator=g) * 0.3
-    base[0] = 1.0
-    bleaf = base.to(device).requires_grad_(True)
-    light = EnvironmentLight(bleaf, 4)
-    leaves = [t.to(device).requires_grad_(True) for t in (pos, n, alb, vp, kr, km)]
-    rgb, ex = light.shade(*[t[None, None] for t in leaves[:4]], kr=leaves[4][None, None], km=leaves[5][None, None])
-    gr = torch.randn(N, 3, generator=g)
-    (rgb.reshape(N, 3) * gr.to(device)).sum().backward()
-    lut = assets.load_fg_lut()
-    ref, _, _ = orc.shade_fwd(pos.numpy(), n.numpy(), alb.numpy(), vp.numpy(), kr.numpy(), km.numpy(), base.numpy(),
-                              lut)
-    e = np.linalg.norm(rgb.detach().cpu().numpy().reshape(N, 3) - ref) / np.linalg.norm(ref)
-    assert e < 1e-5, e
-    d = orc.shade_bwd(pos.numpy(), n.numpy(), alb.numpy(), vp.numpy(), kr.numpy(), km.numpy(), base.numpy(), lut,
-                      gr.numpy(), np.zeros((N, 3), np.float32), np.zeros((N, 3), np.float32))
-    eb = np.linalg.norm(bleaf.grad.cpu().numpy() - d["base"]) / np.linalg.norm(d["base"])
-    assert eb < 1e-4, eb

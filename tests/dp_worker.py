@@ -79,3 +79,89 @@ def run(rank, world, port, out_path):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+# ---- multi-step densification statistics and rank-consistent densify_and_prune ----------
+
+N_STEPS, VIEWS_PER_RANK, P_STATS = 3, 2, 500
+
+
+def view_stats(step, view, P=P_STATS):
+    """A deterministic stand-in for one view's (dL/dmeans2D, radii)."""
+    g = torch.Generator().manual_seed(1000 * step + view)
+    grad = torch.randn(P, 3, generator=g)
+    radii = (torch.rand(P, generator=g) * 12).int() * (torch.rand(P, generator=g) > 0.3).int()
+    return grad, radii
+
+
+def stats_run(rank, world):
+    """N_STEPS steps; each rank renders views (step, rank*VIEWS_PER_RANK + j)."""
+    from gsr import dp
+    running = dict(xyz_gradient_accum=torch.zeros(P_STATS, 1), denom=torch.zeros(P_STATS, 1),
+                   max_radii2D=torch.zeros(P_STATS))
+    ss = dp.StepStats(P_STATS, "cpu")
+    for step in range(N_STEPS):
+        ss.zero()
+        for r in ([rank] if world > 1 else range(2)):
+            for j in range(VIEWS_PER_RANK):
+                ss.add_view(*view_stats(step, r * VIEWS_PER_RANK + j))
+        ss.commit(running, world=world)
+    return running
+
+
+def small_scene(seed=5, P_fg=400, P_sky=40):
+    from gsr.train import RelitScene
+    g = torch.Generator().manual_seed(seed)
+    P = P_fg + P_sky
+    xyz = torch.randn(P, 3, generator=g) + torch.tensor([0.0, 0.0, 5.0])
+    is_sky = torch.zeros(P, dtype=torch.bool)
+    is_sky[torch.randperm(P, generator=g)[:P_sky]] = True
+    xyz[is_sky] = 30.0 * torch.nn.functional.normalize(xyz[is_sky], dim=1)
+    scene = RelitScene(xyz, torch.randn(P, 3, generator=g) * 0.8 - 4.0, torch.randn(P, 4, generator=g),
+                       torch.randn(P, 1, generator=g) * 2.0, torch.randn(P_fg, 3, generator=g),
+                       torch.randn(P_fg, 1, generator=g), torch.randn(P_fg, 1, generator=g), is_sky, 2, "cpu")
+    # non-trivial Adam state, identical on every rank
+    scene.fp.exp_avg.copy_(torch.randn(scene.fp.n, generator=g) * 1e-3)
+    scene.fp.exp_avg_sq.copy_(torch.rand(scene.fp.n, generator=g) * 1e-6)
+    scene.fp.t = 7
+    return scene
+
+
+def densify_run(rank, world, seed=None):
+    """Per-rank stats for 2 steps (different views per rank), reduced per step, then
+    densify_and_prune with the shared generator.  Returns the scene."""
+    from gsr import densify, dp
+    scene = small_scene()
+    P = scene.P
+    ss = dp.StepStats(P, "cpu")
+    for step in range(2):
+        ss.zero()
+        for r in ([rank] if world > 1 else range(2)):
+            for j in range(VIEWS_PER_RANK):
+                g, radii = view_stats(step, r * VIEWS_PER_RANK + j, P)
+                ss.add_view(g * 0.02, radii)
+        ss.commit(scene.stats, world=world)
+    gen = dp.shared_generator("cpu") if seed is None else torch.Generator().manual_seed(seed)
+    densify.densify_and_prune(scene, max_grad=0.02, min_opacity=0.1, extent=2.0, max_screen_size=20,
+                              generator=gen)
+    return scene
+
+
+def run_densify(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsr import dp
+        running = stats_run(rank, world)
+        scene = densify_run(rank, world)
+        fp = scene.fp
+        sums = dp.replica_checksums([fp.flat, fp.exp_avg, fp.exp_avg_sq, scene.is_sky.float()])
+        if rank == 0:
+            out = {k: v.numpy() for k, v in running.items()}
+            out.update(checksums=np.array(sums), P=np.array(scene.P), flat=fp.flat.numpy(), m=fp.exp_avg.numpy(),
+                       v=fp.exp_avg_sq.numpy(), is_sky=scene.is_sky.numpy(), t=np.array(fp.t))
+            np.savez(out_path, **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

@@ -58,3 +58,35 @@ def test_view_parallel_step_matches_sequential(tmp_path):
     np.testing.assert_allclose(got["xyz_gradient_accum"], ref_stats["xyz_gradient_accum"].numpy(), rtol=1e-6,
                                atol=1e-9)
     assert ref_stats["denom"].max().item() >= 2  # views overlap: the sums are non-trivial
+
+
+def test_multi_step_stats_and_rank_consistent_densify(tmp_path):
+    """the running statistics must equal the sequential accumulation after
+    SEVERAL steps (each step's deltas are reduced, not the running totals).  Then one
+    densify_and_prune (gaussian_model.py:610-625) on both ranks from the shared generator:
+    P, parameters, Adam moments, step count and sky flags bit-identical on the ranks."""
+    out = str(tmp_path / "densify.npz")
+    mp.spawn(dp_worker.run_densify, args=(2, free_port(), out), nprocs=2, join=True)
+    got = np.load(out, allow_pickle=False)
+    ref = dp_worker.stats_run(0, 1)
+    assert np.array_equal(got["denom"], ref["denom"].numpy())
+    assert float(ref["denom"].max()) > dp_worker.N_STEPS  # several views per step, several steps
+    assert np.array_equal(got["max_radii2D"], ref["max_radii2D"].numpy())
+    np.testing.assert_allclose(got["xyz_gradient_accum"], ref["xyz_gradient_accum"].numpy(), rtol=1e-6, atol=1e-7)
+    sums = got["checksums"]
+    assert sums.shape[0] == 2 and np.array_equal(sums[0], sums[1]), sums
+    P0 = dp_worker.small_scene().P
+    assert int(got["P"]) != P0  # the surgery did something
+    assert int(got["t"]) == 7
+
+
+def test_densify_matches_sequential_with_same_seed():
+    """Single process: the same views' statistics and the same seed give the same scene as
+    the ranks (clone + split + prune all exercised)."""
+    a = dp_worker.densify_run(0, 1, seed=11)
+    b = dp_worker.densify_run(0, 1, seed=11)
+    assert a.P == b.P and torch.equal(a.fp.flat, b.fp.flat) and torch.equal(a.fp.exp_avg_sq, b.fp.exp_avg_sq)
+    base = dp_worker.small_scene()
+    assert a.P != base.P
+    # the Adam moments of appended rows are zero; kept rows carry theirs
+    assert a.fp.exp_avg.abs().sum() > 0

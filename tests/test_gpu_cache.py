@@ -103,3 +103,30 @@ def test_geometry_change_misses():
                               shs=torch.zeros(means3D.shape[0], 1, 3, device="cuda"), scales=g["scales"],
                               rotations=g["rotations"])
     assert cache.hits == hits
+
+
+def test_cache_is_keyed_on_the_stream():
+    """a hit reuses buffers ordered only on the miss call's stream, so the same
+    geometry rendered on another HIP stream must miss (and still be bit-identical)."""
+    dgr, g, settings = _setup(P=3000)
+    cache = dgr.geometry_cache(True)
+    s = settings((0.0, 0.0, 0.0))
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    c1 = torch.rand(g["means3D"].shape[0], 3, device="cuda", generator=gen)
+    call = lambda c: dgr.GaussianRasterizer(s)(means3D=g["means3D"], means2D=torch.zeros_like(g["means3D"]),
+                                               opacities=g["opacities"], colors_precomp=c, scales=g["scales"],
+                                               rotations=g["rotations"])[0]
+    a = call(c1)
+    m0, h0 = cache.misses, cache.hits
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        b = call(c1)
+    torch.cuda.current_stream().wait_stream(side)
+    assert cache.misses == m0 + 1 and cache.hits == h0
+    c = call(c1)  # back on the main stream: the side stream's entry is not reused either
+    assert cache.misses == m0 + 2
+    d = call(c1)  # same stream again: hit
+    assert cache.hits == h0 + 1
+    torch.cuda.synchronize()
+    assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)

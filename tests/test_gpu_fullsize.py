@@ -1,4 +1,7 @@
-"""GPU parity at BASELINE.json's full size (cfg2: 1.5M Gaussians, SH3, 1920x1080).
+"""GPU parity at BASELINE.json's full sizes: cfg2 (1.5M Gaussians, SH3, 1920x1080) and
+cfg5 (5M Gaussians, SH3, 3840x2160; preprocess bit-exactness and the sampled-tile forward
+and backward), plus cfg1 at exactly its size (10k Gaussians, 256x256, SH0) against the full
+oracle.
 
 The oracle cannot bin and render 28M instances in seconds, so the full-size checks are:
   * every per-Gaussian preprocess output bit-exact against the C oracle (all 1.5M);
@@ -23,12 +26,26 @@ pytestmark = pytest.mark.gpu
 TILE_SAMPLE = 32
 
 
-@pytest.fixture(scope="module")
-def cfg2():
+def _build(name):
     from gsr import scenes
-    cam, gs, c = scenes.build_config("cfg2", device="cpu", seed=0)
+    cam, gs, c = scenes.build_config(name, device="cpu", seed=0)
     st = run_gpu(cam, gs, mode="sh", sh_degree=c["sh_degree"])
     return cam, gs, c, st
+
+
+@pytest.fixture(scope="module")
+def cfg2():
+    return _build("cfg2")
+
+
+@pytest.fixture(scope="module", params=["cfg2", "cfg5"])
+def full(request, cfg2):
+    if request.param == "cfg2":
+        yield cfg2
+    else:
+        data = _build("cfg5")
+        yield data
+        del data
 
 
 def _grads(cam, gs, st, dout, deg):
@@ -38,15 +55,15 @@ def _grads(cam, gs, st, dout, deg):
                                            st["sh"], deg, st["cp"], st["geom"], st["R"], st["binb"], st["img"])
 
 
-def test_cfg2_preprocess_bit_exact(cfg2):
-    cam, gs, c, st = cfg2
+def test_full_preprocess_bit_exact(full):
+    cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     ref = orc.preprocess(np32(gs["means3D"]), np32(gs["scales"]), np32(gs["rotations"]),
                          np32(gs["opacities"]).reshape(-1), np32(gs["shs"]), None, None, np32(cam.world_view_transform),
                          np32(cam.full_proj_transform), np32(cam.camera_center), W, H, cam.tanfovx, cam.tanfovy, 1.0,
                          c["sh_degree"])
     vis = ref["radii"] > 0
-    assert vis.sum() > 1_000_000
+    assert vis.sum() > 0.66 * c["P"]
     np.testing.assert_array_equal(st["radii"].cpu().numpy(), ref["radii"])
     np.testing.assert_array_equal(st["tiles"], ref["tiles_touched"])
     rec = st["rec"]
@@ -106,8 +123,8 @@ def _tile_mask(tiles, gx, W, H):
     return m
 
 
-def test_cfg2_sampled_tiles_forward(cfg2):
-    cam, gs, c, st = cfg2
+def test_full_sampled_tiles_forward(full):
+    cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
     tiles = _sample_tiles(gx, gy)
@@ -116,13 +133,15 @@ def test_cfg2_sampled_tiles_forward(cfg2):
                                  np.zeros(3, np.float32), W, H, tiles=tiles)
     m = _tile_mask(tiles, gx, W, H)
     color = st["color"].cpu().numpy()
-    assert rel_l2(color[:, m], out[:, m]) <= 1e-4
-    assert (st["n_contrib"].reshape(H, W)[m] == nc.reshape(H, W)[m]).mean() > 0.999
-    assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-4
+    assert rel_l2(color[:, m], out[:, m]) <= 1e-6
+    # measured: no blend decision differs (tools/parity_margins.py, profiles/r2_parity_margins.log)
+    np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
+    assert np.abs(color[:, m] - out[:, m]).max() <= 1e-6
+    assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
 
 
-def test_cfg2_sampled_tiles_backward(cfg2):
-    cam, gs, c, st = cfg2
+def test_full_sampled_tiles_backward(full):
+    cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
     P = gs["means3D"].shape[0]
@@ -200,3 +219,75 @@ def test_large_frame_binning_exact(W, H, P):
     assert st["R"] == R and R > 500_000
     np.testing.assert_array_equal(st["point_list"].astype(np.int64), vals.astype(np.int64))
     np.testing.assert_array_equal(st["ranges"].astype(np.int64), ranges.astype(np.int64))
+
+
+def test_cfg1_exact_size_forward_backward():
+    """cfg1 at exactly its size (10k Gaussians, 256x256, SH0) against the full
+    oracle: the forward bars of test_gpu_rasterizer and all eight gradients."""
+    from test_gpu_rasterizer import check_forward, run_oracle
+    from diff_gaussian_rasterization import _C
+    from gsr import scenes
+    cam, gs, c = scenes.build_config("cfg1", device="cpu", seed=0)
+    assert gs["means3D"].shape[0] == 10_000 and (cam.image_width, cam.image_height) == (256, 256)
+    st = run_gpu(cam, gs, mode="sh", sh_degree=0)
+    ref = run_oracle(cam, gs, mode="sh", sh_degree=0)
+    check_forward(st, ref, 256, 256)
+    dout = torch.randn(3, 256, 256, generator=torch.Generator().manual_seed(1))
+    g = _C.rasterize_gaussians_backward(st["bg"], st["means"], st["radii"], st["colors"], st["scales"], st["rots"],
+                                        1.0, st["cov3"], st["vm"], st["pm"], cam.tanfovx, cam.tanfovy, dout.cuda(),
+                                        st["sh"], 0, st["cp"], st["geom"], st["R"], st["binb"], st["img"])
+    gref = orc.backward(ref, np.zeros(3, np.float32), np32(gs["means3D"]), None, np32(gs["scales"]),
+                        np32(gs["rotations"]), 1.0, None, np32(cam.world_view_transform),
+                        np32(cam.full_proj_transform), cam.tanfovx, cam.tanfovy, dout.numpy(), np32(gs["shs"]), 0,
+                        np32(cam.camera_center))
+    names = ["dL_dmean2D", "dL_dcolors", "dL_dopacity", "dL_dmeans3D", "dL_dcov3D", "dL_dsh", "dL_dscales",
+             "dL_drotations"]
+    for n, mine in zip(names, g):
+        r = gref[n]
+        if r.size == 0 or np.abs(r).max() == 0:
+            continue
+        assert rel_l2(mine.detach().cpu().numpy().reshape(r.shape), r) <= 1e-4, n
+
+
+def test_cfg5_relit_render_fused_matches_calls():
+    """cfg5's relight render with backward at 3840x2160 (400k foreground + 40k sky
+    Gaussians): the fused gsr.relit.render (14-channel composite at 4K) against render()'s
+    own call sequence on the drop-in rasterizer, every image and every parameter gradient."""
+    import types
+    import relit_shade
+    from gsr import relit, train
+    scene, views, _ = train.synthetic_relit_scene(400_000, 1, 3840, 2160, 2800.0, "cuda", seed=2)
+    view = views[0]
+    pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+
+    def run(fn):
+        scene.fp.zero_grad()
+        pc = scene.model()
+        light = relit_shade.EnvironmentLight(scene.fp.params["env_sh"][0], sh_degree=4)
+        out = fn(view, pc, light, scene.fp.params["sky_sh"][0:1], 1, pipe, bg, debug=False)
+        keys = sorted(k for k in out if k not in ("viewspace_points", "visibility_filter", "radii"))
+        gen = torch.Generator(device="cuda").manual_seed(6)
+        loss = sum((out[k] * torch.randn(out[k].shape, device="cuda", generator=gen)).sum() for k in keys)
+        loss.backward()
+        return {k: out[k].detach() for k in keys}, out["radii"], scene.fp.grad.clone(), \
+            out["viewspace_points"].grad.clone()
+
+    o_f, r_f, g_f, m_f = run(relit.render)
+    o_r, r_r, g_r, m_r = run(relit.render_calls)
+    assert sorted(o_f) == sorted(o_r) and torch.equal(r_f, r_r)
+    for k in o_r:
+        e = float(torch.linalg.norm((o_f[k] - o_r[k]).double()) / torch.linalg.norm(o_r[k].double()))
+        # normal_ref is a cross product of one-pixel depth differences: at 4K those are ~1e-4
+        # of the depth, so float rounding of the back-projection (the epilogue kernel vs
+        # PyTorch's matrix form) is amplified ~1e4x (measured 4.3e-5)
+        assert e < (2e-4 if k == "normal_ref" else 1e-5), (k, e)
+    for name, off, shape in zip(scene.fp.names, scene.fp.offsets, scene.fp.shapes):
+        n = int(np.prod(shape))
+        a, b = g_f[off:off + n].double(), g_r[off:off + n].double()
+        if not b.any():
+            continue
+        e = float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
+        assert e < 1e-4, (name, e)
+    e = float(torch.linalg.norm((m_f - m_r).double()) / torch.linalg.norm(m_r.double()))
+    assert e < 1e-4, e

@@ -3,7 +3,8 @@ oracle on the same seeded inputs.
 
 Bar (BASELINE.json north_star): bit-exact on tile/key indexing -- radii, tiles_touched,
 screen means, conics, depth keys, num_rendered, the sorted instance list and the tile
-ranges -- and within 1e-4 relative on rendered RGB and on every gradient (relative L2
+ranges -- plus identical per-pixel n_contrib (every blend decision), RGB within 1e-6
+absolute of the oracle per value, and within 1e-4 relative on every gradient (relative L2
 over the tensor: the GPU sums gradients in a different order than the reference's
 atomics, so elementwise bits cannot match; the tolerance is tied to the tensor norm)."""
 import math
@@ -101,11 +102,13 @@ def check_forward(st, ref, W, H):
     color = st["color"].cpu().numpy()
     e = rel_l2(color, ref["color"])
     assert e <= RGB_TOL, f"rgb rel L2 {e:.3e}"
-    # borderline exp() decisions may flip a handful of pixels; everything else agrees to 1e-4
-    bad = np.abs(color - ref["color"]) > 1e-4 * max(1.0, np.abs(ref["color"]).max())
-    assert bad.mean() < 1e-3, f"{bad.sum()} rgb values off by > 1e-4"
-    nc_match = (st["n_contrib"] == ref["n_contrib"]).mean()
-    assert nc_match > 0.999, nc_match
+    # Measured on every case (tools/parity_margins.py, profiles/r2_parity_margins.log): no
+    # blend decision differs from the oracle's expf (n_contrib identical everywhere) and no
+    # value differs by more than 3e-7.  The bars are those maxima with a small margin.
+    np.testing.assert_array_equal(st["n_contrib"], ref["n_contrib"])
+    scale = max(1.0, float(np.abs(ref["color"]).max()))
+    assert np.abs(color - ref["color"]).max() <= 1e-6 * scale, np.abs(color - ref["color"]).max()
+    assert np.abs(st["final_T"] - ref["final_T"]).max() <= 1e-6
     return e
 
 
@@ -281,3 +284,81 @@ def test_bad_means_shape():
         _C.rasterize_gaussians(torch.zeros(3, device=dev), torch.zeros(10, 4, device=dev), e, e, e, e, 1.0, e,
                                torch.eye(4, device=dev), torch.eye(4, device=dev), 1.0, 1.0, 8, 8, e, 0,
                                torch.zeros(3, device=dev), False)
+
+
+@pytest.mark.parametrize("mode", ["colors_scales", "sh3_scales", "colors_cov3D"])
+def test_autograd_node_matches_oracle_node(mode):
+    """_RasterizeGaussians end to end against the same autograd node over the C oracle
+    (oracle/oracle_torch.py, the reference's __init__.py:17-195 surface): every leaf
+    gradient lands on the right input (means3D and means2D are both [P,3], so a swapped
+    order would not show in shapes), with the reference's call pattern (means2D zeros + 0
+    with retain_grad)."""
+    from oracle import oracle_torch
+    dgr, _, _ = _dgr()
+    sh_deg = 3 if mode.startswith("sh3") else 0
+    cam, gs = make_case(P=2500, W=80, H=64, sh_degree=sh_deg, camera="orbit")
+    P = gs["means3D"].shape[0]
+    g = torch.Generator().manual_seed(12)
+    dout = torch.randn(3, 64, 80, generator=g)
+    cov = None
+    if mode == "colors_cov3D":
+        cov = torch.from_numpy(orc.preprocess(np32(gs["means3D"]), np32(gs["scales"]), np32(gs["rotations"]),
+                                              np32(gs["opacities"]).reshape(-1), None, np.zeros((P, 3), np.float32),
+                                              None, np.eye(4, dtype=np.float32), np.eye(4, dtype=np.float32),
+                                              np.zeros(3, np.float32), 16, 16, 1.0, 1.0, 1.0)["cov3D"])
+
+    def run(mod, dev):
+        s = mod.GaussianRasterizationSettings(
+            image_height=64, image_width=80, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+            bg=torch.tensor([0.1, 0.2, 0.3], device=dev), scale_modifier=1.0,
+            viewmatrix=cam.world_view_transform.to(dev), projmatrix=cam.full_proj_transform.to(dev),
+            sh_degree=sh_deg if mode.startswith("sh3") else -1, campos=cam.camera_center.to(dev), prefiltered=False)
+        lv = {"means3D": gs["means3D"], "opacities": gs["opacities"]}
+        if mode.startswith("sh3"):
+            lv["shs"] = gs["shs"]
+        else:
+            lv["colors_precomp"] = gs["colors"]
+        if cov is None:
+            lv.update(scales=gs["scales"], rotations=gs["rotations"])
+        else:
+            lv["cov3D_precomp"] = cov
+        lv = {k: v.clone().to(dev).requires_grad_(True) for k, v in lv.items()}
+        means2D = torch.zeros_like(lv["means3D"], requires_grad=True) + 0
+        means2D.retain_grad()
+        img, radii = mod.GaussianRasterizer(s)(means2D=means2D, **lv)
+        (img * dout.to(dev)).sum().backward()
+        grads = {k: v.grad.detach().cpu().numpy() for k, v in lv.items()}
+        grads["means2D"] = means2D.grad.detach().cpu().numpy()
+        return img.detach().cpu().numpy(), radii.cpu().numpy(), grads
+
+    img, radii, grads = run(dgr, "cuda")
+    w_img, w_radii, w_grads = run(oracle_torch, "cpu")
+    assert np.array_equal(radii, w_radii)
+    assert rel_l2(img, w_img) <= RGB_TOL
+    assert sorted(grads) == sorted(w_grads)
+    errs = {k: rel_l2(grads[k], w_grads[k]) for k in grads}
+    assert all(e <= GRAD_TOL for e in errs.values()), errs
+
+
+@pytest.mark.parametrize("camera", ["identity", "orbit"])
+def test_mark_visible_matches_oracle(camera):
+    """markVisible (rasterizer_impl.cu:54-66, rasterize_points.cu:194-213): present =
+    (view * p).z > 0.2, bit-exact against orc_mark_visible on a cloud straddling the near
+    plane and points behind the camera."""
+    dgr, _C, _ = _dgr()
+    cam, gs = make_case(P=6000, W=64, H=64, camera=camera)
+    g = torch.Generator().manual_seed(5)
+    pts = gs["means3D"].clone()
+    pts[:2000, 2] = torch.rand(2000, generator=g) * 0.6 - 0.1  # around z = 0.2 (identity camera)
+    pts[2000:2500] *= -1.0
+    want = orc.mark_visible(np32(pts), np32(cam.world_view_transform))
+    s = dgr.GaussianRasterizationSettings(image_height=64, image_width=64, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+                                          bg=torch.zeros(3, device="cuda"), scale_modifier=1.0,
+                                          viewmatrix=cam.world_view_transform.cuda(),
+                                          projmatrix=cam.full_proj_transform.cuda(), sh_degree=0,
+                                          campos=cam.camera_center.cuda(), prefiltered=False)
+    got = dgr.GaussianRasterizer(s).markVisible(pts.cuda()).cpu().numpy()
+    assert got.dtype == bool and want.any() and not want.all()
+    np.testing.assert_array_equal(got, want)
+    got2 = _C.mark_visible(pts.cuda(), cam.world_view_transform.cuda(), cam.full_proj_transform.cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got2, want)

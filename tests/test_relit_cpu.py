@@ -68,3 +68,32 @@ def test_fg_index_cache_across_views():
     flags[0] = True  # in-place change (densification): version bump -> rebuilt
     rows2, rank2 = rs._fg_index(flags.squeeze(), 10, cpu)
     assert rows2.tolist() == list(range(1, 7)) and rank2.tolist() == [-1, 0, 1, 2, 3, 4, 5, -1, -1, -1]
+
+
+def test_depth_to_normal_matches_reference_fixture():
+    """gsr.relit.depth_to_normal against the reference's own depth_to_normal
+    (utils/graphics_utils.py:141-169) on the reference Camera of tests/golden/render.npz,
+    forward and depth gradient (tools/gen_golden_render.py)."""
+    import types
+    d = np.load(os.path.join(GOLD, "render.npz"), allow_pickle=False)
+    view = types.SimpleNamespace(world_view_transform=torch.from_numpy(d["world_view_transform"]),
+                                 image_width=int(d["W"]), image_height=int(d["H"]), FoVx=float(d["FoVx"]),
+                                 FoVy=float(d["FoVy"]))
+    depth = torch.from_numpy(d["d2n/depth"]).requires_grad_(True)
+    n = relit.depth_to_normal(view, depth)
+    np.testing.assert_allclose(n.detach().numpy(), d["d2n/normal"], rtol=0, atol=2e-5)
+    w = np.random.default_rng(1099).standard_normal(tuple(n.shape)).astype(np.float32)
+    (n * torch.from_numpy(w)).sum().backward()
+    g, want = depth.grad.numpy(), d["d2n/grad_depth"]
+    assert np.linalg.norm(g - want) / np.linalg.norm(want) < 1e-4
+
+
+def test_oracle_stub_reproduces_reference_render_fixture_shapes():
+    """The fixture's structure: render()'s key set for train (7 images) and debug (11)."""
+    d = np.load(os.path.join(GOLD, "render.npz"), allow_pickle=False)
+    base = ["alpha", "depth", "diffuse_color", "normal", "normal_ref", "render", "specular_color"]
+    assert [str(k) for k in d["black/keys"]] == base
+    assert [str(k) for k in d["white_debug/keys"]] == sorted(base + ["albedo", "metalness", "roughness", "sky_color"])
+    H, W = int(d["H"]), int(d["W"])
+    for k in base:
+        assert d[f"black/out/{k}"].shape == (3, H, W), k
