@@ -2,20 +2,22 @@
 """bench.py -- MPix/s fwd+bwd of the MI355X rasterizer on BASELINE.json's headline config.
 
 Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): 1.5M synthetic Gaussians, SH degree 3,
-1920x1080.  A step is one mini-batch of 4 views (cfg4's per-GPU mini-batch), each one
-rasterizer forward + backward through the drop-in diff_gaussian_rasterization._C (libgsr.so,
-hand-written gfx950 HIP); the views alternate over 3 HIP streams.  With --gpus N > 1 (one
-process per GPU, launched by torch.distributed.run) every rank renders its own views of its
-own scene shard-seed (weak scaling: view-parallel data parallelism) and the
-per-Gaussian gradients of the step are summed over ranks with one RCCL all-reduce.
-`single_view` reports one view at a time on one stream beside it.
+1920x1080.  A step is one view per GPU at N = 1: one rasterizer forward + backward through the
+drop-in diff_gaussian_rasterization._C (libgsr.so, hand-written gfx950 HIP) -- the reference's
+call pair, inputs resident in HBM.  With --gpus N > 1 (one process per GPU, launched by
+torch.distributed.run) every rank holds the same replicated scene and renders 4 distinct
+views per step (cfg4's per-GPU mini-batch), and the per-Gaussian gradients of the step are
+summed over ranks with one RCCL all-reduce (weak scaling: view-parallel data parallelism,
+SURVEY §8e).
 
-Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * 4 * W * H / step time (max over
-ranks).  roofline: the dominant kernel (stage) by HIP-event time inside the timed region, with
-its algorithmic bytes per launch / its average duration.  cpu_baseline: the C
-oracle (oracle/, a scalar port of the reference algorithm) timed on this host on a bounded
-sample (full preprocess + binning + preprocess backward, render fwd+bwd on 64 random tiles,
-extrapolated by tile count).
+Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * V * W * H / step time (max over
+ranks).  Beside it: `single_call` = SURVEY §8d's definition (median of 50 call pairs, HIP
+events), `minibatch_4view` = 4 distinct cameras on 3 HIP streams (throughput).  roofline: the
+dominant kernel by HIP-event time inside the timed region -- the tile passes are VALU-issue
+bound, so for them `bound` is "valu" (PMC instruction count / live launch time against the
+spec issue rate) with the HBM view (SURVEY §8d algorithmic bytes, PMC traffic) under
+`roofline.hbm`.  cpu_baseline: the naive PyTorch-CPU rasterizer (oracle/torch_raster.py) on
+this host's cores (count stated), cfg2 sampled + extrapolated and cfg1's forward in full.
 """
 import argparse
 import json
@@ -51,7 +53,10 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "ren
                 "preprocess_bwd": "k_preprocess_bwd"}
 
 
-VALU_NS_PER_INST = 1.16  # wave64 v_fma_f32 issue cost per SIMD at 8 waves/SIMD (tools/micro/pk_fma.hip, vops.hip)
+# spec VALU issue rate: a wave64 VALU instruction issues over 2 cycles on a SIMD-32, 2.4 GHz
+# (MI355X_MICROARCH.md "Execution model"); 1024 SIMDs -> 1228.8 G wave-instructions/s
+VALU_CLOCK_GHZ = 2.4
+VALU_CYCLES_PER_INST = 2
 
 
 def _pmc_record(stage, workload):
@@ -89,38 +94,60 @@ def unique_bytes(stage, P, Pv, R, T, Npix, M):
             "render_bwd": T * 8 + R * 4 + Pv * 48 + Npix * 20 + Pv * 44}.get(stage)
 
 
-def cpu_baseline(cam, gs_cpu, M, deg, dout_np, ntiles=64, seed=2):
-    from oracle import oracle as orc
-    n = lambda t: t.detach().cpu().numpy().astype(np.float32)
-    W, H = cam.image_width, cam.image_height
-    bg = np.zeros(3, np.float32)
-    t0 = time.perf_counter()
-    geom = orc.preprocess(n(gs_cpu["means3D"]), n(gs_cpu["scales"]), n(gs_cpu["rotations"]),
-                          n(gs_cpu["opacities"]).reshape(-1), n(gs_cpu["shs"]), None, None, n(cam.world_view_transform),
-                          n(cam.full_proj_transform), n(cam.camera_center), W, H, cam.tanfovx, cam.tanfovy, 1.0, deg)
-    R, keys, vals, ranges = orc.binning(geom, W, H)
-    t1 = time.perf_counter()
-    gx, gy = (W + 15) // 16, (H + 15) // 16
-    T = gx * gy
-    tiles = np.random.default_rng(seed).choice(T, size=min(ntiles, T), replace=False).astype(np.int32)
-    t2 = time.perf_counter()
-    color, fT, nc = orc.render_fwd(ranges, vals, geom["means2D"], geom["rgb"], geom["conic_opacity"], bg, W, H,
-                                   tiles=tiles)
-    g = orc.render_bwd(geom["radii"].shape[0], ranges, vals, bg, geom["means2D"], geom["conic_opacity"], geom["rgb"],
-                       fT, nc, dout_np, W, H, tiles=tiles)
-    t3 = time.perf_counter()
-    fwd = dict(geom)
-    fwd["cov3D_used"] = geom["cov3D"]
-    orc.preprocess_bwd(fwd, n(gs_cpu["means3D"]), n(gs_cpu["shs"]), deg, n(gs_cpu["scales"]), n(gs_cpu["rotations"]),
-                       1.0, n(cam.world_view_transform), n(cam.full_proj_transform), W, H, cam.tanfovx, cam.tanfovy,
-                       n(cam.camera_center), g["dL_dmean2D"], g["dL_dconic"], g["dL_dcolors"])
-    t4 = time.perf_counter()
-    est = (t1 - t0) + (t3 - t2) * T / len(tiles) + (t4 - t3)
-    return dict(value=W * H / est / 1e6, unit="MPix/s", cores=1, kind="port",
-                sample=(f"cfg2 ({gs_cpu['means3D'].shape[0]} Gaussians, {W}x{H}, SH{deg}): full preprocess + binning "
-                        f"(R={R}) + preprocess backward, render fwd+bwd on {len(tiles)}/{T} random tiles (seed {seed}) "
-                        f"extrapolated by tile count; single-threaded C oracle; measured {t4 - t0:.1f} s"),
-                seconds_estimated_full=est)
+def cpu_baseline(cam, gs_cpu, deg, dout_cpu, ntiles=64, seed=2, cfg1=True):
+    """The north star's naive PyTorch-CPU rasterizer (oracle/torch_raster.py, checked against
+    the C oracle by tests/test_torch_raster_cpu.py) on this host's cores.  cfg2: the full
+    preprocess and binning of all P Gaussians, render forward + backward on `ntiles` random
+    tiles (seed 2) extrapolated by tile count, and the full preprocess backward (autograd).
+    cfg1 (10k Gaussians, 256x256, SH0): the whole forward, timed in full."""
+    from gsr import scenes
+    from oracle import torch_raster as tr
+    threads = tr.host_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        W, H = cam.image_width, cam.image_height
+        bg = torch.zeros(3)
+        t0 = time.perf_counter()
+        leaves = [gs_cpu["means3D"].clone().requires_grad_(True), gs_cpu["scales"].clone().requires_grad_(True),
+                  gs_cpu["rotations"].clone().requires_grad_(True), gs_cpu["shs"].clone().requires_grad_(True)]
+        pre = tr.preprocess(leaves[0], leaves[1], leaves[2], gs_cpu["opacities"], leaves[3], deg,
+                            cam.world_view_transform.cpu(), cam.full_proj_transform.cpu(), cam.camera_center.cpu(), W,
+                            H, cam.tanfovx, cam.tanfovy)
+        with torch.no_grad():
+            pl, ranges = tr.binning(pre, W, H)
+        t1 = time.perf_counter()
+        T = ranges.shape[0]
+        tiles = tr.sample_tiles(T, ntiles, seed)
+        xy, con, rgb = pre["xy"], pre["conic"].detach(), pre["rgb"].detach()
+        with torch.no_grad():
+            color, fT, nc, _ = tr.render_fwd(tiles, ranges, pl, xy, con, pre["opacity"], rgb, bg, W, H)
+            t2 = time.perf_counter()
+            rb = tr.render_bwd(gs_cpu["means3D"].shape[0], tiles, ranges, pl, xy, con, pre["opacity"], rgb, bg, fT, nc,
+                               tr.from_image(dout_cpu, tiles, W, H), W, H)
+        t3 = time.perf_counter()
+        tr.preprocess_bwd(pre, leaves, rb["dL_dmean2D"], rb["dL_dconic"], rb["dL_dcolors"])
+        t4 = time.perf_counter()
+        est = (t1 - t0) + (t3 - t1) * T / len(tiles) + (t4 - t3)
+        out = dict(value=W * H / est / 1e6, unit="MPix/s", cores=threads, kind="port",
+                   sample=(f"cfg2 ({gs_cpu['means3D'].shape[0]} Gaussians, {W}x{H}, SH{deg}): naive PyTorch-CPU "
+                           f"rasterizer (oracle/torch_raster.py) on {threads} threads; full preprocess + binning "
+                           f"(R={pl.numel()}, {t1 - t0:.2f} s) and preprocess backward ({t4 - t3:.2f} s), render "
+                           f"fwd+bwd on {len(tiles)}/{T} random tiles (seed {seed}, {t3 - t1:.2f} s) extrapolated "
+                           f"by tile count; estimated {est:.1f} s per fwd+bwd"),
+                   seconds_per_fwd_bwd_estimated=round(est, 3))
+        if cfg1:
+            c1cam, c1gs, _ = scenes.build_config("cfg1", device="cpu", seed=0)
+            tc0 = time.perf_counter()
+            tr.rasterize(c1gs["means3D"], c1gs["scales"], c1gs["rotations"], c1gs["opacities"], c1gs["shs"], 0,
+                         c1cam.world_view_transform, c1cam.full_proj_transform, c1cam.camera_center, 256, 256,
+                         c1cam.tanfovx, c1cam.tanfovy, torch.zeros(3))
+            tc = time.perf_counter() - tc0
+            out["cfg1_forward"] = {"seconds": round(tc, 4), "mpix_per_s": round(256 * 256 / tc / 1e6, 4),
+                                   "what": "cfg1 (10k Gaussians, 256x256, SH0) whole forward, timed in full"}
+        return out
+    finally:
+        torch.set_num_threads(prev)
 
 
 class _RelitModel:
@@ -337,11 +364,13 @@ def main():
                                                   "default resolution rule")
     ap.add_argument("--view", type=int, default=0)
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
-    ap.add_argument("--views-per-step", "--views-per-sync", dest="views_per_step", type=int, default=4,
-                    help="views per step (the per-GPU mini-batch; N > 1: one gradient all-reduce per step)")
+    ap.add_argument("--views-per-step", "--views-per-sync", dest="views_per_step", type=int, default=None,
+                    help="views per step per GPU (default 1 at N = 1, 4 at N > 1: the per-GPU mini-batch whose "
+                         "gradients cross the ranks in one all-reduce)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="HIP streams the views of a step (cfg2, default 3) or a training iteration (cfg4, "
+                    help="HIP streams the views of a step (cfg2, default 1) or a training iteration (cfg4, "
                          "default 2) alternate over")
+    ap.add_argument("--no-minibatch", action="store_true", help="skip the 4-view multi-stream extra leg")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     args = ap.parse_args()
 
@@ -383,46 +412,52 @@ def main():
             cam = gcm.render_camera(train[args.view % len(train)])
             cfg = dict(cfg, W=cam.image_width, H=cam.image_height)
     else:
-        cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=rank, P=args.P)
+        # one scene replicated on every rank (the data-parallel replica); the ranks differ in views
+        cam, gs_cpu, cfg = scenes.build_config(args.config, device="cpu", seed=0, P=args.P)
     W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
     P = gs_cpu["means3D"].shape[0]
     g = {k: v.to(dev) for k, v in gs_cpu.items()}
     M = g["shs"].shape[1]
     e = torch.empty(0, device=dev)
     bg = torch.zeros(3, device=dev)
-    vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
     gen = torch.Generator().manual_seed(1)
     dout_cpu = torch.randn(3, H, W, generator=gen)
     dout = dout_cpu.to(dev)
-    V = max(1, args.views_per_step)
-    NS = max(1, min(3 if args.streams is None else args.streams, V))
+    # V views per step per rank (default 1 at N = 1: the reference's one call pair; 4 at N > 1:
+    # cfg4's per-GPU mini-batch, whose gradients accumulate into one bucket and cross the ranks
+    # in ONE RCCL all-reduce).  Rank r renders global views r*V .. r*V+V-1 of the scene.
+    V = max(1, args.views_per_step if args.views_per_step is not None else (1 if world == 1 else 4))
+    NS = max(1, min(1 if args.streams is None else args.streams, V))
+    cams = [scenes.view_camera(cam, rank * V + k).to(dev) for k in range(V)]
+    mats = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in cams]
     main_s = torch.cuda.current_stream(dev)
     vstreams = [main_s] if NS == 1 else [torch.cuda.Stream(dev) for _ in range(NS)]
     state = {}
 
-    def view():
+    def view(k=0):
         """One rasterizer forward + backward through the drop-in _C (the reference's call pair)."""
+        vm, pm, cp = mats[k]
         R, color, radii, geom, binb, img = _C.rasterize_gaussians(
             bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx,
             cam.tanfovy, H, W, g["shs"], deg, cp, False)
         grads = _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm,
                                                 pm, cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb,
                                                 img)
-        state["R"], state["radii"] = R, radii
+        if k == 0:
+            state["R"], state["radii"] = R, radii
         return grads
 
     def step():
-        """One mini-batch of V independent views (cfg4's per-GPU mini-batch), alternating over NS
-        HIP streams so that one view's latency-bound geometry passes overlap another's tile
-        passes.  At N > 1 the views' dL/d(means3D, sh, opacity, scales, rotations) are summed
-        into one flat bucket on the main stream and over the ranks with one RCCL all-reduce."""
+        """V views, one after another (or alternating over NS HIP streams with --streams).  At
+        N > 1 the views' dL/d(means3D, sh, opacity, scales, rotations) are summed into one flat
+        bucket on the main stream and over the ranks with one RCCL all-reduce."""
         for s in vstreams:
             if s is not main_s:
-                s.wait_stream(main_s)  # the previous mini-batch's exchange comes first
+                s.wait_stream(main_s)  # the previous step's exchange comes first
         for i in range(V):
             s = vstreams[i % NS]
             with torch.cuda.stream(s):
-                grads = view()
+                grads = view(i)
             if dist is not None:
                 ts = [grads[3], grads[5], grads[2], grads[6], grads[7]]
                 if s is not main_s:
@@ -466,12 +501,14 @@ def main():
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
+    torch.cuda.synchronize()
     t1 = time.perf_counter()
     _lib.profile_enable(False)
     live = _lib.profile_read(reset=True).get(dom_name, (0.0, 0))
@@ -496,77 +533,124 @@ def main():
     Pv = int((state["radii"] > 0).sum().item())
     T = ((W + 15) // 16) * ((H + 15) // 16)
     per_stage = {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1] > 0}
-    # the dominant stage's average launch time, from its events over the timed region
     dom = (dom_name, live[0] / max(live[1], 1))
-    single = None
-    if world == 1 and (V > 1 or NS > 1):
-        # the reference's call pattern for comparison: one view at a time on one stream
-        for _ in range(3):
-            view()
-        torch.cuda.synchronize()
-        ts0 = time.perf_counter()
+
+    single = mini = None
+    if rank == 0 and world == 1:
+        # SURVEY §8d's definition: W*H / (t_fwd + t_bwd) of ONE call, the median of >= 50 calls
+        # after 10 warm-up, HIP events on the stream the calls run on
         for _ in range(10):
             view()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
+        for a, b in evs:
+            a.record()
+            view()
+            b.record()
         torch.cuda.synchronize()
-        sv = (time.perf_counter() - ts0) * 1e3 / 10
-        single = {"ms_per_view": round(sv, 4), "value": round(W * H / (sv * 1e-3) / 1e6, 3), "unit": "MPix/s",
-                  "what": "one view at a time on one stream (the reference's call pattern)"}
+        t_ms = sorted(a.elapsed_time(b) for a, b in evs)
+        med = t_ms[len(t_ms) // 2]
+        single = {"median_ms": round(med, 4), "p10_ms": round(t_ms[5], 4), "p90_ms": round(t_ms[45], 4),
+                  "calls": len(t_ms), "value": round(W * H / (med * 1e-3) / 1e6, 3), "unit": "MPix/s",
+                  "what": "one rasterizer forward + backward call pair, median of 50 (HIP events, 10 warm-up)"}
+        if not args.no_minibatch:
+            # a 4-view mini-batch of DISTINCT cameras on 3 HIP streams: one view's latency-bound
+            # geometry passes overlap another's tile passes (throughput, not the reference's pattern)
+            mcams = [scenes.view_camera(cam, k).to(dev) for k in range(4)]
+            mm = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in mcams]
+            ss = [torch.cuda.Stream(dev) for _ in range(3)]
+            saved = list(mats)
+            mats[:] = mm + mats[len(mm):] if len(mats) >= len(mm) else mm
+
+            def mstep():
+                for s_ in ss:
+                    s_.wait_stream(main_s)
+                for i in range(4):
+                    with torch.cuda.stream(ss[i % 3]):
+                        view(i)
+                for s_ in ss:
+                    main_s.wait_stream(s_)
+
+            for _ in range(3):
+                mstep()
+            torch.cuda.synchronize()
+            tm = time.perf_counter()
+            nm = max(5, min(args.steps, 20))
+            for _ in range(nm):
+                mstep()
+            torch.cuda.synchronize()
+            mms = (time.perf_counter() - tm) * 1e3 / nm
+            mats[:] = saved
+            mini = {"ms_per_4_views": round(mms, 4), "value": round(4 * W * H / (mms * 1e-3) / 1e6, 3),
+                    "unit": "MPix/s", "what": "4 distinct cameras of the same scene per step, alternating over 3 "
+                                              "HIP streams"}
     dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
-    achieved = dom_bytes / (dom[1] * 1e-3) / 1e9
+    achieved_gbs = dom_bytes / (dom[1] * 1e-3) / 1e9
     workload = (f"ply {os.path.basename(args.ply)}" if args.ply else args.config) + f": {P} Gaussians SH{deg}, {W}x{H}"
     traffic, traffic_src = pmc_traffic(dom[0], workload)
-    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 5),
-                "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src,
-                "kernel": dom[0],
-                "algorithmic_bytes_per_launch": int(dom_bytes), "avg_launch_ms": round(dom[1], 4)}
+    hbm = {"achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes": "algorithmic (SURVEY §8d per-stage figure x "
+                                                                   "this launch's measured P, P_v, R)",
+           "algorithmic_bytes_per_launch": int(dom_bytes),
+           "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src}
     ub = unique_bytes(dom[0], P, Pv, R, T, W * H, M)
     if ub is not None:
-        roofline["unique_bytes_per_launch"] = int(ub)
-        roofline["unique_frac"] = round(ub / (dom[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+        hbm["unique_bytes_per_launch"] = int(ub)
+        hbm["unique_frac"] = round(ub / (dom[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
     kinfo, ksrc = pmc_kernel(dom[0], workload)
-    if kinfo.get("valu_insts"):
-        # the tile passes are VALU-issue-bound: instruction throughput against the measured
-        # wave64 VALU issue rate of the chip
+    if kinfo.get("valu_insts") and dom[0].startswith("render"):
+        # The tile passes are bound by VALU issue (the PMC counters show their HBM traffic at
+        # ~0.3x the algorithmic bytes): instruction throughput against the spec issue rate,
+        # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md).
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        peak = n_simd / (VALU_NS_PER_INST * 1e-9) / 1e9
+        peak = n_simd * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST
         ach = kinfo["valu_insts"] / (dom[1] * 1e-3) / 1e9
-        roofline["valu"] = {"insts_per_launch": int(kinfo["valu_insts"]), "achieved_ginst_s": round(ach, 1),
-                            "peak_ginst_s": round(peak, 1), "frac": round(ach / peak, 4), "source": ksrc,
-                            "peak_basis": f"{n_simd} SIMDs x 1 wave64 v_fma_f32 per {VALU_NS_PER_INST} ns"}
+        roofline = {"bound": "valu", "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "Gwave-inst/s",
+                    "frac": round(ach / peak, 4), "traffic": hbm["traffic"], "kernel": dom[0],
+                    "avg_launch_ms": round(dom[1], 4), "valu_insts_per_launch": int(kinfo["valu_insts"]),
+                    "valu_source": ksrc,
+                    "peak_basis": f"{n_simd} SIMDs x {VALU_CLOCK_GHZ} GHz / {VALU_CYCLES_PER_INST} cycles per "
+                                  "wave64 VALU instruction (spec issue rate)",
+                    "hbm": hbm}
+    else:
+        roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": hbm["traffic"], "kernel": dom[0],
+                    "avg_launch_ms": round(dom[1], 4), "hbm": hbm}
     out = {
         "metric": METRIC, "value": round(world * V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
                                                                        else "") if args.ply else args.config)
-                               + f": {P} Gaussians SH{deg}, {W}x{H}, rasterizer fwd+bwd per view, {V} views per "
-                                 f"step on {NS} HIP streams"
-                   + (", one RCCL grad all-reduce per step" if world > 1 else ""), "gaussians": P, "width": W,
-                   "height": H, "sh_degree": deg, "num_rendered": R, "visible": Pv, "views_per_step": V,
-                   "streams": NS, "parallelism": f"views x{world}"},
+                               + f": {P} Gaussians SH{deg}, {W}x{H}, one rasterizer forward + backward per view, "
+                                 f"{V} view(s) per step per GPU"
+                               + (f" on {NS} HIP streams" if NS > 1 else "")
+                               + (", scene replicated on every rank, distinct cameras per rank, one RCCL grad "
+                                  "all-reduce per step" if world > 1 else ""),
+                   "gaussians": P, "width": W, "height": H, "sh_degree": deg, "num_rendered": R, "visible": Pv,
+                   "views_per_step": V, "streams": NS, "parallelism": f"views x{world}"},
         "roofline": roofline,
         "stage_ms": per_stage,
         "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
                            "stage); roofline.avg_launch_ms is the dominant stage's events inside the timed region",
     }
     if single is not None:
-        out["single_view"] = single
+        out["single_call"] = single
+    if mini is not None:
+        out["minibatch_4view"] = mini
     if dist is not None:
         out["data_parallel"] = {"views_per_step": V, "grad_all_reduce_ms": round(ar_ms, 4),
                                 "grad_bucket_mb": round(state["bucket"].flat.numel() * 4 / 1e6, 2)}
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
-        ms_view = single["ms_per_view"] if single is not None else ms / V
+        ms_view = single["median_ms"] if single is not None else ms / V
+        vm, pm, cp = mats[0]
         out["gpu_reference_algorithm"] = refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_view)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(cam, gs_cpu, M, deg, dout_cpu.numpy(), ntiles=args.cpu_tiles)
-        out["cpu_baseline"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in cb.items()
-                               if k != "seconds_estimated_full"}
+        cb = cpu_baseline(cam, gs_cpu, deg, dout_cpu, ntiles=args.cpu_tiles)
+        out["cpu_baseline"] = {k: (round(v, 6) if isinstance(v, float) else v) for k, v in cb.items()}
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
-
 
 if __name__ == "__main__":
     main()

@@ -116,6 +116,21 @@ def look_at_rotation(cam_pos, target):
     return R, T
 
 
+def view_camera(cam, k):
+    """View k of a multi-view run over one scene: k = 0 is `cam` itself, k > 0 a
+    deterministic nearby camera (offset up to +-0.15 and looking at a point 10 units ahead,
+    jittered by +-0.2), same intrinsics.  Distinct views of the same Gaussians for the
+    mini-batch and data-parallel benchmarks."""
+    if k == 0:
+        return cam
+    rng = np.random.default_rng(100 + k)
+    pos = rng.uniform(-0.15, 0.15, 3)
+    target = np.array([rng.uniform(-0.2, 0.2), rng.uniform(-0.2, 0.2), 10.0])
+    R, T = look_at_rotation(pos, target)
+    return make_camera(cam.image_width, cam.image_height, cam.FoVx, cam.FoVy, R=R, T=T,
+                       device=cam.world_view_transform.device)
+
+
 def rgb2sh(rgb):
     return (rgb - 0.5) / SH_C0
 
