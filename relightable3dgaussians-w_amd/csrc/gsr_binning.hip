@@ -113,12 +113,29 @@ __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
 }
 
+// P_v summed from the preprocess's per-slot totals.  The forward launches the binning before
+// its one host synchronisation (the binning buffer is sized from the previous call's counts,
+// see gsr_capi.cpp), so these kernels read the visible count on the device.  Block-uniform.
+__device__ __forceinline__ int block_visible(int pv_host, const unsigned long long* totals) {
+    if (!totals) return pv_host;
+    static_assert(TOTAL_SLOTS == 128, "two slots per lane of one wave");
+    __shared__ uint32_t s_pv;
+    if (threadIdx.x < 64) {
+        uint32_t v = (uint32_t)totals[TOTAL_STRIDE * threadIdx.x] + (uint32_t)totals[TOTAL_STRIDE * (threadIdx.x + 64)];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (threadIdx.x == 0) s_pv = v;
+    }
+    __syncthreads();
+    return (int)s_pv;
+}
+
 template <int ST_W>
-__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const uint2* rect_sorted, unsigned gsx, int NS, int nb,
-                                                  uint32_t* table, uint32_t* wcounts) {
+__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const uint2* rect_sorted, unsigned gsx,
+                                                  int NS, int nb, uint32_t* table, uint32_t* wcounts) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
-    __syncthreads();
+    Pv = block_visible(Pv, totals);  // (its barrier also orders the zeroing)
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g0 = blk * ST_G;
@@ -173,7 +190,7 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 // deterministic, and each super-tile's entries come out in depth order.
 __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
                                         unsigned gsx, uint32_t* wcnt, unsigned long long* wmask,
-                                        uint32_t* st_keys, uint32_t* st_vals) {
+                                        uint32_t* st_keys, uint32_t* st_vals, uint32_t cap) {
     const int lane = threadIdx.x & 63;
     const unsigned long long bit = 1ull << lane, lt = bit - 1ull;
     // the next chunk's rect and id are loaded while this chunk is ranked
@@ -199,8 +216,10 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
                 const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
-                st_keys[pos] = sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS);
-                st_vals[pos] = gid;
+                if (pos < cap) {  // S beyond the speculative capacity: the forward redoes the binning
+                    st_keys[pos] = sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS);
+                    st_vals[pos] = gid;
+                }
             }
         lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
@@ -217,14 +236,16 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
 }
 
 template <int ST_W>
-__global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                                                     unsigned gsx, int NS, int nb, const uint32_t* table,
-                                                     const uint32_t* wcounts, const uint32_t* bases,
-                                                     uint32_t* st_keys, uint32_t* st_vals) {
+__global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
+                                                     const uint2* rect_sorted, unsigned gsx, int NS, int nb,
+                                                     const uint32_t* table, const uint32_t* wcounts,
+                                                     const uint32_t* bases, uint32_t* st_keys, uint32_t* st_vals,
+                                                     uint32_t cap) {
     extern __shared__ unsigned long long st_lds[];  // [ST_W][NS] lane masks, then [ST_W][NS] run counters
     unsigned long long* wmask_all = st_lds;
     uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + ST_W * NS);
     const int wave = threadIdx.x >> 6;
+    Pv = block_visible(Pv, totals);
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // as k_st_hist: runs of neighbours merge in L2
     const int g0 = blk * ST_G;
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
@@ -241,7 +262,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const uint32_t
     }
     __syncthreads();
     st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, st_keys,
-                  st_vals);
+                  st_vals, cap);
 }
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
@@ -254,8 +275,9 @@ size_t st_bin_temp_bytes(long long Pv, int NS) {
 // per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
 bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
-void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted, unsigned gsx, int NS, void* temp,
-                   uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s) {
+void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
+                   unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
+                   uint32_t cap, hipStream_t s) {
     if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
         (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
         return;
@@ -273,19 +295,19 @@ void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted,
     uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
     if (W == 8)
-        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, rect_sorted, gsx, NS, nb, table,
-                           wcounts);
+        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
+                           table, wcounts);
     else
-        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, rect_sorted, gsx, NS, nb, table,
-                           wcounts);
+        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
+                           table, wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
     hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
     if (W == 8)
-        hipLaunchKernelGGL(k_st_scatter<8>, dim3(nb), dim3(512), 12 * 8 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS,
-                           nb, table, wcounts, bases, st_keys, st_vals);
+        hipLaunchKernelGGL(k_st_scatter<8>, dim3(nb), dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
+                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap);
     else
-        hipLaunchKernelGGL(k_st_scatter<4>, dim3(nb), dim3(256), 12 * 4 * NS, s, Pv, sorted_ids, rect_sorted, gsx, NS,
-                           nb, table, wcounts, bases, st_keys, st_vals);
+        hipLaunchKernelGGL(k_st_scatter<4>, dim3(nb), dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
+                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
@@ -325,7 +347,8 @@ __device__ __forceinline__ StGeom st_geom(unsigned st, unsigned gsx, unsigned gx
 constexpr uint32_t SEG = 1024;
 
 __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_ranges, uint32_t* seg_st,
-                                                    uint32_t* seg_e0, uint32_t* st_seg0, uint32_t* nseg_total) {
+                                                    uint32_t* seg_e0, uint32_t* st_seg0, uint32_t* nseg_total,
+                                                    uint32_t gcap) {
     // single workgroup: exclusive scan of per-super-tile segment counts, then fill the table
     __shared__ uint32_t sh[4];
     uint32_t carry = 0;
@@ -341,7 +364,7 @@ __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_rang
         const uint32_t off = carry + block256_exclusive_scan(n, sh, &tot);
         if (st < nst) {
             st_seg0[st] = off;
-            for (uint32_t k = 0; k < n; k++) {
+            for (uint32_t k = 0; k < n && off + k < gcap; k++) {  // gcap: the table's capacity
                 seg_st[off + k] = (uint32_t)st;
                 seg_e0[off + k] = r.x + k * SEG;
             }
@@ -350,7 +373,7 @@ __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_rang
     }
     if (threadIdx.x == 0) {
         st_seg0[nst] = carry;
-        *nseg_total = carry;
+        *nseg_total = min(carry, gcap);
     }
 }
 
@@ -364,14 +387,16 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
                                                     const uint32_t* st_keys, const uint32_t* st_vals, unsigned gx,
                                                     unsigned gy, unsigned gsx, uint32_t* seg_cnt,
                                                     const uint32_t* seg_base, const uint32_t* tile_start,
-                                                    uint32_t* point_list) {
+                                                    uint32_t* point_list, uint32_t cap_s, uint32_t cap_r) {
     __shared__ uint32_t s_wc[4][ST_TILES];
     const uint32_t gseg = blockIdx.x;
     if (gseg >= *nseg_total) return;
     const unsigned st = seg_st[gseg];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const uint32_t e0 = seg_e0[gseg];
-    const uint32_t e1 = min(e0 + SEG, st_ranges[st].y);
+    // cap_s / cap_r: the entry and list capacities (exceeded only when the forward's
+    // speculative binning buffer was too small; it then redoes the binning)
+    const uint32_t e1 = min(min(e0 + SEG, st_ranges[st].y), cap_s);
     // lane t < 32: running output position of tile t (block-uniform across waves): the
     // segment's base within the tile's list + the tile's list start
     uint32_t run = 0;
@@ -412,7 +437,8 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
                 if ((mask >> t) & 1u) {
                     const uint32_t lo = (uint32_t)bal[t], hi = (uint32_t)(bal[t] >> 32);
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
-                    point_list[bcast(wbase, t) + r] = id;
+                    const uint32_t pos = bcast(wbase, t) + r;
+                    if (pos < cap_r) point_list[pos] = id;
                 }
             }
         }
@@ -425,14 +451,15 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
 // Per (super-tile, local tile): prefix of the segment counts -> segment-relative bases,
 // and the tile's total count.
 __global__ void __launch_bounds__(256) k_seg_prefix(int nst, const uint32_t* st_seg0, unsigned gx, unsigned gy,
-                                                     unsigned gsx, uint32_t* seg_cnt_to_base, uint32_t* tile_cnt) {
+                                                     unsigned gsx, uint32_t* seg_cnt_to_base, uint32_t* tile_cnt,
+                                                     uint32_t gcap) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nst * (int)ST_TILES) return;
     const unsigned st = i / ST_TILES, t = i % ST_TILES;
     const StGeom g = st_geom(st, gsx, gx, gy);
     const unsigned lx = t % GSR_ST_W, ly = t / GSR_ST_W;
     uint32_t run = 0;
-    for (uint32_t k = st_seg0[st]; k < st_seg0[st + 1]; k++) {
+    for (uint32_t k = st_seg0[st]; k < min(st_seg0[st + 1], gcap); k++) {
         const uint32_t c = seg_cnt_to_base[(size_t)k * ST_TILES + t];
         seg_cnt_to_base[(size_t)k * ST_TILES + t] = run;
         run += c;
@@ -523,7 +550,7 @@ size_t tile_lists_temp_bytes(long long S, int nst) {
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, hipStream_t s) {
+                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s) {
     const int T = (int)(gx * gy);
     const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
     uint32_t* seg_st = reinterpret_cast<uint32_t*>(temp);
@@ -531,23 +558,24 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
     uint32_t* st_seg0 = seg_e0 + G;
     uint32_t* nseg_total = st_seg0 + nst + 1;
     uint32_t* seg_cnt = nseg_total + 1;  // [G][32], becomes the segment bases in place
-    hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total);
+    hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total,
+                       (uint32_t)G);
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
                            st_ranges, st_keys, st_vals, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (uint32_t*)nullptr);
+                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t)S, (uint32_t)cap_r);
     }
     // k_seg_prefix writes every tile's count (the super-tiles partition the grid)
     const int np = nst * (int)ST_TILES;
     hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, st_seg0, gx, gy, gsx, seg_cnt,
-                       tile_cnt);
+                       tile_cnt, (uint32_t)G);
     (void)scan_tmp;
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, tile_nmax);
     launch_tile_order((unsigned)T, ranges, nullptr, order, nheavy, heavy_bits, s);
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
                            st_ranges, st_keys, st_vals, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, tile_start,
-                           point_list);
+                           point_list, (uint32_t)S, (uint32_t)cap_r);
     }
 }
 

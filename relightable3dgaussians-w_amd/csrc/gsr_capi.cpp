@@ -159,11 +159,20 @@ char* align_base(void* p) { return reinterpret_cast<char*>(align_up(reinterpret_
 
 struct PinnedHost {
     unsigned long long* p = nullptr;
+    hipEvent_t ev = nullptr;  // recorded after the totals' D2H copy
     ~PinnedHost() {
         if (p) (void)hipHostFree(p);
+        if (ev) (void)hipEventDestroy(ev);
     }
 };
 thread_local PinnedHost g_pinned;
+// the previous forward's counts on this thread: the next call with the same P and image
+// size sizes its binning buffer from them before the host synchronisation
+struct BinHint {
+    int P = -1, W = 0, H = 0;
+    long long R = 0, S = 0;
+};
+thread_local BinHint g_hint;
 
 #define HIP_OK(x)                                              \
     do {                                                       \
@@ -385,72 +394,111 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     }
     GSR_LAUNCH_CHECK();
 
+    // The forward's one host synchronisation (the reference's, rasterizer_impl.cu:281) reads
+    // P_v, R and S.  When an earlier call had the same P and image size, the binning buffer is
+    // sized from its counts with headroom and the binning is launched BEFORE the host waits:
+    // the kernels read P_v on the device and drop entries beyond the capacity, and the GPU
+    // keeps running while the host reads the totals (no idle gap between the depth sort and
+    // the binning).  A capacity overflow (rare: R grew by > 25 %) redoes the binning at the
+    // exact size.  Otherwise (first call, or images too large for the fused binning) the host
+    // waits first and sizes the buffer exactly.
     if (!g_pinned.p)
         HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * gsr::TOTALS_U64, hipHostMallocDefault));
+    if (!g_pinned.ev) HIP_OK(hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming));
     HIP_OK(hipMemcpyAsync(g_pinned.p, totals, totals_bytes, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
-    unsigned long long Pv = 0, R64 = 0, S64 = 0;
-    for (int k = 0; k < gsr::TOTAL_SLOTS; k++) {
-        Pv += g_pinned.p[gsr::TOTAL_STRIDE * k];
-        R64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 1];
-        S64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 2];
-    }
-    const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + gsr::TOTALS_U64 - 1)[0];
-    if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
-    const long long R = (long long)R64, S = (long long)S64;
-
-    const BinLayout bl = bin_layout(R, S, width, height, (long long)Pv);
-    char* bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
-    if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
-    bin = align_base(bin);
-
-    const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
+    HIP_OK(hipEventRecord(g_pinned.ev, s));
     const unsigned gsx = st_x(width), gsy = st_y(height);
     const int NS = (int)(gsx * gsy);
-    uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
-    uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
-    uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
-    const uint32_t* st_sorted_keys = stk;
-    const uint32_t* st_sorted_vals = stv;
-    if (gsr::st_bin_supported(NS)) {
-        GSR_STAGE(ST_DUPLICATE);
-        const uint2* rect_sorted = flip ? at<uint2>(geom, gl.rect_s_alt) : at<uint2>(geom, gl.rect_s);
-        gsr::launch_st_bin((int)Pv, sorted_ids, rect_sorted, gsx, NS, at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges,
-                           s);
-    } else {
-        uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
-        {
-            GSR_STAGE(ST_OFFSETS);
-            gsr::launch_exclusive_scan_u32((long long)Pv, pa.st_count, sorted_ids, offsets,
-                                           at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
+    const bool fused_bin = gsr::st_bin_supported(NS);
+    const bool speculate = fused_bin && g_hint.P == P && g_hint.W == width && g_hint.H == height;
+    unsigned long long Pv = 0, R64 = 0, S64 = 0;
+    auto read_totals = [&]() -> int {
+        HIP_OK(hipEventSynchronize(g_pinned.ev));
+        Pv = R64 = S64 = 0;
+        for (int k = 0; k < gsr::TOTAL_SLOTS; k++) {
+            Pv += g_pinned.p[gsr::TOTAL_STRIDE * k];
+            R64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 1];
+            S64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 2];
         }
-        {
-            GSR_STAGE(ST_DUPLICATE);
-            gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
-        }
-        int flip2;
-        {
-            GSR_STAGE(ST_TILE_SORT);
-            flip2 = gsr::radix_sort_pairs(S, stk, stv, at<uint32_t>(bin, bl.st_keys_alt),
-                                          at<uint32_t>(bin, bl.st_vals_alt), (int)higher_msb((uint32_t)NS),
-                                          at<void>(bin, bl.sort_tmp), s);
-        }
-        st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
-        st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
-        gsr::launch_seg_ranges(S, NS, st_sorted_keys, st_ranges, s);
-    }
-    GSR_LAUNCH_CHECK();
+        const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + gsr::TOTALS_U64 - 1)[0];
+        if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+        if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
+        return GSR_OK;
+    };
+    const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
+    const uint2* rect_sorted = flip ? at<uint2>(geom, gl.rect_s_alt) : at<uint2>(geom, gl.rect_s);
     uint2* ranges = at<uint2>(img, il.ranges);
-    uint32_t* point_list = at<uint32_t>(bin, bl.point);
-    {
-        GSR_STAGE(ST_RANGES);
-        gsr::launch_tile_lists(S, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx, at<uint32_t>(bin, bl.tile_cnt),
-                               at<uint32_t>(bin, bl.tile_start), ranges, at<uint32_t>(bin, bl.scan_tmp),
-                               at<void>(bin, bl.lists_tmp), point_list, at<uint32_t>(img, il.order_fwd),
-                               at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS, at<uint32_t>(img, il.tile_nmax), s);
+    char* bin = nullptr;
+    BinLayout bl{};
+    // binning into a buffer of capacity (capR, capS); dev: read P_v on the device
+    auto bin_pass = [&](long long capR, long long capS, bool dev) -> int {
+        bl = bin_layout(capR, capS, width, height, dev ? P : (long long)Pv);
+        bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
+        if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
+        bin = align_base(bin);
+        uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
+        uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
+        uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
+        const uint32_t* st_sorted_keys = stk;
+        const uint32_t* st_sorted_vals = stv;
+        if (fused_bin) {
+            GSR_STAGE(ST_DUPLICATE);
+            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? totals : nullptr, sorted_ids, rect_sorted, gsx, NS,
+                               at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, (uint32_t)capS, s);
+        } else {
+            uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
+            {
+                GSR_STAGE(ST_OFFSETS);
+                gsr::launch_exclusive_scan_u32((long long)Pv, pa.st_count, sorted_ids, offsets,
+                                               at<uint32_t>(geom, gl.scan_tmp), nullptr, s);
+            }
+            {
+                GSR_STAGE(ST_DUPLICATE);
+                gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
+            }
+            int flip2;
+            {
+                GSR_STAGE(ST_TILE_SORT);
+                flip2 = gsr::radix_sort_pairs(capS, stk, stv, at<uint32_t>(bin, bl.st_keys_alt),
+                                              at<uint32_t>(bin, bl.st_vals_alt), (int)higher_msb((uint32_t)NS),
+                                              at<void>(bin, bl.sort_tmp), s);
+            }
+            st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
+            st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
+            gsr::launch_seg_ranges(capS, NS, st_sorted_keys, st_ranges, s);
+        }
+        GSR_LAUNCH_CHECK();
+        {
+            GSR_STAGE(ST_RANGES);
+            gsr::launch_tile_lists(capS, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx,
+                                   at<uint32_t>(bin, bl.tile_cnt), at<uint32_t>(bin, bl.tile_start), ranges,
+                                   at<uint32_t>(bin, bl.scan_tmp), at<void>(bin, bl.lists_tmp),
+                                   at<uint32_t>(bin, bl.point), at<uint32_t>(img, il.order_fwd),
+                                   at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS, at<uint32_t>(img, il.tile_nmax),
+                                   capR, s);
+        }
+        GSR_LAUNCH_CHECK();
+        return GSR_OK;
+    };
+    int rc;
+    if (speculate) {
+        const long long capR = g_hint.R + g_hint.R / 4 + 65536, capS = g_hint.S + g_hint.S / 4 + 4096;
+        if ((rc = bin_pass(capR, capS, true)) != GSR_OK) return rc;
+        if ((rc = read_totals()) != GSR_OK) return rc;
+        if ((long long)R64 > capR || (long long)S64 > capS) {  // overflow: redo at the exact size
+            if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
+        }
+    } else {
+        if ((rc = read_totals()) != GSR_OK) return rc;
+        if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
     }
-    GSR_LAUNCH_CHECK();
+    const long long R = (long long)R64;
+    g_hint.P = P;
+    g_hint.W = width;
+    g_hint.H = height;
+    g_hint.R = R;
+    g_hint.S = (long long)S64;
+    uint32_t* point_list = at<uint32_t>(bin, bl.point);
 
     gsr::RenderFwdArgs ra;
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;

@@ -38,7 +38,9 @@ struct PreprocessArgs {
 };
 constexpr int TOTAL_SLOTS = 128;  // spread of the totals' atomics (one slot per 1/128 of the blocks)
 constexpr int TOTAL_STRIDE = 16;  // u64 per slot: one 128-B line each, so slots do not share an L2 line
-constexpr int TOTALS_U64 = TOTAL_SLOTS * TOTAL_STRIDE + 1;  // + the error flag
+// + one line holding the error flag (its last u64): 16.1 KiB, a multiple of 16 B, so the
+// zeroing is ONE fill dispatch (an odd tail costs rocclr a second ~5 us dispatch)
+constexpr int TOTALS_U64 = TOTAL_SLOTS * TOTAL_STRIDE + TOTAL_STRIDE;
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s);
@@ -89,8 +91,12 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 // rect_sorted: the rects already in depth order (the depth sort's side payload).
 size_t st_bin_temp_bytes(long long Pv, int NS);
 bool st_bin_supported(int NS);
-void launch_st_bin(int Pv, const uint32_t* sorted_ids, const uint2* rect_sorted, unsigned gsx, int NS, void* temp,
-                   uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges, hipStream_t s);
+// Pv: the visible count, or (with dev_totals non-null) its upper bound P, the kernels then
+// summing the preprocess's per-slot totals on the device.  Entries at positions >= cap are
+// not written (the speculative forward detects the overflow and redoes the binning).
+void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
+                   unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
+                   uint32_t cap, hipStream_t s);
 // In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
 // super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
@@ -102,12 +108,13 @@ constexpr uint32_t ST_KEY_MASK = (1u << ST_KEY_BITS) - 1u;
 // ranges[k] = [first, last+1) of key k in a sorted key array; (0, 0) for absent keys.
 void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s);
 // Per-super-tile tile filters over 1024-entry segments: tile counts, tile starts (scan),
-// ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).
+// ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).  S: the entry capacity (the
+// real count is read from st_ranges on the device); point_list entries >= cap_r are dropped.
 size_t tile_lists_temp_bytes(long long S, int nst);
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, hipStream_t s);
+                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s);
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of

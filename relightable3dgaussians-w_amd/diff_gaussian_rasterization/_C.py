@@ -21,8 +21,29 @@ from gsr import _lib  # noqa: E402
 NUM_CHANNELS = 3
 
 
+_SMALL = {}
+
+
 def _f32(t):
-    return t.contiguous() if t.dtype == torch.float32 else t.float().contiguous()
+    if t.dtype == torch.float32 and t.is_contiguous():
+        return t
+    if t.numel() <= 64:
+        # camera matrices arrive transposed (scene/cameras.py:77, world_view_transform is a
+        # .transpose(0, 1) view): their contiguous copy is cached per (storage, version,
+        # layout, stream), so the six render() calls and each backward do not each launch a copy
+        # kernel.  The cache holds the source, so its memory cannot be recycled into a false hit;
+        # the stream is part of the key, so a hit is ordered after the copy that made it.
+        stream = torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+        key = (t.data_ptr(), t._version, tuple(t.shape), t.stride(), t.dtype, str(t.device), stream)
+        hit = _SMALL.get(key)
+        if hit is not None:
+            return hit[1]
+        c = t.float().contiguous()
+        if len(_SMALL) >= 32:
+            _SMALL.pop(next(iter(_SMALL)))
+        _SMALL[key] = (t, c)
+        return c
+    return t.float().contiguous()
 
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,

@@ -362,3 +362,20 @@ def test_mark_visible_matches_oracle(camera):
     np.testing.assert_array_equal(got, want)
     got2 = _C.mark_visible(pts.cuda(), cam.world_view_transform.cuda(), cam.full_proj_transform.cuda()).cpu().numpy()
     np.testing.assert_array_equal(got2, want)
+
+
+def test_speculative_binning_capacity_and_overflow():
+    """The forward sizes its binning buffer from the previous call with the same P and image
+    size and launches the binning before the host synchronisation (gsr_capi.cpp).  A call
+    whose instance count exceeds that capacity (Gaussians 20x larger) must detect the
+    overflow and redo the binning; the next, small, call runs in the oversized buffer.  Every
+    call is checked against the oracle."""
+    cam, gs = make_case(P=3000, W=96, H=80, sh_degree=0, camera="orbit")
+    big = dict(gs, scales=gs["scales"] * 20.0)
+    Rs = []
+    for g in (gs, gs, big, gs, big):
+        st = run_gpu(cam, g, mode="colors")
+        ref = run_oracle(cam, g, mode="colors")
+        check_forward(st, ref, 96, 80)
+        Rs.append(st["R"])
+    assert Rs[2] > 2 * Rs[1] and Rs[0] == Rs[1] == Rs[3]
