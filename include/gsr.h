@@ -65,6 +65,7 @@ extern "C" {
 #define GSR_E_PREFILTERED (-3)
 #define GSR_E_ALLOC (-4)
 #define GSR_E_OVERFLOW (-5)
+#define GSR_E_DEVICE_CHECK (-6) /* a GSR_DEBUG invariant or the deterministic gather failed */
 
 /* Buffer growth callback: must return a device pointer to at least `nbytes` bytes that
  * stays valid until the matching backward call (the reference's resizeFunctional,
@@ -277,6 +278,25 @@ int gsr_profile_stages(unsigned mask);
 int gsr_profile_stage_count(void);
 const char* gsr_profile_stage_name(int i);
 int gsr_profile_read(double* ms, long long* counts, int n, int reset);
+
+/* Deterministic backward (default off, or GSR_DETERMINISTIC=1 in the
+ * environment): the tile passes write each (tile, Gaussian) pair's partial gradient sums to a
+ * per-instance row instead of adding them with float atomics (the reference's
+ * backward.cu:523,545-554 atomics are run-order dependent, and so are this library's), heavy
+ * tiles are not split, and one pass sums every Gaussian's rows in a fixed order (its tiles
+ * row-major).  Gradients are then bit-reproducible.  Costs a 48 B (3 channels) or
+ * 4*(6+nch) B row per instance of device scratch and a stream synchronisation per backward.
+ * Set it before the forward whose backward should be deterministic. */
+int gsr_set_deterministic(int on);
+int gsr_get_deterministic(void);
+/* 1 when this library was built with -DGSR_DEBUG (`make debug` -> lib/debug/libgsr.so): every
+ * forward then verifies its tile lists against the preprocess (ids, culling, rect coverage,
+ * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a
+ * stream synchronisation, and fails with GSR_E_DEVICE_CHECK naming the first violation. */
+int gsr_debug_build(void);
+/* The same verification on demand, over a forward's three buffers (any build; synchronous). */
+int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
+                      void* img_buffer, void* stream);
 
 const char* gsr_last_error(void);
 const char* gsr_version(void);

@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -174,6 +176,39 @@ struct BinHint {
 };
 thread_local BinHint g_hint;
 
+// Deterministic backward (gsr_set_deterministic / GSR_DETERMINISTIC=1): per-instance partial
+// rows summed in a fixed order (gsr_det.hip) instead of the tile passes' atomics.
+std::atomic<int> g_det{-1};
+bool det_on() {
+    int v = g_det.load();
+    if (v < 0) {
+        const char* e = getenv("GSR_DETERMINISTIC");
+        v = (e && e[0] && e[0] != '0') ? 1 : 0;
+        g_det.store(v);
+    }
+    return v != 0;
+}
+// grow-only device scratch of one thread (the deterministic rows, the debug checks); the
+// calls that use it synchronise their stream before returning, so it is free again
+struct Scratch {
+    void* p = nullptr;
+    size_t n = 0;
+    ~Scratch() {
+        if (p) (void)hipFree(p);
+    }
+    void* get(size_t bytes) {
+        if (bytes > n) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            n = 0;
+            if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+            n = bytes;
+        }
+        return p;
+    }
+};
+thread_local Scratch g_scratch;
+
 #define HIP_OK(x)                                              \
     do {                                                       \
         hipError_t _e = (x);                                   \
@@ -227,6 +262,34 @@ struct StageTimer {
 };
 #define GSR_STAGE(st) StageTimer _timer_##st(st, s)
 
+
+const char* debug_code_name(unsigned c) {
+    static const char* names[] = {"ok", "tile range outside [0, R)", "listed id >= P", "listed Gaussian is culled",
+                                  "tile outside the listed Gaussian's rect", "list not in (depth, index) order",
+                                  "Gaussian not listed exactly area(rect) times", "range lengths do not sum to R",
+                                  "n_contrib exceeds the tile's list"};
+    return c < sizeof(names) / sizeof(names[0]) ? names[c] : "unknown";
+}
+
+// GSR_DEBUG: verify the forward's tile lists and n_contrib (gsr_det.hip), synchronously
+int debug_check_forward(int P, long long R, unsigned gx, unsigned gy, int W, int H, const int* radii, const uint2* rect,
+                        const uint32_t* depth_key, const uint2* ranges, const uint32_t* point_list,
+                        const uint32_t* n_contrib, hipStream_t s) {
+    const size_t bytes = 256 + 4 * (size_t)P;
+    char* sc = reinterpret_cast<char*>(g_scratch.get(bytes));
+    if (!sc) return fail(GSR_E_ALLOC, "GSR_DEBUG: scratch allocation failed");
+    HIP_OK(hipMemsetAsync(sc, 0, bytes, s));
+    auto* rep = reinterpret_cast<gsr::DebugReport*>(sc);
+    gsr::launch_check_lists(P, R, gx, gy, W, H, radii, rect, depth_key, ranges, point_list, n_contrib,
+                            reinterpret_cast<uint32_t*>(sc + 256), reinterpret_cast<unsigned long long*>(sc + 64), rep, s);
+    GSR_LAUNCH_CHECK();
+    gsr::DebugReport h{};
+    HIP_OK(hipMemcpyAsync(&h, rep, sizeof(h), hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    if (h.code)
+        return fail(GSR_E_DEVICE_CHECK, "GSR_DEBUG check failed: %s (%u, %u, %u)", debug_code_name(h.code), h.a, h.b, h.c);
+    return GSR_OK;
+}
 }  // namespace
 
 namespace {
@@ -263,6 +326,37 @@ extern "C" {
 const char* gsr_last_error(void) { return g_err.c_str(); }
 
 const char* gsr_version(void) { return "gsr 0.1 gfx950"; }
+
+int gsr_set_deterministic(int on) {
+    g_det.store(on ? 1 : 0);
+    return GSR_OK;
+}
+
+int gsr_get_deterministic(void) { return det_on() ? 1 : 0; }
+
+int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
+                      void* img_buffer, void* stream_) {
+    if (P < 0 || R < 0 || width <= 0 || height <= 0 || !radii || !geom_buffer || !img_buffer || (R > 0 && !binning_buffer))
+        return fail(GSR_E_ARG, "gsr_check_buffers: bad arguments");
+    const GeomLayout gl = geom_layout(P);
+    const ImgLayout il = img_layout(width, height);
+    const BinLayout bl = bin_layout(R, 0, width, height, 0);
+    char* geom = align_base(geom_buffer);
+    char* img = align_base(img_buffer);
+    char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
+    return debug_check_forward(P, R, tiles_x(width), tiles_y(height), width, height, radii, at<uint2>(geom, gl.rect),
+                               at<uint32_t>(geom, gl.depth_key), at<uint2>(img, il.ranges),
+                               bin ? at<uint32_t>(bin, bl.point) : nullptr, at<uint32_t>(img, il.n_contrib),
+                               reinterpret_cast<hipStream_t>(stream_));
+}
+
+int gsr_debug_build(void) {
+#ifdef GSR_DEBUG
+    return 1;
+#else
+    return 0;
+#endif
+}
 
 int gsr_profile_enable(int on) {
     g_prof.on = on != 0;
@@ -526,6 +620,13 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         }
     }
     GSR_LAUNCH_CHECK();
+#ifdef GSR_DEBUG
+    {
+        const int rc_dbg = debug_check_forward(P, R, gx, gy, width, height, radii, pa.rect, pa.depth_key, ranges,
+                                               point_list, ra.n_contrib, s);
+        if (rc_dbg != GSR_OK) return rc_dbg;
+    }
+#endif
     if (num_rendered) *num_rendered = (int)R;
     return GSR_OK;
 }
@@ -600,6 +701,10 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
         gsr::launch_recolor(P, src_radii, reinterpret_cast<const gsr::Rec*>(src + gl.rec), colors_precomp,
                             at<gsr::Rec>(geom, gl.rec), radii, s);
     }
+    if (det_on()) {  // the deterministic backward's gather reads this call's rects and depth keys
+        HIP_OK(hipMemcpyAsync(geom + gl.depth_key, src + gl.depth_key, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
+        HIP_OK(hipMemcpyAsync(geom + gl.rect, src + gl.rect, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    }
     GSR_LAUNCH_CHECK();
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
     gsr::RenderFwdArgs ra;  // with R == 0 every range is empty: background everywhere
@@ -647,6 +752,19 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         if (mc) HIP_OK(hipMemsetAsync(mc->dL_dfeat, 0, sizeof(float) * (size_t)mc->fstride * P, s));
     }
 
+    // deterministic mode: one partial row per instance, summed per Gaussian in tile order
+    const bool det = det_on() && R > 0;
+    const int pstride = mc ? ((6 + mc->nch + 3) & ~3) : gsr::DET_ROW3;
+    float* partial = nullptr;
+    unsigned* det_missing = nullptr;
+    if (det) {
+        const size_t pbytes = 4 * (size_t)pstride * (size_t)R;
+        char* sc = reinterpret_cast<char*>(g_scratch.get(256 + pbytes));
+        if (!sc) return fail(GSR_E_ALLOC, "gsr_backward: deterministic-mode scratch allocation failed");
+        det_missing = reinterpret_cast<unsigned*>(sc);
+        partial = reinterpret_cast<float*>(sc + 256);
+        HIP_OK(hipMemsetAsync(sc, 0, 256 + pbytes, s));
+    }
     if (R > 0) {
         gsr::RenderBwdArgs ra;
         ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
@@ -661,10 +779,11 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.acc = acc;
         ra.order = at<uint32_t>(img, il.order_bwd);
         ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
+        ra.partial = partial;
         {
             GSR_STAGE(ST_RENDER_BWD);
             gsr::launch_tile_order(gx * gy, ra.ranges, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
-                                   at<uint32_t>(img, il.nheavy) + 8, gsr::BWD_HEAVY_BITS, s);
+                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);
             } else {
@@ -676,11 +795,37 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
                     ma.dL_dout = mc->dL_dout + (size_t)c0 * width * height;
                     ma.acc = acc;
                     ma.dL_dfeat = mc->dL_dfeat + c0;
+                    ma.partial = partial;
+                    ma.pstride = pstride;
+                    ma.pc0 = c0;
                     gsr::launch_render_bwd_mc(ma, s);
                 }
             }
         }
         GSR_LAUNCH_CHECK();
+        if (det) {
+            gsr::DetGatherArgs da{};
+            da.P = P; da.gx = gx; da.gy = gy;
+            da.radii = radii;
+            da.rect = at<uint2>(geom, gl.rect);
+            da.depth_key = at<uint32_t>(geom, gl.depth_key);
+            da.ranges = ra.ranges;
+            da.point_list = ra.point_list;
+            da.partial = partial;
+            da.mode = mc ? 1 : 0;
+            da.pstride = pstride;
+            da.nch = mc ? mc->nch : 0;
+            da.fstride = mc ? mc->fstride : 0;
+            da.acc = acc;
+            da.dL_dfeat = mc ? mc->dL_dfeat : nullptr;
+            da.missing = det_missing;
+            gsr::launch_det_gather(da, s);
+            GSR_LAUNCH_CHECK();
+            unsigned miss = 0;
+            HIP_OK(hipMemcpyAsync(&miss, det_missing, 4, hipMemcpyDeviceToHost, s));
+            HIP_OK(hipStreamSynchronize(s));  // the scratch is free again when this call returns
+            if (miss) return fail(GSR_E_DEVICE_CHECK, "gsr_backward (deterministic): %u instances not found in their tile lists", miss);
+        }
     }
     gsr::PreprocessBwdArgs pb;
     pb.P = P; pb.D = D; pb.M = M;

@@ -156,7 +156,11 @@ struct RenderBwdArgs {
     float* acc;  // [P][ACC_STRIDE]
     const uint32_t* order;  // dispatch order (launch_tile_order)
     const uint32_t* nheavy;
+    // deterministic mode (non-null): each (tile, Gaussian) writes its partial sums to row
+    // [instance] of DET_ROW3 floats instead of adding them into acc (k_det_gather sums them)
+    float* partial;
 };
+constexpr int DET_ROW3 = 12;  // 8 sums + the ninth's four row partials
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 
 // Multi-channel tile passes (gsr_render_mc.hip): one group of <= 16 feature channels.
@@ -179,9 +183,53 @@ struct RenderMcArgs {
     const float* dL_dout;  // backward: [nch][H][W]
     float* acc;            // backward: [P][ACC_STRIDE], slots 0..5
     float* dL_dfeat;       // backward: group's first channel, row stride fstride
+    // deterministic mode (non-null): per-instance rows of pstride floats, [6 geometric sums
+    // (added over the groups)][every channel]; pc0 = this group's first channel
+    float* partial;
+    int pstride, pc0;
 };
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);
+
+// ---- deterministic backward: fixed-order per-Gaussian sum of the per-instance rows (gsr_det.hip)
+// For every Gaussian with radii > 0, its tiles in row-major order (its rect), its position in
+// each tile's list by binary search on (depth key, index) -- the order the binning emits --
+// and the partial row there.  mode 0: DET_ROW3 rows -> acc[0..8]; mode 1: rows of pstride
+// floats -> acc[0..5] and dL_dfeat[0..nch).  acc / dL_dfeat are zeroed by the caller.
+struct DetGatherArgs {
+    int P;
+    unsigned gx, gy;
+    const int* radii;
+    const uint2* rect;
+    const uint32_t* depth_key;
+    const uint2* ranges;
+    const uint32_t* point_list;
+    const float* partial;
+    int mode, pstride, nch, fstride;
+    float* acc;
+    float* dL_dfeat;
+    unsigned* missing;  // counts Gaussians' tiles whose list lacks them (must stay 0)
+};
+void launch_det_gather(const DetGatherArgs& a, hipStream_t s);
+
+// ---- GSR_DEBUG invariant checks (gsr_det.hip) ----------------------------------------------
+// The first failed check (code, three details) is recorded with an atomic CAS; the host reads
+// it after a stream synchronisation.
+struct DebugReport {
+    unsigned code, a, b, c;
+};
+enum DebugCode : unsigned {
+    DBG_OK = 0, DBG_RANGE = 1, DBG_ID = 2, DBG_CULLED = 3, DBG_OUTSIDE_RECT = 4, DBG_ORDER = 5, DBG_COUNT = 6,
+    DBG_TOTAL = 7, DBG_NCONTRIB = 8
+};
+// Tile lists against the preprocess: every range inside [0, R), every listed id < P, visible,
+// its rect covering the tile, (depth key, id) strictly increasing per tile, every visible
+// Gaussian listed exactly area(rect) times, the lengths summing to R; n_contrib[pix] at most
+// its tile's list length.  count: P u32 of zeroed scratch, total: one zeroed u64.
+void launch_check_lists(int P, long long R, unsigned gx, unsigned gy, int W, int H, const int* radii,
+                        const uint2* rect, const uint32_t* depth_key, const uint2* ranges, const uint32_t* point_list,
+                        const uint32_t* n_contrib, uint32_t* count, unsigned long long* total, DebugReport* rep,
+                        hipStream_t s);
 
 // ---- fused Adam over a flat parameter buffer (gsr_adam.hip) ---------------------------
 constexpr int ADAM_MAX_SEGS = 16;

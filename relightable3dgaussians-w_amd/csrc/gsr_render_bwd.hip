@@ -27,6 +27,7 @@ __device__ unsigned long long g_bwd_times[3 * 65536];  // per tile: start, end (
 #define BWD_STAT(k, v)
 #endif
 
+template <bool DET>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -71,6 +72,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     // per-value scale: dL/dmean2D gets op * (W/2, H/2), dL/dconic -op/2, the rest 1
     const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : vidx <= 4 ? -0.5f : 1.f;
     const bool vop = vidx >= 0 && vidx <= 4;
+    // deterministic mode: the slot of this lane's value in the instance's partial row
+    // (values 0..7, then value 8's four row partials)
+    const int pslot = vidx < 8 ? vidx : 8 + row;
 
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
@@ -166,7 +170,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             const float Q0 = swap16_sum(P0, P1), Q1 = swap16_sum(P2, P3), Q2 = S8;
             float v = row_sum3(Q0, Q1, Q2, mb3, mb2);
             v *= vop ? op * vscale : vscale;
-            if (vidx >= 0 && v != 0.f) atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
+            if (DET) {  // one row per instance, summed per Gaussian in tile order (k_det_gather)
+                if (vidx >= 0 && v != 0.f) a.partial[(size_t)(range.x + pos) * DET_ROW3 + pslot] = v;
+            } else if (vidx >= 0 && v != 0.f) {
+                atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
+            }
             }
         };
         // survivors in pairs over two register sets (the next survivor's record is read
@@ -207,11 +215,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
 // whole tile.
+template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_bwd_tile(a, tile, qallow);
+    render_bwd_tile<DET>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -232,7 +241,9 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    hipLaunchKernelGGL(k_render_bwd, dim3(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP)), dim3(64), 0, s, a);
+    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

@@ -138,7 +138,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     }
 }
 
-template <int NC4, int NCH = 4 * NC4>
+template <int NC4, int NCH = 4 * NC4, bool DET = false>
 __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
     constexpr int V = 6 + NCH;       // 6 geometric sums + the feature sums
     constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
@@ -285,7 +285,11 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 for (int t = 0; t < NQ; t++) Qr[t] = swap16_sum(Pp[2 * t], Pp[2 * t + 1]);
                 float v = row_sums_t<NQ>(Qr, mb3, mb2, col);
                 v *= vop ? op * vscale : vscale;
-                if (v != 0.f) {
+                if (DET) {  // the groups run one after another: plain read-modify-write
+                    float* prow = a.partial + (size_t)(range.x + pos) * a.pstride;
+                    if (vidx >= 0 && vidx < 6) prow[vidx] += v;
+                    else if (vfeat) prow[a.pc0 + vidx] = v;
+                } else if (v != 0.f) {
                     const uint32_t gid = Q2.y;
                     if (vidx >= 0 && vidx < 6) atomicAdd(a.acc + (size_t)gid * ACC_STRIDE + vidx, v);
                     else if (vfeat) atomicAdd(a.dL_dfeat + (size_t)gid * a.fstride + (vidx - 6), v);
@@ -303,12 +307,12 @@ __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
-template <int NC4, int NCH = 4 * NC4>
+template <int NC4, int NCH = 4 * NC4, bool DET = false>
 __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_bwd_mc_tile<NC4, NCH>(a, tile, qallow);
+    render_bwd_mc_tile<NC4, NCH, DET>(a, tile, qallow);
 }
 
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
@@ -326,19 +330,25 @@ void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
     }
 }
 
+template <bool DET>
+static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s) {
+    switch ((a.nch + 3) / 4) {
+        case 1: hipLaunchKernelGGL((k_render_bwd_mc<1, 4, DET>), grid, dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_render_bwd_mc<2, 8, DET>), grid, dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_render_bwd_mc<3, 12, DET>), grid, dim3(64), 0, s, a); break;
+        default:
+            if (a.nch == 14) hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET>), grid, dim3(64), 0, s, a);
+            break;
+    }
+}
+
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
     const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
-    switch ((a.nch + 3) / 4) {
-        case 1: hipLaunchKernelGGL(k_render_bwd_mc<1>, grid, dim3(64), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_render_bwd_mc<2>, grid, dim3(64), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_render_bwd_mc<3>, grid, dim3(64), 0, s, a); break;
-        default:
-            if (a.nch == 14) hipLaunchKernelGGL((k_render_bwd_mc<4, 14>), grid, dim3(64), 0, s, a);
-            else hipLaunchKernelGGL(k_render_bwd_mc<4>, grid, dim3(64), 0, s, a);
-            break;
-    }
+    if (a.partial) launch_bwd_mc<true>(a, grid, s);
+    else launch_bwd_mc<false>(a, grid, s);
 }
 
 }  // namespace gsr

@@ -26,9 +26,14 @@ class Layout(C.Structure):
         "geom_rec", "geom_acc", "img_final_T", "img_n_contrib", "img_ranges", "bin_point_list", "bin_tile_keys")]
 
 
+DEBUG_LIB_PATH = os.path.join(PKG_DIR, "lib", "debug", "libgsr.so")
+
+
 def build(jobs=8, arch="gfx950"):
-    """Compile libgsr.so in-tree (hipcc --offload-arch=gfx950)."""
+    """Compile libgsr.so in-tree (hipcc --offload-arch=gfx950), and the GSR_DEBUG
+    invariant-checking variant lib/debug/libgsr.so (selected with GSR_LIB_PATH)."""
     subprocess.check_call(["make", "-s", "-C", CSRC, f"-j{jobs}", f"ARCH={arch}"])
+    subprocess.check_call(["make", "-s", "-C", CSRC, f"-j{jobs}", f"ARCH={arch}", "debug"])
 
 
 def _declare(lib):
@@ -76,6 +81,8 @@ def _declare(lib):
     lib.gsr_profile_stage_name.argtypes = [i]
     lib.gsr_profile_stage_name.restype = C.c_char_p
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
+    lib.gsr_set_deterministic.argtypes = [i]
+    lib.gsr_check_buffers.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
     lib.gsr_last_error.restype = C.c_char_p
     lib.gsr_version.restype = C.c_char_p
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
@@ -83,7 +90,8 @@ def _declare(lib):
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward",
-               "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout"):
+               "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
+               "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers"):
         getattr(lib, fn).restype = C.c_int
 
 
@@ -127,6 +135,29 @@ def fptr(t):
 
 def stream_of(device):
     return torch.cuda.current_stream(device).cuda_stream
+
+
+def set_deterministic(on=True):
+    """Deterministic backward (gsr_set_deterministic): fixed-order gradient sums instead of
+    the tile passes' float atomics; bit-reproducible, slower (a debugging mode)."""
+    check(lib().gsr_set_deterministic(int(bool(on))), "gsr_set_deterministic")
+
+
+def deterministic():
+    return bool(lib().gsr_get_deterministic())
+
+
+def debug_build():
+    """True when the loaded library is the GSR_DEBUG build (lib/debug/libgsr.so)."""
+    return bool(lib().gsr_debug_build())
+
+
+def check_buffers(P, R, W, H, radii, geom, binb, img):
+    """Verify a forward's tile lists and n_contrib against its preprocess (gsr_check_buffers);
+    raises RuntimeError naming the first violated invariant."""
+    check(lib().gsr_check_buffers(int(P), int(R), int(W), int(H), radii.data_ptr(), geom.data_ptr(),
+                                  binb.data_ptr() if binb.numel() else None, img.data_ptr(),
+                                  stream_of(radii.device)), "gsr_check_buffers")
 
 
 def profile_enable(on=True):

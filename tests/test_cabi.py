@@ -73,3 +73,24 @@ def test_every_entry_point_with_parameters_has_ctypes_argtypes():
         if params.strip() in ("", "void"):
             continue
         assert getattr(L, name).argtypes is not None, name
+
+
+def test_debug_build_and_deterministic_toggle():
+    """lib/debug/libgsr.so (GSR_DEBUG) exports the same ABI and reports itself; the product
+    library does not.  The deterministic-backward toggle is host state (no GPU needed)."""
+    from gsr import _lib
+    if not os.path.exists(_lib.DEBUG_LIB_PATH):
+        _lib.build()
+    D = ctypes.CDLL(_lib.DEBUG_LIB_PATH)
+    missing = [s for s in declared_symbols() if not hasattr(D, s)]
+    assert not missing, missing
+    assert D.gsr_debug_build() == 1
+    assert _lib.lib().gsr_debug_build() == 0
+    before = _lib.deterministic()
+    try:
+        _lib.set_deterministic(True)
+        assert _lib.deterministic()
+        _lib.set_deterministic(False)
+        assert not _lib.deterministic()
+    finally:
+        _lib.set_deterministic(before)

@@ -261,33 +261,51 @@ def test_cfg5_relit_render_fused_matches_calls():
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
     bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
 
-    def run(fn):
+    def run(fn, skip=()):
         scene.fp.zero_grad()
         pc = scene.model()
         light = relit_shade.EnvironmentLight(scene.fp.params["env_sh"][0], sh_degree=4)
         out = fn(view, pc, light, scene.fp.params["sky_sh"][0:1], 1, pipe, bg, debug=False)
         keys = sorted(k for k in out if k not in ("viewspace_points", "visibility_filter", "radii"))
         gen = torch.Generator(device="cuda").manual_seed(6)
-        loss = sum((out[k] * torch.randn(out[k].shape, device="cuda", generator=gen)).sum() for k in keys)
+        loss = sum((out[k] * torch.randn(out[k].shape, device="cuda", generator=gen)).sum()
+                   for k in keys if k not in skip)
         loss.backward()
         return {k: out[k].detach() for k in keys}, out["radii"], scene.fp.grad.clone(), \
             out["viewspace_points"].grad.clone()
 
+    def grad_errs(g_f, g_r):
+        errs = {}
+        for name, off, shape in zip(scene.fp.names, scene.fp.offsets, scene.fp.shapes):
+            n = int(np.prod(shape))
+            a, b = g_f[off:off + n].double(), g_r[off:off + n].double()
+            if b.any():
+                errs[name] = float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
+        return errs
+
     o_f, r_f, g_f, m_f = run(relit.render)
     o_r, r_r, g_r, m_r = run(relit.render_calls)
     assert sorted(o_f) == sorted(o_r) and torch.equal(r_f, r_r)
-    for k in o_r:
-        e = float(torch.linalg.norm((o_f[k] - o_r[k]).double()) / torch.linalg.norm(o_r[k].double()))
+    img_errs = {k: float(torch.linalg.norm((o_f[k] - o_r[k]).double()) / torch.linalg.norm(o_r[k].double()))
+                for k in o_r}
+    errs = grad_errs(g_f, g_r)
+    errs["means2D"] = float(torch.linalg.norm((m_f - m_r).double()) / torch.linalg.norm(m_r.double()))
+    _, _, g_f2, m_f2 = run(relit.render, skip=("normal_ref",))
+    _, _, g_r2, m_r2 = run(relit.render_calls, skip=("normal_ref",))
+    errs2 = grad_errs(g_f2, g_r2)
+    errs2["means2D"] = float(torch.linalg.norm((m_f2 - m_r2).double()) / torch.linalg.norm(m_r2.double()))
+    print("images", img_errs, "\ngradients", errs, "\ngradients without normal_ref", errs2)
+    for k, e in img_errs.items():
         # normal_ref is a cross product of one-pixel depth differences: at 4K those are ~1e-4
         # of the depth, so float rounding of the back-projection (the epilogue kernel vs
         # PyTorch's matrix form) is amplified ~1e4x (measured 4.3e-5)
         assert e < (2e-4 if k == "normal_ref" else 1e-5), (k, e)
-    for name, off, shape in zip(scene.fp.names, scene.fp.offsets, scene.fp.shapes):
-        n = int(np.prod(shape))
-        a, b = g_f[off:off + n].double(), g_r[off:off + n].double()
-        if not b.any():
-            continue
-        e = float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
-        assert e < 1e-4, (name, e)
-    e = float(torch.linalg.norm((m_f - m_r).double()) / torch.linalg.norm(m_r.double()))
-    assert e < 1e-4, e
+    # The same amplification reaches every geometric gradient through normal_ref's backward
+    # (the depth channel): measured 1.22-1.26e-4 for xyz, opacity, scaling, rotation and
+    # means2D, deterministic across boxes.  With normal_ref out of the loss the same
+    # gradients agree to 4e-7 .. 6e-6 (profiles/r2b_cfg5_relit_parity.log), so the 1e-4 bar
+    # holds there and the full loss gets 2e-4.
+    for k, e in errs2.items():
+        assert e < 1e-4, ("without normal_ref", k, e)
+    for k, e in errs.items():
+        assert e < 2e-4, (k, e)
