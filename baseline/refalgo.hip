@@ -312,7 +312,7 @@ int gsr_ref_forward(GsrRefCtx* ctx, void* stream, int P, int D, int M, const flo
     if (P == 0) return 0;
     // geometry state
     ctx->rec = (gsr::Rec*)ctx->geom_rec.get(sizeof(gsr::Rec) * (size_t)P);
-    const size_t naux = 4 * al(4 * (size_t)P) + al(8 * (size_t)P) + al(8 * (size_t)gsr::TOTALS_U64);
+    const size_t naux = 4 * al(4 * (size_t)P) + al(8 * (size_t)P);
     char* aux = (char*)ctx->geom_aux.get(naux);
     if (!ctx->rec || !aux) return ref_fail(ctx, "alloc geom");
     uint32_t* tiles = (uint32_t*)aux;
@@ -320,8 +320,6 @@ int gsr_ref_forward(GsrRefCtx* ctx, void* stream, int P, int D, int M, const flo
     uint32_t* st_count = (uint32_t*)(aux + 2 * al(4 * (size_t)P));
     uint32_t* depth_key = (uint32_t*)(aux + 3 * al(4 * (size_t)P));
     uint2* rect = (uint2*)(aux + 4 * al(4 * (size_t)P));
-    unsigned long long* totals = (unsigned long long*)(aux + 4 * al(4 * (size_t)P) + al(8 * (size_t)P));
-    REF_HIP(hipMemsetAsync(totals, 0, 8 * gsr::TOTALS_U64, s));
 
     gsr::PreprocessArgs pa;
     memset(&pa, 0, sizeof(pa));
@@ -333,7 +331,7 @@ int gsr_ref_forward(GsrRefCtx* ctx, void* stream, int P, int D, int M, const flo
     pa.focal_x = W / (2.0f * tan_fovx); pa.focal_y = H / (2.0f * tan_fovy);
     pa.grid_x = gx; pa.grid_y = gy; pa.prefiltered = 0;
     pa.radii = radii; pa.tiles = tiles; pa.st_count = st_count; pa.depth_key = depth_key; pa.rect = rect;
-    pa.rec = ctx->rec; pa.err_flag = (unsigned*)(totals + gsr::TOTALS_U64 - 1); pa.totals = totals;
+    pa.rec = ctx->rec;  // blk_tot / hist0 null: this baseline scans tiles_touched itself
     gsr::launch_preprocess(pa, s);
 
     size_t scan_bytes = 0;

@@ -94,6 +94,54 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
     }
 }
 
+// ---- frame totals for the host (see FrameTotals) ---------------------------------------------
+__device__ __forceinline__ void frame_totals(const FrameTotals& f) {
+    __shared__ unsigned long long st[4][16];
+    unsigned long long v[4] = {0, 0, 0, 0};
+    constexpr int U = 4;  // loads in flight per thread (few registers: it rides in other kernels)
+    for (int b0 = 0; b0 < f.nblk; b0 += U * (int)blockDim.x) {
+        uint4 t[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int b = b0 + u * (int)blockDim.x + (int)threadIdx.x;
+            t[u] = b < f.nblk ? f.blk_tot[b] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            v[0] += t[u].x;
+            v[1] += t[u].y;
+            v[2] += t[u].z;
+            v[3] |= t[u].w;
+        }
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const unsigned long long u = __shfl_xor(v[k], o, 64);
+            v[k] = k == 3 ? (v[k] | u) : v[k] + u;
+        }
+        if (lane == 0) st[k][wave] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        const int k = threadIdx.x;
+        unsigned long long t = 0;
+        for (int w = 0; w < nw; w++) t = k == 3 ? (t | st[k][w]) : t + st[k][w];
+        // each word carries the call's tag in its low 16 bits, so the host needs no ordering
+        // between them (a system-scope release would write back the L2)
+        const unsigned long long w = (t > 0xFFFFFFFFFFFFull ? 0xFFFFFFFFFFFFull : t) << 16 | (f.seq & 0xFFFFull);
+        __hip_atomic_store(f.host + k, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_frame_totals(FrameTotals f) { frame_totals(f); }
+
+void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
+    hipLaunchKernelGGL(k_frame_totals, dim3(1), dim3(256), 0, s, ft);
+}
+
 // ---- 2+3 fused: super-tile entries emitted straight into super-tile order ----------------
 // The depth-sorted visible Gaussians are cut into blocks of ST_G.  k_st_hist counts each
 // block's entries per super-tile (digit-major table [NS][nb]) from the rects in depth order
@@ -113,21 +161,12 @@ __device__ __forceinline__ uint2 st_rect_of(uint2 r) {
     return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
 }
 
-// P_v summed from the preprocess's per-slot totals.  The forward launches the binning before
-// its one host synchronisation (the binning buffer is sized from the previous call's counts,
-// see gsr_capi.cpp), so these kernels read the visible count on the device.  Block-uniform.
-__device__ __forceinline__ int block_visible(int pv_host, const unsigned long long* totals) {
-    if (!totals) return pv_host;
-    static_assert(TOTAL_SLOTS == 128, "two slots per lane of one wave");
-    __shared__ uint32_t s_pv;
-    if (threadIdx.x < 64) {
-        uint32_t v = (uint32_t)totals[TOTAL_STRIDE * threadIdx.x] + (uint32_t)totals[TOTAL_STRIDE * (threadIdx.x + 64)];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (threadIdx.x == 0) s_pv = v;
-    }
-    __syncthreads();
-    return (int)s_pv;
+// P_v from the depth sort's last pass (depth_sort's pv_out).  The forward launches the binning before its one host synchronisation (the
+// binning buffer is sized from the previous call's counts, see gsr_capi.cpp), so these
+// kernels read the visible count on the device.  Block-uniform.
+__device__ __forceinline__ int block_visible(int pv_host, const unsigned long long* pv) {
+    if (!pv) return pv_host;
+    return (int)__builtin_amdgcn_readfirstlane((int)*pv);
 }
 
 template <int ST_W>
@@ -135,7 +174,8 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
                                                   int NS, int nb, uint32_t* table, uint32_t* wcounts) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
-    Pv = block_visible(Pv, totals);  // (its barrier also orders the zeroing)
+    Pv = block_visible(Pv, totals);
+    __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g0 = blk * ST_G;
@@ -157,20 +197,58 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
     }
 }
 
-// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total)
-__global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, uint32_t* bases, uint2* ranges) {
-    __shared__ uint32_t sh[4];
-    uint32_t carry = 0;
+// Segment table of the tile filters (SEG entries per segment, see k_seg_lists), in the
+// tile-list scratch (seg_layout).
+constexpr uint32_t SEG = 1024;
+struct SegTable {
+    uint32_t *seg_st, *seg_e0, *st_seg0, *nseg_total, *seg_cnt;
+    uint32_t gcap;  // capacity of the table (segments)
+};
+__host__ __device__ inline size_t seg_capacity(long long S, int nst) { return (size_t)((S + SEG - 1) / SEG) + (size_t)nst; }
+inline SegTable seg_layout(void* temp, long long S, int nst) {
+    const size_t G = seg_capacity(S, nst);
+    SegTable t;
+    t.seg_st = reinterpret_cast<uint32_t*>(temp);
+    t.seg_e0 = t.seg_st + G;
+    t.st_seg0 = t.seg_e0 + G;
+    t.nseg_total = t.st_seg0 + nst + 1;
+    t.seg_cnt = t.nseg_total + 1;  // [G][32], becomes the segment bases in place
+    t.gcap = (uint32_t)G;
+    return t;
+}
+
+// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total); and
+// (seg non-null) the segment table: every super-tile list cut into segments of SEG entries,
+// segment g covering [seg_e0[g], min(seg_e0[g] + SEG, end of its super-tile)).  One
+// workgroup; the entry totals and the segment counts are scanned together (packed in u64).
+__global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, uint32_t* bases, uint2* ranges,
+                                                   SegTable seg) {
+    __shared__ unsigned long long sh[4];
+    unsigned long long carry = 0;
     for (int c = 0; c < NS; c += 256) {
         const int i = c + threadIdx.x;
         const uint32_t v = i < NS ? tot[i] : 0u;
-        uint32_t t;
-        const uint32_t ex = carry + block256_exclusive_scan(v, sh, &t);
+        const uint32_t n = (v + SEG - 1) / SEG;
+        unsigned long long t;
+        const unsigned long long ex = carry + block256_exclusive_scan(((unsigned long long)n << 32) | v, sh, &t);
+        const uint32_t eb = (uint32_t)ex, sb = (uint32_t)(ex >> 32);
         if (i < NS) {
-            bases[i] = ex;
-            ranges[i] = v ? make_uint2(ex, ex + v) : make_uint2(0u, 0u);
+            bases[i] = eb;
+            ranges[i] = v ? make_uint2(eb, eb + v) : make_uint2(0u, 0u);
+            if (seg.seg_st) {
+                seg.st_seg0[i] = sb;
+                for (uint32_t k = 0; k < n && sb + k < seg.gcap; k++) {
+                    seg.seg_st[sb + k] = (uint32_t)i;
+                    seg.seg_e0[sb + k] = eb + k * SEG;
+                }
+            }
         }
         carry += t;
+    }
+    if (seg.seg_st && threadIdx.x == 0) {
+        const uint32_t ns = (uint32_t)(carry >> 32);
+        seg.st_seg0[NS] = ns;
+        *seg.nseg_total = min(ns, seg.gcap);
     }
 }
 
@@ -240,7 +318,11 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
                                                      const uint2* rect_sorted, unsigned gsx, int NS, int nb,
                                                      const uint32_t* table, const uint32_t* wcounts,
                                                      const uint32_t* bases, uint32_t* st_keys, uint32_t* st_vals,
-                                                     uint32_t cap) {
+                                                     uint32_t cap, FrameTotals ft) {
+    if (ft.host && (int)blockIdx.x == nb) {  // the extra workgroup: the host's frame totals
+        frame_totals(ft);
+        return;
+    }
     extern __shared__ unsigned long long st_lds[];  // [ST_W][NS] lane masks, then [ST_W][NS] run counters
     unsigned long long* wmask_all = st_lds;
     uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + ST_W * NS);
@@ -277,9 +359,16 @@ bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
 void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
                    unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
-                   uint32_t cap, hipStream_t s) {
+                   uint32_t cap, hipStream_t s, const FrameTotals* ftp, void* lists_temp) {
+    FrameTotals ft{};
+    if (ftp) ft = *ftp;
     if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
         (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
+        if (ftp) launch_frame_totals(ft, s);
+        if (lists_temp) {  // an empty segment table
+            const SegTable seg = seg_layout(lists_temp, cap, NS);
+            (void)hipMemsetAsync(seg.st_seg0, 0, 4 * ((size_t)NS + 2), s);
+        }
         return;
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
@@ -301,13 +390,16 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
         hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
                            table, wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
-    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges);
+    SegTable seg{};
+    if (lists_temp) seg = seg_layout(lists_temp, cap, NS);
+    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges, seg);
+    const dim3 grid(nb + (ftp ? 1 : 0));
     if (W == 8)
-        hipLaunchKernelGGL(k_st_scatter<8>, dim3(nb), dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap);
+        hipLaunchKernelGGL(k_st_scatter<8>, grid, dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
+                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap, ft);
     else
-        hipLaunchKernelGGL(k_st_scatter<4>, dim3(nb), dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap);
+        hipLaunchKernelGGL(k_st_scatter<4>, grid, dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
+                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap, ft);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
@@ -342,9 +434,7 @@ __device__ __forceinline__ StGeom st_geom(unsigned st, unsigned gsx, unsigned gx
     return g;
 }
 
-// Segment table: every super-tile list is cut into segments of SEG entries; segment g
-// covers entries [seg_e0[g], min(seg_e0[g] + SEG, end of its super-tile)).
-constexpr uint32_t SEG = 1024;
+// Segment table (the non-fused binning path; the fused one builds it in k_st_bases).
 
 __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_ranges, uint32_t* seg_st,
                                                     uint32_t* seg_e0, uint32_t* st_seg0, uint32_t* nseg_total,
@@ -406,13 +496,25 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
         const unsigned lx = lane % GSR_ST_W, ly = lane / GSR_ST_W;
         if (lx < g.nx && ly < g.ny) run += tile_start[(g.ty0 + ly) * gx + g.tx0 + lx];
     }
-    for (uint32_t b = e0; b < e1; b += 256) {
+    // every batch's keys (and ids) are loaded up front: one memory latency per segment
+    constexpr int NB = SEG / 256;
+    uint32_t kb[NB], vb[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const uint32_t e = e0 + 256u * j + tid;
+        kb[j] = e < e1 ? st_keys[e] : 0u;
+        vb[j] = (WRITE && e < e1) ? st_vals[e] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const uint32_t b = e0 + 256u * j;
+        if (b >= e1) break;  // block-uniform
         const uint32_t e = b + tid;
         uint32_t id = 0, mask = 0;
         if (e < e1) {
             // local tile coverage mask (bit t = (t / 8) row, (t % 8) column)
-            mask = local_rect_mask(st_keys[e] >> ST_KEY_BITS);
-            if (WRITE) id = st_vals[e];
+            mask = local_rect_mask(kb[j] >> ST_KEY_BITS);
+            if (WRITE) id = vb[j];
         }
         uint64_t bal[ST_TILES];
         uint32_t mine = 0;
@@ -476,7 +578,7 @@ __global__ void __launch_bounds__(256) k_seg_prefix(int nst, const uint32_t* st_
 // serialise when all eight bands share one CU.)
 constexpr int TS_LDS = 12288;
 __global__ void __launch_bounds__(1024) k_tile_scan(int T, const uint32_t* cnt, uint32_t* start, uint2* ranges,
-                                                     uint32_t* tile_nmax) {
+                                                     uint32_t* tile_nmax, uint32_t cap_r) {
     __shared__ uint32_t s_cnt[TS_LDS];
     __shared__ uint32_t wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -518,7 +620,7 @@ __global__ void __launch_bounds__(1024) k_tile_scan(int T, const uint32_t* cnt, 
         for (int k = 0; k < 8; k++) {
             if (base + k < T) {
                 start[base + k] = run;
-                ranges[base + k] = v[k] ? make_uint2(run, run + v[k]) : make_uint2(0u, 0u);
+                ranges[base + k] = v[k] ? make_uint2(min(run, cap_r), min(run + v[k], cap_r)) : make_uint2(0u, 0u);
             }
             run += v[k];
         }
@@ -543,23 +645,25 @@ void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2
 }
 
 size_t tile_lists_temp_bytes(long long S, int nst) {
-    const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
+    const size_t G = seg_capacity(S, nst);
     return 4 * (2 * G + (nst + 1) + 1 + G * ST_TILES) + 256;
 }
 
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s) {
+                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s, bool seg_table_ready) {
     const int T = (int)(gx * gy);
-    const size_t G = (size_t)((S + SEG - 1) / SEG) + (size_t)nst;
-    uint32_t* seg_st = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* seg_e0 = seg_st + G;
-    uint32_t* st_seg0 = seg_e0 + G;
-    uint32_t* nseg_total = st_seg0 + nst + 1;
-    uint32_t* seg_cnt = nseg_total + 1;  // [G][32], becomes the segment bases in place
-    hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total,
-                       (uint32_t)G);
+    const SegTable tab = seg_layout(temp, S, nst);
+    const size_t G = tab.gcap;
+    uint32_t* seg_st = tab.seg_st;
+    uint32_t* seg_e0 = tab.seg_e0;
+    uint32_t* st_seg0 = tab.st_seg0;
+    uint32_t* nseg_total = tab.nseg_total;
+    uint32_t* seg_cnt = tab.seg_cnt;
+    if (!seg_table_ready)
+        hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total,
+                           (uint32_t)G);
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
                            st_ranges, st_keys, st_vals, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
@@ -570,7 +674,8 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
     hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, st_seg0, gx, gy, gsx, seg_cnt,
                        tile_cnt, (uint32_t)G);
     (void)scan_tmp;
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, tile_nmax);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, tile_nmax,
+                       (uint32_t)min(cap_r, (long long)0xFFFFFFFFll));
     launch_tile_order((unsigned)T, ranges, nullptr, order, nheavy, heavy_bits, s);
     if (G > 0) {
         hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,

@@ -58,7 +58,7 @@ struct Carver {
 };
 
 struct GeomLayout {
-    size_t totals, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, rect_s, rect_s_alt,
+    size_t tot_dev, blk_tot, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, rect_s, rect_s_alt,
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
@@ -73,7 +73,8 @@ struct BinLayout {
 GeomLayout geom_layout(long long P) {
     Carver c;
     GeomLayout L;
-    L.totals = c.take(8 * gsr::TOTALS_U64);  // [slots][P_v, R, S, pad] + error flag
+    L.tot_dev = c.take(8 * 4);                                // P_v, R, S, error flag
+    L.blk_tot = c.take(16 * (size_t)gsr::pre_blocks(P));      // per preprocess workgroup
     L.radii = c.take(4 * P);
     L.tiles = c.take(4 * P);
     L.st_count = c.take(4 * P);
@@ -89,7 +90,7 @@ GeomLayout geom_layout(long long P) {
     L.rect_s_alt = c.take(8 * P);
     L.offsets = c.take(4 * P);
     L.scan_tmp = c.take(24 * (size_t)gsr::scan_blocks(P) + 16);
-    L.sort_tmp = c.take(gsr::radix_sort_temp_bytes(P));
+    L.sort_tmp = c.take(gsr::depth_sort_temp_bytes(P));
     L.total = c.o + 256;
     return L;
 }
@@ -159,12 +160,14 @@ T* at(void* base, size_t off) {
 
 char* align_base(void* p) { return reinterpret_cast<char*>(align_up(reinterpret_cast<size_t>(p), 256)); }
 
+// Host-mapped, coherent: the depth sort's first histogram launch stores the frame totals
+// in p[0..3], each tagged with the call's sequence number (gsr_sort.hip frame_totals).
 struct PinnedHost {
     unsigned long long* p = nullptr;
-    hipEvent_t ev = nullptr;  // recorded after the totals' D2H copy
+    unsigned long long* p_dev = nullptr;  // its device address
+    unsigned long long seq = 0;
     ~PinnedHost() {
         if (p) (void)hipHostFree(p);
-        if (ev) (void)hipEventDestroy(ev);
     }
 };
 thread_local PinnedHost g_pinned;
@@ -208,6 +211,31 @@ struct Scratch {
     }
 };
 thread_local Scratch g_scratch;
+
+// Wait until the device has stored the four totals of call `seq` (frame_totals: each word is
+// value << 16 | seq mod 2^16) and unpack them into out[0..3].  Spins on the coherent
+// host-mapped words; every 256 polls the stream is queried, so a failed or finished stream
+// ends the wait (a finished stream must have stored them).
+int wait_totals(const unsigned long long* p, unsigned long long seq, hipStream_t s, unsigned long long* out) {
+    const unsigned long long tag = seq & 0xFFFFull;
+    for (unsigned it = 1;; it++) {
+        bool ok = true;
+        for (int k = 0; k < 4; k++) {
+            const unsigned long long w = __atomic_load_n(p + k, __ATOMIC_ACQUIRE);
+            ok = ok && (w & 0xFFFFull) == tag;
+            out[k] = w >> 16;
+        }
+        if (ok) return 0;
+        if ((it & 255u) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q != hipSuccess && q != hipErrorNotReady) return gsr_fail_hip(q, __LINE__);
+            if (q == hipSuccess && (it & 511u) == 0) return gsr_fail_hip(hipErrorUnknown, __LINE__);  // done, no totals
+        }
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+    }
+}
 
 #define HIP_OK(x)                                              \
     do {                                                       \
@@ -447,11 +475,12 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
     const int T = (int)(gx * gy);
     if (!radii) radii = at<int>(geom, gl.radii);
+    if (P == 0) {  // the reference renders nothing (rasterize_points.cu:84-86): zero image
+        if (out_color) HIP_OK(hipMemsetAsync(out_color, 0, sizeof(float) * 3 * (size_t)width * height, s));
+        return GSR_OK;
+    }
 
-    unsigned long long* totals = at<unsigned long long>(geom, gl.totals);
-    const size_t totals_bytes = 8 * gsr::TOTALS_U64;
-    unsigned* err_flag = reinterpret_cast<unsigned*>(totals + gsr::TOTALS_U64 - 1);
-    HIP_OK(hipMemsetAsync(totals, 0, totals_bytes, s));  // per-slot P_v, R, S (preprocess atomics) + error flag
+    unsigned long long* tot_dev = at<unsigned long long>(geom, gl.tot_dev);
 
     gsr::PreprocessArgs pa;
     pa.P = P; pa.D = D; pa.M = M;
@@ -466,55 +495,62 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     pa.depth_key = at<uint32_t>(geom, gl.depth_key);
     pa.rect = at<uint2>(geom, gl.rect);
     pa.rec = at<gsr::Rec>(geom, gl.rec);
-    pa.err_flag = err_flag;
-    pa.totals = totals;
+    pa.blk_tot = at<uint4>(geom, gl.blk_tot);
     {
         GSR_STAGE(ST_PREPROCESS);
         gsr::launch_preprocess(pa, s);
     }
     GSR_LAUNCH_CHECK();
 
+    // The forward's one host synchronisation (the reference's, rasterizer_impl.cu:281) reads
+    // P_v, R and S: one workgroup sums the preprocess's per-workgroup totals into host-mapped
+    // words tagged with this call's sequence number, and the host polls them (a D2H copy or an
+    // event on the stream each left a 6-19 us bubble between kernels).
+    //  * Speculative (an earlier call had the same P and image size): the binning buffer is
+    //    sized from that call's counts with headroom; the binning and the forward tile pass
+    //    are launched BEFORE the host waits (the kernels read P_v on the device, drop entries
+    //    beyond the capacity and clamp the tile ranges to it), and the totals ride in an extra
+    //    workgroup of the super-tile scatter.  A capacity overflow (rare: R grew by > 25 %)
+    //    redoes the binning and the tile pass at the exact size.
+    //  * Otherwise (first call, or images too large for the fused binning) the totals run
+    //    right after the preprocess, the host waits while the depth sort runs, and sizes the
+    //    binning buffer exactly.
+    if (!g_pinned.p) {
+        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * 8, hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_OK(hipHostGetDevicePointer(reinterpret_cast<void**>(&g_pinned.p_dev), g_pinned.p, 0));
+        memset(g_pinned.p, 0, 8 * 8);
+    }
+    const unsigned long long seq = ++g_pinned.seq;
+    const gsr::FrameTotals ft{pa.blk_tot, gsr::pre_blocks(P), g_pinned.p_dev, seq};
+    const unsigned gsx = st_x(width), gsy = st_y(height);
+    const int NS = (int)(gsx * gsy);
+    const bool fused_bin = gsr::st_bin_supported(NS);
+    const bool speculate = fused_bin && g_hint.P == P && g_hint.W == width && g_hint.H == height;
+    if (!speculate) gsr::launch_frame_totals(ft, s);
+
     // Depth sort of all P Gaussians: culled ones carry key 0xFFFFFFFF and sort last, so the
     // first P_v sorted entries are the visible Gaussians in the reference's (depth, index)
-    // order -- no separate visibility compaction.  Runs before the one host sync.
+    // order -- no separate visibility compaction.  Its last pass stores P_v to tot_dev.
     uint32_t* vis_key = at<uint32_t>(geom, gl.vis_key);
     uint32_t* vis_val = at<uint32_t>(geom, gl.vis_val);
     int flip;
     {
         GSR_STAGE(ST_DEPTH_SORT);
-        flip = gsr::radix_sort_pairs_from(P, pa.depth_key, nullptr, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
-                                          at<uint32_t>(geom, gl.vis_val_alt), 32, at<void>(geom, gl.sort_tmp), s,
-                                          pa.rect, at<uint2>(geom, gl.rect_s), at<uint2>(geom, gl.rect_s_alt));
+        flip = gsr::depth_sort(P, pa.depth_key, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
+                               at<uint32_t>(geom, gl.vis_val_alt), pa.rect, at<uint2>(geom, gl.rect_s),
+                               at<uint2>(geom, gl.rect_s_alt), at<void>(geom, gl.sort_tmp), tot_dev, s);
     }
     GSR_LAUNCH_CHECK();
 
-    // The forward's one host synchronisation (the reference's, rasterizer_impl.cu:281) reads
-    // P_v, R and S.  When an earlier call had the same P and image size, the binning buffer is
-    // sized from its counts with headroom and the binning is launched BEFORE the host waits:
-    // the kernels read P_v on the device and drop entries beyond the capacity, and the GPU
-    // keeps running while the host reads the totals (no idle gap between the depth sort and
-    // the binning).  A capacity overflow (rare: R grew by > 25 %) redoes the binning at the
-    // exact size.  Otherwise (first call, or images too large for the fused binning) the host
-    // waits first and sizes the buffer exactly.
-    if (!g_pinned.p)
-        HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&g_pinned.p), 8 * gsr::TOTALS_U64, hipHostMallocDefault));
-    if (!g_pinned.ev) HIP_OK(hipEventCreateWithFlags(&g_pinned.ev, hipEventDisableTiming));
-    HIP_OK(hipMemcpyAsync(g_pinned.p, totals, totals_bytes, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipEventRecord(g_pinned.ev, s));
-    const unsigned gsx = st_x(width), gsy = st_y(height);
-    const int NS = (int)(gsx * gsy);
-    const bool fused_bin = gsr::st_bin_supported(NS);
-    const bool speculate = fused_bin && g_hint.P == P && g_hint.W == width && g_hint.H == height;
     unsigned long long Pv = 0, R64 = 0, S64 = 0;
     auto read_totals = [&]() -> int {
-        HIP_OK(hipEventSynchronize(g_pinned.ev));
-        Pv = R64 = S64 = 0;
-        for (int k = 0; k < gsr::TOTAL_SLOTS; k++) {
-            Pv += g_pinned.p[gsr::TOTAL_STRIDE * k];
-            R64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 1];
-            S64 += g_pinned.p[gsr::TOTAL_STRIDE * k + 2];
-        }
-        const unsigned errv = reinterpret_cast<unsigned*>(g_pinned.p + gsr::TOTALS_U64 - 1)[0];
+        unsigned long long t[4];
+        const int rc = wait_totals(g_pinned.p, seq, s, t);
+        if (rc != GSR_OK) return rc;
+        Pv = t[0];
+        R64 = t[1];
+        S64 = t[2];
+        const unsigned long long errv = t[3];
         if (errv) return fail(GSR_E_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
         if (R64 > 0x7fffffffull) return fail(GSR_E_OVERFLOW, "gsr_forward: %llu instances overflow int", R64);
         return GSR_OK;
@@ -524,7 +560,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     uint2* ranges = at<uint2>(img, il.ranges);
     char* bin = nullptr;
     BinLayout bl{};
-    // binning into a buffer of capacity (capR, capS); dev: read P_v on the device
+    // binning into a buffer of capacity (capR, capS); dev: read P_v on the device (and run the
+    // frame totals in the scatter)
     auto bin_pass = [&](long long capR, long long capS, bool dev) -> int {
         bl = bin_layout(capR, capS, width, height, dev ? P : (long long)Pv);
         bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
@@ -537,8 +574,9 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         const uint32_t* st_sorted_vals = stv;
         if (fused_bin) {
             GSR_STAGE(ST_DUPLICATE);
-            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? totals : nullptr, sorted_ids, rect_sorted, gsx, NS,
-                               at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, (uint32_t)capS, s);
+            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, NS,
+                               at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, (uint32_t)capS, s,
+                               dev ? &ft : nullptr, at<void>(bin, bl.lists_tmp));
         } else {
             uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
             {
@@ -569,39 +607,22 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                                    at<uint32_t>(bin, bl.scan_tmp), at<void>(bin, bl.lists_tmp),
                                    at<uint32_t>(bin, bl.point), at<uint32_t>(img, il.order_fwd),
                                    at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS, at<uint32_t>(img, il.tile_nmax),
-                                   capR, s);
+                                   capR, s, fused_bin);
         }
         GSR_LAUNCH_CHECK();
         return GSR_OK;
     };
-    int rc;
-    if (speculate) {
-        const long long capR = g_hint.R + g_hint.R / 4 + 65536, capS = g_hint.S + g_hint.S / 4 + 4096;
-        if ((rc = bin_pass(capR, capS, true)) != GSR_OK) return rc;
-        if ((rc = read_totals()) != GSR_OK) return rc;
-        if ((long long)R64 > capR || (long long)S64 > capS) {  // overflow: redo at the exact size
-            if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
-        }
-    } else {
-        if ((rc = read_totals()) != GSR_OK) return rc;
-        if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
-    }
-    const long long R = (long long)R64;
-    g_hint.P = P;
-    g_hint.W = width;
-    g_hint.H = height;
-    g_hint.R = R;
-    g_hint.S = (long long)S64;
-    uint32_t* point_list = at<uint32_t>(bin, bl.point);
-
     gsr::RenderFwdArgs ra;
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
-    ra.ranges = ranges; ra.point_list = point_list; ra.rec = pa.rec; ra.bg = background;
+    ra.ranges = ranges; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
     ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
-    {
+    // the forward tile pass over the binning in `bin`
+    auto render_pass = [&]() -> int {
+        uint32_t* point_list = at<uint32_t>(bin, bl.point);
+        ra.point_list = point_list;
         GSR_STAGE(ST_RENDER_FWD);
         // dispatch order, nheavy and the zeroed tile_nmax come from launch_tile_lists' tile scan
         if (!mc) {
@@ -618,8 +639,31 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                 gsr::launch_render_fwd_mc(ma, s);
             }
         }
+        GSR_LAUNCH_CHECK();
+        return GSR_OK;
+    };
+    int rc;
+    if (speculate) {
+        const long long capR = g_hint.R + g_hint.R / 4 + 65536, capS = g_hint.S + g_hint.S / 4 + 4096;
+        if ((rc = bin_pass(capR, capS, true)) != GSR_OK) return rc;
+        if ((rc = render_pass()) != GSR_OK) return rc;
+        if ((rc = read_totals()) != GSR_OK) return rc;
+        if ((long long)R64 > capR || (long long)S64 > capS) {  // overflow: redo at the exact size
+            if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
+            if ((rc = render_pass()) != GSR_OK) return rc;
+        }
+    } else {
+        if ((rc = read_totals()) != GSR_OK) return rc;
+        if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
+        if ((rc = render_pass()) != GSR_OK) return rc;
     }
-    GSR_LAUNCH_CHECK();
+    const long long R = (long long)R64;
+    g_hint.P = P;
+    g_hint.W = width;
+    g_hint.H = height;
+    g_hint.R = R;
+    g_hint.S = (long long)S64;
+    uint32_t* point_list = at<uint32_t>(bin, bl.point);
 #ifdef GSR_DEBUG
     {
         const int rc_dbg = debug_check_forward(P, R, gx, gy, width, height, radii, pa.rect, pa.depth_key, ranges,

@@ -33,14 +33,12 @@ struct PreprocessArgs {
     uint32_t* depth_key;
     uint2* rect;
     Rec* rec;
-    unsigned* err_flag;
-    unsigned long long* totals;  // [TOTAL_SLOTS][TOTAL_STRIDE]: [0..2] += P_v, R, S (zeroed by the caller; the host sums)
+    // per 256-Gaussian workgroup (optional, null to skip): blk_tot[b] = (visible, instances
+    // R, super-tile entries S, prefiltered-error flag)
+    uint4* blk_tot;
 };
-constexpr int TOTAL_SLOTS = 128;  // spread of the totals' atomics (one slot per 1/128 of the blocks)
-constexpr int TOTAL_STRIDE = 16;  // u64 per slot: one 128-B line each, so slots do not share an L2 line
-// + one line holding the error flag (its last u64): 16.1 KiB, a multiple of 16 B, so the
-// zeroing is ONE fill dispatch (an odd tail costs rocclr a second ~5 us dispatch)
-constexpr int TOTALS_U64 = TOTAL_SLOTS * TOTAL_STRIDE + TOTAL_STRIDE;
+constexpr int PRE_THREADS = 256;
+inline int pre_blocks(long long P) { return (int)((P + PRE_THREADS - 1) / PRE_THREADS); }
 
 void launch_preprocess(const PreprocessArgs& a, hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* viewmatrix, bool* present, hipStream_t s);
@@ -85,6 +83,28 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
 // table[d][0..nb) -> exclusive prefix within each of ndigits rows; digit_tot[d] = row total
 void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot, hipStream_t s);
 
+// The forward's depth sort of all P keys (stable LSD, 4 passes of 8 bits, values = indices,
+// an 8-B side payload moving along).  The last pass also stores the visible count P_v (the
+// start of the culled keys' top byte 0xFF) to *pv_out.  Returns 1 if the result is in the
+// alt buffers.
+size_t depth_sort_temp_bytes(long long P);
+int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
+               uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
+               unsigned long long* pv_out, hipStream_t s);
+
+// The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
+// (P_v, R, S, error) and stores them to host-mapped memory as (value << 16 | seq mod 2^16)
+// words; the host polls until all four carry its call's tag (no copy or event on the stream:
+// each left a 6-19 us bubble between kernels).  Run as an extra workgroup of the super-tile
+// scatter (launch_st_bin), or on its own (launch_frame_totals).
+struct FrameTotals {
+    const uint4* blk_tot;
+    int nblk;
+    unsigned long long* host;  // device address of the host-mapped words
+    unsigned long long seq;
+};
+void launch_frame_totals(const FrameTotals& ft, hipStream_t s);
+
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
 // Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
 // order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1365.
@@ -92,11 +112,14 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 size_t st_bin_temp_bytes(long long Pv, int NS);
 bool st_bin_supported(int NS);
 // Pv: the visible count, or (with dev_totals non-null) its upper bound P, the kernels then
-// summing the preprocess's per-slot totals on the device.  Entries at positions >= cap are
+// reading the visible count *dev_totals (depth_sort's pv_out) on the device.  Entries at positions >= cap are
 // not written (the speculative forward detects the overflow and redoes the binning).
+// ft (optional): the frame totals run as one extra workgroup of the scatter.  lists_temp
+// (optional): launch_tile_lists' scratch, whose segment table is then built here (pass
+// seg_table_ready to launch_tile_lists).
 void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
                    unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
-                   uint32_t cap, hipStream_t s);
+                   uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr, void* lists_temp = nullptr);
 // In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
 // super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
@@ -109,12 +132,15 @@ constexpr uint32_t ST_KEY_MASK = (1u << ST_KEY_BITS) - 1u;
 void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s);
 // Per-super-tile tile filters over 1024-entry segments: tile counts, tile starts (scan),
 // ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).  S: the entry capacity (the
-// real count is read from st_ranges on the device); point_list entries >= cap_r are dropped.
+// real count is read from st_ranges on the device); point_list entries >= cap_r are dropped
+// and the ranges are clamped to cap_r, so a tile pass over an overflowed binning reads only
+// written entries (the forward then redoes the binning).
 size_t tile_lists_temp_bytes(long long S, int nst);
 void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
                        unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
                        uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s);
+                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s,
+                       bool seg_table_ready = false);
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of

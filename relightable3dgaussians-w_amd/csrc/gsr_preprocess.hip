@@ -41,7 +41,8 @@ __device__ __forceinline__ void load_gauss(const PreprocessArgs& a, const int id
 // super-tile counts (0 when culled).
 template <int MAXD = 3>
 __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const int idx, const GaussIn& g,
-                                               uint32_t& tiles, uint32_t& stc, const float* sh_row) {
+                                               uint32_t& tiles, uint32_t& stc, const float* sh_row, uint32_t& key_out,
+                                               bool& err) {
     tiles = stc = 0;
     int irad = 0;
     uint32_t key = 0xFFFFFFFFu;  // culled Gaussians sort after every visible depth
@@ -50,7 +51,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
         // in_frustum (auxiliary.h:139-164): near cull only
         const float3 p_view = xform_point4x3(p_orig, a.viewmatrix);
         if (p_view.z <= 0.2f) {
-            if (a.prefiltered) atomicOr(a.err_flag, 1u);
+            if (a.prefiltered) err = true;
             break;
         }
         const float4 p_hom = xform_point4x4(p_orig, a.projmatrix);
@@ -102,19 +103,38 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
               ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
     } while (false);
     a.depth_key[idx] = key;
+    key_out = key;
     a.radii[idx] = irad;
     a.tiles[idx] = tiles;
     a.st_count[idx] = stc;
 }
 
-// Preprocess + the frame totals (visible count P_v, instances R, super-tile entries S):
-// workgroup sums, one atomic per workgroup and total into one of TOTAL_SLOTS slots (a
-// single address per total serialises ~6k atomics; the host adds the slots).
+// Workgroup epilogue: the workgroup's totals (visible, R, S, error), a plain store -- no
+// atomics and no zero-filled buffer: the depth sort's first histogram launch sums them.
+__device__ __forceinline__ void preprocess_block_out(const PreprocessArgs& a, uint32_t tiles, uint32_t stc, bool err) {
+    __shared__ uint32_t s_w[4][PRE_THREADS / 64];
+    uint32_t v[4] = {tiles > 0 ? 1u : 0u, tiles, stc, err ? 1u : 0u};
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
+        if (lane == 0) s_w[k][wave] = v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && a.blk_tot) {
+        uint32_t t[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) t[k] = s_w[k][0] + s_w[k][1] + s_w[k][2] + s_w[k][3];
+        a.blk_tot[blockIdx.x] = make_uint4(t[0], t[1], t[2], t[3]);
+    }
+}
+
+// Preprocess + the per-workgroup totals.
 // The workgroup's SH rows (256 x M x 3 floats, contiguous) are first copied to LDS with
 // 16-B coalesced loads (row stride M*3+1 against bank conflicts); each thread then reads
 // its own row from LDS instead of 12 strided 16-B loads.
 __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
-    __shared__ unsigned long long sh[3][4];
     extern __shared__ float s_sh[];
     const int g0 = blockIdx.x * blockDim.x;
     const int idx = g0 + threadIdx.x;
@@ -145,23 +165,11 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
         }
         __syncthreads();
     }
-    uint32_t tiles = 0, stc = 0;
+    uint32_t tiles = 0, stc = 0, key = 0;
+    bool err = false;
     if (idx < a.P)
-        preprocess_one(a, idx, gin, tiles, stc, staged ? s_sh + threadIdx.x * stride : nullptr);
-    unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-        if (lane == 0) sh[k][wave] = v[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const int k = threadIdx.x;
-        const unsigned long long t = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
-        if (t) atomicAdd(a.totals + TOTAL_STRIDE * (blockIdx.x % TOTAL_SLOTS) + k, t);
-    }
+        preprocess_one(a, idx, gin, tiles, stc, staged ? s_sh + threadIdx.x * stride : nullptr, key, err);
+    preprocess_block_out(a, tiles, stc, err);
 }
 
 // SH path with M in {1, 4, 9, 16}: each thread loads its own SH row into registers with
@@ -170,7 +178,6 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
 // LDS-staged k_preprocess, which serves any other M).
 template <int M>
 __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
-    __shared__ unsigned long long sh[3][4];
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     GaussIn gin;
     float shr[3 * M];
@@ -191,22 +198,11 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
             for (int k = 0; k < 3 * M; k++) shr[k] = a.shs[(size_t)idx * 3 * M + k];
         }
     }
-    uint32_t tiles = 0, stc = 0;
-    if (idx < a.P) preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr);
-    unsigned long long v[3] = {tiles > 0 ? 1ull : 0ull, tiles, stc};
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o, 64);
-        if (lane == 0) sh[k][wave] = v[k];
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const int k = threadIdx.x;
-        const unsigned long long t = sh[k][0] + sh[k][1] + sh[k][2] + sh[k][3];
-        if (t) atomicAdd(a.totals + TOTAL_STRIDE * (blockIdx.x % TOTAL_SLOTS) + k, t);
-    }
+    uint32_t tiles = 0, stc = 0, key = 0;
+    bool err = false;
+    if (idx < a.P)
+        preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr, key, err);
+    preprocess_block_out(a, tiles, stc, err);
 }
 
 

@@ -205,7 +205,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     a.dL_dmean2D[3 * idx + 0] = dm2x;
     a.dL_dmean2D[3 * idx + 1] = dm2y;
     a.dL_dmean2D[3 * idx + 2] = 0.f;
-    *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
+    if (a.dL_dconic)  // the reference allocates it but returns it to no one (rasterize_points.cu:145,186)
+        *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
     a.dL_dopacity[idx] = dop;
     if (a.dL_dcolor) {  // absent for the multi-channel composite (its features have their own gradient)
         a.dL_dcolor[3 * idx + 0] = dcol0;

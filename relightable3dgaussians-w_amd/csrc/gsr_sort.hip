@@ -62,29 +62,51 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const 
 }
 
 // hist[d][0..nb) -> exclusive prefix within digit d; digit_tot[d] = the digit's total
-__global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int nb, uint32_t* digit_tot) {
-    __shared__ uint32_t sh[4];
-    uint32_t* h = hist + (long long)blockIdx.x * nb;
+// One row in place: each thread owns a contiguous chunk (all its loads in flight at once),
+// one block scan of the chunk sums, then the chunk prefixes (one pass instead of one block
+// scan per 256 columns: the depth sort's first table has ~6k columns per row at 1.5M keys).
+__device__ __forceinline__ void digit_row_scan(uint32_t* h, int ncol, uint32_t* total, uint32_t* sh) {
+    constexpr int CH = 32;  // columns per thread per round (8192 per round)
     uint32_t carry = 0;
-    for (int c = 0; c < nb; c += SORT_THREADS) {
-        const int i = c + threadIdx.x;
-        const uint32_t v = i < nb ? h[i] : 0u;
+    for (int c0 = 0; c0 < ncol; c0 += CH * SORT_THREADS) {
+        const int b = c0 + threadIdx.x * CH;
+        uint32_t v[CH], sum = 0;
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+            v[k] = b + k < ncol ? h[b + k] : 0u;
+            sum += v[k];
+        }
         uint32_t tot;
-        const uint32_t ex = block256_exclusive_scan(v, sh, &tot);
-        if (i < nb) h[i] = carry + ex;
+        uint32_t run = carry + block256_exclusive_scan(sum, sh, &tot);
+#pragma unroll
+        for (int k = 0; k < CH; k++) {
+            if (b + k < ncol) h[b + k] = run;
+            run += v[k];
+        }
         carry += tot;
     }
-    if (threadIdx.x == 0) digit_tot[blockIdx.x] = carry;
+    if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int nb, uint32_t* digit_tot) {
+    __shared__ uint32_t sh[4];
+    digit_row_scan(hist + (long long)blockIdx.x * nb, nb, digit_tot + blockIdx.x, sh);
 }
 
 // AUX: an 8-byte side payload (the Gaussians' tile rects) moves with every pair, so that the
 // depth-sorted order never has to gather it at random afterwards
+// The offsets table has ocol columns (0: nb) and block blk's column is blk * ostride (the
+// preprocess-made first table of the depth sort has 8 columns per 2048-key block).
+// (Counting the NEXT pass's histogram here with global atomics per key, instead of the
+// separate k_radix_hist, measured 5-15x slower: ~1.5M L2 atomics per pass.)
 template <bool AUX>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
                                                                   const uint32_t* offsets, const uint32_t* digit_tot,
                                                                   int nb, uint32_t* keys_out, uint32_t* vals_out,
-                                                                  const uint2* aux_in, uint2* aux_out) {
+                                                                  const uint2* aux_in, uint2* aux_out, int ocol = 0,
+                                                                  int ostride = 1,
+                                                                  unsigned long long* pv_out = nullptr) {
     __shared__ uint32_t s_keys[SORT_TILE];
     __shared__ uint32_t s_vals[SORT_TILE];
     __shared__ uint2 s_aux[AUX ? SORT_TILE : 1];
@@ -136,7 +158,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         wh[3][d] = start + c0 + c1 + c2;
         dstart[d] = start;
         const uint32_t dbase = block256_exclusive_scan(digit_tot[d], scan_sh, (uint32_t*)nullptr);
-        goff[d] = dbase + offsets[(long long)d * nb + blk];
+        // the depth sort's top-byte pass: culled keys (0xFFFFFFFF) are exactly digit 255, so
+        // its start is the visible count P_v
+        if (pv_out && blockIdx.x == 0 && d == 255) *pv_out = dbase;
+        goff[d] = dbase + offsets[(long long)d * (ocol ? ocol : nb) + (long long)blk * ostride];
     }
     __syncthreads();
 #pragma unroll
@@ -208,6 +233,40 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
         cur ^= 1;
     }
     return cur ^ 1;  // the buffer pair written last
+}
+
+size_t depth_sort_temp_bytes(long long P) {
+    const size_t nb = (size_t)sort_blocks(P);
+    return 4 * (256 * nb + 256) + 256;
+}
+
+int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
+               uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
+               unsigned long long* pv_out, hipStream_t s) {
+    if (P <= 0) return -1;
+    const int nb = sort_blocks(P);
+    uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
+    uint32_t* digit_tot = hist + 256LL * nb;
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = nullptr;  // values 0..P-1
+    uint32_t* out_k[2] = {keys, keys_alt};
+    uint32_t* out_v[2] = {vals, vals_alt};
+    const uint2* ain = aux_in;
+    uint2* out_a[2] = {aux, aux_alt};
+    int cur = 0;
+    for (int pass = 0; pass < 4; pass++) {
+        const int shift = 8 * pass;
+        hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, shift, 255u, hist, nb);
+        hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
+        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift, 255u, hist,
+                           digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1,
+                           pass == 3 ? pv_out : (unsigned long long*)nullptr);
+        ain = out_a[cur];
+        kin = out_k[cur];
+        vin = out_v[cur];
+        cur ^= 1;
+    }
+    return cur ^ 1;
 }
 
 int radix_sort_pairs(long long n, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt,

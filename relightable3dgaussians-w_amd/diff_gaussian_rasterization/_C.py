@@ -121,17 +121,18 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     P = means3D.size(0)
     H, W = dL_dout_color.size(1), dL_dout_color.size(2)
     M = sh.size(1) if sh.numel() != 0 and sh.size(0) != 0 else 0
-    alloc = torch.zeros if P == 0 else torch.empty
-    f = dict(dtype=torch.float32, device=dev)
-    dL_dmeans2D = alloc((P, 3), **f)
-    dL_dcolors = alloc((P, NUM_CHANNELS), **f)
-    dL_dconic = alloc((P, 2, 2), **f)
-    dL_dopacity = alloc((P, 1), **f)
-    dL_dmeans3D = alloc((P, 3), **f)
-    dL_dcov3D = alloc((P, 6), **f)
-    dL_dsh = alloc((P, M, 3), **f)
-    dL_dscales = alloc((P, 3), **f)
-    dL_drotations = alloc((P, 4), **f)
+    # one allocation for the eight outputs (views of one flat buffer: each is written in full,
+    # and the allocator calls were the host-side cost of this call); the reference's
+    # dL_dconic is never returned, so it is not computed (NULL)
+    widths = (3, NUM_CHANNELS, 1, 3, 6, 3 * M, 3, 4)
+    flat = (torch.zeros if P == 0 else torch.empty)(P * sum(widths), dtype=torch.float32, device=dev)
+    outs, o = [], 0
+    for w in widths:
+        outs.append(flat[o:o + P * w])
+        o += P * w
+    dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations = (
+        outs[0].view(P, 3), outs[1].view(P, NUM_CHANNELS), outs[2].view(P, 1), outs[3].view(P, 3),
+        outs[4].view(P, 6), outs[5].view(P, M, 3), outs[6].view(P, 3), outs[7].view(P, 4))
     if P != 0:
         keep = [_f32(x) for x in (background, means3D, sh, colors, scales, rotations, cov3D_precomp, viewmatrix,
                                   projmatrix, campos, dL_dout_color)]
@@ -142,7 +143,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             P, int(degree), M, int(R), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(sh_), _lib.fptr(col_),
             _lib.fptr(sc_), float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_),
             _lib.fptr(cp_), float(tan_fovx), float(tan_fovy), radii_.data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
-            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(),
+            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), None,
             dL_dopacity.data_ptr(), dL_dcolors.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
             dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(), _lib.stream_of(dev))
         _lib.check(ret, "rasterize_gaussians_backward")
@@ -217,7 +218,7 @@ def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch,
     H, W = dL_dout.size(1), dL_dout.size(2)
     alloc = torch.zeros if P == 0 else torch.empty
     f = dict(dtype=torch.float32, device=dev)
-    dL_dmeans2D, dL_dconic, dL_dopacity = alloc((P, 3), **f), alloc((P, 2, 2), **f), alloc((P, 1), **f)
+    dL_dmeans2D, dL_dopacity = alloc((P, 3), **f), alloc((P, 1), **f)
     dL_dfeat = alloc((P, feat.size(1)), **f)
     dL_dmeans3D, dL_dcov3D = alloc((P, 3), **f), alloc((P, 6), **f)
     dL_dscales, dL_drotations = alloc((P, 3), **f), alloc((P, 4), **f)
@@ -230,7 +231,7 @@ def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch,
             P, int(nch), feat.size(1), _lib.fptr(feat), int(R), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(sc_),
             float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
             float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
-            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), dL_dconic.data_ptr(), dL_dopacity.data_ptr(),
+            ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(),
             dL_dfeat.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), dL_dscales.data_ptr(),
             dL_drotations.data_ptr(), _lib.stream_of(dev))
         _lib.check(ret, "rasterize_gaussians_channels_backward")
