@@ -14,8 +14,36 @@
 
 namespace gsr {
 
+// One Gaussian's inputs, loaded before the workgroup's SH rows are staged (every global load
+// of the thread in flight at once instead of one dependent round trip after the barrier).
+struct BwdIn {
+    float4 l0, l1;  // accumulator line [0..8)
+    float l2;       // [8]
+    int radius;
+    float3 mean;
+    float4 rot;
+    float3 scl;
+    float cov[6];
+};
+
+__device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx, BwdIn& in) {
+    const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
+    in.l0 = line[0];
+    in.l1 = line[1];
+    in.l2 = a.acc[(size_t)idx * ACC_STRIDE + 8];
+    in.radius = a.radii[idx];
+    in.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    if (a.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) in.cov[i] = a.cov3D_precomp[6 * idx + i];
+    } else {
+        in.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
+        in.scl = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+    }
+}
+
 template <int MC, bool DO_SH = true>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* row);
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* row);
 
 // auxiliary.h:107-117
 __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
@@ -74,12 +102,14 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
     const int M3 = a.M * 3, sh_stride = M3 + 1;
     const int g0 = blockIdx.x * blockDim.x;
     const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
+    BwdIn in;
+    if (g0 + (int)threadIdx.x < a.P) load_bwd_in(a, g0 + threadIdx.x, in);
     if (a.shs) {
         load_rows(s_sh, sh_stride, a.shs + (size_t)g0 * M3, rows, M3);
         __syncthreads();
     }
     const int idx = g0 + threadIdx.x;
-    if (idx < a.P) preprocess_bwd_one<0>(a, idx, s_sh + threadIdx.x * sh_stride);
+    if (idx < a.P) preprocess_bwd_one<0>(a, idx, in, s_sh + threadIdx.x * sh_stride);
     if (a.dL_dsh) {
         __syncthreads();
         store_rows(a.dL_dsh + (size_t)g0 * M3, s_sh, sh_stride, rows, M3);
@@ -195,11 +225,10 @@ __device__ __forceinline__ float3 sh_bwd_row(const PreprocessBwdArgs& a, float3 
 // geometry kernel + a register-row SH kernel, 63 + 196 us -- its strided 16-B row stores
 // write partial lines, where the LDS-staged rows leave the workgroup as whole lines.)
 template <int MC, bool DO_SH>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, float* row) {
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* row) {
     // ---- unpack the render-backward accumulator line ------------------------------
-    const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
-    const float4 l0 = line[0], l1 = line[1];
-    const float l2 = a.acc[(size_t)idx * ACC_STRIDE + 8];
+    const float4 l0 = in.l0, l1 = in.l1;
+    const float l2 = in.l2;
     const float dm2x = l0.x, dm2y = l0.y, dcx = l0.z, dcy = l0.w, dcw = l1.x, dop = l1.y;
     const float dcol0 = l1.z, dcol1 = l1.w, dcol2 = l2;
     a.dL_dmean2D[3 * idx + 0] = dm2x;
@@ -217,7 +246,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     float* dcov = a.dL_dcov3D + 6 * idx;
     float* dsh = row;  // written back by the caller when dL_dsh is requested
     const bool want_dsh = DO_SH && a.dL_dsh != nullptr;
-    if (!(a.radii[idx] > 0)) {
+    if (!(in.radius > 0)) {
         a.dL_dmean3D[3 * idx + 0] = 0.f;
         a.dL_dmean3D[3 * idx + 1] = 0.f;
         a.dL_dmean3D[3 * idx + 2] = 0.f;
@@ -239,16 +268,16 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         }
         return;
     }
-    const float3 mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
+    const float3 mean = in.mean;
     float cov3[6];
     float4 rot = make_float4(0.f, 0.f, 0.f, 0.f);
     float3 scl = make_float3(0.f, 0.f, 0.f);
     if (a.cov3D_precomp) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) cov3[i] = a.cov3D_precomp[6 * idx + i];
+        for (int i = 0; i < 6; i++) cov3[i] = in.cov[i];
     } else {
-        rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
-        scl = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
+        rot = in.rot;
+        scl = in.scl;
         cov3d_from(scl.x, scl.y, scl.z, a.scale_modifier, rot, cov3);
     }
 
