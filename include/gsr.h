@@ -260,10 +260,10 @@ int gsr_knn_mean_dist(int P, const float* points, float* mean_dists, void* works
 /* Private-buffer introspection for tests and profiling: byte offsets of the arrays the
  * forward leaves in its three buffers (layout is private between forward and backward). */
 typedef struct gsr_layout {
-    size_t geom_bytes, img_bytes, bin_bytes;
+    size_t geom_bytes, img_bytes, bin_bytes;  /* bin_bytes: the fixed part (header + super-tile ranges) */
     size_t geom_radii, geom_tiles, geom_depth_key, geom_rect, geom_rec, geom_acc;
-    size_t img_final_T, img_n_contrib, img_ranges;
-    size_t bin_point_list, bin_tile_keys;
+    size_t img_final_T, img_n_contrib, img_ranges, img_tile_nmax, img_tile_emax;
+    size_t bin_st_ranges, bin_entries;
 } gsr_layout;
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
 
@@ -294,6 +294,14 @@ int gsr_get_deterministic(void);
  * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a
  * stream synchronisation, and fails with GSR_E_DEVICE_CHECK naming the first violation. */
 int gsr_debug_build(void);
+/* The binning buffer holds super-tile lists: every (visible Gaussian, 8x4-tile super-tile its
+ * rect touches) entry, per super-tile in (depth, index) order with the entry's local tile rect;
+ * the tile passes filter a tile's list from them.  This writes the reference's point_list [R]
+ * (binningState.point_list after the sort, rasterizer_impl.cu:79-99,303-308) and the tile
+ * ranges [T] (imgState.ranges, identifyTileRanges, rasterizer_impl.cu:101-138) from them:
+ * tests, the GSR_DEBUG checks and the deterministic backward.  Synchronous. */
+int gsr_materialize_lists(int R, int width, int height, void* binning_buffer, unsigned* point_list, unsigned* ranges,
+                          void* stream);
 /* The same verification on demand, over a forward's three buffers (any build; synchronous). */
 int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
                       void* img_buffer, void* stream);

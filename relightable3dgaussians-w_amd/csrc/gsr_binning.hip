@@ -197,9 +197,10 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
     }
 }
 
-// Segment table of the tile filters (SEG entries per segment, see k_seg_lists), in the
-// tile-list scratch (seg_layout).
+// Segment table of the materialised tile lists (SEG entries per segment, see k_seg_lists),
+// in the materialisation scratch (seg_layout).
 constexpr uint32_t SEG = 1024;
+constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32
 struct SegTable {
     uint32_t *seg_st, *seg_e0, *st_seg0, *nseg_total, *seg_cnt;
     uint32_t gcap;  // capacity of the table (segments)
@@ -217,39 +218,26 @@ inline SegTable seg_layout(void* temp, long long S, int nst) {
     return t;
 }
 
-// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total); and
-// (seg non-null) the segment table: every super-tile list cut into segments of SEG entries,
-// segment g covering [seg_e0[g], min(seg_e0[g] + SEG, end of its super-tile)).  One
-// workgroup; the entry totals and the segment counts are scanned together (packed in u64).
+// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total),
+// clamped to the entry capacity (the scatter drops entries beyond it: a tile pass over an
+// overflowed binning then reads only written entries, and the forward redoes the binning);
+// header[0] = the entry count S (read back by the list materialisation)
 __global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, uint32_t* bases, uint2* ranges,
-                                                   SegTable seg) {
-    __shared__ unsigned long long sh[4];
-    unsigned long long carry = 0;
+                                                   unsigned long long* header, uint32_t cap) {
+    __shared__ uint32_t sh[4];
+    uint32_t carry = 0;
     for (int c = 0; c < NS; c += 256) {
         const int i = c + threadIdx.x;
         const uint32_t v = i < NS ? tot[i] : 0u;
-        const uint32_t n = (v + SEG - 1) / SEG;
-        unsigned long long t;
-        const unsigned long long ex = carry + block256_exclusive_scan(((unsigned long long)n << 32) | v, sh, &t);
-        const uint32_t eb = (uint32_t)ex, sb = (uint32_t)(ex >> 32);
+        uint32_t t;
+        const uint32_t ex = carry + block256_exclusive_scan(v, sh, &t);
         if (i < NS) {
-            bases[i] = eb;
-            ranges[i] = v ? make_uint2(eb, eb + v) : make_uint2(0u, 0u);
-            if (seg.seg_st) {
-                seg.st_seg0[i] = sb;
-                for (uint32_t k = 0; k < n && sb + k < seg.gcap; k++) {
-                    seg.seg_st[sb + k] = (uint32_t)i;
-                    seg.seg_e0[sb + k] = eb + k * SEG;
-                }
-            }
+            bases[i] = ex;
+            ranges[i] = v ? make_uint2(min(ex, cap), min(ex + v, cap)) : make_uint2(0u, 0u);
         }
         carry += t;
     }
-    if (seg.seg_st && threadIdx.x == 0) {
-        const uint32_t ns = (uint32_t)(carry >> 32);
-        seg.st_seg0[NS] = ns;
-        *seg.nseg_total = min(ns, seg.gcap);
-    }
+    if (threadIdx.x == 0) header[0] = min(carry, cap);
 }
 
 // Orders a wave's LDS accesses across lanes (LDS executes one wave's instructions in order)
@@ -267,8 +255,8 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 // the run and clears the mask.  Order-independent atomics only, so the output is
 // deterministic, and each super-tile's entries come out in depth order.
 __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                                        unsigned gsx, uint32_t* wcnt, unsigned long long* wmask,
-                                        uint32_t* st_keys, uint32_t* st_vals, uint32_t cap) {
+                                        unsigned gsx, uint32_t* wcnt, unsigned long long* wmask, uint2* ent,
+                                        uint32_t cap) {
     const int lane = threadIdx.x & 63;
     const unsigned long long bit = 1ull << lane, lt = bit - 1ull;
     // the next chunk's rect and id are loaded while this chunk is ranked
@@ -294,10 +282,8 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
                 const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
-                if (pos < cap) {  // S beyond the speculative capacity: the forward redoes the binning
-                    st_keys[pos] = sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS);
-                    st_vals[pos] = gid;
-                }
+                if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
+                    ent[pos] = make_uint2(sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS), gid);
             }
         lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
@@ -317,8 +303,8 @@ template <int ST_W>
 __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
                                                      const uint2* rect_sorted, unsigned gsx, int NS, int nb,
                                                      const uint32_t* table, const uint32_t* wcounts,
-                                                     const uint32_t* bases, uint32_t* st_keys, uint32_t* st_vals,
-                                                     uint32_t cap, FrameTotals ft) {
+                                                     const uint32_t* bases, uint2* ent, uint32_t cap,
+                                                     FrameTotals ft) {
     if (ft.host && (int)blockIdx.x == nb) {  // the extra workgroup: the host's frame totals
         frame_totals(ft);
         return;
@@ -343,8 +329,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
         }
     }
     __syncthreads();
-    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, st_keys,
-                  st_vals, cap);
+    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
 }
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
@@ -358,17 +343,14 @@ size_t st_bin_temp_bytes(long long Pv, int NS) {
 bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
 void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
-                   uint32_t cap, hipStream_t s, const FrameTotals* ftp, void* lists_temp) {
+                   unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
+                   uint32_t cap, hipStream_t s, const FrameTotals* ftp) {
     FrameTotals ft{};
     if (ftp) ft = *ftp;
     if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
         (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
+        (void)hipMemsetAsync(header, 0, 8, s);
         if (ftp) launch_frame_totals(ft, s);
-        if (lists_temp) {  // an empty segment table
-            const SegTable seg = seg_layout(lists_temp, cap, NS);
-            (void)hipMemsetAsync(seg.st_seg0, 0, 4 * ((size_t)NS + 2), s);
-        }
         return;
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
@@ -390,16 +372,14 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
         hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
                            table, wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
-    SegTable seg{};
-    if (lists_temp) seg = seg_layout(lists_temp, cap, NS);
-    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges, seg);
+    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges, header, cap);
     const dim3 grid(nb + (ftp ? 1 : 0));
     if (W == 8)
         hipLaunchKernelGGL(k_st_scatter<8>, grid, dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap, ft);
+                           gsx, NS, nb, table, wcounts, bases, ent, cap, ft);
     else
         hipLaunchKernelGGL(k_st_scatter<4>, grid, dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, st_keys, st_vals, cap, ft);
+                           gsx, NS, nb, table, wcounts, bases, ent, cap, ft);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
@@ -419,8 +399,16 @@ __global__ void __launch_bounds__(256) k_seg_ranges(long long n, const uint32_t*
     if (i == n - 1) ranges[cur].y = (uint32_t)n;
 }
 
-// ---- 4. per-super-tile tile filters ------------------------------------------------------
-constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32
+// the non-fused path's sorted (key, id) pairs -> entries; header[0] = S
+__global__ void __launch_bounds__(256) k_pack_entries(long long n, const uint32_t* keys, const uint32_t* vals,
+                                                       uint2* ent, unsigned long long* header) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) header[0] = (unsigned long long)n;
+    if (i < n) ent[i] = make_uint2(keys[i], vals[i]);
+}
+
+// ---- 4. tile lists from the super-tile lists (materialised for tests, the GSR_DEBUG checks
+// and the deterministic backward; the tile passes filter the super-tile lists themselves) ----
 
 struct StGeom {
     unsigned tx0, ty0, nx, ny;
@@ -434,7 +422,7 @@ __device__ __forceinline__ StGeom st_geom(unsigned st, unsigned gsx, unsigned gx
     return g;
 }
 
-// Segment table (the non-fused binning path; the fused one builds it in k_st_bases).
+// Segment table of the materialisation.
 
 __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_ranges, uint32_t* seg_st,
                                                     uint32_t* seg_e0, uint32_t* st_seg0, uint32_t* nseg_total,
@@ -474,7 +462,7 @@ __global__ void __launch_bounds__(256) k_seg_table(int nst, const uint2* st_rang
 template <bool WRITE>
 __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, const uint32_t* seg_st,
                                                     const uint32_t* seg_e0, const uint2* st_ranges,
-                                                    const uint32_t* st_keys, const uint32_t* st_vals, unsigned gx,
+                                                    const uint2* ent, unsigned gx,
                                                     unsigned gy, unsigned gsx, uint32_t* seg_cnt,
                                                     const uint32_t* seg_base, const uint32_t* tile_start,
                                                     uint32_t* point_list, uint32_t cap_s, uint32_t cap_r) {
@@ -502,8 +490,9 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
 #pragma unroll
     for (int j = 0; j < NB; j++) {
         const uint32_t e = e0 + 256u * j + tid;
-        kb[j] = e < e1 ? st_keys[e] : 0u;
-        vb[j] = (WRITE && e < e1) ? st_vals[e] : 0u;
+        const uint2 v = e < e1 ? ent[e] : make_uint2(0u, 0u);
+        kb[j] = v.x;
+        vb[j] = v.y;
     }
 #pragma unroll
     for (int j = 0; j < NB; j++) {
@@ -627,7 +616,8 @@ __global__ void __launch_bounds__(1024) k_tile_scan(int T, const uint32_t* cnt, 
         carry += all;
         __syncthreads();
     }
-    for (int t = tid; t < T; t += 1024) tile_nmax[t] = 0;
+    if (tile_nmax)
+        for (int t = tid; t < T; t += 1024) tile_nmax[t] = 0;
 }
 
 // ---- host launchers ---------------------------------------------------------------------
@@ -638,50 +628,46 @@ void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets,
                        st_vals);
 }
 
-void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s) {
+void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, const uint32_t* sorted_vals, uint2* ranges,
+                       uint2* ent, unsigned long long* header, hipStream_t s) {
     (void)hipMemsetAsync(ranges, 0, sizeof(uint2) * (size_t)nseg, s);
-    if (n == 0) return;
-    hipLaunchKernelGGL(k_seg_ranges, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, sorted_keys, ranges);
+    if (n == 0) {
+        (void)hipMemsetAsync(header, 0, 8, s);
+        return;
+    }
+    const unsigned nb = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(k_seg_ranges, dim3(nb), dim3(256), 0, s, n, sorted_keys, ranges);
+    hipLaunchKernelGGL(k_pack_entries, dim3(nb), dim3(256), 0, s, n, sorted_keys, sorted_vals, ent, header);
 }
 
-size_t tile_lists_temp_bytes(long long S, int nst) {
+size_t materialize_temp_bytes(long long S, int nst, int T) {
     const size_t G = seg_capacity(S, nst);
-    return 4 * (2 * G + (nst + 1) + 1 + G * ST_TILES) + 256;
+    return 4 * (2 * G + (nst + 1) + 1 + G * ST_TILES) + 8 * (size_t)T + 1024;
 }
 
-void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
-                       unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
-                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s, bool seg_table_ready) {
+void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint2* ent, unsigned gx, unsigned gy,
+                        unsigned gsx, void* temp, uint32_t* point_list, uint2* ranges, long long R, hipStream_t s) {
     const int T = (int)(gx * gy);
     const SegTable tab = seg_layout(temp, S, nst);
     const size_t G = tab.gcap;
-    uint32_t* seg_st = tab.seg_st;
-    uint32_t* seg_e0 = tab.seg_e0;
-    uint32_t* st_seg0 = tab.st_seg0;
-    uint32_t* nseg_total = tab.nseg_total;
-    uint32_t* seg_cnt = tab.seg_cnt;
-    if (!seg_table_ready)
-        hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, seg_st, seg_e0, st_seg0, nseg_total,
-                           (uint32_t)G);
-    if (G > 0) {
-        hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
-                           st_ranges, st_keys, st_vals, gx, gy, gsx, seg_cnt, (const uint32_t*)nullptr,
-                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t)S, (uint32_t)cap_r);
-    }
+    uint32_t* tile_cnt = tab.seg_cnt + G * ST_TILES;
+    uint32_t* tile_start = tile_cnt + T;
+    hipLaunchKernelGGL(k_seg_table, dim3(1), dim3(256), 0, s, nst, st_ranges, tab.seg_st, tab.seg_e0, tab.st_seg0,
+                       tab.nseg_total, (uint32_t)G);
+    if (G > 0)
+        hipLaunchKernelGGL(k_seg_lists<false>, dim3((unsigned)G), dim3(256), 0, s, tab.nseg_total, tab.seg_st,
+                           tab.seg_e0, st_ranges, ent, gx, gy, gsx, tab.seg_cnt, (const uint32_t*)nullptr,
+                           (const uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t)S, (uint32_t)R);
     // k_seg_prefix writes every tile's count (the super-tiles partition the grid)
     const int np = nst * (int)ST_TILES;
-    hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, st_seg0, gx, gy, gsx, seg_cnt,
-                       tile_cnt, (uint32_t)G);
-    (void)scan_tmp;
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, tile_nmax,
-                       (uint32_t)min(cap_r, (long long)0xFFFFFFFFll));
-    launch_tile_order((unsigned)T, ranges, nullptr, order, nheavy, heavy_bits, s);
-    if (G > 0) {
-        hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, nseg_total, seg_st, seg_e0,
-                           st_ranges, st_keys, st_vals, gx, gy, gsx, (uint32_t*)nullptr, seg_cnt, tile_start,
-                           point_list, (uint32_t)S, (uint32_t)cap_r);
-    }
+    hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, tab.st_seg0, gx, gy, gsx,
+                       tab.seg_cnt, tile_cnt, (uint32_t)G);
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, (uint32_t*)nullptr,
+                       (uint32_t)min(R, (long long)0xFFFFFFFFll));
+    if (G > 0)
+        hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, tab.nseg_total, tab.seg_st,
+                           tab.seg_e0, st_ranges, ent, gx, gy, gsx, (uint32_t*)nullptr, tab.seg_cnt, tile_start,
+                           point_list, (uint32_t)S, (uint32_t)R);
 }
 
 }  // namespace gsr

@@ -62,12 +62,12 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, order_fwd, order_bwd, nheavy, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, order_fwd, order_bwd, nheavy, total;
 };
+// The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
+// S (all the backward needs), then the forward's binning scratch.
 struct BinLayout {
-    size_t point, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_bin_tmp, st_ranges, tile_cnt, tile_start,
-        scan_tmp,
-        lists_tmp, total;
+    size_t header, st_ranges, ent, st_keys, st_vals, st_keys_alt, st_vals_alt, sort_tmp, st_bin_tmp, total;
 };
 
 GeomLayout geom_layout(long long P) {
@@ -105,8 +105,9 @@ ImgLayout img_layout(int W, int H) {
     const size_t T = (size_t)tiles_x(W) * tiles_y(H);
     L.final_T = c.take(4 * N);
     L.n_contrib = c.take(4 * N);
-    L.ranges = c.take(8 * T);
+    L.ranges = c.take(8 * T);  // the reference's tile ranges: filled only by the list materialisation
     L.tile_nmax = c.take(4 * T);
+    L.tile_emax = c.take(4 * T);
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
     L.nheavy = c.take(4 * 16);  // forward [0..8), backward [8..16)
@@ -117,25 +118,22 @@ ImgLayout img_layout(int W, int H) {
 unsigned st_x(int W) { return (tiles_x(W) + GSR_ST_W - 1) / GSR_ST_W; }
 unsigned st_y(int H) { return (tiles_y(H) + GSR_ST_H - 1) / GSR_ST_H; }
 
-// point_list first: the backward needs only it (offset 0, independent of S)
-BinLayout bin_layout(long long R, long long S, int W, int H, long long Pv) {
+// capS: the entry capacity (0: the fixed part only, as the backward computes it)
+BinLayout bin_layout(long long capS, int W, int H, long long Pv) {
     Carver c;
     BinLayout L;
-    const size_t NS = (size_t)st_x(W) * st_y(H), T = (size_t)tiles_x(W) * tiles_y(H);
+    const size_t NS = (size_t)st_x(W) * st_y(H);
     const bool fused = gsr::st_bin_supported((int)NS);
-    L.point = c.take(4 * R);
-    L.st_keys = c.take(4 * S);
-    L.st_vals = c.take(4 * S);
-    // emit + sort fallback for very large images (NS > 4096 super-tiles)
-    L.st_keys_alt = c.take(fused ? 0 : 4 * S);
-    L.st_vals_alt = c.take(fused ? 0 : 4 * S);
-    L.sort_tmp = c.take(fused ? 0 : gsr::radix_sort_temp_bytes(S));
-    L.st_bin_tmp = c.take(fused ? gsr::st_bin_temp_bytes(Pv, (int)NS) : 0);
+    L.header = c.take(16);
     L.st_ranges = c.take(8 * NS);
-    L.tile_cnt = c.take(4 * T);
-    L.tile_start = c.take(4 * T);
-    L.scan_tmp = c.take(4 * (size_t)gsr::scan_blocks((long long)T) + 16);
-    L.lists_tmp = c.take(gsr::tile_lists_temp_bytes(S, (int)NS));
+    L.ent = c.take(8 * capS);
+    // emit + sort path for very large images (NS > 1365 super-tiles)
+    L.st_keys = c.take(fused ? 0 : 4 * capS);
+    L.st_vals = c.take(fused ? 0 : 4 * capS);
+    L.st_keys_alt = c.take(fused ? 0 : 4 * capS);
+    L.st_vals_alt = c.take(fused ? 0 : 4 * capS);
+    L.sort_tmp = c.take(fused ? 0 : gsr::radix_sort_temp_bytes(capS));
+    L.st_bin_tmp = c.take(fused ? gsr::st_bin_temp_bytes(Pv, (int)NS) : 0);
     L.total = c.o + 256;
     return L;
 }
@@ -210,7 +208,8 @@ struct Scratch {
         return p;
     }
 };
-thread_local Scratch g_scratch;
+thread_local Scratch g_scratch;   // deterministic rows
+thread_local Scratch g_scratch2;  // list materialisation, debug checks
 
 // Wait until the device has stored the four totals of call `seq` (frame_totals: each word is
 // value << 16 | seq mod 2^16) and unpack them into out[0..3].  Spins on the coherent
@@ -249,7 +248,7 @@ enum Stage {
     ST_BWD_ZERO, ST_RENDER_BWD, ST_PREPROCESS_BWD, ST_SHADE_FWD, ST_SHADE_BWD, ST_COUNT
 };
 const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "st_emit",
-                                     "st_sort",     "tile_lists",       "render_fwd",     "bwd_zero",     "render_bwd",
+                                     "st_sort",     "tile_order",       "render_fwd",     "bwd_zero",     "render_bwd",
                                      "preprocess_bwd", "shade_fwd", "shade_bwd"};
 // Forward calls run on the Python thread and backward calls on autograd's device thread,
 // so the pending list and the event pool are guarded by one mutex.
@@ -299,16 +298,46 @@ const char* debug_code_name(unsigned c) {
     return c < sizeof(names) / sizeof(names[0]) ? names[c] : "unknown";
 }
 
-// GSR_DEBUG: verify the forward's tile lists and n_contrib (gsr_det.hip), synchronously
+// The reference's point_list [R] and tile ranges [T] from a forward's super-tile lists
+// (synchronous: reads S from the binning buffer's header).  out_pl / out_ranges: device
+// buffers of R and T entries; scratch from g_scratch2 beyond `keep` bytes.
+int materialize_lists(long long R, int W, int H, const char* bin, uint32_t* out_pl, uint2* out_ranges, hipStream_t s) {
+    const BinLayout bl = bin_layout(0, W, H, 0);
+    unsigned long long S = 0;
+    HIP_OK(hipMemcpyAsync(&S, bin + bl.header, 8, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    const unsigned gx = tiles_x(W), gy = tiles_y(H), gsx = st_x(W);
+    const int NS = (int)(st_x(W) * st_y(H)), T = (int)(gx * gy);
+    void* tmp = g_scratch2.get(gsr::materialize_temp_bytes((long long)S, NS, T));
+    if (!tmp) return fail(GSR_E_ALLOC, "list materialisation: scratch allocation failed");
+    gsr::launch_materialize((long long)S, NS, reinterpret_cast<const uint2*>(bin + bl.st_ranges),
+                            reinterpret_cast<const uint2*>(bin + bl.ent), gx, gy, gsx, tmp, out_pl, out_ranges, R, s);
+    GSR_LAUNCH_CHECK();
+    HIP_OK(hipStreamSynchronize(s));
+    return GSR_OK;
+}
+
+// GSR_DEBUG: verify the forward's tile lists (materialised) and n_contrib (gsr_det.hip),
+// synchronously
 int debug_check_forward(int P, long long R, unsigned gx, unsigned gy, int W, int H, const int* radii, const uint2* rect,
-                        const uint32_t* depth_key, const uint2* ranges, const uint32_t* point_list,
-                        const uint32_t* n_contrib, hipStream_t s) {
-    const size_t bytes = 256 + 4 * (size_t)P;
+                        const uint32_t* depth_key, const char* bin, const uint32_t* n_contrib, hipStream_t s) {
+    const size_t T = (size_t)gx * gy;
+    const size_t off_pl = 256 + 4 * (size_t)P, off_rg = off_pl + ((4 * (size_t)R + 255) & ~(size_t)255);
+    const size_t bytes = off_rg + 8 * T + 256;
+    // the report, counters and lists in g_scratch; materialisation scratch in g_scratch2
     char* sc = reinterpret_cast<char*>(g_scratch.get(bytes));
     if (!sc) return fail(GSR_E_ALLOC, "GSR_DEBUG: scratch allocation failed");
-    HIP_OK(hipMemsetAsync(sc, 0, bytes, s));
+    uint32_t* pl = reinterpret_cast<uint32_t*>(sc + off_pl);
+    uint2* ranges = reinterpret_cast<uint2*>(sc + off_rg);
+    if (R > 0 && bin) {
+        const int rc = materialize_lists(R, W, H, bin, pl, ranges, s);
+        if (rc != GSR_OK) return rc;
+    } else {
+        HIP_OK(hipMemsetAsync(ranges, 0, 8 * T, s));
+    }
+    HIP_OK(hipMemsetAsync(sc, 0, off_pl, s));
     auto* rep = reinterpret_cast<gsr::DebugReport*>(sc);
-    gsr::launch_check_lists(P, R, gx, gy, W, H, radii, rect, depth_key, ranges, point_list, n_contrib,
+    gsr::launch_check_lists(P, R, gx, gy, W, H, radii, rect, depth_key, ranges, pl, n_contrib,
                             reinterpret_cast<uint32_t*>(sc + 256), reinterpret_cast<unsigned long long*>(sc + 64), rep, s);
     GSR_LAUNCH_CHECK();
     gsr::DebugReport h{};
@@ -333,11 +362,13 @@ struct McSpec {
 };
 constexpr int MC_GROUP = 16;
 
-gsr::RenderMcArgs mc_args(int W, int H, unsigned gx, unsigned gy, const uint2* ranges, const uint32_t* point_list,
-                          const gsr::Rec* rec, const uint32_t* order, const uint32_t* nheavy, const McSpec& mc, int c0) {
+gsr::RenderMcArgs mc_args(int W, int H, unsigned gx, unsigned gy, unsigned gsx, const uint2* st_ranges, const uint2* ent,
+                          const gsr::Rec* rec, const uint32_t* order, const uint32_t* nheavy, uint32_t* tile_nmax,
+                          uint32_t* tile_emax, const McSpec& mc, int c0) {
     gsr::RenderMcArgs m{};
     m.W = W; m.H = H; m.grid_x = gx; m.grid_y = gy;
-    m.ranges = ranges; m.point_list = point_list; m.rec = rec;
+    m.st_ranges = st_ranges; m.ent = ent; m.gsx = gsx; m.rec = rec;
+    m.tile_nmax = tile_nmax; m.tile_emax = tile_emax;
     m.feat = reinterpret_cast<const float4*>(mc.features + c0);
     m.fstride4 = mc.fstride / 4;
     m.fstride = mc.fstride;
@@ -368,14 +399,24 @@ int gsr_check_buffers(int P, int R, int width, int height, const int* radii, voi
         return fail(GSR_E_ARG, "gsr_check_buffers: bad arguments");
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R, 0, width, height, 0);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
     return debug_check_forward(P, R, tiles_x(width), tiles_y(height), width, height, radii, at<uint2>(geom, gl.rect),
-                               at<uint32_t>(geom, gl.depth_key), at<uint2>(img, il.ranges),
-                               bin ? at<uint32_t>(bin, bl.point) : nullptr, at<uint32_t>(img, il.n_contrib),
+                               at<uint32_t>(geom, gl.depth_key), bin, at<uint32_t>(img, il.n_contrib),
                                reinterpret_cast<hipStream_t>(stream_));
+}
+
+int gsr_materialize_lists(int R, int width, int height, void* binning_buffer, unsigned* point_list, unsigned* ranges,
+                          void* stream_) {
+    if (R < 0 || width <= 0 || height <= 0 || !ranges || (R > 0 && (!binning_buffer || !point_list)))
+        return fail(GSR_E_ARG, "gsr_materialize_lists: bad arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
+    if (R == 0) {
+        HIP_OK(hipMemsetAsync(ranges, 0, 8 * (size_t)tiles_x(width) * tiles_y(height), s));
+        return GSR_OK;
+    }
+    return materialize_lists(R, width, height, align_base(binning_buffer), point_list, reinterpret_cast<uint2*>(ranges), s);
 }
 
 int gsr_debug_build(void) {
@@ -425,7 +466,8 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     if (!out || P < 0 || R < 0 || width < 0 || height < 0) return fail(GSR_E_ARG, "gsr_get_layout: bad arguments");
     const GeomLayout g = geom_layout(P);
     const ImgLayout im = img_layout(width, height);
-    const BinLayout b = bin_layout(R, 0, width, height, 0);
+    const BinLayout b = bin_layout(0, width, height, 0);
+    (void)R;
     out->geom_bytes = g.total;
     out->img_bytes = im.total;
     out->bin_bytes = b.total;
@@ -438,8 +480,10 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     out->img_final_T = im.final_T;
     out->img_n_contrib = im.n_contrib;
     out->img_ranges = im.ranges;
-    out->bin_point_list = b.point;
-    out->bin_tile_keys = b.st_keys;
+    out->img_tile_nmax = im.tile_nmax;
+    out->img_tile_emax = im.tile_emax;
+    out->bin_st_ranges = b.st_ranges;
+    out->bin_entries = b.ent;
     return GSR_OK;
 }
 
@@ -557,27 +601,26 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     };
     const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
     const uint2* rect_sorted = flip ? at<uint2>(geom, gl.rect_s_alt) : at<uint2>(geom, gl.rect_s);
-    uint2* ranges = at<uint2>(img, il.ranges);
     char* bin = nullptr;
     BinLayout bl{};
-    // binning into a buffer of capacity (capR, capS); dev: read P_v on the device (and run the
+    // binning into a buffer of entry capacity capS; dev: read P_v on the device (and run the
     // frame totals in the scatter)
-    auto bin_pass = [&](long long capR, long long capS, bool dev) -> int {
-        bl = bin_layout(capR, capS, width, height, dev ? P : (long long)Pv);
+    auto bin_pass = [&](long long capS, bool dev) -> int {
+        bl = bin_layout(capS, width, height, dev ? P : (long long)Pv);
         bin = reinterpret_cast<char*>(binning_buffer(binning_ctx, bl.total));
         if (!bin) return fail(GSR_E_ALLOC, "gsr_forward: binning allocation failed");
         bin = align_base(bin);
-        uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
-        uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
+        uint2* ent = at<uint2>(bin, bl.ent);
         uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
-        const uint32_t* st_sorted_keys = stk;
-        const uint32_t* st_sorted_vals = stv;
+        unsigned long long* header = at<unsigned long long>(bin, bl.header);
         if (fused_bin) {
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, NS,
-                               at<void>(bin, bl.st_bin_tmp), stk, stv, st_ranges, (uint32_t)capS, s,
-                               dev ? &ft : nullptr, at<void>(bin, bl.lists_tmp));
+                               at<void>(bin, bl.st_bin_tmp), ent, st_ranges, header, (uint32_t)capS, s,
+                               dev ? &ft : nullptr);
         } else {
+            uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
+            uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
             uint32_t* offsets = at<uint32_t>(geom, gl.offsets);
             {
                 GSR_STAGE(ST_OFFSETS);
@@ -595,46 +638,46 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                                               at<uint32_t>(bin, bl.st_vals_alt), (int)higher_msb((uint32_t)NS),
                                               at<void>(bin, bl.sort_tmp), s);
             }
-            st_sorted_keys = flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk;
-            st_sorted_vals = flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv;
-            gsr::launch_seg_ranges(capS, NS, st_sorted_keys, st_ranges, s);
+            gsr::launch_seg_ranges(capS, NS, flip2 ? at<uint32_t>(bin, bl.st_keys_alt) : stk,
+                                   flip2 ? at<uint32_t>(bin, bl.st_vals_alt) : stv, st_ranges, ent, header, s);
         }
         GSR_LAUNCH_CHECK();
         {
+            // the forward's dispatch order (a tile's cost: its super-tile's entry count); zeroes
+            // the tile maxima the tile pass raises
             GSR_STAGE(ST_RANGES);
-            gsr::launch_tile_lists(capS, NS, st_ranges, st_sorted_keys, st_sorted_vals, gx, gy, gsx,
-                                   at<uint32_t>(bin, bl.tile_cnt), at<uint32_t>(bin, bl.tile_start), ranges,
-                                   at<uint32_t>(bin, bl.scan_tmp), at<void>(bin, bl.lists_tmp),
-                                   at<uint32_t>(bin, bl.point), at<uint32_t>(img, il.order_fwd),
-                                   at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS, at<uint32_t>(img, il.tile_nmax),
-                                   capR, s, fused_bin);
+            gsr::launch_tile_order_st((unsigned)T, gx, gsx, st_ranges, at<uint32_t>(img, il.order_fwd),
+                                      at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS,
+                                      at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.tile_emax), s);
         }
         GSR_LAUNCH_CHECK();
         return GSR_OK;
     };
     gsr::RenderFwdArgs ra;
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
-    ra.ranges = ranges; ra.rec = pa.rec; ra.bg = background;
+    ra.gsx = gsx; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
     ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
+    ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     // the forward tile pass over the binning in `bin`
     auto render_pass = [&]() -> int {
-        uint32_t* point_list = at<uint32_t>(bin, bl.point);
-        ra.point_list = point_list;
+        ra.st_ranges = at<uint2>(bin, bl.st_ranges);
+        ra.ent = at<uint2>(bin, bl.ent);
         GSR_STAGE(ST_RENDER_FWD);
-        // dispatch order, nheavy and the zeroed tile_nmax come from launch_tile_lists' tile scan
         if (!mc) {
             gsr::launch_render_fwd(ra, s);
         } else {
             for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
-                gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, ranges, point_list, pa.rec, ra.order, ra.nheavy, *mc, c0);
+                gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, gsx, ra.st_ranges, ra.ent, pa.rec, ra.order,
+                                               ra.nheavy, ra.tile_nmax, ra.tile_emax, *mc, c0);
                 ma.out = mc->out + (size_t)c0 * width * height;
                 if (c0 == 0) {  // the other groups would write the same values
                     ma.final_T = ra.final_T;
                     ma.n_contrib = ra.n_contrib;
-                    ma.tile_nmax = ra.tile_nmax;
+                } else {
+                    ma.tile_nmax = nullptr;
                 }
                 gsr::launch_render_fwd_mc(ma, s);
             }
@@ -644,17 +687,17 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     };
     int rc;
     if (speculate) {
-        const long long capR = g_hint.R + g_hint.R / 4 + 65536, capS = g_hint.S + g_hint.S / 4 + 4096;
-        if ((rc = bin_pass(capR, capS, true)) != GSR_OK) return rc;
+        const long long capS = g_hint.S + g_hint.S / 4 + 4096;
+        if ((rc = bin_pass(capS, true)) != GSR_OK) return rc;
         if ((rc = render_pass()) != GSR_OK) return rc;
         if ((rc = read_totals()) != GSR_OK) return rc;
-        if ((long long)R64 > capR || (long long)S64 > capS) {  // overflow: redo at the exact size
-            if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
+        if ((long long)S64 > capS) {  // overflow: redo at the exact size
+            if ((rc = bin_pass((long long)S64, false)) != GSR_OK) return rc;
             if ((rc = render_pass()) != GSR_OK) return rc;
         }
     } else {
         if ((rc = read_totals()) != GSR_OK) return rc;
-        if ((rc = bin_pass((long long)R64, (long long)S64, false)) != GSR_OK) return rc;
+        if ((rc = bin_pass((long long)S64, false)) != GSR_OK) return rc;
         if ((rc = render_pass()) != GSR_OK) return rc;
     }
     const long long R = (long long)R64;
@@ -663,11 +706,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     g_hint.H = height;
     g_hint.R = R;
     g_hint.S = (long long)S64;
-    uint32_t* point_list = at<uint32_t>(bin, bl.point);
 #ifdef GSR_DEBUG
     {
-        const int rc_dbg = debug_check_forward(P, R, gx, gy, width, height, radii, pa.rect, pa.depth_key, ranges,
-                                               point_list, ra.n_contrib, s);
+        const int rc_dbg = debug_check_forward(P, R, gx, gy, width, height, radii, pa.rect, pa.depth_key, bin,
+                                               ra.n_contrib, s);
         if (rc_dbg != GSR_OK) return rc_dbg;
     }
 #endif
@@ -727,13 +769,13 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
                       int* radii, void* stream_) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     if (P < 0 || R < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_forward_reuse: bad sizes");
-    if (!geometry_buffer || !src_geom_buffer || !src_radii || !image_buffer || !colors_precomp || !radii ||
-        (R > 0 && !binning_buffer))
-        return fail(GSR_E_ARG, "gsr_forward_reuse: missing buffers");
     if (P == 0) return GSR_OK;
+    if (!geometry_buffer || !src_geom_buffer || !src_radii || !image_buffer || !colors_precomp || !radii ||
+        !binning_buffer)
+        return fail(GSR_E_ARG, "gsr_forward_reuse: missing buffers");
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R, 0, width, height, 0);
+    const BinLayout bl = bin_layout(0, width, height, 0);
     char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
     if (!geom) return fail(GSR_E_ALLOC, "gsr_forward_reuse: buffer allocation failed");
     geom = align_base(geom);
@@ -751,14 +793,18 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     }
     GSR_LAUNCH_CHECK();
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
-    gsr::RenderFwdArgs ra;  // with R == 0 every range is empty: background everywhere
+    gsr::RenderFwdArgs ra;  // with R == 0 every super-tile list is empty: background everywhere
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
-    ra.ranges = at<uint2>(img, il.ranges); ra.point_list = bin ? at<uint32_t>(bin, bl.point) : nullptr;
+    ra.gsx = st_x(width);
+    ra.st_ranges = bin ? at<uint2>(bin, bl.st_ranges) : nullptr;
+    ra.ent = bin ? at<uint2>(bin, bl.ent) : nullptr;
     ra.rec = at<gsr::Rec>(geom, gl.rec); ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
     ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
+    ra.tile_emax = at<uint32_t>(img, il.tile_emax);
+    if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {
         GSR_STAGE(ST_RENDER_FWD);
         gsr::launch_render_fwd(ra, s);  // the cached call's dispatch order is still valid
@@ -783,7 +829,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
     const float focal_x = width / (2.0f * tan_fovx);
     const GeomLayout gl = geom_layout(P);
     const ImgLayout il = img_layout(width, height);
-    const BinLayout bl = bin_layout(R, 0, width, height, 0);
+    const BinLayout bl = bin_layout(0, width, height, 0);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
@@ -796,24 +842,36 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         if (mc) HIP_OK(hipMemsetAsync(mc->dL_dfeat, 0, sizeof(float) * (size_t)mc->fstride * P, s));
     }
 
-    // deterministic mode: one partial row per instance, summed per Gaussian in tile order
+    // deterministic mode: one partial row per instance (indexed by the materialised lists),
+    // summed per Gaussian in tile order
     const bool det = det_on() && R > 0;
     const int pstride = mc ? ((6 + mc->nch + 3) & ~3) : gsr::DET_ROW3;
     float* partial = nullptr;
     unsigned* det_missing = nullptr;
+    uint32_t* det_pl = nullptr;
+    uint2* det_ranges = nullptr;
     if (det) {
-        const size_t pbytes = 4 * (size_t)pstride * (size_t)R;
-        char* sc = reinterpret_cast<char*>(g_scratch.get(256 + pbytes));
+        const size_t pbytes = 4 * (size_t)pstride * (size_t)R, T = (size_t)gx * gy;
+        const size_t off_pl = align_up(256 + pbytes, 256), off_rg = align_up(off_pl + 4 * (size_t)R, 256);
+        char* sc = reinterpret_cast<char*>(g_scratch.get(off_rg + 8 * T));
         if (!sc) return fail(GSR_E_ALLOC, "gsr_backward: deterministic-mode scratch allocation failed");
         det_missing = reinterpret_cast<unsigned*>(sc);
         partial = reinterpret_cast<float*>(sc + 256);
+        det_pl = reinterpret_cast<uint32_t*>(sc + off_pl);
+        det_ranges = reinterpret_cast<uint2*>(sc + off_rg);
         HIP_OK(hipMemsetAsync(sc, 0, 256 + pbytes, s));
+        const int rc = materialize_lists(R, width, height, bin, det_pl, det_ranges, s);
+        if (rc != GSR_OK) return rc;
     }
     if (R > 0) {
         gsr::RenderBwdArgs ra;
         ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
-        ra.ranges = at<uint2>(img, il.ranges);
-        ra.point_list = at<uint32_t>(bin, bl.point);
+        ra.st_ranges = at<uint2>(bin, bl.st_ranges);
+        ra.ent = at<uint2>(bin, bl.ent);
+        ra.gsx = st_x(width);
+        ra.tile_emax = at<uint32_t>(img, il.tile_emax);
+        ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
+        ra.ranges = det_ranges;
         ra.rec = at<gsr::Rec>(geom, gl.rec);
         ra.colors = colors_precomp;
         ra.bg = background;
@@ -826,14 +884,16 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.partial = partial;
         {
             GSR_STAGE(ST_RENDER_BWD);
-            gsr::launch_tile_order(gx * gy, ra.ranges, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
+            gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);
             } else {
                 for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
-                    gsr::RenderMcArgs ma = mc_args(width, height, gx, gy, ra.ranges, ra.point_list, ra.rec, ra.order,
-                                                   ra.nheavy, *mc, c0);
+                    gsr::RenderMcArgs ma = mc_args(width, height, gx, gy, ra.gsx, ra.st_ranges, ra.ent, ra.rec, ra.order,
+                                                   ra.nheavy, at<uint32_t>(img, il.tile_nmax),
+                                                   at<uint32_t>(img, il.tile_emax), *mc, c0);
+                    ma.ranges = det_ranges;
                     ma.final_T = const_cast<float*>(ra.final_T);
                     ma.n_contrib = const_cast<uint32_t*>(ra.n_contrib);
                     ma.dL_dout = mc->dL_dout + (size_t)c0 * width * height;
@@ -853,8 +913,8 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
             da.radii = radii;
             da.rect = at<uint2>(geom, gl.rect);
             da.depth_key = at<uint32_t>(geom, gl.depth_key);
-            da.ranges = ra.ranges;
-            da.point_list = ra.point_list;
+            da.ranges = det_ranges;
+            da.point_list = det_pl;
             da.partial = partial;
             da.mode = mc ? 1 : 0;
             da.pstride = pstride;

@@ -106,41 +106,44 @@ struct FrameTotals {
 void launch_frame_totals(const FrameTotals& ft, hipStream_t s);
 
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
-// Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
-// order (keys carry the local rect code), plus the super-tile ranges.  NS <= 1365.
-// rect_sorted: the rects already in depth order (the depth sort's side payload).
-size_t st_bin_temp_bytes(long long Pv, int NS);
-bool st_bin_supported(int NS);
-// Pv: the visible count, or (with dev_totals non-null) its upper bound P, the kernels then
-// reading the visible count *dev_totals (depth_sort's pv_out) on the device.  Entries at positions >= cap are
-// not written (the speculative forward detects the overflow and redoes the binning).
-// ft (optional): the frame totals run as one extra workgroup of the scatter.  lists_temp
-// (optional): launch_tile_lists' scratch, whose segment table is then built here (pass
-// seg_table_ready to launch_tile_lists).
-void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, int NS, void* temp, uint32_t* st_keys, uint32_t* st_vals, uint2* st_ranges,
-                   uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr, void* lists_temp = nullptr);
-// In depth order, every visible Gaussian emits one (super-tile, gaussian) entry per
-// super-tile its rect touches, at offsets[s] (exclusive scan of st_count in depth order).
-void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
-                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
+// The binning stops at SUPER-TILE lists: one entry per (visible Gaussian, 8x4-tile super-tile
+// its rect touches), entry = (local tile rect code << ST_KEY_BITS | super-tile id, Gaussian
+// id), every super-tile's entries contiguous and in (depth, index) order.  A tile's list (the
+// reference's point_list range) is the subsequence of its super-tile's entries whose local
+// rect covers the tile; the tile passes filter it on the fly (TileList, gsr_tile.hpp), and
+// launch_materialize writes the reference's point_list + ranges when asked (tests, the
+// GSR_DEBUG checks, the deterministic backward).
 // Super-tile keys: id in bits [0, ST_KEY_BITS), the entry's local tile rect above (so at
 // most 2^20 super-tiles; the sort orders only the id bits).
 constexpr int ST_KEY_BITS = 20;
 constexpr uint32_t ST_KEY_MASK = (1u << ST_KEY_BITS) - 1u;
-// ranges[k] = [first, last+1) of key k in a sorted key array; (0, 0) for absent keys.
-void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, uint2* ranges, hipStream_t s);
-// Per-super-tile tile filters over 1024-entry segments: tile counts, tile starts (scan),
-// ranges, point_list.  temp: tile_lists_temp_bytes(S, nst).  S: the entry capacity (the
-// real count is read from st_ranges on the device); point_list entries >= cap_r are dropped
-// and the ranges are clamped to cap_r, so a tile pass over an overflowed binning reads only
-// written entries (the forward then redoes the binning).
-size_t tile_lists_temp_bytes(long long S, int nst);
-void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint32_t* st_keys, const uint32_t* st_vals,
-                       unsigned gx, unsigned gy, unsigned gsx, uint32_t* tile_cnt, uint32_t* tile_start, uint2* ranges,
-                       uint32_t* scan_tmp, void* temp, uint32_t* point_list, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, uint32_t* tile_nmax, long long cap_r, hipStream_t s,
-                       bool seg_table_ready = false);
+// Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
+// order, plus the super-tile ranges and header[0] = S.  NS <= 1365.
+// rect_sorted: the rects already in depth order (the depth sort's side payload).
+size_t st_bin_temp_bytes(long long Pv, int NS);
+bool st_bin_supported(int NS);
+// Pv: the visible count, or (with dev_totals non-null) its upper bound P, the kernels then
+// reading the visible count *dev_totals (depth_sort's pv_out) on the device.  Entries at
+// positions >= cap are not written (the speculative forward detects the overflow and redoes
+// the binning).  ft (optional): the frame totals run as one extra workgroup of the scatter.
+void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
+                   unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
+                   uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr);
+// Large images (NS > 1365): in depth order, every visible Gaussian emits one (super-tile,
+// gaussian) pair per super-tile its rect touches, at offsets[s] (exclusive scan of st_count
+// in depth order); the pairs are then radix-sorted by super-tile and packed into entries.
+void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
+                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
+// ranges[k] = [first, last+1) of super-tile k in the sorted pairs ((0, 0) when absent), the
+// pairs packed into ent, header[0] = n.
+void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, const uint32_t* sorted_vals, uint2* ranges,
+                       uint2* ent, unsigned long long* header, hipStream_t s);
+// The reference's point_list [R] and tile ranges [T] from the super-tile lists (S entries):
+// per 1024-entry segment a count pass, a per-tile prefix over segments, a scan over tiles,
+// and a write pass.  temp: materialize_temp_bytes(S, nst, T).
+size_t materialize_temp_bytes(long long S, int nst, int T);
+void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint2* ent, unsigned gx, unsigned gy,
+                        unsigned gsx, void* temp, uint32_t* point_list, uint2* ranges, long long R, hipStream_t s);
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of
@@ -148,15 +151,23 @@ void launch_tile_lists(long long S, int nst, const uint2* st_ranges, const uint3
 // cost >= 2^heavy_bits.
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
                        int heavy_bits, hipStream_t s);
-constexpr int FWD_HEAVY_BITS = 13;  // list length >= 8192
+// The forward's order: a tile's cost is its super-tile's entry count (st_ranges; the tile's
+// own list length is not known without materialising it); also zeroes zero_a / zero_b [ntile]
+// (the forward's tile_nmax / tile_emax atomicMax targets).
+void launch_tile_order_st(unsigned ntile, unsigned gx, unsigned gsx, const uint2* st_ranges, uint32_t* order,
+                          uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, hipStream_t s);
+constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 11;  // largest n_contrib >= 2048
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
+// The tile passes read each tile's list from its super-tile's entries (TileList):
+// st_ranges [NS], ent [S], gsx super-tiles per row.
 struct RenderFwdArgs {
     int W, H;
     unsigned grid_x, grid_y;
-    const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* st_ranges;
+    const uint2* ent;
+    unsigned gsx;
     const Rec* rec;
     const float* bg;
     float* out_color;
@@ -164,15 +175,20 @@ struct RenderFwdArgs {
     uint32_t* n_contrib;
     const uint32_t* order;  // dispatch order (launch_tile_order)
     const uint32_t* nheavy;
-    uint32_t* tile_nmax;    // out (atomicMax; zeroed by the caller)    // out: per tile, the largest n_contrib (the backward's cost)
+    uint32_t* tile_nmax;  // out: per tile, the largest n_contrib (the backward's cost; atomicMax, zeroed)
+    uint32_t* tile_emax;  // out: per tile, 1 + the entry index of that last contributor (where the backward starts)
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
 struct RenderBwdArgs {
     int W, H;
     unsigned grid_x, grid_y;
-    const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* st_ranges;
+    const uint2* ent;
+    unsigned gsx;
+    const uint32_t* tile_emax;  // the forward's: where each tile's back-to-front walk starts
+    const uint32_t* tile_nmax;  // the forward's: that entry's list position + 1
+    const uint2* ranges;  // deterministic mode only: the materialised tile ranges (partial row index)
     const Rec* rec;
     const float* colors;  // optional: colour source if not in rec (unused: rec holds colour)
     const float* bg;
@@ -193,8 +209,11 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
 struct RenderMcArgs {
     int W, H;
     unsigned grid_x, grid_y;
-    const uint2* ranges;
-    const uint32_t* point_list;
+    const uint2* st_ranges;
+    const uint2* ent;
+    unsigned gsx;
+    uint32_t* tile_emax;  // forward: out (atomicMax when non-null); backward: in
+    const uint2* ranges;  // deterministic backward only (materialised)
     const Rec* rec;
     const float4* feat;  // group's first channel; row stride fstride4 float4
     int fstride4, fstride;

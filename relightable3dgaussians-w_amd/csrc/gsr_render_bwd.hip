@@ -5,7 +5,9 @@
 //  * one wave per 16x16 tile (WaveTile), each lane owns one pixel of each 8x8 quadrant;
 //    quadrant q replays only positions below its largest n_contrib (positions past every
 //    pixel's last contributor are skipped by the reference too);
-//  * batches of 64 list entries, back to front: each lane gathers one record and tests it
+//  * the tile's list from its super-tile's entries (TileList, gsr_tile.hpp), back to front
+//    from the forward's last contributor; batches of 64 list entries: each lane gathers one
+//    record and tests it
 //    against the four quadrants (box_reachable, limited by the quadrant's n_contrib); the
 //    wave walks the surviving lanes (s_ff1 + v_readlane broadcasts);
 //  * per Gaussian, the reachable quadrants run the reference's per-pixel recurrence
@@ -32,7 +34,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const uint2 range = a.ranges[tile];
     const int HW = a.H * a.W;
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
@@ -80,14 +81,22 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     unsigned long long st[8] = {};
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
-    for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
-        const uint32_t i = b0 + lane;
-        const uint32_t p = nmax - 1u - i;  // back to front
-        uint32_t id = 0, qm = 0;
+    // the tile's list back to front from its last contributor (the forward's tile_emax and
+    // tile_nmax: the entry and, over the whole tile, its list position + 1)
+    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    __shared__ TileListLds s_list;
+    TileList<false> tl;
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
+    for (;;) {
+        tl.fill(s_list);
+        uint32_t id = 0, p = 0, ei = 0;
+        const uint32_t nb = tl.take(s_list, id, p, ei);
+        if (nb == 0) break;
+        uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float rc = 0.f;
-        if (i < nmax) {
-            id = a.point_list[range.x + p];
+        if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
@@ -100,18 +109,18 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), __uint_as_float(p));
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
-        BWD_STAT(0, nmax - b0 < 64u ? nmax - b0 : 64u);
+        BWD_STAT(0, nb);
         BWD_STAT(1, __popcll(todo));
         if (!todo) continue;
         // one survivor (record A, B, Cq at batch slot k), back to front
-        auto grad_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
+        auto grad_one = [&](const float4& A, const float4& B, const float4& Cq) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
             const float c0 = B.z, c1 = B.w, c2 = Cq.x;
-            const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
+            const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.w));
             // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
             // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
             // S6..8 = sum alpha T dL/dpix
@@ -171,7 +180,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             float v = row_sum3(Q0, Q1, Q2, mb3, mb2);
             v *= vop ? op * vscale : vscale;
             if (DET) {  // one row per instance, summed per Gaussian in tile order (k_det_gather)
-                if (vidx >= 0 && v != 0.f) a.partial[(size_t)(range.x + pos) * DET_ROW3 + pslot] = v;
+                if (vidx >= 0 && v != 0.f) a.partial[(size_t)(rbase + pos) * DET_ROW3 + pslot] = v;
             } else if (vidx >= 0 && v != 0.f) {
                 atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
             }
@@ -187,7 +196,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
             const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
-            grad_one(A, B, Cq, k);
+            grad_one(A, B, Cq);
             if (!more) break;
             more = todo != 0ull;
             k = more ? __builtin_ctzll(todo) : kn;
@@ -195,7 +204,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             A = s_a[k];
             B = s_b[k];
             Cq = s_c[k];
-            grad_one(An, Bn, Cn, kn);
+            grad_one(An, Bn, Cn);
             if (!more) break;
         }
     }

@@ -3,7 +3,8 @@
 // gfx950 design:
 //  * one wave per 16x16 tile (WaveTile): each lane owns 4 pixels, one per 8x8 quadrant;
 //    tiles are remapped so each XCD's L2 serves a contiguous band of the image (xcd_remap);
-//  * batches of 64 list entries: each lane gathers one 48-B record and tests it
+//  * the tile's list comes from its super-tile's entries (TileList, gsr_tile.hpp), filtered
+//    and queued in LDS; batches of 64 list entries: each lane gathers one 48-B record and tests it
 //    conservatively against the four quadrants (box_reachable); the wave then walks the
 //    surviving lanes in list order (s_ff1), broadcasting each record with v_readlane, and
 //    blends it only into the quadrants it can reach (wave-uniform branches).  The range
@@ -29,12 +30,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
+    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    __shared__ TileListLds s_list;
+    TileList<true> tl;
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
-    __shared__ float2 s_c[64];
+    __shared__ float4 s_c[64];  // (colour b, quadrant mask, list position, entry index)
     float T[4], C0[4], C1[4], C2[4];
     float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
     uint32_t last[4];
@@ -51,14 +54,18 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
 #endif
-    for (int b0 = 0; b0 < n && live; b0 += 64) {
-        const int j = b0 + lane;
+    uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
+    while (live) {
+        tl.fill(s_list);
+        uint32_t id = 0, j = 0, ei = 0;
+        const uint32_t nb = tl.take(s_list, id, j, ei);
+        if (nb == 0) break;
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float rc = 0.f;
-        if (j < n) {
-            const Rec r = a.rec[a.point_list[range.x + j]];
-            qm = wt.reach(r, (uint32_t)j, nullptr);
+        if ((uint32_t)lane < nb) {
+            const Rec r = a.rec[id];
+            qm = wt.reach(r, j, nullptr);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
             rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, r.b.z, r.b.w);
@@ -70,16 +77,17 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float2(rc, __uint_as_float(qm));
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(j), __uint_as_float(ei));
         wave_lds_sync();
         uint64_t todo = __ballot((qm & live) != 0);
-        FWD_STAT(0, n - b0 < 64 ? n - b0 : 64);
+        FWD_STAT(0, nb);
         FWD_STAT(1, __popcll(todo));
         if (!todo) continue;
         // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
-        auto blend_one = [&](const float4& A, const float4& B, const float2& Cq, int k) __attribute__((always_inline)) {
+        auto blend_one = [&](const float4& A, const float4& B, const float4& Cq) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
-            const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
+            const uint32_t pos1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.z)) + 1u;
+            lmask blended = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
@@ -100,25 +108,25 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 C2[q] += Cq.x * w;
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
+                blended |= blend;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
                 }
             }
+            if (blended) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.w));
         };
         // survivors in pairs over two register sets (the next survivor's record is read
         // while the current one blends, and no register copies between them)
         int k = __builtin_ctzll(todo);
         todo &= todo - 1;
-        float4 A = s_a[k], B = s_b[k];
-        float2 Cq = s_c[k];
+        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
         for (;;) {
             bool more = todo != 0ull;
             const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn];
-            const float2 Cn = s_c[kn];
-            blend_one(A, B, Cq, k);
+            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
+            blend_one(A, B, Cq);
             if (!live || !more) break;
             more = todo != 0ull;
             k = more ? __builtin_ctzll(todo) : kn;
@@ -126,7 +134,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             A = s_a[k];
             B = s_b[k];
             Cq = s_c[k];
-            blend_one(An, Bn, Cn, kn);
+            blend_one(An, Bn, Cn);
             if (!live || !more) break;
         }
     }
@@ -152,7 +160,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         const uint32_t m = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nm = m > nm ? m : nm;
     }
-    if (lane == 0) atomicMax(&a.tile_nmax[tile], nm);
+    if (lane == 0 && nm) {
+        atomicMax(&a.tile_nmax[tile], nm);
+        atomicMax(&a.tile_emax[tile], elast + 1u);
+    }
 }
 
 

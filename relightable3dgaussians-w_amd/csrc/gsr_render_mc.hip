@@ -30,13 +30,15 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const uint2 range = a.ranges[tile];
-    const int n = (int)(range.y - range.x);
+    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    __shared__ TileListLds s_list;
+    TileList<true> tl;
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
-    __shared__ uint32_t s_q[64];
+    __shared__ uint32_t s_q[64], s_j[64], s_e[64];  // quadrant mask, list position, entry index
     float T[4], Cc[4][NCH], lim[4];
     uint32_t last[4];
     uint32_t live = 0;
@@ -50,17 +52,20 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         lim[q] = in ? 1.0f / 255.0f : __builtin_inff();
         if (((qallow >> q) & 1u) && __ballot(in)) live |= 1u << q;
     }
-    for (int b0 = 0; b0 < n && live; b0 += 64) {
-        const int j = b0 + lane;
+    uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere
+    while (live) {
+        tl.fill(s_list);
+        uint32_t id = 0, j = 0, ei = 0;
+        const uint32_t nb = tl.take(s_list, id, j, ei);
+        if (nb == 0) break;
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float4 f[NC4];
 #pragma unroll
         for (int g = 0; g < NC4; g++) f[g] = ra;
-        if (j < n) {
-            const uint32_t id = a.point_list[range.x + j];
+        if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, (uint32_t)j, nullptr);
+            qm = wt.reach(r, j, nullptr);
             ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
             rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
@@ -70,6 +75,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_q[lane] = qm;
+        s_j[lane] = j;
+        s_e[lane] = ei;
 #pragma unroll
         for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
         wave_lds_sync();
@@ -82,7 +89,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
 #pragma unroll
             for (int g = 0; g < NC4; g++) F[g] = s_f[g][k];
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[k]) & live;
-            const uint32_t pos1 = (uint32_t)(b0 + k) + 1u;
+            const uint32_t pos1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_j[k]) + 1u;
+            lmask blended = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
@@ -106,11 +114,13 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 for (int c = 0; c < NCH; c++) Cc[q][c] += Fs[c] * w;
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
+                blended |= blend;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
                 }
             }
+            if (blended) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[k]);
         }
     }
     const int HW = a.H * a.W;
@@ -134,7 +144,10 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
             const uint32_t mq = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
             nm = mq > nm ? mq : nm;
         }
-        if (lane == 0) atomicMax(&a.tile_nmax[tile], nm);
+        if (lane == 0 && nm) {
+            atomicMax(&a.tile_nmax[tile], nm);
+            atomicMax(&a.tile_emax[tile], elast + 1u);
+        }
     }
 }
 
@@ -146,13 +159,13 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const uint2 range = a.ranges[tile];
     const int HW = a.H * a.W;
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
     __shared__ uint2 s_q[64];  // (quadrant mask, Gaussian id)
+    __shared__ uint32_t s_j[64];  // list position
     float T[4], Tb[4], dp[4][NCH], Sr[4];  // Sr: the recurrence as in gsr_render_bwd.hip
     uint32_t last[4], qlim[4];
     uint32_t nmax = 0;
@@ -183,16 +196,23 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     const bool vop = vidx >= 0 && vidx <= 4;
     const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
 
-    for (uint32_t b0 = 0; b0 < nmax; b0 += 64) {
-        const uint32_t i = b0 + lane;
-        const uint32_t p = nmax - 1u - i;
-        uint32_t id = 0, qm = 0;
+    // back to front from the tile's last contributor (as gsr_render_bwd.hip)
+    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    __shared__ TileListLds s_list;
+    TileList<false> tl;
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
+    for (;;) {
+        tl.fill(s_list);
+        uint32_t id = 0, p = 0, ei = 0;
+        const uint32_t nb = tl.take(s_list, id, p, ei);
+        if (nb == 0) break;
+        uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float4 f[NC4];
 #pragma unroll
         for (int g = 0; g < NC4; g++) f[g] = ra;
-        if (i < nmax) {
-            id = a.point_list[range.x + p];
+        if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
             ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
@@ -204,6 +224,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_q[lane] = make_uint2(qm, id);
+        s_j[lane] = p;
 #pragma unroll
         for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
         wave_lds_sync();
@@ -224,7 +245,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             }
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)Q2.x);
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
-            const uint32_t pos = nmax - 1u - (b0 + (uint32_t)k);
+            const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_j[k]);
             float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f;
             float SF[NCH];
 #pragma unroll
@@ -286,7 +307,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 float v = row_sums_t<NQ>(Qr, mb3, mb2, col);
                 v *= vop ? op * vscale : vscale;
                 if (DET) {  // the groups run one after another: plain read-modify-write
-                    float* prow = a.partial + (size_t)(range.x + pos) * a.pstride;
+                    float* prow = a.partial + (size_t)(rbase + pos) * a.pstride;
                     if (vidx >= 0 && vidx < 6) prow[vidx] += v;
                     else if (vfeat) prow[a.pc0 + vidx] = v;
                 } else if (v != 0.f) {

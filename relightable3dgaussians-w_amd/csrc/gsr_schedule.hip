@@ -17,8 +17,23 @@ namespace gsr {
 
 // One workgroup per band: order[lo .. lo+len) = the band's tiles, cost buckets descending;
 // nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4 ways).
+// The cost of tile t: cost[t]; else with st_ranges its super-tile's entry count (the
+// forward: gx tiles per row, gsx super-tiles per row); else its list length.  zero_a / zero_b
+// (optional): zeroed per tile (the forward's atomicMax targets).
+__device__ __forceinline__ uint32_t tile_cost(unsigned t, const uint2* ranges, const uint32_t* cost,
+                                              const uint2* st_ranges, unsigned gx, unsigned gsx) {
+    if (cost) return cost[t];
+    if (st_ranges) {
+        const uint2 r = st_ranges[(t / gx) / GSR_ST_H * gsx + (t % gx) / GSR_ST_W];
+        return r.y - r.x;
+    }
+    return ranges[t].y - ranges[t].x;
+}
+
 __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost,
-                                                      uint32_t* order, uint32_t* nheavy, int heavy_bits) {
+                                                      uint32_t* order, uint32_t* nheavy, int heavy_bits,
+                                                      const uint2* st_ranges, unsigned gx, unsigned gsx,
+                                                      uint32_t* zero_a, uint32_t* zero_b) {
     __shared__ uint32_t hist[33];
     __shared__ uint32_t cur[33];
     unsigned lo, len;
@@ -27,8 +42,12 @@ __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
         const unsigned t = lo + i;
-        const uint32_t c = cost ? cost[t] : ranges[t].y - ranges[t].x;
+        const uint32_t c = tile_cost(t, ranges, cost, st_ranges, gx, gsx);
         atomicAdd(&hist[c ? 32 - __clz(c) : 0], 1u);  // bucket = bit length of the cost
+        if (zero_a) {
+            zero_a[t] = 0u;
+            zero_b[t] = 0u;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -43,7 +62,7 @@ __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
         const unsigned t = lo + i;
-        const uint32_t c = cost ? cost[t] : ranges[t].y - ranges[t].x;
+        const uint32_t c = tile_cost(t, ranges, cost, st_ranges, gx, gsx);
 #ifdef GSR_NATURAL_ORDER
         order[lo + i] = t;
 #else
@@ -55,7 +74,15 @@ __global__ void __launch_bounds__(1024) k_tile_order(unsigned ntile, const uint2
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
                        int heavy_bits, hipStream_t s) {
     if (ntile == 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, ntile, ranges, cost, order, nheavy, heavy_bits);
+    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, ntile, ranges, cost, order, nheavy, heavy_bits,
+                       (const uint2*)nullptr, 0u, 0u, (uint32_t*)nullptr, (uint32_t*)nullptr);
+}
+
+void launch_tile_order_st(unsigned ntile, unsigned gx, unsigned gsx, const uint2* st_ranges, uint32_t* order,
+                          uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, hipStream_t s) {
+    if (ntile == 0) return;
+    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(1024), 0, s, ntile, (const uint2*)nullptr, (const uint32_t*)nullptr,
+                       order, nheavy, heavy_bits, st_ranges, gx, gsx, zero_a, zero_b);
 }
 
 }  // namespace gsr

@@ -51,6 +51,102 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---- a tile's list, read from its super-tile's entries -------------------------------------
+// The binning stops at super-tile lists (gsr_binning.hip): the entries of every Gaussian that
+// touches an 8x4-tile super-tile, in (depth, index) order, each carrying its local tile rect.
+// A tile's list -- the reference's point_list range, entry for entry -- is the subsequence of
+// its super-tile's entries whose local rect covers the tile.  TileList filters 64 entries per
+// step (one 8-B load per lane, prefetched a step ahead; a rect test; a ballot) and appends the
+// covering ones, with their list positions and entry indices, to a 128-slot LDS ring; the
+// tile passes take full batches of 64 from the ring, so their per-batch work is what it was
+// over a materialised list.  Forward: front to back from position 0.  Backward: back to front
+// from a given entry (exclusive) whose preceding covering entries number pos0.
+constexpr uint32_t TL_RING = 128;
+struct TileListLds {  // per wave
+    uint32_t id[TL_RING], pos[TL_RING], e[TL_RING];
+};
+
+template <bool FWD>
+struct TileList {
+    const uint2* ent;
+    uint32_t e;    // FWD: next entry to filter; BWD: entries below e remain
+    uint32_t lim;  // FWD: end (exclusive); BWD: bottom (inclusive)
+    uint32_t pos;  // FWD: position of the next covering entry; BWD: covering entries below e
+    uint32_t head, tail;
+    uint32_t lx, ly;
+    uint2 nx;  // this lane's entry of the next step
+
+    __device__ __forceinline__ void prefetch() {
+        const uint32_t lane = threadIdx.x & 63;
+        if (FWD) nx = e + lane < lim ? ent[e + lane] : make_uint2(0u, 0u);
+        else nx = e > lim + lane ? ent[e - 1u - lane] : make_uint2(0u, 0u);
+    }
+    // first/last: the super-tile's entry range [first, last); BWD: start below `top` with pos0
+    __device__ __forceinline__ void init(const uint2* ent_, uint2 st_range, unsigned tile, unsigned gx, uint32_t top,
+                                         uint32_t pos0) {
+        ent = ent_;
+        const unsigned tx = tile % gx, ty = tile / gx;
+        lx = tx % GSR_ST_W;
+        ly = ty % GSR_ST_H;
+        head = tail = 0;
+        if (FWD) {
+            e = st_range.x;
+            lim = st_range.y;
+            pos = 0;
+        } else {
+            e = top;
+            lim = st_range.x;
+            pos = pos0;
+        }
+        prefetch();
+    }
+    __device__ __forceinline__ bool covers(uint32_t key) const {
+        const uint32_t code = key >> 20, cx0 = code & 7u, cx1 = (code >> 3) & 7u, cy0 = (code >> 6) & 3u,
+                       cy1 = (code >> 8) & 3u;  // inclusive maxima
+        return (lx - cx0) <= (cx1 - cx0) && (ly - cy0) <= (cy1 - cy0);  // unsigned: also lx >= cx0
+    }
+    __device__ __forceinline__ bool more() const { return FWD ? e < lim : e > lim; }
+    // filter until >= 64 entries are queued or the list is exhausted
+    __device__ __forceinline__ void fill(TileListLds& L) {
+        const uint32_t lane = threadIdx.x & 63;
+        wave_lds_sync();
+        while (tail - head < 64u && more()) {
+            const uint2 v = nx;
+            const uint32_t i = FWD ? e + lane : e - 1u - lane;
+            const bool valid = FWD ? i < lim : e > lim + lane;
+            if (FWD) e = min(e + 64u, lim);
+            else e = e > lim + 64u ? e - 64u : lim;
+            prefetch();
+            const bool c = valid && covers(v.x);
+            const uint64_t cm = __ballot(c);
+            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+            if (c) {
+                const uint32_t slot = (tail + r) & (TL_RING - 1u);
+                L.id[slot] = v.y;
+                L.pos[slot] = FWD ? pos + r : pos - 1u - r;
+                L.e[slot] = i;
+            }
+            const uint32_t n = (uint32_t)__popcll(cm);
+            tail += n;
+            pos = FWD ? pos + n : pos - n;
+        }
+        wave_lds_sync();
+    }
+    // up to 64 queued entries: the count (wave-uniform); lanes below it get theirs
+    __device__ __forceinline__ uint32_t take(const TileListLds& L, uint32_t& id, uint32_t& p, uint32_t& ei) {
+        const uint32_t lane = threadIdx.x & 63;
+        const uint32_t n = min(64u, tail - head);
+        if (lane < n) {
+            const uint32_t slot = (head + lane) & (TL_RING - 1u);
+            id = L.id[slot];
+            p = L.pos[slot];
+            ei = L.e[slot];
+        }
+        head += n;
+        return n;
+    }
+};
+
 // The tile passes evaluate Gaussians in log2 units: the conic is pre-scaled by log2(e) when
 // a record is staged (once per record and batch), so exp(power) is one v_exp_f32 (exp2) per
 // evaluation with no multiply.  Forward and backward stage and evaluate identically, so the

@@ -23,7 +23,8 @@ _lock = threading.Lock()
 class Layout(C.Structure):
     _fields_ = [(n, C.c_size_t) for n in (
         "geom_bytes", "img_bytes", "bin_bytes", "geom_radii", "geom_tiles", "geom_depth_key", "geom_rect",
-        "geom_rec", "geom_acc", "img_final_T", "img_n_contrib", "img_ranges", "bin_point_list", "bin_tile_keys")]
+        "geom_rec", "geom_acc", "img_final_T", "img_n_contrib", "img_ranges", "img_tile_nmax", "img_tile_emax",
+        "bin_st_ranges", "bin_entries")]
 
 
 DEBUG_LIB_PATH = os.path.join(PKG_DIR, "lib", "debug", "libgsr.so")
@@ -83,6 +84,7 @@ def _declare(lib):
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_set_deterministic.argtypes = [i]
     lib.gsr_check_buffers.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
+    lib.gsr_materialize_lists.argtypes = [i, i, i, vp, vp, vp, vp]
     lib.gsr_last_error.restype = C.c_char_p
     lib.gsr_version.restype = C.c_char_p
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
@@ -91,7 +93,7 @@ def _declare(lib):
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
-               "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers"):
+               "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
 
 
@@ -158,6 +160,18 @@ def check_buffers(P, R, W, H, radii, geom, binb, img):
     check(lib().gsr_check_buffers(int(P), int(R), int(W), int(H), radii.data_ptr(), geom.data_ptr(),
                                   binb.data_ptr() if binb.numel() else None, img.data_ptr(),
                                   stream_of(radii.device)), "gsr_check_buffers")
+
+
+def materialize_lists(R, W, H, binb):
+    """The reference's point_list (int32 [R]) and tile ranges (int32 [T, 2]) of a forward, written
+    from its binning buffer's super-tile lists (gsr_materialize_lists; synchronous)."""
+    dev = binb.device
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    pl = torch.empty(max(int(R), 1), dtype=torch.int32, device=dev)
+    rg = torch.empty((T, 2), dtype=torch.int32, device=dev)
+    check(lib().gsr_materialize_lists(int(R), int(W), int(H), binb.data_ptr() if binb.numel() else None,
+                                      pl.data_ptr(), rg.data_ptr(), stream_of(dev)), "gsr_materialize_lists")
+    return pl[:int(R)], rg
 
 
 def profile_enable(on=True):

@@ -35,8 +35,8 @@ def test_library_exports_every_declared_symbol():
 def test_layout_query_is_consistent():
     from gsr import _lib
     L = _lib.layout(1000, 12345, 1920, 1080)
-    assert L.geom_bytes > 1000 * (48 + 64) and L.bin_bytes > 12345 * 4 and L.img_bytes >= 1920 * 1080 * 8
-    for off in (L.geom_rec, L.geom_acc, L.img_ranges, L.bin_point_list):
+    assert L.geom_bytes > 1000 * (48 + 64) and L.bin_bytes >= 8 * 255 and L.img_bytes >= 1920 * 1080 * 8
+    for off in (L.geom_rec, L.geom_acc, L.img_ranges, L.bin_st_ranges, L.bin_entries):
         assert off % 256 == 0
 
 

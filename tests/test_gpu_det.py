@@ -93,6 +93,8 @@ def test_deterministic_multichannel():
 
 
 def test_check_buffers_accepts_and_rejects():
+    """gsr_check_buffers materialises the reference's lists from the super-tile entries and
+    verifies them; a corrupted entry must be named."""
     from gsr import _lib
     case = next(c for c in CASES if c["name"] == "dense_small")
     cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"])
@@ -100,20 +102,23 @@ def test_check_buffers_accepts_and_rejects():
     P, R, W, H = case["P"], st["R"], case["W"], case["H"]
     _lib.check_buffers(P, R, W, H, st["radii"], st["geom"], st["binb"], st["img"])
     L = _lib.layout(P, R, W, H)
-    pl = _view(st["binb"], L.bin_point_list, R, torch.int32)  # aliases the binning buffer
-    lens = st["ranges"][:, 1] - st["ranges"][:, 0]
-    t = int(np.argmax(lens))
-    assert lens[t] >= 2
-    x = int(st["ranges"][t, 0])
-    a, b = int(pl[x]), int(pl[x + 1])
-    pl[x], pl[x + 1] = b, a  # two neighbours of one tile list swapped
+    NS = ((W + 15) // 16 + 7) // 8 * (((H + 15) // 16 + 3) // 4)
+    st_ranges = _view(st["binb"], L.bin_st_ranges, 2 * NS, torch.int32).view(NS, 2).cpu().numpy()
+    S = int(st_ranges[:, 1].max())
+    ent = _view(st["binb"], L.bin_entries, 2 * S, torch.int32).view(S, 2)  # aliases the binning buffer
+    k = int(np.argmax(st_ranges[:, 1] - st_ranges[:, 0]))
+    x = int(st_ranges[k, 0])
+    saved = ent[x + 1].clone()
+    ent[x + 1] = ent[x]  # a duplicated entry: its tiles list one Gaussian twice
     with pytest.raises(RuntimeError, match="order"):
         _lib.check_buffers(P, R, W, H, st["radii"], st["geom"], st["binb"], st["img"])
-    pl[x], pl[x + 1] = a, b
+    ent[x + 1] = saved
     _lib.check_buffers(P, R, W, H, st["radii"], st["geom"], st["binb"], st["img"])
-    pl[x] = P  # an id past the end
+    saved = ent[x].clone()
+    ent[x, 1] = P  # an id past the end
     with pytest.raises(RuntimeError, match="id >= P"):
         _lib.check_buffers(P, R, W, H, st["radii"], st["geom"], st["binb"], st["img"])
+    ent[x] = saved
 
 
 def test_debug_build_parity_suite():

@@ -69,8 +69,11 @@ def run_gpu(cam, gs, mode="colors", bg=(0.0, 0.0, 0.0), scale_modifier=1.0, sh_d
     st["rec"] = _view(geom, L.geom_rec, 12 * P, torch.float32).view(P, 12).cpu().numpy()
     st["tiles"] = _view(geom, L.geom_tiles, P, torch.int32).cpu().numpy().view(np.uint32)
     st["depth_key"] = _view(geom, L.geom_depth_key, P, torch.int32).cpu().numpy().view(np.uint32)
-    st["point_list"] = _view(binb, L.bin_point_list, R, torch.int32).cpu().numpy().view(np.uint32)
-    st["ranges"] = _view(img, L.img_ranges, 2 * gx * gy, torch.int32).cpu().numpy().view(np.uint32).reshape(-1, 2)
+    # the reference's point_list and tile ranges, written from the super-tile lists the
+    # binning leaves (the tile passes read those directly)
+    pl, rg = _lib.materialize_lists(R, W, H, binb)
+    st["point_list"] = pl.cpu().numpy().view(np.uint32)
+    st["ranges"] = rg.cpu().numpy().view(np.uint32).reshape(-1, 2)
     st["final_T"] = _view(img, L.img_final_T, W * H, torch.float32).cpu().numpy()
     st["n_contrib"] = _view(img, L.img_n_contrib, W * H, torch.int32).cpu().numpy().view(np.uint32)
     return st
