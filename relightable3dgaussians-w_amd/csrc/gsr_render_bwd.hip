@@ -90,9 +90,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
         tl.fill(s_list);
-        uint32_t id = 0, p = 0, ei = 0;
-        const uint32_t nb = tl.take(s_list, id, p, ei);
+        uint32_t id = 0, ei = 0, p0 = 0;
+        const uint32_t nb = tl.take(s_list, id, ei, p0);
         if (nb == 0) break;
+        const uint32_t p = p0 - (uint32_t)lane;  // list position (back to front)
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float rc = 0.f;
@@ -109,18 +110,18 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), __uint_as_float(p));
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nb);
         BWD_STAT(1, __popcll(todo));
         if (!todo) continue;
         // one survivor (record A, B, Cq at batch slot k), back to front
-        auto grad_one = [&](const float4& A, const float4& B, const float4& Cq) __attribute__((always_inline)) {
+        auto grad_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
             const float c0 = B.z, c1 = B.w, c2 = Cq.x;
-            const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.w));
+            const uint32_t pos = p0 - (uint32_t)k;
             // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
             // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
             // S6..8 = sum alpha T dL/dpix
@@ -196,7 +197,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
             const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
-            grad_one(A, B, Cq);
+            grad_one(A, B, Cq, k);
             if (!more) break;
             more = todo != 0ull;
             k = more ? __builtin_ctzll(todo) : kn;
@@ -204,7 +205,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             A = s_a[k];
             B = s_b[k];
             Cq = s_c[k];
-            grad_one(An, Bn, Cn);
+            grad_one(An, Bn, Cn, kn);
             if (!more) break;
         }
     }

@@ -37,7 +37,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
-    __shared__ float4 s_c[64];  // (colour b, quadrant mask, list position, entry index)
+    __shared__ float2 s_c[64];  // (colour b, quadrant mask)
+    __shared__ uint32_t s_e[64];  // entry index
     float T[4], C0[4], C1[4], C2[4];
     float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
     uint32_t last[4];
@@ -57,9 +58,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
     while (live) {
         tl.fill(s_list);
-        uint32_t id = 0, j = 0, ei = 0;
-        const uint32_t nb = tl.take(s_list, id, j, ei);
+        uint32_t id = 0, ei = 0, p0 = 0;
+        const uint32_t nb = tl.take(s_list, id, ei, p0);
         if (nb == 0) break;
+        const uint32_t j = p0 + (uint32_t)lane;  // list position
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float rc = 0.f;
@@ -77,16 +79,18 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(j), __uint_as_float(ei));
+        s_c[lane] = make_float2(rc, __uint_as_float(qm));
+        s_e[lane] = ei;
         wave_lds_sync();
         uint64_t todo = __ballot((qm & live) != 0);
         FWD_STAT(0, nb);
         FWD_STAT(1, __popcll(todo));
         if (!todo) continue;
         // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
-        auto blend_one = [&](const float4& A, const float4& B, const float4& Cq) __attribute__((always_inline)) {
+        int klast = -1;  // batch slot of the latest survivor that blended anywhere
+        auto blend_one = [&](const float4& A, const float4& B, const float2& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
-            const uint32_t pos1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.z)) + 1u;
+            const uint32_t pos1 = p0 + (uint32_t)k + 1u;
             lmask blended = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -114,19 +118,21 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
                 }
             }
-            if (blended) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.w));
+            if (blended) klast = k;
         };
         // survivors in pairs over two register sets (the next survivor's record is read
         // while the current one blends, and no register copies between them)
         int k = __builtin_ctzll(todo);
         todo &= todo - 1;
-        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
+        float4 A = s_a[k], B = s_b[k];
+        float2 Cq = s_c[k];
         for (;;) {
             bool more = todo != 0ull;
             const int kn = more ? __builtin_ctzll(todo) : k;
             todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
-            blend_one(A, B, Cq);
+            const float4 An = s_a[kn], Bn = s_b[kn];
+            const float2 Cn = s_c[kn];
+            blend_one(A, B, Cq, k);
             if (!live || !more) break;
             more = todo != 0ull;
             k = more ? __builtin_ctzll(todo) : kn;
@@ -134,9 +140,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             A = s_a[k];
             B = s_b[k];
             Cq = s_c[k];
-            blend_one(An, Bn, Cn);
+            blend_one(An, Bn, Cn, kn);
             if (!live || !more) break;
         }
+        if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }
 #ifdef GSR_RENDER_STATS
     if (lane == 0)

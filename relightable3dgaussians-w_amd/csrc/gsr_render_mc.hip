@@ -38,7 +38,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
-    __shared__ uint32_t s_q[64], s_j[64], s_e[64];  // quadrant mask, list position, entry index
+    __shared__ uint32_t s_q[64], s_e[64];  // quadrant mask, entry index
     float T[4], Cc[4][NCH], lim[4];
     uint32_t last[4];
     uint32_t live = 0;
@@ -55,9 +55,10 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere
     while (live) {
         tl.fill(s_list);
-        uint32_t id = 0, j = 0, ei = 0;
-        const uint32_t nb = tl.take(s_list, id, j, ei);
+        uint32_t id = 0, ei = 0, p0 = 0;
+        const uint32_t nb = tl.take(s_list, id, ei, p0);
         if (nb == 0) break;
+        const uint32_t j = p0 + (uint32_t)lane;
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float4 f[NC4];
@@ -75,12 +76,12 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_q[lane] = qm;
-        s_j[lane] = j;
         s_e[lane] = ei;
 #pragma unroll
         for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
         wave_lds_sync();
         uint64_t todo = __ballot((qm & live) != 0);
+        int klast = -1;  // batch slot of the latest survivor that blended anywhere
         while (todo && live) {
             const int k = __builtin_ctzll(todo);
             todo &= todo - 1;
@@ -89,7 +90,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
 #pragma unroll
             for (int g = 0; g < NC4; g++) F[g] = s_f[g][k];
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[k]) & live;
-            const uint32_t pos1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_j[k]) + 1u;
+            const uint32_t pos1 = p0 + (uint32_t)k + 1u;
             lmask blended = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -120,8 +121,9 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
                 }
             }
-            if (blended) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[k]);
+            if (blended) klast = k;
         }
+        if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }
     const int HW = a.H * a.W;
 #pragma unroll
@@ -165,7 +167,6 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
     __shared__ uint2 s_q[64];  // (quadrant mask, Gaussian id)
-    __shared__ uint32_t s_j[64];  // list position
     float T[4], Tb[4], dp[4][NCH], Sr[4];  // Sr: the recurrence as in gsr_render_bwd.hip
     uint32_t last[4], qlim[4];
     uint32_t nmax = 0;
@@ -204,9 +205,10 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
     for (;;) {
         tl.fill(s_list);
-        uint32_t id = 0, p = 0, ei = 0;
-        const uint32_t nb = tl.take(s_list, id, p, ei);
+        uint32_t id = 0, ei = 0, p0 = 0;
+        const uint32_t nb = tl.take(s_list, id, ei, p0);
         if (nb == 0) break;
+        const uint32_t p = p0 - (uint32_t)lane;
         uint32_t qm = 0;
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float4 f[NC4];
@@ -224,7 +226,6 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         s_a[lane] = ra;
         s_b[lane] = rb;
         s_q[lane] = make_uint2(qm, id);
-        s_j[lane] = p;
 #pragma unroll
         for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
         wave_lds_sync();
@@ -245,7 +246,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             }
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)Q2.x);
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
-            const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_j[k]);
+            const uint32_t pos = p0 - (uint32_t)k;
             float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f;
             float SF[NCH];
 #pragma unroll

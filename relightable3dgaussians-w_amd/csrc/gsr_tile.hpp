@@ -63,25 +63,32 @@ __device__ __forceinline__ void wave_lds_sync() {
 // from a given entry (exclusive) whose preceding covering entries number pos0.
 constexpr uint32_t TL_RING = 128;
 struct TileListLds {  // per wave
-    uint32_t id[TL_RING], pos[TL_RING], e[TL_RING];
+    uint32_t id[TL_RING], e[TL_RING];
 };
 
-template <bool FWD>
+// FWD: front to back; the entries' list positions are consecutive, so a batch's are its first
+// position (take's p0, wave-uniform) + slot.  BWD: back to front, positions p0 - slot.
+// KEEP_E: also queue the entry indices (the forward records where its last contributor sits).
+template <bool FWD, bool KEEP_E = FWD>
 struct TileList {
     const uint2* ent;
-    uint32_t e;    // FWD: next entry to filter; BWD: entries below e remain
-    uint32_t lim;  // FWD: end (exclusive); BWD: bottom (inclusive)
-    uint32_t pos;  // FWD: position of the next covering entry; BWD: covering entries below e
+    uint32_t e;      // FWD: next entry to filter; BWD: entries below e remain
+    uint32_t lim;    // FWD: end (exclusive); BWD: bottom (inclusive)
     uint32_t head, tail;
+    uint32_t tpos;   // list position of the next entry to take (BWD: counting down)
     uint32_t lx, ly;
-    uint2 nx;  // this lane's entry of the next step
+    uint2 nx, nx2;   // this lane's entries of the next two steps (loads issued two steps ahead)
 
-    __device__ __forceinline__ void prefetch() {
+    __device__ __forceinline__ uint2 load_step(uint32_t eb) const {  // the step starting at eb (BWD: top eb)
         const uint32_t lane = threadIdx.x & 63;
-        if (FWD) nx = e + lane < lim ? ent[e + lane] : make_uint2(0u, 0u);
-        else nx = e > lim + lane ? ent[e - 1u - lane] : make_uint2(0u, 0u);
+        if (FWD) return eb + lane < lim ? ent[eb + lane] : make_uint2(0u, 0u);
+        return eb > lim + lane ? ent[eb - 1u - lane] : make_uint2(0u, 0u);
     }
-    // first/last: the super-tile's entry range [first, last); BWD: start below `top` with pos0
+    __device__ __forceinline__ uint32_t step_after(uint32_t eb) const {
+        return FWD ? min(eb + 64u, lim) : (eb > lim + 64u ? eb - 64u : lim);
+    }
+    // st_range: the super-tile's entries [first, last); BWD: start below `top`, whose covering
+    // predecessors number pos0
     __device__ __forceinline__ void init(const uint2* ent_, uint2 st_range, unsigned tile, unsigned gx, uint32_t top,
                                          uint32_t pos0) {
         ent = ent_;
@@ -92,13 +99,14 @@ struct TileList {
         if (FWD) {
             e = st_range.x;
             lim = st_range.y;
-            pos = 0;
+            tpos = 0;
         } else {
             e = top;
             lim = st_range.x;
-            pos = pos0;
+            tpos = pos0 - 1u;
         }
-        prefetch();
+        nx = load_step(e);
+        nx2 = load_step(step_after(e));
     }
     __device__ __forceinline__ bool covers(uint32_t key) const {
         const uint32_t code = key >> 20, cx0 = code & 7u, cx1 = (code >> 3) & 7u, cy0 = (code >> 6) & 3u,
@@ -114,35 +122,34 @@ struct TileList {
             const uint2 v = nx;
             const uint32_t i = FWD ? e + lane : e - 1u - lane;
             const bool valid = FWD ? i < lim : e > lim + lane;
-            if (FWD) e = min(e + 64u, lim);
-            else e = e > lim + 64u ? e - 64u : lim;
-            prefetch();
+            e = step_after(e);
+            nx = nx2;
+            nx2 = load_step(step_after(e));
             const bool c = valid && covers(v.x);
             const uint64_t cm = __ballot(c);
             const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
             if (c) {
                 const uint32_t slot = (tail + r) & (TL_RING - 1u);
                 L.id[slot] = v.y;
-                L.pos[slot] = FWD ? pos + r : pos - 1u - r;
-                L.e[slot] = i;
+                if (KEEP_E) L.e[slot] = i;
             }
-            const uint32_t n = (uint32_t)__popcll(cm);
-            tail += n;
-            pos = FWD ? pos + n : pos - n;
+            tail += (uint32_t)__popcll(cm);
         }
         wave_lds_sync();
     }
-    // up to 64 queued entries: the count (wave-uniform); lanes below it get theirs
-    __device__ __forceinline__ uint32_t take(const TileListLds& L, uint32_t& id, uint32_t& p, uint32_t& ei) {
+    // up to 64 queued entries: the count (wave-uniform); lanes below it get theirs; p0: the
+    // batch's first list position (FWD: lane's = p0 + lane; BWD: p0 - lane)
+    __device__ __forceinline__ uint32_t take(const TileListLds& L, uint32_t& id, uint32_t& ei, uint32_t& p0) {
         const uint32_t lane = threadIdx.x & 63;
         const uint32_t n = min(64u, tail - head);
         if (lane < n) {
             const uint32_t slot = (head + lane) & (TL_RING - 1u);
             id = L.id[slot];
-            p = L.pos[slot];
-            ei = L.e[slot];
+            if (KEEP_E) ei = L.e[slot];
         }
         head += n;
+        p0 = tpos;
+        tpos = FWD ? tpos + n : tpos - n;
         return n;
     }
 };
