@@ -68,7 +68,10 @@ def _pmc_record(stage, workload):
         b = d.get("bench_under_profiler") or {}
         if (b.get("config") or {}).get("workload", "").split(",")[0] != workload.split(",")[0]:
             continue
-        return d.get("kernels", {}).get(STAGE_KERNEL.get(stage, ""), {}), os.path.relpath(f, ROOT)
+        ks = d.get("kernels", {})
+        want = STAGE_KERNEL.get(stage, "")
+        name = want if want in ks else next((k for k in ks if k.startswith(want + "<")), None)  # template args
+        return (ks.get(name, {}) if name else {}), os.path.relpath(f, ROOT)
     return {}, None
 
 
@@ -86,12 +89,13 @@ def pmc_traffic(stage, workload):
 
 
 def unique_bytes(stage, P, Pv, R, T, Npix, M):
-    """Compulsory HBM bytes of the tile passes if every array were read once: the point list
-    (R ids), each visible Gaussian's 48-B record once, the image state, the gradient lines.
-    SURVEY §8d's figure counts one 40-B record read per instance (R x 40) instead; the
-    records are re-read from L2 across the tiles a Gaussian touches."""
-    return {"render_fwd": T * 8 + R * 4 + Pv * 48 + Npix * 20,
-            "render_bwd": T * 8 + R * 4 + Pv * 48 + Npix * 20 + Pv * 44}.get(stage)
+    """Compulsory HBM bytes of the tile passes if every array were read once: each visible
+    Gaussian's 48-B record and its super-tile entries (~1.5 per Gaussian at 8 B; the tile
+    passes filter each tile's list from them, no R-sized point list exists), the image state,
+    the gradient lines.  SURVEY §8d's figure counts one 40-B record read per instance (R x 40)
+    instead; the records are re-read from L2 across the tiles a Gaussian touches."""
+    return {"render_fwd": T * 8 + Pv * (48 + 12) + Npix * 20,
+            "render_bwd": T * 8 + Pv * (48 + 12) + Npix * 20 + Pv * 44}.get(stage)
 
 
 def cpu_baseline(cam, gs_cpu, deg, dout_cpu, ntiles=64, seed=2, cfg1=True):
