@@ -663,7 +663,7 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
     hipLaunchKernelGGL(k_seg_prefix, dim3((np + 255) / 256), dim3(256), 0, s, nst, tab.st_seg0, gx, gy, gsx,
                        tab.seg_cnt, tile_cnt, (uint32_t)G);
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, T, tile_cnt, tile_start, ranges, (uint32_t*)nullptr,
-                       (uint32_t)min(R, (long long)0xFFFFFFFFll));
+                       (uint32_t)(R < 0xFFFFFFFFll ? R : 0xFFFFFFFFll));
     if (G > 0)
         hipLaunchKernelGGL(k_seg_lists<true>, dim3((unsigned)G), dim3(256), 0, s, tab.nseg_total, tab.seg_st,
                            tab.seg_e0, st_ranges, ent, gx, gy, gsx, (uint32_t*)nullptr, tab.seg_cnt, tile_start,

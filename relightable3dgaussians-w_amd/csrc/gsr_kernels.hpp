@@ -277,7 +277,7 @@ void launch_check_lists(int P, long long R, unsigned gx, unsigned gy, int W, int
                         hipStream_t s);
 
 // ---- fused Adam over a flat parameter buffer (gsr_adam.hip) ---------------------------
-constexpr int ADAM_MAX_SEGS = 16;
+constexpr int ADAM_MAX_SEGS = 32;
 struct AdamSegs {
     int n;                               // segments (param groups), <= ADAM_MAX_SEGS
     long long end[ADAM_MAX_SEGS];        // exclusive end element of each segment (ascending)

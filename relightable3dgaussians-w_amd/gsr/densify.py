@@ -69,6 +69,7 @@ class _Rows:
             self.t[name] = [buf[off:off + n].view(shape).clone() for buf in (fp.flat.detach(), fp.exp_avg,
                                                                            fp.exp_avg_sq)]
         self.is_sky = scene.is_sky.reshape(-1).clone()
+        self.global_groups = scene.global_groups
 
     def get(self, name):
         return self.t[name][0]
@@ -82,7 +83,7 @@ class _Rows:
     def keep(self, mask: torch.Tensor) -> None:
         fg_mask = mask[~self.is_sky]
         for name in self.t:
-            if name in ("env_sh", "sky_sh"):
+            if name in self.global_groups:  # embeddings and MLP weights: not per Gaussian
                 continue
             m = fg_mask if name in FG_GROUPS else mask
             self.t[name] = [x[m] for x in self.t[name]]

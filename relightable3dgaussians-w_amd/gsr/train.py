@@ -18,10 +18,17 @@ densification statistics, one torch.optim.Adam step over nine param groups
     come from a segment table, and the all-reduced sum is turned into the mean over the
     step's views by the kernel's grad scale.
 
-Out of scope (the caller's, unchanged): the embedding MLP (here a per-view environment/sky
-SH table stands in for its output), the envlight / min-scale / sky-depth regularisers,
-densify_and_prune's tensor surgery and sky Gaussians' radius/angle parameterisation (sky
-Gaussians share the xyz group here).
+The iteration is the reference's (train.py:62-120): the view's embedding row through MLPNet
+(scene/net_models.py:16-52, dropout in training mode) gives the environment SH (+ N(0, 0.025)
+noise) and the sky SH; the losses are the reconstruction, sky-BRDF and normal terms plus the
+envlight (envl_sh_loss), min-scale and sky-depth regularisers with the configured weights
+(configs/optimizer/optimization_params.yaml).  The embedding table and the MLP weights are
+segments of the same flat buffer, so their gradients cross the ranks in the same all-reduce.
+
+Differences kept on purpose: sky Gaussians keep their xyz in the xyz group (the reference
+stores their (theta, phi) angles on a fixed shell, gaussian_model.py:96-103); the random
+draws (dropout masks, SH noise, envlight directions) come from one device generator per
+scene instead of the global CPU/GPU RNG, so a step is reproducible and synchronisation-free.
 """
 from __future__ import annotations
 
@@ -38,7 +45,18 @@ from . import _lib
 # (xyz and scaling lrs carry the scene's spatial_lr_scale, applied by the caller)
 GAUSSIAN_GROUPS = (("xyz", 3, 0.00016), ("albedo", 3, 0.0025), ("opacity", 1, 0.05), ("scaling", 3, 0.001),
                    ("rotation", 4, 0.001), ("roughness", 1, 0.0002), ("metalness", 1, 0.0002))
-LIGHT_LR = 0.0002  # mlp_lr: the per-view lighting table stands in for the embedding MLP's output
+MLP_LR = 0.0002         # mlp_lr (configs/optimizer/optimization_params.yaml)
+EMBEDDINGS_LR = 0.0002  # embeddings_lr
+EMBEDDING_DIM = 32      # configs/relightable3DG-W.yaml embeddings_dim
+# MLPNet(sh_degree_envl=4, sh_degree_sky=1, embedding_dim=32, dense_layer_size=256)
+# (scene/net_models.py:16-40): (parameter name as in the reference's state_dict, out, in)
+MLP_LAYERS = (("base.0", 256, 32), ("base.3", 256, 256), ("base.5", 128, 256), ("sh_sky_outlayer", 12, 128),
+              ("sh_envl_layers.0", 128, 128), ("sh_envl_outlayer", 75, 128))
+MLP_DROPOUT = 0.2
+ENV_NOISE_STD = 0.025   # train.py:70
+# loss weights (configs/optimizer/optimization_params.yaml)
+LAMBDA_DSSIM, LAMBDA_SKY_BRDF, LAMBDA_NORMAL = 0.2, 0.5, 0.05
+LAMBDA_ENVLIGHT, LAMBDA_SCALE, LAMBDA_SKY_GAUSS = 100.0, 100.0, 0.05
 
 
 class FlatParams:
@@ -287,12 +305,146 @@ def view_loss_torch(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_br
     return loss + lambda_normal * (1 - (n * nr).sum(dim=0))[None].mean()
 
 
+# ---- the environment-light MLP and the regularisers (train.py:66-120) ---------------------
+
+def mlp_forward(params: Dict[str, torch.Tensor], emb: torch.Tensor, drop_mask=None):
+    """MLPNet.forward (scene/net_models.py:43-52) on the named weights ``mlp.<layer>.weight``
+    / ``.bias`` of ``params``: Linear(32, 256) -> Dropout(0.2) -> ReLU -> Linear(256, 256) ->
+    ReLU -> Linear(256, 128) -> ReLU, then the sky head Linear(128, 12) and the environment head
+    Linear(128, 128) -> ReLU -> Linear(128, 75).  ``drop_mask`` [B, 256]: the training-mode
+    dropout multiplier (0 or 1/(1-p)); None is eval mode.  Returns (env [B,25,3], sky [B,4,3])."""
+    def lin(x, name):
+        return F.linear(x, params[f"mlp.{name}.weight"], params[f"mlp.{name}.bias"])
+    h = lin(emb, "base.0")
+    if drop_mask is not None:
+        h = h * drop_mask
+    h = F.relu(h)
+    h = F.relu(lin(h, "base.3"))
+    h = F.relu(lin(h, "base.5"))
+    sky = lin(h, "sh_sky_outlayer").view(-1, 4, 3)
+    env = lin(F.relu(lin(h, "sh_envl_layers.0")), "sh_envl_outlayer").view(-1, 25, 3)
+    return env, sky
+
+
+def sh_basis(deg: int, d: torch.Tensor) -> torch.Tensor:
+    """The real SH basis of utils/sh_utils.py:81-151 (constants :35-64) at unit directions
+    d [N,3], degrees 0-4: [N, (deg+1)^2], so eval_sh(deg, sh, d) = basis @ sh per channel."""
+    if not 0 <= deg <= 4:
+        raise ValueError("sh_basis: degrees 0-4")
+    x, y, z = d[:, 0], d[:, 1], d[:, 2]
+    b = [torch.full_like(x, 0.28209479177387814)]
+    if deg > 0:
+        c1 = 0.4886025119029199
+        b += [-c1 * y, c1 * z, -c1 * x]
+    if deg > 1:
+        xx, yy, zz, xy, yz, xz = x * x, y * y, z * z, x * y, y * z, x * z
+        b += [1.0925484305920792 * xy, -1.0925484305920792 * yz, 0.31539156525252005 * (2.0 * zz - xx - yy),
+              -1.0925484305920792 * xz, 0.5462742152960396 * (xx - yy)]
+    if deg > 2:
+        b += [-0.5900435899266435 * y * (3 * xx - yy), 2.890611442640554 * xy * z,
+              -0.4570457994644658 * y * (4 * zz - xx - yy), 0.3731763325901154 * z * (2 * zz - 3 * xx - 3 * yy),
+              -0.4570457994644658 * x * (4 * zz - xx - yy), 1.445305721320277 * z * (xx - yy),
+              -0.5900435899266435 * x * (xx - 3 * yy)]
+    if deg > 3:
+        b += [2.5033429417967046 * xy * (xx - yy), -1.7701307697799304 * yz * (3 * xx - yy),
+              0.9461746957575601 * xy * (7 * zz - 1), -0.6690465435572892 * yz * (7 * zz - 3),
+              0.10578554691520431 * (zz * (35 * zz - 30) + 3), -0.6690465435572892 * xz * (7 * zz - 3),
+              0.47308734787878004 * (xx - yy) * (7 * zz - 1), -1.7701307697799304 * xz * (xx - 3 * yy),
+              0.6258357354491761 * (xx * (xx - 3 * yy) - yy * (3 * xx - yy))]
+    return torch.stack(b, dim=-1)
+
+
+def envl_sh_loss(sh_env: torch.Tensor, sh_degree: int, N_samples: int = 10, dirs: torch.Tensor = None,
+                 generator: torch.Generator = None) -> torch.Tensor:
+    """utils/loss_utils.py:185-207: the environment SH [1,K,3] evaluated at N_samples random
+    directions (U(-1,1)^3 normalised; ``dirs`` [N_samples,3] supplies the unnormalised draw),
+    and the mean squared negative part of the 3 N_samples values (0 when none is negative).
+    No host synchronisation: the reference's boolean selection becomes a masked sum / count."""
+    if dirs is None:
+        dirs = torch.empty(N_samples, 3, device=sh_env.device).uniform_(-1, 1, generator=generator)
+    d = dirs / dirs.norm(dim=1, keepdim=True)
+    vals = sh_basis(sh_degree, d) @ sh_env.reshape(-1, 3)[: (sh_degree + 1) ** 2]  # [N, 3]
+    neg = (vals < 0).to(vals.dtype)
+    n = neg.sum()
+    return torch.where(n > 0, (vals * vals * neg).sum() / n.clamp(min=1), torch.zeros_like(n))
+
+
+def min_scale_loss(radii: torch.Tensor, gaussians) -> torch.Tensor:
+    """utils/loss_utils.py:210-220: the mean over visible foreground Gaussians of their
+    smallest scale (get_scaling sorted along the last axis, column 0); masked sum / count."""
+    vis = (radii > 0) & ~gaussians.get_is_sky.reshape(-1)
+    smin = gaussians.get_scaling.min(dim=-1).values
+    w = vis.to(smin.dtype)
+    return (smin * w).sum() / w.sum()
+
+
+def depth_loss_gaussians(gaussians, camera, visibility_filter: torch.Tensor, gamma: float = 0.02) -> torch.Tensor:
+    """utils/loss_utils.py:140-148: exp(-gamma (mean sky depth - mean foreground depth)) over
+    the visible Gaussians, the foreground mean detached.  The view-space depth is the third
+    column of the row-vector world-to-view matrix (GaussianModel.get_depth, :125-130),
+    evaluated elementwise: a batched [4,4] x [P,4,1] matmul, or a [P,3] x [3] gemv (rocBLAS
+    gemvt: 1.1 ms at P = 1.5M), costs more than the whole render of the view."""
+    wvt = camera.world_view_transform
+    x = gaussians.get_xyz
+    depth = x[:, 0] * wvt[0, 2] + x[:, 1] * wvt[1, 2] + x[:, 2] * wvt[2, 2] + wvt[3, 2]
+    sky = gaussians.get_is_sky.reshape(-1)
+    ws = (sky & visibility_filter).to(depth.dtype)
+    wf = (~sky & visibility_filter).to(depth.dtype)
+    avg_sky = (depth * ws).sum() / ws.sum()
+    avg_fg = ((depth * wf).sum() / wf.sum()).detach()
+    return torch.exp(-gamma * (avg_sky - avg_fg))
+
+
+def view_regularisers(pc, radii: torch.Tensor, viewmats: torch.Tensor, env_sh: torch.Tensor, dirs: torch.Tensor,
+                      gamma: float = 0.02) -> torch.Tensor:
+    """The three regularisers of train.py:101-118 for V views at once, as [V] losses:
+    LAMBDA_ENVLIGHT envl_sh_loss(env_sh[v]) + LAMBDA_SCALE min_scale_loss(radii[v])
+    + LAMBDA_SKY_GAUSS depth_loss_gaussians(view v), each equal to the single-view function
+    above.  radii [V,P], viewmats [V,4,4] (row-vector world-to-view), env_sh [V,25,3], dirs
+    [V,10,3].  Batched over views, the per-Gaussian work is ~15 [V,P] kernels each way instead
+    of ~15 [P] kernels per view per function."""
+    V = radii.shape[0]
+
+    def rows(x):  # per-view sums of a [V,P] tensor: V full reductions (PyTorch's reduction
+        # over the inner axis of a [4, 1.5M] tensor runs at ~0.2 TB/s: 114 us per call)
+        return torch.stack([x[v].sum() for v in range(V)])
+    sky = pc.get_is_sky.reshape(-1)
+    vis = radii > 0
+    wf = (vis & ~sky).to(torch.float32)                        # visible foreground
+    ws = (vis & sky).to(torch.float32)                         # visible sky
+    nf, ns = rows(wf), rows(ws)
+    smin = pc.get_scaling.min(dim=-1).values                   # [P]
+    ms = rows(wf * smin) / nf
+    x = pc.get_xyz
+    c = viewmats[:, :, 2]                                      # [V,4]: the depth column
+    depth = x[:, 0] * c[:, 0:1] + x[:, 1] * c[:, 1:2] + x[:, 2] * c[:, 2:3] + c[:, 3:4]   # [V,P]
+    avg_sky = rows(depth * ws) / ns
+    avg_fg = (rows(depth * wf) / nf).detach()
+    dl = torch.exp(-gamma * (avg_sky - avg_fg))
+    d = dirs / dirs.norm(dim=-1, keepdim=True)
+    vals = torch.bmm(sh_basis(4, d.reshape(-1, 3)).reshape(V, -1, 25), env_sh.reshape(V, 25, 3))  # [V,10,3]
+    neg = (vals < 0).to(vals.dtype)
+    n = neg.sum(dim=(1, 2))
+    el = torch.where(n > 0, (vals * vals * neg).sum(dim=(1, 2)) / n.clamp(min=1), torch.zeros_like(n))
+    return LAMBDA_ENVLIGHT * el + LAMBDA_SCALE * ms + LAMBDA_SKY_GAUSS * dl
+
+
+def draw_step_randomness(n_views: int, device, generator: torch.Generator = None) -> Dict[str, torch.Tensor]:
+    """The iteration's random draws for ``n_views`` views: MLPNet's dropout multipliers
+    [V,256] (0 or 1/(1-p)), the environment SH noise [V,25,3] ~ N(0, 0.025) (train.py:70) and
+    the envlight regulariser's unnormalised directions [V,10,3] ~ U(-1,1)."""
+    keep = torch.rand(n_views, MLP_LAYERS[0][1], device=device, generator=generator) >= MLP_DROPOUT
+    return {"dropout": keep.float() / (1.0 - MLP_DROPOUT),
+            "noise": torch.randn(n_views, 25, 3, device=device, generator=generator) * ENV_NOISE_STD,
+            "dirs": torch.rand(n_views, 10, 3, device=device, generator=generator) * 2.0 - 1.0}
+
+
 # ---- the model view render() reads and the step ------------------------------------------
 
 class RelitScene:
-    """A relightable scene on one rank: FlatParams with the Gaussian groups plus a per-view
-    environment SH (deg 4, [V,25,3]) and sky SH (deg 1, [V,4,3]) table, and the constant
-    sky flags.  ``model()`` gives the activated attributes as render() reads them
+    """A relightable scene on one rank: FlatParams with the Gaussian groups, the per-view
+    embedding table [n_views, 32] (relit3DGW_model.py:66-67) and MLPNet's weights (the
+    ``mlp.*`` groups, PyTorch's default Linear initialisation), and the constant sky flags.  ``model()`` gives the activated attributes as render() reads them
     (gaussian_model.py:74-180: exp scaling, normalised rotation, sigmoid opacity and
     materials)."""
 
@@ -305,16 +457,25 @@ class RelitScene:
             if name in ("xyz", "scaling"):
                 lr *= spatial_lr_scale
             spec.append((name, (rows, cols), lr))
-        spec += [("env_sh", (n_views, 25, 3), LIGHT_LR), ("sky_sh", (n_views, 4, 3), LIGHT_LR)]
+        spec.append(("embeddings", (n_views, EMBEDDING_DIM), EMBEDDINGS_LR))
+        for name, fout, fin in MLP_LAYERS:
+            spec += [(f"mlp.{name}.weight", (fout, fin), MLP_LR), (f"mlp.{name}.bias", (fout,), MLP_LR)]
         self.fp = FlatParams(spec, device)
         for name, v in (("xyz", xyz), ("scaling", scaling_raw), ("rotation", rotation_raw), ("opacity", opacity_raw),
                         ("albedo", albedo_raw), ("roughness", rough_raw), ("metalness", metal_raw)):
             self.fp.load(name, v)
         g = torch.Generator().manual_seed(seed)
-        env = torch.randn(n_views, 25, 3, generator=g) * 0.3
-        env[:, 0] = 1.0
-        self.fp.load("env_sh", env)
-        self.fp.load("sky_sh", torch.randn(n_views, 4, 3, generator=g) * 0.3)
+        # embeddings: unit rows, as initialize_embeddings normalises its encoder's outputs
+        self.fp.load("embeddings", F.normalize(torch.randn(n_views, EMBEDDING_DIM, generator=g), dim=-1))
+        for name, fout, fin in MLP_LAYERS:  # nn.Linear's default: U(-1/sqrt(in), 1/sqrt(in))
+            bound = 1.0 / math.sqrt(fin)
+            self.fp.load(f"mlp.{name}.weight", (torch.rand(fout, fin, generator=g) * 2 - 1) * bound)
+            self.fp.load(f"mlp.{name}.bias", (torch.rand(fout, generator=g) * 2 - 1) * bound)
+        # one device generator for the iteration's random draws (dropout, SH noise, directions)
+        self.rng = torch.Generator(device=device)
+        self.rng.manual_seed(seed + 12345)
+        self.id_cache = {}
+        self.global_groups = {"embeddings"} | {n for n in self.fp.names if n.startswith("mlp.")}
         self.is_sky = is_sky.to(device).reshape(-1, 1).bool()
         self.P = P
         self.stats = {"xyz_gradient_accum": torch.zeros(P, 1, device=device),
@@ -341,14 +502,20 @@ _BLACK = {}
 
 
 def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
-               world: int = 1, bg=None, streams=None) -> torch.Tensor:
+               world: int = 1, bg=None, streams=None, rand: Dict[str, torch.Tensor] = None) -> torch.Tensor:
     """One data-parallel iteration: this rank's views rendered and back-propagated, one
     all-reduce of the flat gradient, the densification statistics reduced, one fused Adam
     step with the mean gradient over all ranks' views.  ``streams``: HIP streams the views
     alternate over (None: the current stream).  The views are independent until the
     optimizer step, so one view's latency-bound geometry passes overlap another's tile
-    passes; autograd runs each view's backward on its forward's stream.  Returns this
-    rank's summed loss as a device scalar (no host synchronisation inside the step)."""
+    passes; autograd runs each view's backward on its forward's stream.  ``rand``: the
+    iteration's random draws (draw_step_randomness; default: from the scene's generator).
+    Returns this rank's summed loss as a device scalar (no host synchronisation inside the
+    step).
+
+    Per view (train.py:66-120): envlight_sh, sky_sh = MLPNet(embedding); render() with
+    envlight_sh + noise; loss = reconstruction + sky-BRDF + normal (view_loss)
+    + 100 envl_sh_loss(envlight_sh) + 100 min_scale_loss(radii) + 0.05 depth_loss_gaussians."""
     import relit_shade
 
     from . import relit
@@ -366,23 +533,38 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     # the activations are computed once per iteration and the views' losses share one
     # backward (autograd sums the views' gradients exactly as sequential backwards would)
     pc = scene.model()
-    # per-view lighting slices are taken on the main stream too (their leaves live there)
-    env = [fp.params["env_sh"][vid] for vid in view_ids]
-    sky = [fp.params["sky_sh"][vid:vid + 1] for vid in view_ids]
+    # the environment MLP runs once for the rank's views, on the main stream (its leaves live
+    # there): embeddings -> MLPNet (training-mode dropout) -> env SH (+ noise) and sky SH
+    V = len(views)
+    if rand is None:
+        rand = draw_step_randomness(V, dev, scene.rng)
+    key = tuple(int(v) for v in view_ids)
+    ids = scene.id_cache.get(key)
+    if ids is None:  # one host-to-device copy per view set, not per iteration
+        ids = scene.id_cache[key] = torch.as_tensor(key, device=dev, dtype=torch.long)
+    env_sh, sky_sh = mlp_forward(fp.params, fp.params["embeddings"][ids], rand["dropout"])
+    env_lit = env_sh + rand["noise"]
     losses, outs = [], []
     for i, (view, gt) in enumerate(zip(views, gts)):
         s = streams[i % len(streams)]
         s.wait_stream(main)
         with torch.cuda.stream(s):
-            light = relit_shade.EnvironmentLight(env[i], sh_degree=4)
-            out = relit.render(view, pc, light, sky[i], 1, pipe, bg, debug=False)
-            losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask))
+            light = relit_shade.EnvironmentLight(env_lit[i], sh_degree=4)
+            out = relit.render(view, pc, light, sky_sh[i:i + 1], 1, pipe, bg, debug=False)
+            losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask, LAMBDA_DSSIM, LAMBDA_SKY_BRDF,
+                                    LAMBDA_NORMAL))
         outs.append(out)
     for s in streams:
         main.wait_stream(s)
     for t in losses:
         t.record_stream(main)
-    total = torch.stack(losses).sum()
+    # envlight, min-scale and sky-depth regularisers of every view at once, on the main stream
+    radii = torch.stack([o["radii"] for o in outs])
+    for o in outs:
+        o["radii"].record_stream(main)
+    vms = torch.stack([v.world_view_transform for v in views]).float()
+    reg = view_regularisers(pc, radii, vms, env_sh, rand["dirs"])
+    total = torch.stack(losses).sum() + reg.sum()
     total.backward()
     for s in streams:
         main.wait_stream(s)

@@ -260,23 +260,32 @@ def test_cfg5_relit_render_fused_matches_calls():
     view = views[0]
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
     bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    g = torch.Generator().manual_seed(2)  # the lighting: env SH deg 4 (DC 1) and sky SH deg 1
+    env0 = torch.randn(25, 3, generator=g) * 0.3
+    env0[0] = 1.0
+    sky0 = torch.randn(1, 4, 3, generator=g) * 0.3
+    light_leaves = {"env_sh": env0.cuda().requires_grad_(True), "sky_sh": sky0.cuda().requires_grad_(True)}
 
     def run(fn, skip=()):
         scene.fp.zero_grad()
+        for t in light_leaves.values():
+            t.grad = None
         pc = scene.model()
-        light = relit_shade.EnvironmentLight(scene.fp.params["env_sh"][0], sh_degree=4)
-        out = fn(view, pc, light, scene.fp.params["sky_sh"][0:1], 1, pipe, bg, debug=False)
+        light = relit_shade.EnvironmentLight(light_leaves["env_sh"], sh_degree=4)
+        out = fn(view, pc, light, light_leaves["sky_sh"], 1, pipe, bg, debug=False)
         keys = sorted(k for k in out if k not in ("viewspace_points", "visibility_filter", "radii"))
         gen = torch.Generator(device="cuda").manual_seed(6)
         loss = sum((out[k] * torch.randn(out[k].shape, device="cuda", generator=gen)).sum()
                    for k in keys if k not in skip)
         loss.backward()
-        return {k: out[k].detach() for k in keys}, out["radii"], scene.fp.grad.clone(), \
-            out["viewspace_points"].grad.clone()
+        grads = torch.cat([scene.fp.grad] + [light_leaves[k].grad.reshape(-1) for k in ("env_sh", "sky_sh")])
+        return {k: out[k].detach() for k in keys}, out["radii"], grads, out["viewspace_points"].grad.clone()
 
     def grad_errs(g_f, g_r):
         errs = {}
-        for name, off, shape in zip(scene.fp.names, scene.fp.offsets, scene.fp.shapes):
+        segs = list(zip(scene.fp.names, scene.fp.offsets, scene.fp.shapes))
+        segs += [("env_sh", scene.fp.n, (75,)), ("sky_sh", scene.fp.n + 75, (12,))]
+        for name, off, shape in segs:
             n = int(np.prod(shape))
             a, b = g_f[off:off + n].double(), g_r[off:off + n].double()
             if b.any():

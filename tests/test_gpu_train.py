@@ -69,6 +69,8 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
     streams = None if nstreams == 1 else [torch.cuda.Stream() for _ in range(nstreams)]
     scene, views, gts = train.synthetic_relit_scene(3000, 2, 160, 96, 120.0, dev, seed=3)
     fp = scene.fp
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
     # the reference-style step: separate leaves, autograd, torch.optim.Adam over the groups
     leaves = {n: fp.params[n].detach().clone().requires_grad_(True) for n in fp.names}
     opt = torch.optim.Adam([{"params": [leaves[n]], "lr": lr} for n, lr in zip(fp.names, fp.lrs)], lr=0.01,
@@ -77,24 +79,31 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
     bg = torch.zeros(3, device=dev)
     for it in range(2):
         opt.zero_grad(set_to_none=True)
+        rand = train.draw_step_randomness(2, dev, gen)
+        env_sh, sky_sh = train.mlp_forward(leaves, leaves["embeddings"][[0, 1]], rand["dropout"])
         for vid, (view, gt) in enumerate(zip(views, gts)):
             pc = types.SimpleNamespace(
                 get_xyz=leaves["xyz"], get_scaling=torch.exp(leaves["scaling"]),
                 get_rotation=F.normalize(leaves["rotation"]), get_opacity=torch.sigmoid(leaves["opacity"]),
                 get_albedo=torch.sigmoid(leaves["albedo"]), get_roughness=torch.sigmoid(leaves["roughness"]),
                 get_metalness=torch.sigmoid(leaves["metalness"]), get_is_sky=scene.is_sky)
-            light = relit_shade.EnvironmentLight(leaves["env_sh"][vid], sh_degree=4)
-            out = relit.render(view, pc, light, leaves["sky_sh"][vid:vid + 1], 1, pipe, bg, debug=False)
+            light = relit_shade.EnvironmentLight(env_sh[vid] + rand["noise"][vid], sh_degree=4)
+            out = relit.render(view, pc, light, sky_sh[vid:vid + 1], 1, pipe, bg, debug=False)
             loss = train.view_loss(out, gt, view.sky_mask.expand_as(gt), view.occluders_mask.expand_as(gt))
-            loss.backward()
+            loss = loss + 100.0 * train.envl_sh_loss(env_sh[vid:vid + 1], 4, dirs=rand["dirs"][vid])
+            loss = loss + 100.0 * train.min_scale_loss(out["radii"], pc)
+            loss = loss + 0.05 * train.depth_loss_gaussians(pc, view, out["radii"] > 0)
+            loss.backward(retain_graph=vid == 0)
         for p in leaves.values():
             p.grad /= len(views)
         opt.step()
-        loss_flat = train.train_step(scene, views, [0, 1], gts, streams=streams)
+        loss_flat = train.train_step(scene, views, [0, 1], gts, streams=streams, rand=rand)
     torch.cuda.synchronize()
     assert torch.isfinite(loss_flat)
     for n in fp.names:
         e = rel_l2(fp.params[n].detach().cpu().numpy(), leaves[n].detach().cpu().numpy())
         assert e < 1e-4, (n, e)
+    for n in ("embeddings", "mlp.base.0.weight", "mlp.sh_envl_outlayer.bias", "mlp.sh_sky_outlayer.weight"):
+        assert float(fp.grad[fp.offsets[fp.names.index(n)]:fp.ends[fp.names.index(n)]].abs().sum()) > 0, n
     assert float(scene.stats["denom"].max()) == 4.0  # 2 views x 2 iterations
     assert float(scene.stats["xyz_gradient_accum"].sum()) > 0

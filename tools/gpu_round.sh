@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
