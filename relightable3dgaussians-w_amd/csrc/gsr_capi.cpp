@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <unordered_set>
 #include <string>
 #include <vector>
 
@@ -176,6 +177,21 @@ struct BinHint {
     long long R = 0, S = 0;
 };
 thread_local BinHint g_hint;
+
+// Geometry buffers whose gradient accumulators the forward zeroed (in the depth sort's digit
+// scans) and no backward has used yet: the backward skips its zero-fill for them.  A second
+// backward over the same forward, or a geometry buffer made by gsr_forward_reuse, zero-fills.
+std::mutex g_zeroed_mu;
+std::unordered_set<const void*> g_zeroed;
+void zeroed_set(const void* geom, bool on) {
+    std::lock_guard<std::mutex> lk(g_zeroed_mu);
+    if (on) g_zeroed.insert(geom);
+    else g_zeroed.erase(geom);
+}
+bool zeroed_take(const void* geom) {
+    std::lock_guard<std::mutex> lk(g_zeroed_mu);
+    return g_zeroed.erase(geom) > 0;
+}
 
 // Deterministic backward (gsr_set_deterministic / GSR_DETERMINISTIC=1): per-instance partial
 // rows summed in a fixed order (gsr_det.hip) instead of the tile passes' atomics.
@@ -582,8 +598,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         GSR_STAGE(ST_DEPTH_SORT);
         flip = gsr::depth_sort(P, pa.depth_key, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
                                at<uint32_t>(geom, gl.vis_val_alt), pa.rect, at<uint2>(geom, gl.rect_s),
-                               at<uint2>(geom, gl.rect_s_alt), at<void>(geom, gl.sort_tmp), tot_dev, s);
+                               at<uint2>(geom, gl.rect_s_alt), at<void>(geom, gl.sort_tmp), tot_dev, s,
+                               at<void>(geom, gl.acc), sizeof(float) * gsr::ACC_STRIDE * (size_t)P);
     }
+    zeroed_set(geom, true);  // the backward's accumulators are zero from here on
     GSR_LAUNCH_CHECK();
 
     unsigned long long Pv = 0, R64 = 0, S64 = 0;
@@ -779,6 +797,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
     if (!geom) return fail(GSR_E_ALLOC, "gsr_forward_reuse: buffer allocation failed");
     geom = align_base(geom);
+    zeroed_set(geom, false);  // its accumulators are not zeroed here: the backward zero-fills
     const char* src = align_base(const_cast<void*>(src_geom_buffer));
     char* img = align_base(image_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
@@ -836,9 +855,10 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
     if (!radii) radii = at<int>(geom, gl.radii);
     float* acc = at<float>(geom, gl.acc);
-    {
+    const bool acc_zero = zeroed_take(geom);  // zeroed by this buffer's forward, unused since
+    if (!acc_zero || mc) {
         GSR_STAGE(ST_BWD_ZERO);
-        HIP_OK(hipMemsetAsync(acc, 0, sizeof(float) * gsr::ACC_STRIDE * (size_t)P, s));
+        if (!acc_zero) HIP_OK(hipMemsetAsync(acc, 0, sizeof(float) * gsr::ACC_STRIDE * (size_t)P, s));
         if (mc) HIP_OK(hipMemsetAsync(mc->dL_dfeat, 0, sizeof(float) * (size_t)mc->fstride * P, s));
     }
 

@@ -90,7 +90,7 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 size_t depth_sort_temp_bytes(long long P);
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
-               unsigned long long* pv_out, hipStream_t s);
+               unsigned long long* pv_out, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0);
 
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
 // (P_v, R, S, error) and stores them to host-mapped memory as (value << 16 | seq mod 2^16)

@@ -88,7 +88,22 @@ __device__ __forceinline__ void digit_row_scan(uint32_t* h, int ncol, uint32_t* 
     if (threadIdx.x == 0) *total = carry;
 }
 
-__global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int nb, uint32_t* digit_tot) {
+// Workgroups past the ndig digits zero-fill a slice of `zero` (the depth sort carries the
+// backward's gradient accumulators this way: the digit scans are latency-bound launches, and a
+// separate memset before the backward's tile pass cost 13 us + a 6 us launch gap).
+constexpr int ZERO_F4_PER_THREAD = 8;
+__global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int nb, uint32_t* digit_tot,
+                                                             float4* zero = nullptr, long long zero_n4 = 0,
+                                                             int ndig = 0x7fffffff) {
+    if ((int)blockIdx.x >= ndig) {  // zero-fill workgroups (only the depth sort sets ndig)
+        const long long b = (long long)(blockIdx.x - ndig) * SORT_THREADS * ZERO_F4_PER_THREAD + threadIdx.x;
+#pragma unroll
+        for (int k = 0; k < ZERO_F4_PER_THREAD; k++) {
+            const long long i = b + (long long)k * SORT_THREADS;
+            if (i < zero_n4) zero[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        return;
+    }
     __shared__ uint32_t sh[4];
     digit_row_scan(hist + (long long)blockIdx.x * nb, nb, digit_tot + blockIdx.x, sh);
 }
@@ -242,7 +257,7 @@ size_t depth_sort_temp_bytes(long long P) {
 
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
-               unsigned long long* pv_out, hipStream_t s) {
+               unsigned long long* pv_out, hipStream_t s, void* zero, size_t zero_bytes) {
     if (P <= 0) return -1;
     const int nb = sort_blocks(P);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
@@ -257,7 +272,13 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
     for (int pass = 0; pass < 4; pass++) {
         const int shift = 8 * pass;
         hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, shift, 255u, hist, nb);
-        hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
+        // a quarter of the zero-fill (16-B multiples) rides in each pass's digit scan
+        const long long n4 = (long long)(zero ? zero_bytes / 16 : 0);
+        const long long q0 = n4 * pass / 4, q1 = n4 * (pass + 1) / 4;
+        const long long per_blk = (long long)SORT_THREADS * ZERO_F4_PER_THREAD;
+        const unsigned zb = (unsigned)((q1 - q0 + per_blk - 1) / per_blk);
+        hipLaunchKernelGGL(k_digit_scan, dim3(256 + zb), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot,
+                           zb ? reinterpret_cast<float4*>(zero) + q0 : (float4*)nullptr, q1 - q0, 256);
         hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift, 255u, hist,
                            digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1,
                            pass == 3 ? pv_out : (unsigned long long*)nullptr);
