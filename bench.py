@@ -45,7 +45,10 @@ def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
         "preprocess": P * 12 + Pv * (32 + S) + P * 8 + Pv * 67,
         "render_fwd": T * 8 + R * 40 + Npix * 20,
         "render_bwd": T * 8 + R * 40 + Npix * 20 + Pv * 44,
-        "preprocess_bwd": P * 4 + Pv * (12 + 12 + 12 + 12 + 3 + 12 + 16 + 24 + 12 * M) + Pv * (12 + 12 + 16 + 12 * M),
+        # this design's compulsory bytes: reads radii, the 9-float accumulator line,
+        # means, scales, rotations, SH; writes every output row of every Gaussian (the reference's
+        # zero-filled buffers: dmean2D, dcolor, dopacity, dmean3D, dcov3D, dscale, drot, dsh)
+        "preprocess_bwd": P * (4 + 36 + 12 + 12 + 16 + 12 * M) + P * (12 + 12 + 4 + 12 + 24 + 12 + 16 + 12 * M),
     }.get(stage)
 
 

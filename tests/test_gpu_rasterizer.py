@@ -382,3 +382,25 @@ def test_speculative_binning_capacity_and_overflow():
         check_forward(st, ref, 96, 80)
         Rs.append(st["R"])
     assert Rs[2] > 2 * Rs[1] and Rs[0] == Rs[1] == Rs[3]
+
+
+def test_second_backward_over_one_forward():
+    """The forward zeroes the gradient accumulators (inside the depth sort's digit scans) and
+    the first backward skips its zero-fill; a second backward over the same buffers (autograd's
+    retain_graph) must zero-fill again and return the same gradients."""
+    _, _C, _ = _dgr()
+    cam, gs = make_case(P=3000, W=128, H=96, sh_degree=2, camera="orbit")
+    st = run_gpu(cam, gs, mode="sh", sh_degree=2)
+    W, H = cam.image_width, cam.image_height
+    dout = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4)).cuda()
+
+    def bwd():
+        return _C.rasterize_gaussians_backward(
+            st["bg"], st["means"], st["radii"], st["colors"], st["scales"], st["rots"], 1.0, st["cov3"], st["vm"],
+            st["pm"], cam.tanfovx, cam.tanfovy, dout, st["sh"], 2, st["cp"], st["geom"], st["R"], st["binb"],
+            st["img"])
+    g1 = [t.clone() for t in bwd()]
+    g2 = bwd()
+    for a, b in zip(g1, g2):
+        if a.numel():
+            assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) < 1e-6
