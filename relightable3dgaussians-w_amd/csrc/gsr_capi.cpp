@@ -185,8 +185,14 @@ std::mutex g_zeroed_mu;
 std::unordered_set<const void*> g_zeroed;
 void zeroed_set(const void* geom, bool on) {
     std::lock_guard<std::mutex> lk(g_zeroed_mu);
-    if (on) g_zeroed.insert(geom);
-    else g_zeroed.erase(geom);
+    if (on) {
+        // forwards without a backward (inference) leave entries behind: bounded, since a
+        // forgotten entry only costs a backward its zero-fill
+        if (g_zeroed.size() >= 4096) g_zeroed.clear();
+        g_zeroed.insert(geom);
+    } else {
+        g_zeroed.erase(geom);
+    }
 }
 bool zeroed_take(const void* geom) {
     std::lock_guard<std::mutex> lk(g_zeroed_mu);
