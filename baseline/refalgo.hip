@@ -254,7 +254,7 @@ struct Grow {
 }  // namespace
 
 struct GsrRefCtx {
-    Grow geom_rec, geom_aux, keys, vals, keys_alt, vals_alt, sort_tmp, scan_tmp, img, acc;
+    Grow geom_rec, geom_aux, keys, vals, keys_alt, vals_alt, sort_tmp, scan_tmp, img, acc, shjac;
     int P = 0, W = 0, H = 0, R = 0;
     float* final_T = nullptr;
     uint32_t* n_contrib = nullptr;
@@ -332,6 +332,7 @@ int gsr_ref_forward(GsrRefCtx* ctx, void* stream, int P, int D, int M, const flo
     pa.grid_x = gx; pa.grid_y = gy; pa.prefiltered = 0;
     pa.radii = radii; pa.tiles = tiles; pa.st_count = st_count; pa.depth_key = depth_key; pa.rect = rect;
     pa.rec = ctx->rec;  // blk_tot / hist0 null: this baseline scans tiles_touched itself
+    pa.shjac = (shs && !colors_precomp) ? (float*)ctx->shjac.get(sizeof(float) * gsr::SHJAC_ROWS * (size_t)P) : nullptr;
     gsr::launch_preprocess(pa, s);
 
     size_t scan_bytes = 0;
@@ -397,6 +398,7 @@ int gsr_ref_backward(GsrRefCtx* ctx, void* stream, int D, int M, const float* bg
     pb.tan_fovx = tan_fovx; pb.tan_fovy = tan_fovy;
     pb.focal_x = W / (2.0f * tan_fovx); pb.focal_y = H / (2.0f * tan_fovy);
     pb.acc = acc;
+    pb.shjac = (const float*)ctx->shjac.get(sizeof(float) * gsr::SHJAC_ROWS * (size_t)P);
     pb.dL_dmean2D = dL_dmean2D; pb.dL_dconic = dL_dconic; pb.dL_dopacity = dL_dopacity; pb.dL_dcolor = dL_dcolor;
     pb.dL_dmean3D = dL_dmean3D; pb.dL_dcov3D = dL_dcov3D; pb.dL_dsh = M > 0 ? dL_dsh : nullptr;
     pb.dL_dscale = dL_dscale; pb.dL_drot = dL_drot;

@@ -59,7 +59,7 @@ struct Carver {
 };
 
 struct GeomLayout {
-    size_t tot_dev, blk_tot, radii, tiles, st_count, depth_key, rect, rec, acc, vis_key, vis_val, vis_key_alt, vis_val_alt, rect_s, rect_s_alt,
+    size_t tot_dev, blk_tot, radii, tiles, st_count, depth_key, rect, rec, acc, shjac, vis_key, vis_val, vis_key_alt, vis_val_alt, rect_s, rect_s_alt,
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
@@ -83,6 +83,7 @@ GeomLayout geom_layout(long long P) {
     L.rect = c.take(8 * P);
     L.rec = c.take(sizeof(gsr::Rec) * P);
     L.acc = c.take(4 * gsr::ACC_STRIDE * P);
+    L.shjac = c.take(4 * (size_t)gsr::SHJAC_ROWS * P);  // SH path: the forward's Jacobian for the backward
     L.vis_key = c.take(4 * P);
     L.vis_val = c.take(4 * P);
     L.vis_key_alt = c.take(4 * P);
@@ -561,6 +562,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     pa.depth_key = at<uint32_t>(geom, gl.depth_key);
     pa.rect = at<uint2>(geom, gl.rect);
     pa.rec = at<gsr::Rec>(geom, gl.rec);
+    pa.shjac = (shs && !colors_precomp) ? at<float>(geom, gl.shjac) : nullptr;
     pa.blk_tot = at<uint4>(geom, gl.blk_tot);
     {
         GSR_STAGE(ST_PREPROCESS);
@@ -964,6 +966,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
     pb.viewmatrix = viewmatrix; pb.projmatrix = projmatrix; pb.campos = campos;
     pb.tan_fovx = tan_fovx; pb.tan_fovy = tan_fovy; pb.focal_x = focal_x; pb.focal_y = focal_y;
     pb.acc = acc;
+    pb.shjac = at<float>(geom, gl.shjac);
     pb.dL_dmean2D = dL_dmean2D; pb.dL_dconic = dL_dconic; pb.dL_dopacity = dL_dopacity; pb.dL_dcolor = dL_dcolor;
     pb.dL_dmean3D = dL_dmean3D; pb.dL_dcov3D = dL_dcov3D; pb.dL_dsh = M > 0 ? dL_dsh : nullptr;
     pb.dL_dscale = dL_dscale; pb.dL_drot = dL_drot;

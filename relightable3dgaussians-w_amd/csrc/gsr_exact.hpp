@@ -137,4 +137,53 @@ __device__ __forceinline__ float3 sh_to_rgb_raw(int deg, float3 pos, const float
     return make_float3(res[0] + 0.5f, res[1] + 0.5f, res[2] + 0.5f);
 }
 
+// d(SH colour)/d(unit view direction) per channel (backward.cu:61-113, the dRGBdx/dy/dz of
+// the SH backward) at the direction (x, y, z), from the SH row `sh` ([M][3]).  The forward
+// preprocess evaluates it once and stores it for the backward (gsr_preprocess.hip); both TUs
+// compile with contraction off, so it is the arithmetic the backward would do, bit for bit.
+template <int MAXD = 3>
+__device__ __forceinline__ void sh_dir_jacobian(int deg, float x, float y, float z, const float* sh, float (&ddx)[3],
+                                                float (&ddy)[3], float (&ddz)[3]) {
+#define SHC(k, c) sh[3 * (k) + (c)]
+#pragma unroll
+    for (int c = 0; c < 3; c++) ddx[c] = ddy[c] = ddz[c] = 0.f;
+    if (MAXD > 0 && deg > 0) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            ddx[c] = -SH_C1 * SHC(3, c);
+            ddy[c] = -SH_C1 * SHC(1, c);
+            ddz[c] = SH_C1 * SHC(2, c);
+        }
+        if (MAXD > 1 && deg > 1) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
+                          SH_C2_4 * 2.f * x * SHC(8, c);
+                ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
+                          SH_C2_4 * 2.f * -y * SHC(8, c);
+                ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
+            }
+            if (MAXD > 2 && deg > 2) {
+                const float xx = x * x, yy = y * y, zz = z * z;
+                const float xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
+                               SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
+                               SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
+                               SH_C3_5 * SHC(14, c) * 2.f * xz + SH_C3_6 * SHC(15, c) * 3.f * (xx - yy));
+                    ddy[c] += (SH_C3_0 * SHC(9, c) * 3.f * (xx - yy) + SH_C3_1 * SHC(10, c) * xz +
+                               SH_C3_2 * SHC(11, c) * (-3.f * yy + 4.f * zz - xx) +
+                               SH_C3_3 * SHC(12, c) * -3.f * 2.f * yz + SH_C3_4 * SHC(13, c) * -2.f * xy +
+                               SH_C3_5 * SHC(14, c) * -2.f * yz + SH_C3_6 * SHC(15, c) * -3.f * 2.f * xy);
+                    ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
+                               SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
+                               SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
+                }
+            }
+        }
+    }
+#undef SHC
+}
+
 }  // namespace gsr

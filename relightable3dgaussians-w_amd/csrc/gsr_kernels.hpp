@@ -9,6 +9,7 @@
 
 namespace gsr {
 
+constexpr int SHJAC_ROWS = 10;
 struct PreprocessArgs {
     int P, D, M;
     const float* means3D;
@@ -33,6 +34,9 @@ struct PreprocessArgs {
     uint32_t* depth_key;
     uint2* rect;
     Rec* rec;
+    // SH path, visible Gaussians (optional): d(colour)/d(view direction) and the clamp flags
+    // for the backward, SoA [SHJAC_ROWS][P]: rows 0-8 ddx[c], ddy[c], ddz[c]; row 9 the flags
+    float* shjac;
     // per 256-Gaussian workgroup (optional, null to skip): blk_tot[b] = (visible, instances
     // R, super-tile entries S, prefiltered-error flag)
     uint4* blk_tot;
@@ -327,6 +331,7 @@ struct PreprocessBwdArgs {
     const float* campos;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const float* acc;  // [P][ACC_STRIDE] from the render backward
+    const float* shjac;  // [SHJAC_ROWS][P] from the forward preprocess (required with shs)
     // outputs (fully written, no pre-zeroing needed)
     float* dL_dmean2D;
     float* dL_dconic;

@@ -87,6 +87,23 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
         } else if (a.shs) {
             const float3 raw = sh_to_rgb_raw<MAXD>(a.D, p_orig, a.campos, sh_row);
             rgb = make_float3(raw.x < 0 ? 0.f : raw.x, raw.y < 0 ? 0.f : raw.y, raw.z < 0 ? 0.f : raw.z);
+            if (a.shjac) {
+                // the SH backward's view-direction Jacobian and clamp flags (backward.cu:20-139),
+                // stored so the backward reads 40 B instead of the 12 M-byte SH row
+                float3 dir = make_float3(p_orig.x - a.campos[0], p_orig.y - a.campos[1], p_orig.z - a.campos[2]);
+                const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
+                float ddx[3], ddy[3], ddz[3];
+                sh_dir_jacobian<MAXD>(a.D, dir.x / len, dir.y / len, dir.z / len, sh_row, ddx, ddy, ddz);
+                const size_t P = (size_t)a.P;
+                float* jp = a.shjac + idx;
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    jp[(size_t)c * P] = ddx[c];
+                    jp[(size_t)(3 + c) * P] = ddy[c];
+                    jp[(size_t)(6 + c) * P] = ddz[c];
+                }
+                jp[9 * P] = __uint_as_float((raw.x < 0 ? 1u : 0u) | (raw.y < 0 ? 2u : 0u) | (raw.z < 0 ? 4u : 0u));
+            }
         } else {
             rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record
         }

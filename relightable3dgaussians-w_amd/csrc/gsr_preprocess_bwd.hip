@@ -4,9 +4,12 @@
 // backward's 64-B accumulator line into the reference's output tensors.
 //
 // One kernel instead of two + nine memsets: every output element is written here
-// (zeros for culled Gaussians), so the caller's buffers need no zero-fill.  cov3D and
-// the SH clamp flags are recomputed with the forward's exact (contraction-off) code
-// instead of being stored and re-read.
+// (zeros for culled Gaussians), so the caller's buffers need no zero-fill.  cov3D is
+// recomputed with the forward's exact (contraction-off) code instead of being stored and
+// re-read.  The SH part never reads the SH rows: the forward preprocess stored each visible
+// Gaussian's d(colour)/d(view direction) and clamp flags (40 B, gsr_preprocess.hip), and
+// dL/dsh = basis(dir) x dL/dcolour is written from the basis and the masked colour gradient
+// staged per Gaussian in LDS (80 B) by a coalesced 16-B writer.
 #pragma clang fp contract(off)
 #include "gsr_exact.hpp"
 
@@ -14,8 +17,7 @@
 
 namespace gsr {
 
-// One Gaussian's inputs, loaded before the workgroup's SH rows are staged (every global load
-// of the thread in flight at once instead of one dependent round trip after the barrier).
+// One Gaussian's inputs, all loads issued up front.
 struct BwdIn {
     float4 l0, l1;  // accumulator line [0..8)
     float l2;       // [8]
@@ -24,6 +26,8 @@ struct BwdIn {
     float4 rot;
     float3 scl;
     float cov[6];
+    float jac[9];   // SH path: ddx[c], ddy[c], ddz[c] from the forward
+    uint32_t clampf;
 };
 
 __device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx, BwdIn& in) {
@@ -40,10 +44,15 @@ __device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx,
         in.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
         in.scl = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
     }
+    if (a.shs) {  // coalesced SoA rows
+        const size_t P = (size_t)a.P;
+#pragma unroll
+        for (int k = 0; k < 9; k++) in.jac[k] = a.shjac[(size_t)k * P + idx];
+        in.clampf = __float_as_uint(a.shjac[9 * P + idx]);
+    }
 }
 
-template <int MC, bool DO_SH = true>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* row);
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* brow);
 
 // auxiliary.h:107-117
 __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
@@ -56,176 +65,46 @@ __device__ __forceinline__ float3 dnormvdv3(float3 v, float3 dv) {
     return o;
 }
 
-// SH rows ([M][3] floats = 192 B at degree 3) of the workgroup's Gaussians are one
-// contiguous block in HBM: it is moved as a flat array of 16-B words (every lane busy,
-// many loads in flight) and scattered into LDS rows of stride M*3+1 (odd: conflict-free
-// per-thread row access); the gradient rows go back out the same way.
-__device__ __forceinline__ void load_rows(float* s, int stride, const float* g, int rows, int width) {
-    const int n = rows * width;
-    if ((width & 3) == 0) {
-        const float4* g4 = reinterpret_cast<const float4*>(g);
-        for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
-            const float4 v = g4[f];
-            const int e0 = f * 4, r = e0 / width, e = e0 - r * width;
-            float* d = s + r * stride + e;
-            d[0] = v.x;
-            d[1] = v.y;
-            d[2] = v.z;
-            d[3] = v.w;
-        }
-    } else {
-        for (int f = threadIdx.x; f < n; f += blockDim.x) {
-            const int r = f / width;
-            s[r * stride + f - r * width] = g[f];
-        }
-    }
-}
-__device__ __forceinline__ void store_rows(float* g, const float* s, int stride, int rows, int width) {
-    const int n = rows * width;
-    if ((width & 3) == 0) {
-        float4* g4 = reinterpret_cast<float4*>(g);
-        for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
-            const int e0 = f * 4, r = e0 / width, e = e0 - r * width;
-            const float* d = s + r * stride + e;
-            g4[f] = make_float4(d[0], d[1], d[2], d[3]);
-        }
-    } else {
-        for (int f = threadIdx.x; f < n; f += blockDim.x) {
-            const int r = f / width;
-            g[f] = s[r * stride + f - r * width];
-        }
-    }
-}
+// LDS row per Gaussian for the dL/dsh writer: the 16 SH basis values (zero above the
+// evaluated degree, and for culled Gaussians), the masked colour gradient g[3], one pad
+constexpr int BROW = 20;
 
 __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
-    extern __shared__ float s_sh[];
-    const int M3 = a.M * 3, sh_stride = M3 + 1;
+    __shared__ float s_b[256 * BROW];
     const int g0 = blockIdx.x * blockDim.x;
-    const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
-    BwdIn in;
-    if (g0 + (int)threadIdx.x < a.P) load_bwd_in(a, g0 + threadIdx.x, in);
-    if (a.shs) {
-        load_rows(s_sh, sh_stride, a.shs + (size_t)g0 * M3, rows, M3);
-        __syncthreads();
-    }
     const int idx = g0 + threadIdx.x;
-    if (idx < a.P) preprocess_bwd_one<0>(a, idx, in, s_sh + threadIdx.x * sh_stride);
+    BwdIn in;
+    if (idx < a.P) load_bwd_in(a, idx, in);
+    if (idx < a.P) preprocess_bwd_one(a, idx, in, s_b + threadIdx.x * BROW);
     if (a.dL_dsh) {
+        // dL/dsh[k][c] = basis[k] g[c] (backward.cu:20-139): the workgroup's rows ([M][3] floats
+        // each, contiguous) leave as 16-B stores, each element from its Gaussian's LDS row
         __syncthreads();
-        store_rows(a.dL_dsh + (size_t)g0 * M3, s_sh, sh_stride, rows, M3);
+        const int M3 = a.M * 3;
+        const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
+        float* out = a.dL_dsh + (size_t)g0 * M3;
+        const int n = rows * M3;
+        auto elem = [&](int e) -> float {
+            const int r = e / M3, w = e - r * M3, k = w / 3, c = w - 3 * k;
+            const float* b = s_b + r * BROW;
+            return k < 16 ? b[k] * b[16 + c] : 0.f;
+        };
+        if ((M3 & 3) == 0) {
+            float4* o4 = reinterpret_cast<float4*>(out);
+            for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
+                const int e0 = 4 * f;
+                o4[f] = make_float4(elem(e0), elem(e0 + 1), elem(e0 + 2), elem(e0 + 3));
+            }
+        } else {
+            for (int e = threadIdx.x; e < n; e += blockDim.x) out[e] = elem(e);
+        }
     }
 }
 
-// backward.cu:20-139 for one Gaussian: reads the SH coefficients from `row`, overwrites
-// them with dL/dsh (each degree block reads its coefficients before overwriting them) and
-// returns the view-direction part of dL/dmean3D.  MC as preprocess_bwd_one.
-template <int MC>
-__device__ __forceinline__ float3 sh_bwd_row(const PreprocessBwdArgs& a, float3 mean, float* row, float dcol0,
-                                             float dcol1, float dcol2) {
-    // backward.cu:20-139 on this Gaussian's LDS row (coalesced in/out, see below);
-    // each degree block reads its coefficients before overwriting them with dL/dsh.
-    float* sh = row;
-    constexpr int MAXD = MC == 0 ? 3 : (MC >= 16 ? 3 : MC >= 9 ? 2 : MC >= 4 ? 1 : 0);
-    const float3 raw = sh_to_rgb_raw<MAXD>(a.D, mean, a.campos, sh);  // clamp flags, as the forward
-    const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
-    const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
-    const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
-    float g[3] = {dcol0 * (raw.x < 0 ? 0 : 1), dcol1 * (raw.y < 0 ? 0 : 1), dcol2 * (raw.z < 0 ? 0 : 1)};
-    float ddx[3] = {0, 0, 0}, ddy[3] = {0, 0, 0}, ddz[3] = {0, 0, 0};
-    const int deg = a.D;
-    float* dsh = sh;
-#define SHC(k, c) sh[3 * (k) + (c)]
-#pragma unroll
-    for (int c = 0; c < 3; c++) dsh[c] = SH_C0 * g[c];
-    if ((MC == 0 || MC >= 4) && deg > 0) {
-        const float b1 = -SH_C1 * y, b2 = SH_C1 * z, b3 = -SH_C1 * x;
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            ddx[c] = -SH_C1 * SHC(3, c);
-            ddy[c] = -SH_C1 * SHC(1, c);
-            ddz[c] = SH_C1 * SHC(2, c);
-            dsh[3 + c] = b1 * g[c];
-            dsh[6 + c] = b2 * g[c];
-            dsh[9 + c] = b3 * g[c];
-        }
-        if ((MC == 0 || MC >= 9) && deg > 1) {
-            const float xx = x * x, yy = y * y, zz = z * z;
-            const float xy = x * y, yz = y * z, xz = x * z;
-            const float b4 = SH_C2_0 * xy, b5 = SH_C2_1 * yz, b6 = SH_C2_2 * (2.f * zz - xx - yy);
-            const float b7 = SH_C2_3 * xz, b8 = SH_C2_4 * (xx - yy);
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                ddx[c] += SH_C2_0 * y * SHC(4, c) + SH_C2_2 * 2.f * -x * SHC(6, c) + SH_C2_3 * z * SHC(7, c) +
-                          SH_C2_4 * 2.f * x * SHC(8, c);
-                ddy[c] += SH_C2_0 * x * SHC(4, c) + SH_C2_1 * z * SHC(5, c) + SH_C2_2 * 2.f * -y * SHC(6, c) +
-                          SH_C2_4 * 2.f * -y * SHC(8, c);
-                ddz[c] += SH_C2_1 * y * SHC(5, c) + SH_C2_2 * 2.f * 2.f * z * SHC(6, c) + SH_C2_3 * x * SHC(7, c);
-                dsh[12 + c] = b4 * g[c];
-                dsh[15 + c] = b5 * g[c];
-                dsh[18 + c] = b6 * g[c];
-                dsh[21 + c] = b7 * g[c];
-                dsh[24 + c] = b8 * g[c];
-            }
-            if ((MC == 0 || MC >= 16) && deg > 2) {
-                const float b9 = SH_C3_0 * y * (3.f * xx - yy);
-                const float b10 = SH_C3_1 * xy * z;
-                const float b11 = SH_C3_2 * y * (4.f * zz - xx - yy);
-                const float b12 = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                const float b13 = SH_C3_4 * x * (4.f * zz - xx - yy);
-                const float b14 = SH_C3_5 * z * (xx - yy);
-                const float b15 = SH_C3_6 * x * (xx - 3.f * yy);
-#pragma unroll
-                for (int c = 0; c < 3; c++) {
-                    ddx[c] += (SH_C3_0 * SHC(9, c) * 3.f * 2.f * xy + SH_C3_1 * SHC(10, c) * yz +
-                               SH_C3_2 * SHC(11, c) * -2.f * xy + SH_C3_3 * SHC(12, c) * -3.f * 2.f * xz +
-                               SH_C3_4 * SHC(13, c) * (-3.f * xx + 4.f * zz - yy) +
-                               SH_C3_5 * SHC(14, c) * 2.f * xz + SH_C3_6 * SHC(15, c) * 3.f * (xx - yy));
-                    ddy[c] += (SH_C3_0 * SHC(9, c) * 3.f * (xx - yy) + SH_C3_1 * SHC(10, c) * xz +
-                               SH_C3_2 * SHC(11, c) * (-3.f * yy + 4.f * zz - xx) +
-                               SH_C3_3 * SHC(12, c) * -3.f * 2.f * yz + SH_C3_4 * SHC(13, c) * -2.f * xy +
-                               SH_C3_5 * SHC(14, c) * -2.f * yz + SH_C3_6 * SHC(15, c) * -3.f * 2.f * xy);
-                    ddz[c] += (SH_C3_1 * SHC(10, c) * xy + SH_C3_2 * SHC(11, c) * 4.f * 2.f * yz +
-                               SH_C3_3 * SHC(12, c) * 3.f * (2.f * zz - xx - yy) +
-                               SH_C3_4 * SHC(13, c) * 4.f * 2.f * xz + SH_C3_5 * SHC(14, c) * (xx - yy));
-                    dsh[27 + c] = b9 * g[c];
-                    dsh[30 + c] = b10 * g[c];
-                    dsh[33 + c] = b11 * g[c];
-                    dsh[36 + c] = b12 * g[c];
-                    dsh[39 + c] = b13 * g[c];
-                    dsh[42 + c] = b14 * g[c];
-                    dsh[45 + c] = b15 * g[c];
-                }
-            }
-        }
-    }
-#undef SHC
-    // coefficients above the evaluated degree get zero gradient (torch::zeros in the reference)
-    const int kmin = deg < 0 ? 0 : (deg > 3 ? 16 : (deg + 1) * (deg + 1));
-    if constexpr (MC > 0) {
-#pragma unroll
-        for (int k = 0; k < MC; k++)
-            if (k >= kmin) dsh[3 * k] = dsh[3 * k + 1] = dsh[3 * k + 2] = 0.f;
-    } else {
-        for (int k = kmin; k < a.M; k++) {
-            dsh[3 * k] = 0.f;
-            dsh[3 * k + 1] = 0.f;
-            dsh[3 * k + 2] = 0.f;
-        }
-    }
-    const float3 dL_ddir = make_float3(ddx[0] * g[0] + ddx[1] * g[1] + ddx[2] * g[2],
-                                       ddy[0] * g[0] + ddy[1] * g[1] + ddy[2] * g[2],
-                                       ddz[0] * g[0] + ddz[1] * g[1] + ddz[2] * g[2]);
-    return dnormvdv3(dir_orig, dL_ddir);
-}
-
-// `row` holds the Gaussian's SH coefficients (MC > 0: a register array of 3 MC floats; MC
-// == 0: an LDS row of a.M * 3 floats, k_preprocess_bwd).  The SH backward reads the
-// coefficients from the row and overwrites them with dL/dsh.  (Measured slower at cfg2:
-// register rows, 242 vs 199 us -- 182 VGPRs leave 2 waves per SIMD; and a split into a
-// geometry kernel + a register-row SH kernel, 63 + 196 us -- its strided 16-B row stores
-// write partial lines, where the LDS-staged rows leave the workgroup as whole lines.)
-template <int MC, bool DO_SH>
-__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* row) {
+// One Gaussian: every per-Gaussian output, and (with dL_dsh) its LDS row for the dL/dsh
+// writer.  (A register SH row cost 182 VGPRs; the LDS-staged SH rows of round 1 held the
+// occupancy to 3 waves per SIMD.)
+__device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* brow) {
     // ---- unpack the render-backward accumulator line ------------------------------
     const float4 l0 = in.l0, l1 = in.l1;
     const float l2 = in.l2;
@@ -244,8 +123,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     }
 
     float* dcov = a.dL_dcov3D + 6 * idx;
-    float* dsh = row;  // written back by the caller when dL_dsh is requested
-    const bool want_dsh = DO_SH && a.dL_dsh != nullptr;
+    const bool want_dsh = a.dL_dsh != nullptr;
     if (!(in.radius > 0)) {
         a.dL_dmean3D[3 * idx + 0] = 0.f;
         a.dL_dmean3D[3 * idx + 1] = 0.f;
@@ -253,12 +131,8 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 #pragma unroll
         for (int i = 0; i < 6; i++) dcov[i] = 0.f;
         if (want_dsh) {
-            if constexpr (MC > 0) {
 #pragma unroll
-                for (int i = 0; i < 3 * MC; i++) dsh[i] = 0.f;
-            } else {
-                for (int i = 0; i < a.M * 3; i++) dsh[i] = 0.f;
-            }
+            for (int i = 0; i < BROW; i++) brow[i] = 0.f;
         }
         if (a.dL_dscale) {
             a.dL_dscale[3 * idx + 0] = 0.f;
@@ -364,11 +238,60 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     dm.y += (proj[4] * m_w - proj[7] * mul1) * dm2x + (proj[5] * m_w - proj[7] * mul2) * dm2y;
     dm.z += (proj[8] * m_w - proj[11] * mul1) * dm2x + (proj[9] * m_w - proj[11] * mul2) * dm2y;
 
-    if (DO_SH && a.shs) {
-        const float3 d = sh_bwd_row<MC>(a, mean, row, dcol0, dcol1, dcol2);
+    if (a.shs) {
+        // backward.cu:20-139 from the forward's Jacobian and clamp flags
+        const float3 dir_orig = make_float3(mean.x - a.campos[0], mean.y - a.campos[1], mean.z - a.campos[2]);
+        const float g[3] = {dcol0 * ((in.clampf & 1u) ? 0 : 1), dcol1 * ((in.clampf & 2u) ? 0 : 1),
+                            dcol2 * ((in.clampf & 4u) ? 0 : 1)};
+        const float3 dL_ddir = make_float3(in.jac[0] * g[0] + in.jac[1] * g[1] + in.jac[2] * g[2],
+                                           in.jac[3] * g[0] + in.jac[4] * g[1] + in.jac[5] * g[2],
+                                           in.jac[6] * g[0] + in.jac[7] * g[1] + in.jac[8] * g[2]);
+        const float3 d = dnormvdv3(dir_orig, dL_ddir);
         dm.x += d.x;
         dm.y += d.y;
         dm.z += d.z;
+        if (want_dsh) {
+            // the SH basis at the view direction (the factors of dL/dsh, backward.cu:72-136);
+            // coefficients above the evaluated degree get zero (torch::zeros in the reference)
+            const float len = sqrtf(dir_orig.x * dir_orig.x + dir_orig.y * dir_orig.y + dir_orig.z * dir_orig.z);
+            const float x = dir_orig.x / len, y = dir_orig.y / len, z = dir_orig.z / len;
+            const int deg = a.D;
+            float b[16];
+            b[0] = SH_C0;
+#pragma unroll
+            for (int k = 1; k < 16; k++) b[k] = 0.f;
+            if (deg > 0) {
+                b[1] = -SH_C1 * y;
+                b[2] = SH_C1 * z;
+                b[3] = -SH_C1 * x;
+                if (deg > 1) {
+                    const float xx = x * x, yy = y * y, zz = z * z;
+                    const float xy = x * y, yz = y * z, xz = x * z;
+                    b[4] = SH_C2_0 * xy;
+                    b[5] = SH_C2_1 * yz;
+                    b[6] = SH_C2_2 * (2.f * zz - xx - yy);
+                    b[7] = SH_C2_3 * xz;
+                    b[8] = SH_C2_4 * (xx - yy);
+                    if (deg > 2) {
+                        b[9] = SH_C3_0 * y * (3.f * xx - yy);
+                        b[10] = SH_C3_1 * xy * z;
+                        b[11] = SH_C3_2 * y * (4.f * zz - xx - yy);
+                        b[12] = SH_C3_3 * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                        b[13] = SH_C3_4 * x * (4.f * zz - xx - yy);
+                        b[14] = SH_C3_5 * z * (xx - yy);
+                        b[15] = SH_C3_6 * x * (xx - 3.f * yy);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 16; k++) brow[k] = b[k];
+            brow[16] = g[0];
+            brow[17] = g[1];
+            brow[18] = g[2];
+        }
+    } else if (want_dsh) {
+#pragma unroll
+        for (int i = 0; i < BROW; i++) brow[i] = 0.f;
     }
     a.dL_dmean3D[3 * idx + 0] = dm.x;
     a.dL_dmean3D[3 * idx + 1] = dm.y;
@@ -429,10 +352,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s) {
     if (a.P == 0) return;
-    // 256 Gaussians per workgroup while their SH rows fit 64 KiB of LDS, else 64
-    const size_t row = a.shs ? (size_t)(a.M * 3 + 1) * sizeof(float) : 0;
-    const int threads = row * 256 <= 65536 ? 256 : 64;
-    hipLaunchKernelGGL(k_preprocess_bwd, dim3((a.P + threads - 1) / threads), dim3(threads), row * threads, s, a);
+    hipLaunchKernelGGL(k_preprocess_bwd, dim3((a.P + 255) / 256), dim3(256), 0, s, a);
 }
 
 }  // namespace gsr
