@@ -94,6 +94,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
                 const float len = sqrtf(dir.x * dir.x + dir.y * dir.y + dir.z * dir.z);
                 float ddx[3], ddy[3], ddz[3];
                 sh_dir_jacobian<MAXD>(a.D, dir.x / len, dir.y / len, dir.z / len, sh_row, ddx, ddy, ddz);
+                const float fl = __uint_as_float((raw.x < 0 ? 1u : 0u) | (raw.y < 0 ? 2u : 0u) | (raw.z < 0 ? 4u : 0u));
                 const size_t P = (size_t)a.P;
                 float* jp = a.shjac + idx;
 #pragma unroll
@@ -102,7 +103,7 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
                     jp[(size_t)(3 + c) * P] = ddy[c];
                     jp[(size_t)(6 + c) * P] = ddz[c];
                 }
-                jp[9 * P] = __uint_as_float((raw.x < 0 ? 1u : 0u) | (raw.y < 0 ? 2u : 0u) | (raw.z < 0 ? 4u : 0u));
+                jp[9 * P] = fl;
             }
         } else {
             rgb = make_float3(0.f, 0.f, 0.f);  // multi-channel composite: features live outside the record

@@ -44,8 +44,8 @@ __device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx,
         in.rot = *reinterpret_cast<const float4*>(a.rotations + 4 * idx);
         in.scl = make_float3(a.scales[3 * idx], a.scales[3 * idx + 1], a.scales[3 * idx + 2]);
     }
-    if (a.shs) {  // coalesced SoA rows
-        const size_t P = (size_t)a.P;
+    if (a.shs) {
+        const size_t P = (size_t)a.P;  // coalesced SoA rows
 #pragma unroll
         for (int k = 0; k < 9; k++) in.jac[k] = a.shjac[(size_t)k * P + idx];
         in.clampf = __float_as_uint(a.shjac[9 * P + idx]);
