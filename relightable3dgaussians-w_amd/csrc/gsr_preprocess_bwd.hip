@@ -84,19 +84,31 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
         const int rows = (a.P - g0) < (int)blockDim.x ? (a.P - g0) : (int)blockDim.x;
         float* out = a.dL_dsh + (size_t)g0 * M3;
         const int n = rows * M3;
-        auto elem = [&](int e) -> float {
-            const int r = e / M3, w = e - r * M3, k = w / 3, c = w - 3 * k;
-            const float* b = s_b + r * BROW;
-            return k < 16 ? b[k] * b[16 + c] : 0.f;
-        };
         if ((M3 & 3) == 0) {
+            // a float4 never straddles two rows (3M % 4 == 0): its row from one float
+            // multiply (exact for these small indices), its (coefficient, channel) pairs from
+            // the first one
+            const int F4 = M3 >> 2;
+            const float invF4 = 1.0f / (float)F4;
             float4* o4 = reinterpret_cast<float4*>(out);
             for (int f = threadIdx.x; f < (n >> 2); f += blockDim.x) {
-                const int e0 = 4 * f;
-                o4[f] = make_float4(elem(e0), elem(e0 + 1), elem(e0 + 2), elem(e0 + 3));
+                const int r = (int)(((float)f + 0.5f) * invF4);
+                const unsigned w0 = 4u * (unsigned)(f - r * F4), k0 = w0 / 3u, c0 = w0 - 3u * k0;
+                const float* b = s_b + r * BROW;
+                float v[4];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const unsigned c = c0 + i, hi = c >= 3u ? 1u : 0u, k = k0 + hi, cc = c - 3u * hi;
+                    v[i] = k < 16u ? b[k] * b[16 + cc] : 0.f;
+                }
+                o4[f] = make_float4(v[0], v[1], v[2], v[3]);
             }
         } else {
-            for (int e = threadIdx.x; e < n; e += blockDim.x) out[e] = elem(e);
+            for (int e = threadIdx.x; e < n; e += blockDim.x) {
+                const int r = e / M3, w = e - r * M3, k = w / 3, c = w - 3 * k;
+                const float* b = s_b + r * BROW;
+                out[e] = k < 16 ? b[k] * b[16 + c] : 0.f;
+            }
         }
     }
 }
