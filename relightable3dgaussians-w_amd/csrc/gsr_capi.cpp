@@ -907,13 +907,19 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
         ra.dL_dpix = dL_dpix;
         ra.acc = acc;
-        ra.order = at<uint32_t>(img, il.order_bwd);
-        ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
+#ifdef GSR_BWD_REUSE_ORDER
+        const bool own_order = det;
+#else
+        const bool own_order = true;
+#endif
+        ra.order = at<uint32_t>(img, own_order ? il.order_bwd : il.order_fwd);
+        ra.nheavy = at<uint32_t>(img, il.nheavy) + (own_order ? 8 : 0);
         ra.partial = partial;
         {
             GSR_STAGE(ST_RENDER_BWD);
-            gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
-                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
+            if (own_order)
+                gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
+                                       at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);
             } else {

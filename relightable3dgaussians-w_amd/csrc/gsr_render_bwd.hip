@@ -23,8 +23,12 @@ namespace gsr {
 
 #ifdef GSR_RENDER_STATS
 __device__ unsigned long long g_bwd_stats[8];
-__device__ unsigned long long g_bwd_times[3 * 65536];  // per tile: start, end (s_memrealtime), hw id
+__device__ unsigned long long g_bwd_times[4 * 65536];  // per tile: start, end (s_memrealtime), hw id, largest n_contrib
+#ifdef GSR_TIMES_ONLY  // per-tile timing only (tools/xcd_balance.py): no per-evaluation counters
+#define BWD_STAT(k, v)
+#else
 #define BWD_STAT(k, v) st[k] += (v)
+#endif
 #else
 #define BWD_STAT(k, v)
 #endif
@@ -83,10 +87,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 #endif
     // the tile's list back to front from its last contributor (the forward's tile_emax and
     // tile_nmax: the entry and, over the whole tile, its list position + 1)
-    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sti = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<false> tl;
-    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
         tl.fill(s_list);
@@ -212,10 +216,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {
         for (int k = 0; k < 6; k++) atomicAdd(&g_bwd_stats[k], st[k]);
-        if (tile < 65536) {
-            g_bwd_times[3 * tile] = t_start;
-            g_bwd_times[3 * tile + 1] = __builtin_amdgcn_s_memrealtime();
-            g_bwd_times[3 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+        if (tile < 65536 && qallow == 15u) {
+            g_bwd_times[4 * tile] = t_start;
+            g_bwd_times[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+            g_bwd_times[4 * tile + 3] = nmax;
+            g_bwd_times[4 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
                                         ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
         }
     }
@@ -229,13 +234,13 @@ template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row
     render_bwd_tile<DET>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
 extern "C" int gsr_debug_bwd_times(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_times), sizeof(unsigned long long) * 3 * n) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_times), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
 }
 extern "C" int gsr_debug_bwd_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stats), sizeof(g_bwd_stats)) != hipSuccess) return -1;
@@ -251,7 +256,7 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    const dim3 grid(tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }

@@ -21,7 +21,12 @@ namespace gsr {
 
 #ifdef GSR_RENDER_STATS
 __device__ unsigned long long g_fwd_stats[8];
+__device__ unsigned long long g_fwd_times[4 * 65536];  // per tile: start, end (s_memrealtime), hw id, cost estimate
+#ifdef GSR_TIMES_ONLY  // per-tile timing only (tools/xcd_balance.py): no per-evaluation counters
+#define FWD_STAT(k, v)
+#else
 #define FWD_STAT(k, v) st[k] += (v)
+#endif
 #else
 #define FWD_STAT(k, v)
 #endif
@@ -30,10 +35,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sti = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<true> tl;
-    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, 0u, 0u);
+    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
@@ -54,6 +59,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     }
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
     while (live) {
@@ -146,8 +152,16 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }
 #ifdef GSR_RENDER_STATS
-    if (lane == 0)
+    if (lane == 0) {
         for (int k = 0; k < 5; k++) atomicAdd(&g_fwd_stats[k], st[k]);
+        if (tile < 65536 && qallow == 15u) {
+            g_fwd_times[4 * tile] = t_start;
+            g_fwd_times[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();
+            g_fwd_times[4 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                                        ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+            g_fwd_times[4 * tile + 3] = a.st_ranges[sti].y - a.st_ranges[sti].x;
+        }
+    }
 #endif
     const int HW = a.H * a.W;
 #pragma unroll
@@ -179,11 +193,14 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 6))) k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
     render_fwd_tile(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
+extern "C" int gsr_debug_fwd_times(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_times), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
 extern "C" int gsr_debug_fwd_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_stats), sizeof(g_fwd_stats)) != hipSuccess) return -1;
     if (reset) {
@@ -198,7 +215,7 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    hipLaunchKernelGGL(k_render_fwd, dim3(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP)), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

@@ -325,7 +325,7 @@ template <int NC4, int NCH = 4 * NC4>
 __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
@@ -333,14 +333,14 @@ template <int NC4, int NCH = 4 * NC4, bool DET = false>
 __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row
     render_bwd_mc_tile<NC4, NCH, DET>(a, tile, qallow);
 }
 
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    const dim3 grid(tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
     switch ((a.nch + 3) / 4) {
         case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;
@@ -368,7 +368,7 @@ static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s)
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(8 * ((ntile + 7) / 8 + 3 * HEAVY_CAP));
+    const dim3 grid(tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) launch_bwd_mc<true>(a, grid, s);
     else launch_bwd_mc<false>(a, grid, s);
 }

@@ -21,28 +21,48 @@ __device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, un
 
 // Work unit of a one-wave workgroup of the tile passes: block b serves unit b / 8 of XCD
 // band b mod 8.  The band's first min(nheavy, HEAVY_CAP) tiles (heaviest first) are split
-// into four units, one per 8x8 quadrant; every other tile is one unit.  Sets tile and the
-// quadrant mask; false when the block has nothing to do.  (Four-wave workgroups holding a
-// heavy tile's quadrants measured slower on balanced scenes: a workgroup waits for four
-// free wave slots on one CU, so single waves cannot backfill.)
-constexpr unsigned HEAVY_CAP = 64;  // split tiles per band
+// into four units, one per 8x8 quadrant; so are its last min(ntail, rest) tiles (the lightest:
+// the pass's tail then drains in quarter-tile units while the chip is still full, instead of
+// one whole tile per wave slot); every other tile is one unit.  Sets tile and the quadrant
+// mask; false when the block has nothing to do.  (Four-wave workgroups holding a heavy
+// tile's quadrants measured slower on balanced scenes: a workgroup waits for four free wave
+// slots on one CU, so single waves cannot backfill.)
+constexpr unsigned HEAVY_CAP = 64;  // split heavy tiles per band
+#ifndef GSR_FWD_TAIL
+#define GSR_FWD_TAIL 128
+#endif
+#ifndef GSR_BWD_TAIL
+#define GSR_BWD_TAIL 0
+#endif
+constexpr unsigned FWD_TAIL_SPLIT = GSR_FWD_TAIL;  // split tail tiles per band, forward passes
+constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
-                                          unsigned& tile, uint32_t& qallow) {
+                                          unsigned& tile, uint32_t& qallow, unsigned ntail) {
     const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
     unsigned lo, len;
     band_of(band, ntile, lo, len);
-    const unsigned h = min(nheavy[band], HEAVY_CAP);
+    const unsigned h = min(min(nheavy[band], HEAVY_CAP), len);
+    const unsigned t = min(ntail, len - h);
+    const unsigned whole = len - h - t;
     unsigned pos;
     if (u < 4u * h) {
         pos = u >> 2;
         qallow = 1u << (u & 3u);
-    } else {
+    } else if (u < 4u * h + whole) {
         pos = h + (u - 4u * h);
         qallow = 15u;
+    } else {
+        const unsigned v = u - 4u * h - whole;
+        pos = h + whole + (v >> 2);
+        qallow = 1u << (v & 3u);
     }
     if (pos >= len) return false;
     tile = order[lo + pos];
     return true;
+}
+// blocks of a tile pass launch: the longest band's units (heavy and tail tiles count four)
+__host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned ntail) {
+    return 8u * ((ntile + 7u) / 8u + 3u * HEAVY_CAP + 3u * ntail);
 }
 // LDS ordering within one wave (the tile passes' waves share no LDS)
 __device__ __forceinline__ void wave_lds_sync() {

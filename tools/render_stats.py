@@ -50,11 +50,16 @@ def main(cfg="cfg2"):
                      "queue_wait_us_total": v[6] / 100.0 if name == "bwd" else None,
                      "tiles_via_queue": v[7] if name == "bwd" else None}
     n = T
-    tb = (C.c_ulonglong * (3 * n))()
-    L.gsr_debug_bwd_times(tb, n)
+    tb = (C.c_ulonglong * (4 * n))()
     import numpy as np
-    t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 3).astype(np.int64)
+    if os.environ.get("GSR_STATS_DUMP"):
+        L.gsr_debug_fwd_times(tb, n)
+        np.save(os.environ["GSR_STATS_DUMP"] + "_fwd.npy", np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64))
+    L.gsr_debug_bwd_times(tb, n)
+    t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64)
     st, en, hw = t[:, 0], t[:, 1], t[:, 2]
+    if os.environ.get("GSR_STATS_DUMP"):
+        np.save(os.environ["GSR_STATS_DUMP"] + "_bwd.npy", t)
     dur = (en - st) / 100.0  # s_memrealtime: 100 MHz -> us
     span = (en.max() - st.min()) / 100.0
     hwid = hw & 0xffffffff
