@@ -63,7 +63,7 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, order_fwd, order_bwd, nheavy, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, order_fwd, order_bwd, nheavy, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -100,6 +100,12 @@ GeomLayout geom_layout(long long P) {
 unsigned tiles_x(int W) { return (unsigned)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X); }
 unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y); }
 
+#ifdef GSR_BWD_COST_NMAX
+#define BWD_COST il.tile_nmax
+#else
+#define BWD_COST il.tile_cost
+#endif
+
 ImgLayout img_layout(int W, int H) {
     Carver c;
     ImgLayout L;
@@ -110,6 +116,7 @@ ImgLayout img_layout(int W, int H) {
     L.ranges = c.take(8 * T);  // the reference's tile ranges: filled only by the list materialisation
     L.tile_nmax = c.take(4 * T);
     L.tile_emax = c.take(4 * T);
+    L.tile_cost = c.take(4 * T);  // the backward's cost estimate: sum of the quadrants' largest n_contrib
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
     L.nheavy = c.take(4 * 16);  // forward [0..8), backward [8..16)
@@ -674,7 +681,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
             GSR_STAGE(ST_RANGES);
             gsr::launch_tile_order_st((unsigned)T, gx, gsx, st_ranges, at<uint32_t>(img, il.order_fwd),
                                       at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS,
-                                      at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.tile_emax), s);
+                                      at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.tile_emax),
+                                      at<uint32_t>(img, il.tile_cost), s);
         }
         GSR_LAUNCH_CHECK();
         return GSR_OK;
@@ -687,6 +695,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
+    ra.tile_cost = at<uint32_t>(img, il.tile_cost);
     // the forward tile pass over the binning in `bin`
     auto render_pass = [&]() -> int {
         ra.st_ranges = at<uint2>(bin, bl.st_ranges);
@@ -698,6 +707,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
             for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
                 gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, gsx, ra.st_ranges, ra.ent, pa.rec, ra.order,
                                                ra.nheavy, ra.tile_nmax, ra.tile_emax, *mc, c0);
+                ma.tile_cost = ra.tile_cost;
                 ma.out = mc->out + (size_t)c0 * width * height;
                 if (c0 == 0) {  // the other groups would write the same values
                     ma.final_T = ra.final_T;
@@ -831,6 +841,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.nheavy = at<uint32_t>(img, il.nheavy);
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
+    ra.tile_cost = nullptr;  // already summed by the cached call's forward
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {
         GSR_STAGE(ST_RENDER_FWD);
@@ -918,7 +929,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         {
             GSR_STAGE(ST_RENDER_BWD);
             if (own_order)
-                gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.order_bwd),
+                gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, BWD_COST), at<uint32_t>(img, il.order_bwd),
                                        at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);

@@ -159,7 +159,8 @@ void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost
 // own list length is not known without materialising it); also zeroes zero_a / zero_b [ntile]
 // (the forward's tile_nmax / tile_emax atomicMax targets).
 void launch_tile_order_st(unsigned ntile, unsigned gx, unsigned gsx, const uint2* st_ranges, uint32_t* order,
-                          uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, hipStream_t s);
+                          uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
+                          hipStream_t s);
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 11;  // largest n_contrib >= 2048
 
@@ -181,6 +182,7 @@ struct RenderFwdArgs {
     const uint32_t* nheavy;
     uint32_t* tile_nmax;  // out: per tile, the largest n_contrib (the backward's cost; atomicMax, zeroed)
     uint32_t* tile_emax;  // out: per tile, 1 + the entry index of that last contributor (where the backward starts)
+    uint32_t* tile_cost;  // out (when non-null): per tile, the sum of its quadrants' largest n_contrib (atomicAdd, zeroed)
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -227,6 +229,7 @@ struct RenderMcArgs {
     float* final_T;      // forward: written when non-null
     uint32_t* n_contrib;
     uint32_t* tile_nmax;  // forward: atomicMax when non-null
+    uint32_t* tile_cost;  // forward: atomicAdd of the quadrants' largest n_contrib when non-null
     const uint32_t* order;
     const uint32_t* nheavy;
     const float* dL_dout;  // backward: [nch][H][W]

@@ -175,15 +175,17 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
         }
     }
-    uint32_t nm = 0;
+    uint32_t nm = 0, nsum = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t m = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nm = m > nm ? m : nm;
+        nsum += m;
     }
     if (lane == 0 && nm) {
         atomicMax(&a.tile_nmax[tile], nm);
         atomicMax(&a.tile_emax[tile], elast + 1u);
+        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nsum);
     }
 }
 

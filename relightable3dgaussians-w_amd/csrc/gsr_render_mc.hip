@@ -140,15 +140,17 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         }
     }
     if (a.tile_nmax) {
-        uint32_t nm = 0;
+        uint32_t nm = 0, nsum = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t mq = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
             nm = mq > nm ? mq : nm;
+            nsum += mq;
         }
         if (lane == 0 && nm) {
             atomicMax(&a.tile_nmax[tile], nm);
             atomicMax(&a.tile_emax[tile], elast + 1u);
+            if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nsum);
         }
     }
 }
