@@ -162,7 +162,7 @@ void launch_tile_order_st(unsigned ntile, unsigned gx, unsigned gsx, const uint2
                           uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
                           hipStream_t s);
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
-constexpr int BWD_HEAVY_BITS = 11;  // largest n_contrib >= 2048
+constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 // The tile passes read each tile's list from its super-tile's entries (TileList):

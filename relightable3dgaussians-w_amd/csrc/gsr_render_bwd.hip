@@ -140,7 +140,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 const float G = tile_exp2(power);
                 const float alpha = fminf(0.99f, op * G);
                 // active: pos < last && !(power > 0) && !(alpha < 1/255)
-                const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();
+                // (compare results are 0 on inactive lanes, and every lane is on: no exec masking)
+                const lmask act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
                 if (act == 0ull) continue;  // wave-uniform
                 BWD_STAT(3, 1);
                 BWD_STAT(4, __popcll(act));

@@ -96,7 +96,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
         auto blend_one = [&](const float4& A, const float4& B, const float2& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
-            const uint32_t pos1 = p0 + (uint32_t)k + 1u;
+            // the list position + 1 in a VGPR once per survivor (the selects below cannot read
+            // it from an SGPR beside their SGPR mask: one constant-bus read per VOP3 on gfx950)
+            uint32_t pos1;
+            asm("v_mov_b32 %0, %1" : "=v"(pos1) : "s"(p0 + (uint32_t)k + 1u));
             lmask blended = 0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -105,13 +108,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
                 const float alpha = fminf(0.99f, B.y * tile_exp2(power));
                 // hit: !(power > 0) && alpha >= lim (masks and selects in SGPR pairs, see m_ge)
-                const lmask hit = ~m_gt0(power) & m_ge(alpha, lim[q]) & exec_mask();
+                // (compare results are 0 on inactive lanes, and the walk runs with every lane on:
+                // no exec masking; each mask op below is one SALU instruction)
+                const lmask hit = m_ge(alpha, lim[q]) & ~m_gt0(power);
                 FWD_STAT(2, 1);
                 FWD_STAT(3, hit != 0ull);
                 FWD_STAT(4, __popcll(hit));
                 const float test_T = T[q] * (1 - alpha);
-                const lmask sat = hit & m_lt(test_T, 0.0001f);  // saturating Gaussian is not blended
-                const lmask blend = hit & ~sat;
+                const lmask lt = m_lt(test_T, 0.0001f);  // saturating Gaussian is not blended
+                const lmask blend = hit & ~lt, sat = hit & lt;
                 const float w = sel(blend, alpha * T[q], 0.f);
                 C0[q] += B.z * w;
                 C1[q] += B.w * w;

@@ -98,10 +98,12 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
                 const float power = gauss_power(A.z, A.w, B.x, dx, dy);
                 const float alpha = fminf(0.99f, B.y * tile_exp2(power));
-                const lmask hit = ~m_gt0(power) & m_ge(alpha, lim[q]) & exec_mask();
+                // (compare results are 0 on inactive lanes, and the walk runs with every lane on:
+                // no exec masking; each mask op below is one SALU instruction)
+                const lmask hit = m_ge(alpha, lim[q]) & ~m_gt0(power);
                 const float test_T = T[q] * (1 - alpha);
-                const lmask sat = hit & m_lt(test_T, 0.0001f);
-                const lmask blend = hit & ~sat;
+                const lmask lt = m_lt(test_T, 0.0001f);
+                const lmask blend = hit & ~lt, sat = hit & lt;
                 const float w = sel(blend, alpha * T[q], 0.f);
                 float Fs[4 * NC4];
 #pragma unroll
@@ -261,7 +263,8 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 const float power = gauss_power(ka, kb, kc, dx, dy);
                 const float G = tile_exp2(power);
                 const float alpha = fminf(0.99f, op * G);
-                const lmask act = m_ult(pos, last[q]) & ~m_gt0(power) & ~m_lt(alpha, 1.0f / 255.0f) & exec_mask();
+                // (compare results are 0 on inactive lanes, and every lane is on: no exec masking)
+                const lmask act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
                 if (act == 0ull) continue;
                 any = true;
                 const float ae = sel(act, alpha, 0.f);
