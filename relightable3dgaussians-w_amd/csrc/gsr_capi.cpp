@@ -100,12 +100,6 @@ GeomLayout geom_layout(long long P) {
 unsigned tiles_x(int W) { return (unsigned)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X); }
 unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y); }
 
-#ifdef GSR_BWD_COST_NMAX
-#define BWD_COST il.tile_nmax
-#else
-#define BWD_COST il.tile_cost
-#endif
-
 ImgLayout img_layout(int W, int H) {
     Carver c;
     ImgLayout L;
@@ -918,19 +912,13 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.n_contrib = at<uint32_t>(img, il.n_contrib);
         ra.dL_dpix = dL_dpix;
         ra.acc = acc;
-#ifdef GSR_BWD_REUSE_ORDER
-        const bool own_order = det;
-#else
-        const bool own_order = true;
-#endif
-        ra.order = at<uint32_t>(img, own_order ? il.order_bwd : il.order_fwd);
-        ra.nheavy = at<uint32_t>(img, il.nheavy) + (own_order ? 8 : 0);
+        ra.order = at<uint32_t>(img, il.order_bwd);
+        ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         ra.partial = partial;
         {
             GSR_STAGE(ST_RENDER_BWD);
-            if (own_order)
-                gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, BWD_COST), at<uint32_t>(img, il.order_bwd),
-                                       at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
+            gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
+                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);
             } else {
