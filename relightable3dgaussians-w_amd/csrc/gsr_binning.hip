@@ -20,6 +20,7 @@
 #include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
+#include "gsr_order.hpp"
 
 namespace gsr {
 
@@ -146,8 +147,8 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 // The depth-sorted visible Gaussians are cut into blocks of ST_G.  k_st_hist counts each
 // block's entries per super-tile (digit-major table [NS][nb]) from the rects in depth order
 // (carried through the depth sort, so nothing is gathered at random); k_digit_scan (gsr_sort.hip) turns every super-tile's row into
-// block offsets + a total; k_st_bases scans the totals into super-tile bases and ranges;
-// k_st_scatter re-enumerates each block's entries in (Gaussian, super-tile) order and
+// block offsets + a total; k_st_scatter scans the totals into super-tile bases and ranges,
+// re-enumerates each block's entries in (Gaussian, super-tile) order and
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
@@ -218,28 +219,6 @@ inline SegTable seg_layout(void* temp, long long S, int nst) {
     return t;
 }
 
-// bases[s] = exclusive scan of the super-tile totals; ranges[s] = [base, base + total),
-// clamped to the entry capacity (the scatter drops entries beyond it: a tile pass over an
-// overflowed binning then reads only written entries, and the forward redoes the binning);
-// header[0] = the entry count S (read back by the list materialisation)
-__global__ void __launch_bounds__(256) k_st_bases(int NS, const uint32_t* tot, uint32_t* bases, uint2* ranges,
-                                                   unsigned long long* header, uint32_t cap) {
-    __shared__ uint32_t sh[4];
-    uint32_t carry = 0;
-    for (int c = 0; c < NS; c += 256) {
-        const int i = c + threadIdx.x;
-        const uint32_t v = i < NS ? tot[i] : 0u;
-        uint32_t t;
-        const uint32_t ex = carry + block256_exclusive_scan(v, sh, &t);
-        if (i < NS) {
-            bases[i] = ex;
-            ranges[i] = v ? make_uint2(min(ex, cap), min(ex + v, cap)) : make_uint2(0u, 0u);
-        }
-        carry += t;
-    }
-    if (threadIdx.x == 0) header[0] = min(carry, cap);
-}
-
 // Orders a wave's LDS accesses across lanes (LDS executes one wave's instructions in order)
 // without the vmcnt wait a wavefront fence adds: the ranking must not wait for its own
 // scattered stores or the next chunk's prefetch.
@@ -299,17 +278,24 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
     }
 }
 
+// Workgroups: nb scatter blocks, then (optional) the frame totals, then (optional) the
+// forward's dispatch order, one workgroup per XCD band (costs from the super-tile totals, so
+// neither needs a launch of its own).  Each scatter block scans the super-tile totals into
+// the super-tile bases itself (block 0 also writes the ranges and header[0] = S).
 template <int ST_W>
 __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
                                                      const uint2* rect_sorted, unsigned gsx, int NS, int nb,
                                                      const uint32_t* table, const uint32_t* wcounts,
-                                                     const uint32_t* bases, uint2* ent, uint32_t cap,
-                                                     FrameTotals ft) {
-    if (ft.host && (int)blockIdx.x == nb) {  // the extra workgroup: the host's frame totals
-        frame_totals(ft);
+                                                     const uint32_t* tot, uint2* st_ranges, unsigned long long* header,
+                                                     uint2* ent, uint32_t cap, FrameTotals ft, TileOrderArgs ord) {
+    if ((int)blockIdx.x >= nb) {
+        const int x = (int)blockIdx.x - nb - (ft.host ? 1 : 0);
+        if (x < 0) frame_totals(ft);  // the extra workgroup: the host's frame totals
+        else tile_order_band((unsigned)x, ord);
         return;
     }
     extern __shared__ unsigned long long st_lds[];  // [ST_W][NS] lane masks, then [ST_W][NS] run counters
+    __shared__ uint32_t s_scan[ST_W];
     unsigned long long* wmask_all = st_lds;
     uint32_t* wcnt_all = reinterpret_cast<uint32_t*>(st_lds + ST_W * NS);
     const int wave = threadIdx.x >> 6;
@@ -317,17 +303,29 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // as k_st_hist: runs of neighbours merge in L2
     const int g0 = blk * ST_G;
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
-    // each wave's run of super-tile s starts after the block's earlier waves (k_st_hist's
-    // per-wave counts)
+    // super-tile s's base (exclusive scan of the totals); each wave's run of s starts there +
+    // the block's offset + the counts of the block's earlier waves (k_st_hist's per-wave counts)
     const uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
-    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
-        uint32_t run = bases[i] + table[(size_t)i * nb + blk];
-        for (int w = 0; w < ST_W; w++) {
-            wmask_all[w * NS + i] = 0ull;
-            wcnt_all[w * NS + i] = run;
-            run += wc[w * NS + i];
+    uint32_t carry = 0;
+    for (int c = 0; c < NS; c += 64 * ST_W) {
+        const int i = c + (int)threadIdx.x;
+        const uint32_t v = i < NS ? tot[i] : 0u;
+        uint32_t t;
+        const uint32_t ex = carry + block_exclusive_scan<ST_W>(v, s_scan, &t);
+        if (i < NS) {
+            // ranges clamped to the entry capacity (the scatter drops entries beyond it: a tile
+            // pass over an overflowed binning reads only written entries, the forward redoes it)
+            if (blockIdx.x == 0) st_ranges[i] = v ? make_uint2(min(ex, cap), min(ex + v, cap)) : make_uint2(0u, 0u);
+            uint32_t run = ex + table[(size_t)i * nb + blk];
+            for (int w = 0; w < ST_W; w++) {
+                wmask_all[w * NS + i] = 0ull;
+                wcnt_all[w * NS + i] = run;
+                run += wc[w * NS + i];
+            }
         }
+        carry += t;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) header[0] = min(carry, cap);
     __syncthreads();
     st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
 }
@@ -344,13 +342,20 @@ bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
 void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
                    unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
-                   uint32_t cap, hipStream_t s, const FrameTotals* ftp) {
+                   uint32_t cap, hipStream_t s, const FrameTotals* ftp, const TileOrderArgs* ordp) {
     FrameTotals ft{};
     if (ftp) ft = *ftp;
-    if (Pv <= 0) {  // otherwise k_st_bases writes every super-tile's range
+    TileOrderArgs ord{};
+    if (ordp) ord = *ordp;
+    if (Pv <= 0) {  // otherwise the scatter writes every super-tile's range
         (void)hipMemsetAsync(st_ranges, 0, sizeof(uint2) * (size_t)NS, s);
         (void)hipMemsetAsync(header, 0, 8, s);
         if (ftp) launch_frame_totals(ft, s);
+        if (ordp) {  // every tile's cost is 0: its super-tile range, zeroed above
+            ord.st_ranges = st_ranges;
+            ord.st_tot = nullptr;
+            launch_tile_order_args(ord, s);
+        }
         return;
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
@@ -363,7 +368,6 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     };
     uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
-    uint32_t* bases = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
     if (W == 8)
         hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
@@ -372,14 +376,14 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
         hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
                            table, wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
-    hipLaunchKernelGGL(k_st_bases, dim3(1), dim3(256), 0, s, NS, tot, bases, st_ranges, header, cap);
-    const dim3 grid(nb + (ftp ? 1 : 0));
+    if (ordp) ord.st_tot = tot;
+    const dim3 grid(nb + (ftp ? 1 : 0) + (ordp && ord.ntile ? 8 : 0));
     if (W == 8)
         hipLaunchKernelGGL(k_st_scatter<8>, grid, dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, ent, cap, ft);
+                           gsx, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
     else
         hipLaunchKernelGGL(k_st_scatter<4>, grid, dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, bases, ent, cap, ft);
+                           gsx, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)

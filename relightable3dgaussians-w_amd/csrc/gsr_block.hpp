@@ -41,4 +41,24 @@ __device__ __forceinline__ T block256_exclusive_scan(T v, T* sh, T* total) {
     return off + inc - v;
 }
 
+// Exclusive scan of one value per thread across a workgroup of NW waves; `sh` holds NW
+// elements of T.  Returns the exclusive prefix; *total gets the sum.
+template <int NW, typename T>
+__device__ __forceinline__ T block_exclusive_scan(T v, T* sh, T* total) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const T inc = wave_inclusive_scan(v);
+    if (lane == 63) sh[wave] = inc;
+    __syncthreads();
+    T off = T(0), tot = T(0);
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const T x = sh[w];
+        off += w < wave ? x : T(0);
+        tot += x;
+    }
+    if (total) *total = tot;
+    __syncthreads();
+    return off + inc - v;
+}
+
 }  // namespace gsr

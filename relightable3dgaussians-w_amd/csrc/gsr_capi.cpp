@@ -640,11 +640,20 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         uint2* ent = at<uint2>(bin, bl.ent);
         uint2* st_ranges = at<uint2>(bin, bl.st_ranges);
         unsigned long long* header = at<unsigned long long>(bin, bl.header);
-        if (fused_bin) {
+        // the forward's dispatch order (a tile's cost: its super-tile's entry count); zeroes
+        // the tile maxima and summed cost the tile pass raises
+        gsr::TileOrderArgs ord{};
+        ord.ntile = (unsigned)T; ord.gx = gx; ord.gsx = gsx; ord.order = at<uint32_t>(img, il.order_fwd);
+        ord.nheavy = at<uint32_t>(img, il.nheavy); ord.heavy_bits = gsr::FWD_HEAVY_BITS;
+        ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
+        ord.zero_c = at<uint32_t>(img, il.tile_cost);
+        if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, NS,
                                at<void>(bin, bl.st_bin_tmp), ent, st_ranges, header, (uint32_t)capS, s,
-                               dev ? &ft : nullptr);
+                               dev ? &ft : nullptr, &ord);
+            GSR_LAUNCH_CHECK();
+            return GSR_OK;
         } else {
             uint32_t* stk = at<uint32_t>(bin, bl.st_keys);
             uint32_t* stv = at<uint32_t>(bin, bl.st_vals);
@@ -670,13 +679,9 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         }
         GSR_LAUNCH_CHECK();
         {
-            // the forward's dispatch order (a tile's cost: its super-tile's entry count); zeroes
-            // the tile maxima the tile pass raises
             GSR_STAGE(ST_RANGES);
-            gsr::launch_tile_order_st((unsigned)T, gx, gsx, st_ranges, at<uint32_t>(img, il.order_fwd),
-                                      at<uint32_t>(img, il.nheavy), gsr::FWD_HEAVY_BITS,
-                                      at<uint32_t>(img, il.tile_nmax), at<uint32_t>(img, il.tile_emax),
-                                      at<uint32_t>(img, il.tile_cost), s);
+            ord.st_ranges = st_ranges;
+            gsr::launch_tile_order_args(ord, s);
         }
         GSR_LAUNCH_CHECK();
         return GSR_OK;

@@ -96,11 +96,26 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
                unsigned long long* pv_out, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0);
 
+// One pass's dispatch order (k_tile_order, or extra workgroups of the binning scatter).
+struct TileOrderArgs {
+    unsigned ntile, gx, gsx;
+    const uint2* ranges;      // cost = list length (materialised ranges), or
+    const uint32_t* cost;     // an explicit per-tile cost, or
+    const uint2* st_ranges;   // the tile's super-tile entry count from its range, or
+    const uint32_t* st_tot;   // from the super-tile totals
+    uint32_t* order;
+    uint32_t* nheavy;
+    int heavy_bits;
+    uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
+};
+
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
 // (P_v, R, S, error) and stores them to host-mapped memory as (value << 16 | seq mod 2^16)
 // words; the host polls until all four carry its call's tag (no copy or event on the stream:
 // each left a 6-19 us bubble between kernels).  Run as an extra workgroup of the super-tile
 // scatter (launch_st_bin), or on its own (launch_frame_totals).
+void launch_tile_order_args(const TileOrderArgs& a, hipStream_t s);  // k_tile_order, 8 bands
+
 struct FrameTotals {
     const uint4* blk_tot;
     int nblk;
@@ -132,7 +147,7 @@ bool st_bin_supported(int NS);
 // the binning).  ft (optional): the frame totals run as one extra workgroup of the scatter.
 void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
                    unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
-                   uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr);
+                   uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr, const TileOrderArgs* order = nullptr);
 // Large images (NS > 1365): in depth order, every visible Gaussian emits one (super-tile,
 // gaussian) pair per super-tile its rect touches, at offsets[s] (exclusive scan of st_count
 // in depth order); the pairs are then radix-sorted by super-tile and packed into entries.
@@ -150,17 +165,13 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
                         unsigned gsx, void* temp, uint32_t* point_list, uint2* ranges, long long R, hipStream_t s);
 
 // ---- tile order (gsr_schedule.hip) ------------------------------------------------------
+
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of
 // the tile's list length when cost is null); nheavy[8]: per band, the leading tiles with
 // cost >= 2^heavy_bits.
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
                        int heavy_bits, hipStream_t s);
-// The forward's order: a tile's cost is its super-tile's entry count (st_ranges; the tile's
-// own list length is not known without materialising it); also zeroes zero_a / zero_b [ntile]
-// (the forward's tile_nmax / tile_emax atomicMax targets).
-void launch_tile_order_st(unsigned ntile, unsigned gx, unsigned gsx, const uint2* st_ranges, uint32_t* order,
-                          uint32_t* nheavy, int heavy_bits, uint32_t* zero_a, uint32_t* zero_b, uint32_t* zero_c,
-                          hipStream_t s);
+
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
 

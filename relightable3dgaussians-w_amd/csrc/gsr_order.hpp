@@ -1,0 +1,102 @@
+// gsr_order.hpp -- a tile pass's dispatch order for one XCD band (k_tile_order in
+// gsr_schedule.hip, or extra workgroups of the binning scatter in gsr_binning.hip).
+#pragma once
+#include "gsr_kernels.hpp"
+#include "gsr_tile.hpp"
+
+namespace gsr {
+
+// The cost of tile t: cost[t]; else its super-tile's entry count (the forward: st_tot, or
+// st_ranges; gx tiles per row, gsx super-tiles per row); else its list length.
+__device__ __forceinline__ uint32_t tile_cost(unsigned t, const TileOrderArgs& a) {
+    if (a.cost) return a.cost[t];
+    if (a.st_tot || a.st_ranges) {
+        const unsigned st = (t / a.gx) / GSR_ST_H * a.gsx + (t % a.gx) / GSR_ST_W;
+        if (a.st_tot) return a.st_tot[st];
+        const uint2 r = a.st_ranges[st];
+        return r.y - r.x;
+    }
+    return a.ranges ? a.ranges[t].y - a.ranges[t].x : 0u;
+}
+
+// Cost bucket: the bit length of c and its next two bits (4 buckets per octave), 0 for c = 0.
+#ifdef GSR_COARSE_BUCKETS
+constexpr int NBUCKET = 33;
+__device__ __forceinline__ int cost_bucket(uint32_t c) { return c ? 32 - __clz(c) : 0; }
+__device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return heavy_bits + 1; }
+#else
+#ifndef GSR_BUCKET_BITS
+#define GSR_BUCKET_BITS 3
+#endif
+constexpr int BUCKET_FRAC = GSR_BUCKET_BITS;  // 2^BUCKET_FRAC buckets per octave
+constexpr int NBUCKET = 33 << BUCKET_FRAC;
+__device__ __forceinline__ int cost_bucket(uint32_t c) {
+    if (!c) return 0;
+    const int L = 32 - __clz(c);
+    const uint32_t fm = (1u << BUCKET_FRAC) - 1u;
+    const uint32_t f = L > BUCKET_FRAC ? (c >> (L - 1 - BUCKET_FRAC)) & fm : (c << (BUCKET_FRAC + 1 - L)) & fm;
+    return (L << BUCKET_FRAC) + (int)f;
+}
+__device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return (heavy_bits + 1) << BUCKET_FRAC; }
+#endif
+
+// One band's order (any block size): order[lo .. lo+len) = the band's tiles, cost buckets
+// descending; nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4
+// ways).  Also zeroes the optional per-tile targets of the forward (tile maxima, summed cost).
+__device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderArgs& a) {
+    __shared__ uint32_t hist[NBUCKET];
+    __shared__ uint32_t cur[NBUCKET];
+    __shared__ uint32_t scan[512];
+    unsigned lo, len;
+    band_of(band, a.ntile, lo, len);
+    for (int i = threadIdx.x; i < NBUCKET; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
+        const unsigned t = lo + i;
+        atomicAdd(&hist[cost_bucket(tile_cost(t, a))], 1u);
+        if (a.zero_a) {
+            a.zero_a[t] = 0u;
+            a.zero_b[t] = 0u;
+            if (a.zero_c) a.zero_c[t] = 0u;
+        }
+    }
+    __syncthreads();
+    // cur[b] = tiles in buckets above b (heaviest bucket first): a block scan over the
+    // buckets in descending order, thread j holding bucket NBUCKET - 1 - j (one thread serially
+    // when the block is smaller than the bucket count)
+    if (blockDim.x >= NBUCKET && blockDim.x <= 512) {
+        const int j = threadIdx.x, bj = NBUCKET - 1 - j;
+        const uint32_t hj = bj >= 0 ? hist[bj] : 0u;
+        scan[j] = hj;
+        __syncthreads();
+        for (int o = 1; o < NBUCKET; o <<= 1) {
+            const uint32_t v = j >= o ? scan[j - o] : 0u;
+            __syncthreads();
+            scan[j] += v;
+            __syncthreads();
+        }
+        if (bj >= 0) cur[bj] = scan[j] - hj;
+    } else if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int b = NBUCKET - 1; b >= 0; b--) {
+            cur[b] = run;
+            run += hist[b];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int hb = bucket_heavy_from(a.heavy_bits);
+        a.nheavy[band] = hb < NBUCKET ? cur[hb] + hist[hb] : 0u;  // cost >= 2^heavy_bits
+    }
+    __syncthreads();
+    for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
+        const unsigned t = lo + i;
+#ifdef GSR_NATURAL_ORDER
+        a.order[lo + i] = t;
+#else
+        a.order[lo + atomicAdd(&cur[cost_bucket(tile_cost(t, a))], 1u)] = t;
+#endif
+    }
+}
+
+}  // namespace gsr
