@@ -101,7 +101,11 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
                     const unsigned c = c0 + i, hi = c >= 3u ? 1u : 0u, k = k0 + hi, cc = c - 3u * hi;
                     v[i] = k < 16u ? b[k] * b[16 + cc] : 0.f;
                 }
-                o4[f] = make_float4(v[0], v[1], v[2], v[3]);
+                // non-temporal: the 12M-byte rows are written once and read by the optimizer
+                // later; caching them evicted the next forward's inputs from the Infinity Cache
+                // (next preprocess 0.126 -> 0.112 ms, this kernel +4 us)
+                typedef float f4v __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store((f4v){v[0], v[1], v[2], v[3]}, reinterpret_cast<f4v*>(o4 + f));
             }
         } else {
             for (int e = threadIdx.x; e < n; e += blockDim.x) {
