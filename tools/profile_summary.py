@@ -79,8 +79,8 @@ def main(tag="r01"):
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary {tag}\n\nbench.py cfg2 (1.5M Gaussians, SH3, 1920x1080) under rocprofv3; "
                 "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch.\n\n")
-        f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s | VALU Minst/launch |\n"
-                "|---|---|---|---|---|---|---|---|---|\n")
+        f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s | VALU Minst/launch "
+                "| SALU Minst/launch |\n|---|---|---|---|---|---|---|---|---|---|\n")
         for k, v in sorted(res.items(), key=lambda kv: -kv[1]["pct"]):
             tb = v["traffic_bytes"]
             f.write(f"| {k} | {v['calls']} | {v['avg_ms']:.4f} | {v['pct']:.1f} | "
@@ -88,7 +88,8 @@ def main(tag="r01"):
                     f"{'' if v['write_kib'] is None else round(v['write_kib'])} | "
                     f"{'' if tb is None else round(tb / 1e6, 2)} | "
                     f"{'' if tb is None else round(tb / (v['avg_ms'] * 1e-3) / 1e9, 1)} | "
-                    f"{'' if v['valu_insts'] is None else round(v['valu_insts'] / 1e6, 2)} |\n")
+                    f"{'' if v['valu_insts'] is None else round(v['valu_insts'] / 1e6, 2)} | "
+                    f"{'' if v['salu_insts'] is None else round(v['salu_insts'] / 1e6, 2)} |\n")
         if bench:
             f.write(f"\nbench line under the profiler: value {bench['value']} MPix/s, ms/step {bench['ms_per_step']}"
                     f"\n\nstage_ms (HIP events): {json.dumps(bench.get('stage_ms'))}\n")
