@@ -193,25 +193,25 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             }
         };
         // survivors in pairs over two register sets (the next survivor's record is read
-        // while the current one runs, and no register copies between them)
-        int k = __builtin_ctzll(todo);
-        todo &= todo - 1;
+        // while the current one runs, and no register copies between them); s_ff1 gives -1
+        // when none is left, s_bitset0 clears the taken bit
+        int k = sgpr_ff1(todo);
+        todo = sgpr_clear_bit(todo, k);
         float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
         for (;;) {
-            bool more = todo != 0ull;
-            const int kn = more ? __builtin_ctzll(todo) : k;
-            todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn], Cn = s_c[kn];
+            const int kn = sgpr_ff1(todo), kl = kn > 0 ? kn : 0;
+            todo = sgpr_clear_bit(todo, kl);
+            const float4 An = s_a[kl], Bn = s_b[kl], Cn = s_c[kl];
             grad_one(A, B, Cq, k);
-            if (!more) break;
-            more = todo != 0ull;
-            k = more ? __builtin_ctzll(todo) : kn;
-            todo &= todo - 1;
-            A = s_a[k];
-            B = s_b[k];
-            Cq = s_c[k];
+            if (kn < 0) break;
+            k = sgpr_ff1(todo);
+            const int kl2 = k > 0 ? k : 0;
+            todo = sgpr_clear_bit(todo, kl2);
+            A = s_a[kl2];
+            B = s_b[kl2];
+            Cq = s_c[kl2];
             grad_one(An, Bn, Cn, kn);
-            if (!more) break;
+            if (k < 0) break;
         }
     }
 #ifdef GSR_RENDER_STATS

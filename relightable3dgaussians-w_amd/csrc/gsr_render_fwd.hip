@@ -42,7 +42,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
-    __shared__ float2 s_c[64];  // (colour b, quadrant mask)
+    __shared__ float4 s_c[64];  // (colour b, quadrant mask, -, -): 16-B rows, one LDS address for all three reads
     __shared__ uint32_t s_e[64];  // entry index
     float T[4], C0[4], C1[4], C2[4];
     float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
@@ -85,16 +85,17 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float2(rc, __uint_as_float(qm));
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), 0.f, 0.f);
         s_e[lane] = ei;
         wave_lds_sync();
-        uint64_t todo = __ballot((qm & live) != 0);
+        const uint64_t todo0 = __ballot((qm & live) != 0);
         FWD_STAT(0, nb);
-        FWD_STAT(1, __popcll(todo));
-        if (!todo) continue;
+        FWD_STAT(1, __popcll(todo0));
+        if (!todo0) continue;
         // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
-        auto blend_one = [&](const float4& A, const float4& B, const float2& Cq, int k) __attribute__((always_inline)) {
+        uint64_t todo = todo0;
+        auto blend_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
             // the list position + 1 in a VGPR once per survivor (the selects below cannot read
             // it from an SGPR beside their SGPR mask: one constant-bus read per VOP3 on gfx950)
@@ -126,33 +127,35 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 blended |= blend;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
-                    if (!(m_lt(lim[q], 1.f) & exec_mask())) live &= ~(1u << q);
+                    if (!(m_lt(lim[q], 1.f) & exec_mask())) {
+                        live &= ~(1u << q);
+                        if (!live) todo = 0;  // the walk ends at the next survivor it would take
+                    }
                 }
             }
             if (blended) klast = k;
         };
         // survivors in pairs over two register sets (the next survivor's record is read
-        // while the current one blends, and no register copies between them)
-        int k = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        float4 A = s_a[k], B = s_b[k];
-        float2 Cq = s_c[k];
+        // while the current one blends, and no register copies between them); the walk's
+        // bookkeeping is a handful of SALU ops per survivor (s_ff1 gives -1 when none is left,
+        // s_bitset0 clears the taken bit, the record rows share one LDS address)
+        int k = sgpr_ff1(todo);
+        todo = sgpr_clear_bit(todo, k);
+        float4 A = s_a[k], B = s_b[k], Cq = s_c[k];
         for (;;) {
-            bool more = todo != 0ull;
-            const int kn = more ? __builtin_ctzll(todo) : k;
-            todo &= todo - 1;
-            const float4 An = s_a[kn], Bn = s_b[kn];
-            const float2 Cn = s_c[kn];
+            const int kn = sgpr_ff1(todo), kl = kn > 0 ? kn : 0;
+            todo = sgpr_clear_bit(todo, kl);
+            const float4 An = s_a[kl], Bn = s_b[kl], Cn = s_c[kl];
             blend_one(A, B, Cq, k);
-            if (!live || !more) break;
-            more = todo != 0ull;
-            k = more ? __builtin_ctzll(todo) : kn;
-            todo &= todo - 1;
-            A = s_a[k];
-            B = s_b[k];
-            Cq = s_c[k];
+            if (kn < 0) break;
+            k = sgpr_ff1(todo);
+            const int kl2 = k > 0 ? k : 0;
+            todo = sgpr_clear_bit(todo, kl2);
+            A = s_a[kl2];
+            B = s_b[kl2];
+            Cq = s_c[kl2];
             blend_one(An, Bn, Cn, kn);
-            if (!live || !more) break;
+            if (k < 0) break;
         }
         if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }

@@ -83,8 +83,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         uint64_t todo = __ballot((qm & live) != 0);
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
         while (todo && live) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
+            const int k = sgpr_ff1(todo);
+            todo = sgpr_clear_bit(todo, k);
             const float4 A = s_a[k], B = s_b[k];
             float4 F[NC4];
 #pragma unroll
@@ -235,8 +235,8 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         while (todo) {
-            const int k = __builtin_ctzll(todo);
-            todo &= todo - 1;
+            const int k = sgpr_ff1(todo);
+            todo = sgpr_clear_bit(todo, k);
             const float4 A = s_a[k], B = s_b[k];
             const uint2 Q2 = s_q[k];
             float F[4 * NC4];

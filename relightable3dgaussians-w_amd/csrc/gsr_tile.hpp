@@ -377,6 +377,17 @@ __device__ __forceinline__ uint32_t sel(lmask m, uint32_t t, uint32_t f) {
     return r;
 }
 __device__ __forceinline__ lmask exec_mask() { return __builtin_amdgcn_read_exec(); }
+// index of the lowest set bit of a wave-uniform mask, -1 when it is 0 (s_ff1_i32_b64)
+__device__ __forceinline__ int sgpr_ff1(uint64_t m) {
+    int r;
+    asm("s_ff1_i32_b64 %0, %1" : "=s"(r) : "s"(m));
+    return r;
+}
+// m with bit b cleared (s_bitset0_b64; b wave-uniform)
+__device__ __forceinline__ uint64_t sgpr_clear_bit(uint64_t m, int b) {
+    asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(b));
+    return m;
+}
 
 // Row sums of NQ registers' 16-lane rows at once, transposed as row_sum3 (mirror steps pair
 // registers, lone ones add to themselves), then quad_perm steps; lane column c returns
