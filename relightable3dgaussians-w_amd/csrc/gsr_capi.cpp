@@ -129,7 +129,7 @@ BinLayout bin_layout(long long capS, int W, int H, long long Pv) {
     const bool fused = gsr::st_bin_supported((int)NS);
     L.header = c.take(16);
     L.st_ranges = c.take(8 * NS);
-    L.ent = c.take(8 * capS);
+    L.ent = c.take(8 * (capS + 64));  // + slack: the tile passes' list loads read up to one entry past a range
     // emit + sort path for very large images (NS > 1365 super-tiles)
     L.st_keys = c.take(fused ? 0 : 4 * capS);
     L.st_vals = c.take(fused ? 0 : 4 * capS);

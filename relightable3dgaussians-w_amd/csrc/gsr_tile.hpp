@@ -81,7 +81,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // tile passes take full batches of 64 from the ring, so their per-batch work is what it was
 // over a materialised list.  Forward: front to back from position 0.  Backward: back to front
 // from a given entry (exclusive) whose preceding covering entries number pos0.
-constexpr uint32_t TL_RING = 128;
+constexpr uint32_t TL_RING = 256;
 struct TileListLds {  // per wave
     uint32_t id[TL_RING], e[TL_RING];
 };
@@ -99,10 +99,14 @@ struct TileList {
     uint32_t lx, ly;
     uint2 nx, nx2;   // this lane's entries of the next two steps (loads issued two steps ahead)
 
-    __device__ __forceinline__ uint2 load_step(uint32_t eb) const {  // the step starting at eb (BWD: top eb)
+    // the step starting at eb (BWD: top eb).  Unconditional: lanes past the range read an
+    // entry at its edge (the entry array has 64 slack entries, so even an empty range at the
+    // end reads inside it) and step() masks them, so a prefetch register is never written
+    // twice (a zero default + a masked load made the compiler wait for every load in flight)
+    __device__ __forceinline__ uint2 load_step(uint32_t eb) const {
         const uint32_t lane = threadIdx.x & 63;
-        if (FWD) return eb + lane < lim ? ent[eb + lane] : make_uint2(0u, 0u);
-        return eb > lim + lane ? ent[eb - 1u - lane] : make_uint2(0u, 0u);
+        if (FWD) return ent[min(eb + lane, lim)];
+        return ent[max((int)eb - 1 - (int)lane, (int)lim)];
     }
     __device__ __forceinline__ uint32_t step_after(uint32_t eb) const {
         return FWD ? min(eb + 64u, lim) : (eb > lim + 64u ? eb - 64u : lim);
@@ -134,26 +138,34 @@ struct TileList {
         return (lx - cx0) <= (cx1 - cx0) && (ly - cy0) <= (cy1 - cy0);  // unsigned: also lx >= cx0
     }
     __device__ __forceinline__ bool more() const { return FWD ? e < lim : e > lim; }
-    // filter until >= 64 entries are queued or the list is exhausted
-    __device__ __forceinline__ void fill(TileListLds& L) {
+    __device__ __forceinline__ bool want() const { return tail - head < 64u && more(); }
+    // one filter step: this lane's entry v of the step at e (advances e)
+    __device__ __forceinline__ void step(TileListLds& L, const uint2 v) {
         const uint32_t lane = threadIdx.x & 63;
+        const uint32_t i = FWD ? e + lane : e - 1u - lane;
+        const bool valid = FWD ? i < lim : e > lim + lane;
+        e = step_after(e);
+        const bool c = valid && covers(v.x);
+        const uint64_t cm = __ballot(c);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
+        if (c) {
+            const uint32_t slot = (tail + r) & (TL_RING - 1u);
+            L.id[slot] = v.y;
+            if (KEEP_E) L.e[slot] = i;
+        }
+        tail += (uint32_t)__popcll(cm);
+    }
+    // filter until >= 64 entries are queued or the list is exhausted, two steps at a time:
+    // the two prefetch registers are consumed in a fixed order and each is reloaded right
+    // after it is consumed, so no register copy waits on a load in flight (a step past the
+    // end queues nothing; the ring holds the up to 63 + 128 entries this leaves queued)
+    __device__ __forceinline__ void fill(TileListLds& L) {
         wave_lds_sync();
-        while (tail - head < 64u && more()) {
-            const uint2 v = nx;
-            const uint32_t i = FWD ? e + lane : e - 1u - lane;
-            const bool valid = FWD ? i < lim : e > lim + lane;
-            e = step_after(e);
-            nx = nx2;
+        while (want()) {
+            step(L, nx);
+            nx = load_step(step_after(e));
+            step(L, nx2);
             nx2 = load_step(step_after(e));
-            const bool c = valid && covers(v.x);
-            const uint64_t cm = __ballot(c);
-            const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(cm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)cm, 0u));
-            if (c) {
-                const uint32_t slot = (tail + r) & (TL_RING - 1u);
-                L.id[slot] = v.y;
-                if (KEEP_E) L.e[slot] = i;
-            }
-            tail += (uint32_t)__popcll(cm);
         }
         wave_lds_sync();
     }
