@@ -618,6 +618,12 @@ def main():
                     "peak_basis": f"{n_simd} SIMDs x {VALU_CLOCK_GHZ} GHz / {VALU_CYCLES_PER_INST} cycles per "
                                   "wave64 VALU instruction (spec issue rate)",
                     "hbm": hbm}
+        if kinfo.get("salu_insts"):
+            # the scalar instructions the same waves issue (mask logic, walk bookkeeping,
+            # branches): a co-bound, DESIGN.md §3 (an added SALU op per evaluation costs more
+            # than an added VALU op)
+            roofline["salu_insts_per_launch"] = int(kinfo["salu_insts"])
+            roofline["salu_per_valu"] = round(kinfo["salu_insts"] / kinfo["valu_insts"], 3)
     else:
         roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": hbm["traffic"], "kernel": dom[0],
