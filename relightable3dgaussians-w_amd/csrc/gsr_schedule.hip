@@ -2,12 +2,13 @@
 //
 // The tile passes run one wave per tile, and tiles differ in cost by an order of magnitude
 // (list length, early saturation).  Each XCD band of the image (the bands of xcd_remap:
-// neighbouring tiles share Gaussian records in that XCD's L2) is ordered heaviest-first by
-// a log2 bucketing of a cost estimate; the passes dispatch block b on position b / 8 of band
-// b mod 8, so the hardware dispatcher runs a longest-first schedule per XCD.  Tiles above a
-// cost threshold (lists in the thousands: dense centres of real scenes) are split over the
-// four waves of their workgroup, one 8x8 quadrant each; the rest run four to a workgroup,
-// one wave each (TileUnit in gsr_tile.hpp).
+// neighbouring tiles share Gaussian records in that XCD's L2) is ordered heaviest-first in
+// 8 buckets per octave of a cost estimate (gsr_order.hpp); the passes dispatch block b on
+// position b / 8 of band b mod 8, so the hardware dispatcher runs a longest-first schedule
+// per XCD.  Tiles above a cost threshold (lists in the thousands: dense centres of real
+// scenes) and, in the forward, each band's lightest tiles run as four one-wave units, one
+// per 8x8 quadrant; the rest as one wave each (tile_unit in gsr_tile.hpp).  The forward's
+// order runs inside the binning scatter (gsr_binning.hip); this file launches the others.
 // (A persistent variant pulling tiles from per-XCD atomic queues measured 2x slower: the
 // returning atomics cost ~13 us per pull under load.)
 #include "gsr_order.hpp"

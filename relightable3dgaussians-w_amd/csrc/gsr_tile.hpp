@@ -77,7 +77,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // A tile's list -- the reference's point_list range, entry for entry -- is the subsequence of
 // its super-tile's entries whose local rect covers the tile.  TileList filters 64 entries per
 // step (one 8-B load per lane, prefetched a step ahead; a rect test; a ballot) and appends the
-// covering ones, with their list positions and entry indices, to a 128-slot LDS ring; the
+// covering ones, with their list positions and entry indices, to a 256-slot LDS ring; the
 // tile passes take full batches of 64 from the ring, so their per-batch work is what it was
 // over a materialised list.  Forward: front to back from position 0.  Backward: back to front
 // from a given entry (exclusive) whose preceding covering entries number pos0.
