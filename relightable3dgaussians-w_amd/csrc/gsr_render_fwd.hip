@@ -102,6 +102,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             uint32_t pos1;
             asm("v_mov_b32 %0, %1" : "=v"(pos1) : "s"(p0 + (uint32_t)k + 1u));
             lmask blended = 0;
+            FWD_STAT(5, m == 15u);
+            FWD_STAT(6, m != 0u);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
@@ -161,7 +163,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     }
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {
-        for (int k = 0; k < 5; k++) atomicAdd(&g_fwd_stats[k], st[k]);
+        for (int k = 0; k < 7; k++) atomicAdd(&g_fwd_stats[k], st[k]);
         if (tile < 65536 && qallow == 15u) {
             g_fwd_times[4 * tile] = t_start;
             g_fwd_times[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();

@@ -47,6 +47,7 @@ def main(cfg="cfg2"):
                      "quad_evals_with_work_per_tile": v[3] / T,
                      "lanes_per_working_eval": v[4] / max(v[3], 1),
                      "gaussians_with_work_per_tile": (v[5] / T) if name == "bwd" else None,
+                     "survivors_reaching_all_quadrants": (v[5] / max(v[6], 1)) if name == "fwd" else None,
                      "queue_wait_us_total": v[6] / 100.0 if name == "bwd" else None,
                      "tiles_via_queue": v[7] if name == "bwd" else None}
     n = T
