@@ -379,6 +379,9 @@ def main():
                          "default 2) alternate over")
     ap.add_argument("--no-minibatch", action="store_true", help="skip the 4-view multi-stream extra leg")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
+    ap.add_argument("--event-steps", type=int, default=5,
+                    help="record the dominant stage's HIP events on the last N timed steps (default 5; two "
+                         "event records cost ~10 us per view, so on every step they would be ~1 %% of it)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -485,14 +488,15 @@ def main():
         if dist is not None:
             state["bucket"].all_reduce()
 
-    for _ in range(args.warmup):
-        step()
+    step()  # first-call setup (allocations, the speculative binning's sizes)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    # Stage breakdown: three profiled views, one at a time on one stream (every stage
-    # bracketed by HIP events), before the timed region.  Inside it only the dominant stage
-    # keeps its events, so the step time carries two events per view instead of sixteen.
+    # Stage breakdown (before the W warmup steps, so the timed region follows them directly
+    # and starts on a busy GPU's clocks): three profiled views, one at a time on one stream
+    # (every stage bracketed by HIP events).  Inside it only the dominant stage
+    # keeps its events, on the last --event-steps steps, so the step time carries two events
+    # per view on those steps instead of sixteen on every one.
     _lib.profile_read(reset=True)
     _lib.profile_stages(None)
     _lib.profile_enable(True)
@@ -503,14 +507,22 @@ def main():
     stages = _lib.profile_read(reset=True)
     dom_name = max(((k, v[0] / v[1]) for k, v in stages.items() if v[1] > 0 and k in STAGE_KERNEL),
                    key=lambda kv: kv[1])[0]
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
     _lib.profile_stages([dom_name])
-    _lib.profile_enable(True)
+    ev_from = max(0, args.steps - max(1, args.event_steps))
+    _lib.profile_enable(ev_from <= 0)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k_step in range(args.steps):
+        if k_step == ev_from and ev_from > 0:
+            _lib.profile_enable(True)
         step()
     torch.cuda.synchronize()
     if dist is not None:
@@ -644,7 +656,8 @@ def main():
         "roofline": roofline,
         "stage_ms": per_stage,
         "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
-                           "stage); roofline.avg_launch_ms is the dominant stage's events inside the timed region",
+                           "stage); roofline.avg_launch_ms is the dominant stage's events on the last "
+                           f"{min(args.steps, max(1, args.event_steps))} steps of the timed region",
     }
     if single is not None:
         out["single_call"] = single
