@@ -59,6 +59,7 @@ STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "ren
 # spec VALU issue rate: a wave64 VALU instruction issues over 2 cycles on a SIMD-32, 2.4 GHz
 # (MI355X_MICROARCH.md "Execution model"); 1024 SIMDs -> 1228.8 G wave-instructions/s
 VALU_CLOCK_GHZ = 2.4
+SETTLE_STEPS = 16  # untimed steps right before the timed region, at least (W warmup + settle)
 VALU_CYCLES_PER_INST = 2
 
 
@@ -507,7 +508,10 @@ def main():
     stages = _lib.profile_read(reset=True)
     dom_name = max(((k, v[0] / v[1]) for k, v in stages.items() if v[1] > 0 and k in STAGE_KERNEL),
                    key=lambda kv: kv[1])[0]
-    for _ in range(args.warmup):
+    # at least SETTLE_STEPS untimed steps in a row before the timed region (the W warmup steps
+    # plus settle steps): with 3 warmup steps a 10-step run read ~1 % slower than with 20
+    settle = max(0, SETTLE_STEPS - args.warmup)
+    for _ in range(settle + args.warmup):
         step()
     torch.cuda.synchronize()
     if dist is not None:
@@ -644,6 +648,7 @@ def main():
         "metric": METRIC, "value": round(world * V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "untimed_steps_before_timing": settle + args.warmup,
         "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
                                                                        else "") if args.ply else args.config)
                                + f": {P} Gaussians SH{deg}, {W}x{H}, one rasterizer forward + backward per view, "
