@@ -33,7 +33,8 @@ def test_fused_ssim_matches_conv2d(shape, mask_kind):
     (3.0 * v1).backward()
     (3.0 * v2).backward()
     torch.cuda.synchronize()
-    assert abs(float(v1) - float(v2)) <= 1e-5 * abs(float(v2)) + 1e-7, (float(v1), float(v2))
+    f1, f2 = float(v1.detach()), float(v2.detach())
+    assert abs(f1 - f2) <= 1e-5 * abs(f2) + 1e-7, (f1, f2)
     e = rel_l2(a1.grad.cpu().numpy(), a2.grad.cpu().numpy())
     assert e < 1e-4, e
 
