@@ -37,3 +37,17 @@ s.record()
 for _ in range(N): pair()
 en.record(); torch.cuda.synchronize()
 print(f"event span per pair {s.elapsed_time(en)/N:.4f} ms")
+
+# how much GPU work is still queued when the forward call returns (an event recorded right
+# after it returns completes when that work is done)
+lag = []
+for _ in range(30):
+    R, color, radii, geom, binb, img = _C.rasterize_gaussians(bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, H, W, g["shs"], deg, cp, False)
+    t_ret = time.perf_counter()
+    ev = torch.cuda.Event()
+    ev.record()
+    ev.synchronize()
+    lag.append((time.perf_counter() - t_ret) * 1e3)
+    _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb, img)
+lag.sort()
+print(f"GPU work queued at the forward's return: median {lag[len(lag)//2]:.4f} ms (min {lag[0]:.4f}, max {lag[-1]:.4f})")
