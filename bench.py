@@ -258,41 +258,47 @@ def bench_relight(args, dev):
             "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
 
 
-def bench_train(args, dev, dist, rank, world):
+TRAIN_VIEWS_PER_RANK = 4
+TRAIN_ITERATION = 15001  # past reg_normal_from_iter (15000): the normal-consistency term is on
+
+
+def train_leg(args, dev, dist, rank, world, backend, steps, warmup):
     """cfg4: the data-parallel relightable training iteration.  Every rank
-    holds the whole scene (1.5M Gaussians: 1.36M foreground + 10 % sky, cfg2 distribution,
-    1920x1080) and renders its own 4 views per iteration through the fused render(), with
-    the reference's reconstruction (L1 + D-SSIM), sky-BRDF and normal losses and backward;
-    then one RCCL all-reduce of the flat gradient buffer, the densification statistics'
-    SUM/MAX, and one fused Adam launch (gsr/train.py).  value = iterations/s (whole job;
-    weak scaling: 4 views per rank per iteration)."""
+    holds the whole scene (1.5M Gaussians: 1.36M foreground + 10 % sky on their (theta, phi)
+    shell, cfg2 distribution, 1920x1080) and renders its own 4 views per iteration through the
+    fused render(), with the reference's losses (L1 + D-SSIM, sky-BRDF, normal consistency,
+    envlight, min-scale, sky depth) and backward; then one all-reduce of the flat gradient
+    buffer, the densification statistics' SUM/MAX, and one fused Adam launch (gsr/train.py).
+    The iteration number is past reg_normal_from_iter, so every loss term of train.py:77-118
+    is on.  Returns the leg's numbers (iterations/s: whole job, weak scaling -- 4 views per
+    rank per iteration; the time is the max over ranks)."""
     from gsr import train
-    vpr = 4
+    vpr = TRAIN_VIEWS_PER_RANK
     P_fg = args.P or 1_363_637
     W, H, focal = 1920, 1080, 1400.0
     scene, views, gts = train.synthetic_relit_scene(P_fg, vpr * world, W, H, focal, dev, seed=0)
+    scene.iteration = TRAIN_ITERATION - 1
     mine = list(range(rank * vpr, (rank + 1) * vpr))
     my_views, my_gts = [views[i] for i in mine], [gts[i] for i in mine]
-    group = None
     ns = max(1, min(2 if args.streams is None else args.streams, vpr))
     streams = None if ns == 1 else [torch.cuda.Stream(dev) for _ in range(ns)]
 
     def step():
-        return train.train_step(scene, my_views, mine, my_gts, group=group, world=world, streams=streams)
+        return train.train_step(scene, my_views, mine, my_gts, world=world, streams=streams)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         loss = step()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    ms = (time.perf_counter() - t0) * 1e3 / steps
     ar_ms = None
     if dist is not None:
         t = torch.tensor([ms], device=dev)
@@ -307,20 +313,101 @@ def bench_train(args, dev, dist, rank, world):
             dist.all_reduce(scene.fp.grad)
         torch.cuda.synchronize()
         ar_ms = (time.perf_counter() - t1) * 1e3 / 10
+    return {"value": round(1e3 / ms, 3), "unit": "iters/s", "ms_per_iter": round(ms, 4), "steps": steps,
+            "warmup": warmup, "views_per_s": round(vpr * world * 1e3 / ms, 3),
+            "workload": f"cfg4: {scene.P} Gaussians ({P_fg} fg + {scene.P - P_fg} sky), {W}x{H}, {vpr} views per "
+                        f"GPU per iteration, env SH deg 4, sky SH deg 1, iteration {TRAIN_ITERATION} (every loss "
+                        "term on)",
+            "gaussians": scene.P, "views_per_iter": vpr * world, "streams": ns, "flat_params": scene.fp.n,
+            "grad_bucket_mb": round(scene.fp.n * 4 / 1e6, 2),
+            "grad_all_reduce_ms": None if ar_ms is None else round(ar_ms, 4),
+            "all_reduce_backend": backend, "final_loss_rank0": round(float(loss) / vpr, 6)}
+
+
+def bench_train(args, dev, dist, rank, world, backend, joined):
+    """--config cfg4: the training iteration alone (train_leg) as the JSON line."""
+    r = train_leg(args, dev, dist, rank, world, backend, args.steps, args.warmup)
     if rank == 0:
         print(json.dumps({
             "metric": "train iters/s (relit render + losses + backward + grad all-reduce + Adam, 4 views per GPU)",
-            "value": round(1e3 / ms, 3), "unit": "iters/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
+            "value": r["value"], "unit": "iters/s", "n_gpus": world, "ranks_joined": joined, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": r["ms_per_iter"], "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"cfg4: {scene.P} Gaussians ({P_fg} fg + {scene.P - P_fg} sky), {W}x{H}, "
-                                   f"{vpr} views per GPU per iteration, env SH deg 4, sky SH deg 1",
-                       "gaussians": scene.P, "width": W, "height": H, "views_per_iter": vpr * world,
-                       "parallelism": f"views x{world}", "flat_params": scene.fp.n, "streams": ns},
-            "views_per_s": round(vpr * world * 1e3 / ms, 3),
-            "grad_all_reduce_ms": None if ar_ms is None else round(ar_ms, 4),
-            "grad_bucket_mb": round(scene.fp.n * 4 / 1e6, 2),
-            "final_loss_rank0": round(float(loss) / vpr, 6)}), flush=True)
+            "config": {"workload": r["workload"], "gaussians": r["gaussians"], "width": 1920, "height": 1080,
+                       "views_per_iter": r["views_per_iter"],
+                       "parallelism": f"views x{world}" + (f" ({backend})" if backend else ""),
+                       "flat_params": r["flat_params"], "streams": r["streams"]},
+            "views_per_s": r["views_per_s"], "grad_all_reduce_ms": r["grad_all_reduce_ms"],
+            "all_reduce_backend": backend, "grad_bucket_mb": r["grad_bucket_mb"],
+            "final_loss_rank0": r["final_loss_rank0"]}), flush=True)
+
+
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed launcher around it:
+    start the N rank processes here -- a `torch.distributed.run` child (one process per GPU,
+    127.0.0.1 rendezvous) running this same command line -- relay their output, and fail
+    unless the rank-0 line reports N ranks joined.  This process never touches the GPU
+    (`import torch` does not initialise HIP), so the ranks own their devices."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "4"))
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout:
+        sys.stdout.write(ln)
+        sys.stdout.flush()
+        if ln.startswith("{"):
+            try:
+                line = json.loads(ln)
+            except ValueError:
+                pass
+    rc = proc.wait()
+    if rc != 0:
+        return rc
+    if line is None or line.get("n_gpus") != n or line.get("ranks_joined") != n:
+        got = None if line is None else (line.get("n_gpus"), line.get("ranks_joined"))
+        print(f"bench.py: launched {n} ranks but the rank-0 line reports (n_gpus, ranks_joined) = {got}",
+              file=sys.stderr)
+        return 3
+    return 0
+
+
+def dist_setup(args):
+    """(dist, rank, world, local, backend, ranks_joined) for this process.  One process per GPU
+    over RCCL ("nccl"); GSR_DIST_BACKEND=gloo rehearses the N > 1 path (several ranks may then
+    share a GPU: ranks wrap around the visible devices).  ranks_joined counts the processes
+    that reached the first collective."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if world == 1:
+        return None, 0, 1, local, None, 1
+    import torch.distributed as dist
+    backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+    if args.launch_probe:  # CPU-only check of the launcher (tests/test_bench_launch.py)
+        backend = "gloo"
+        dist.init_process_group("gloo")
+        one = torch.ones(1)
+    else:
+        local = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(local)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+        one = torch.ones(1, device=torch.device("cuda", local))
+    dist.all_reduce(one)
+    return dist, rank, world, local, backend, int(one.item())
 
 
 def refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_ours):
@@ -357,7 +444,9 @@ def refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_ours):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank process each); N > 1 without WORLD_SIZE in the environment starts the N "
+                         "ranks itself (torch.distributed.run child, 127.0.0.1 rendezvous)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="cfg2")
@@ -383,30 +472,32 @@ def main():
     ap.add_argument("--event-steps", type=int, default=5,
                     help="record the dominant stage's HIP events on the last N timed steps (default 5; two "
                          "event records cost ~10 us per view, so on every step they would be ~1 %% of it)")
+    ap.add_argument("--no-train", action="store_true", help="skip the cfg4 training-iteration leg (train iters/s)")
+    ap.add_argument("--train-steps", type=int, default=None, help="timed iterations of the training leg "
+                                                                  "(default min(--steps, 20))")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="N > 1: all-reduce each step's gradient bucket before the next step starts (default: the "
+                         "exchange of step i runs on the collective stream under step i+1's views)")
+    ap.add_argument("--launch-probe", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        # one process per GPU over RCCL ("nccl"); GSR_DIST_BACKEND=gloo rehearses the N > 1 path
-        # with several ranks on one GPU (ranks wrap around the visible devices)
-        backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
-        local = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            dist.init_process_group(backend)
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    dist, rank, world, local, backend, joined = dist_setup(args)
+    if args.launch_probe:
+        if rank == 0:
+            print(json.dumps({"metric": "launch probe", "n_gpus": world, "ranks_joined": joined,
+                              "backend": backend}), flush=True)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if args.config in ("cfg3", "cfg5-relit"):
         bench_relight(args, dev)
         return
     if args.config == "cfg4":
-        bench_train(args, dev, dist, rank, world)
+        bench_train(args, dev, dist, rank, world, backend, joined)
         if dist is not None:
             dist.destroy_process_group()
         return
@@ -458,13 +549,30 @@ def main():
             state["R"], state["radii"] = R, radii
         return grads
 
+    overlap = dist is not None and not args.no_overlap
+    state["k"], state["work"] = 0, [None, None]
+
+    def drain():
+        """Wait (on the current stream) for every exchange still in flight."""
+        for j, w in enumerate(state["work"]):
+            if w is not None:
+                w.wait()
+                state["work"][j] = None
+
     def step():
         """V views, one after another (or alternating over NS HIP streams with --streams).  At
         N > 1 the views' dL/d(means3D, sh, opacity, scales, rotations) are summed into one flat
-        bucket on the main stream and over the ranks with one RCCL all-reduce."""
+        bucket on the main stream and over the ranks with one all-reduce.  Two buckets
+        alternate: step i's all-reduce is issued asynchronously (the collective's own stream
+        waits for the bucket) and runs under step i+1's views; a bucket is refilled only after
+        its previous exchange has finished (work.wait orders the stream after it)."""
+        kb = state["k"] % (2 if overlap else 1)
+        if dist is not None and state["work"][kb] is not None:
+            state["work"][kb].wait()
+            state["work"][kb] = None
         for s in vstreams:
             if s is not main_s:
-                s.wait_stream(main_s)  # the previous step's exchange comes first
+                s.wait_stream(main_s)  # the bucket's previous exchange comes first
         for i in range(V):
             s = vstreams[i % NS]
             with torch.cuda.stream(s):
@@ -475,9 +583,9 @@ def main():
                     main_s.wait_stream(s)
                     for t in ts:
                         t.record_stream(main_s)
-                if "bucket" not in state:
-                    state["bucket"] = gdp.GradBucket(ts)
-                b = state["bucket"]
+                if "buckets" not in state:
+                    state["buckets"] = [gdp.GradBucket(ts) for _ in range(2 if overlap else 1)]
+                b = state["buckets"][kb]
                 if i == 0:
                     b.pack(ts)
                 else:
@@ -487,9 +595,13 @@ def main():
             if s is not main_s:
                 main_s.wait_stream(s)
         if dist is not None:
-            state["bucket"].all_reduce()
+            state["work"][kb] = dist.all_reduce(state["buckets"][kb].flat, async_op=True)
+            if not overlap:
+                drain()
+        state["k"] += 1
 
     step()  # first-call setup (allocations, the speculative binning's sizes)
+    drain()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -513,6 +625,7 @@ def main():
     settle = max(0, SETTLE_STEPS - args.warmup)
     for _ in range(settle + args.warmup):
         step()
+    drain()  # the timed region starts with no exchange in flight ...
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -528,6 +641,7 @@ def main():
         if k_step == ev_from and ev_from > 0:
             _lib.profile_enable(True)
         step()
+    drain()  # ... and ends with every step's exchange finished
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -545,11 +659,11 @@ def main():
     ar_ms = None
     if dist is not None:
         for _ in range(2):
-            state["bucket"].all_reduce()
+            state["buckets"][0].all_reduce()
         torch.cuda.synchronize()
         ta = time.perf_counter()
         for _ in range(5):
-            state["bucket"].all_reduce()
+            state["buckets"][0].all_reduce()
         torch.cuda.synchronize()
         ar_ms = (time.perf_counter() - ta) * 1e3 / 5
     R = int(state["R"])
@@ -640,24 +754,39 @@ def main():
             # than an added VALU op)
             roofline["salu_insts_per_launch"] = int(kinfo["salu_insts"])
             roofline["salu_per_valu"] = round(kinfo["salu_insts"] / kinfo["valu_insts"], 3)
+    elif dom[0].startswith("render"):
+        # a tile pass with no committed instruction count for this workload: its bound is VALU
+        # issue, and the HBM fraction of its algorithmic bytes is not a roofline
+        # (the R x 40 record reads are served from LDS/L2), so no fraction is claimed
+        roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "Gwave-inst/s", "frac": None,
+                    "traffic": hbm["traffic"], "kernel": dom[0], "avg_launch_ms": round(dom[1], 4),
+                    "frac_null_reason": f"no committed rocprofv3 SQ_INSTS_VALU pass of workload '{workload}' "
+                                        "(profiles/r*_hbm_traffic.json)", "hbm": hbm}
     else:
         roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": hbm["frac"], "traffic": hbm["traffic"], "kernel": dom[0],
                     "avg_launch_ms": round(dom[1], 4), "hbm": hbm}
+    if roofline["bound"] == "hbm" and roofline["frac"] is not None and roofline["frac"] > 1.0:
+        # more algorithmic bytes per second than HBM delivers: part of them came from a cache,
+        # so the figure is no HBM fraction
+        roofline.update(frac=None, frac_null_reason="algorithmic bytes / launch time exceed the HBM peak (served "
+                                                    "from L2 / Infinity Cache)")
     out = {
         "metric": METRIC, "value": round(world * V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s",
-        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "untimed_steps_before_timing": settle + args.warmup,
+        "n_gpus": world, "ranks_joined": joined, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic", "untimed_steps_before_timing": settle + args.warmup,
         "config": {"workload": (f"ply {os.path.basename(args.ply)}" + (f" + COLMAP view {args.view}" if args.colmap
                                                                        else "") if args.ply else args.config)
                                + f": {P} Gaussians SH{deg}, {W}x{H}, one rasterizer forward + backward per view, "
                                  f"{V} view(s) per step per GPU"
                                + (f" on {NS} HIP streams" if NS > 1 else "")
-                               + (", scene replicated on every rank, distinct cameras per rank, one RCCL grad "
-                                  "all-reduce per step" if world > 1 else ""),
+                               + (f", scene replicated on every rank, distinct cameras per rank, one {backend} "
+                                  "grad all-reduce per step" + (" (overlapped with the next step's views)" if overlap
+                                                                else "") if world > 1 else ""),
                    "gaussians": P, "width": W, "height": H, "sh_degree": deg, "num_rendered": R, "visible": Pv,
-                   "views_per_step": V, "streams": NS, "parallelism": f"views x{world}"},
+                   "views_per_step": V, "streams": NS,
+                   "parallelism": f"views x{world}" + (f" ({backend})" if backend else "")},
         "roofline": roofline,
         "stage_ms": per_stage,
         "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
@@ -669,8 +798,15 @@ def main():
     if mini is not None:
         out["minibatch_4view"] = mini
     if dist is not None:
-        out["data_parallel"] = {"views_per_step": V, "grad_all_reduce_ms": round(ar_ms, 4),
-                                "grad_bucket_mb": round(state["bucket"].flat.numel() * 4 / 1e6, 2)}
+        out["data_parallel"] = {"views_per_step": V, "backend": backend, "grad_all_reduce_ms": round(ar_ms, 4),
+                                "grad_all_reduce_what": "the step's bucket all-reduced alone, 5 times back to back",
+                                "exchange_overlapped": overlap,
+                                "grad_bucket_mb": round(state["buckets"][0].flat.numel() * 4 / 1e6, 2)}
+    if not args.no_train and not args.ply:
+        # the metric's second half: train iters/s of the cfg4 iteration at this N
+        state.pop("buckets", None)
+        out["train"] = train_leg(args, dev, dist, rank, world, backend,
+                                 args.train_steps or min(args.steps, 20), max(3, min(args.warmup, 10)))
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
         ms_view = single["median_ms"] if single is not None else ms / V
         vm, pm, cp = mats[0]

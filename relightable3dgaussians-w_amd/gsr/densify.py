@@ -16,10 +16,11 @@ Follows scene/gaussian_model.py:
   prune_points        :465-485  rows removed from every group and from the Adam moments
                                 (_prune_optimizer :438-462)
 
-Per-Gaussian groups hold P rows (xyz, scaling, rotation, opacity) or one row per foreground
-Gaussian in foreground order (albedo, roughness, metalness).  Sky Gaussians keep their xyz
-in the xyz group here (the reference stores their (theta, phi) angles on a fixed shell;
-the shell projection of split samples is applied the same way).
+Per-Gaussian groups hold P rows (scaling, rotation, opacity), one row per foreground
+Gaussian in foreground order (xyz, albedo, roughness, metalness) or one row per sky Gaussian
+in sky order (sky_angles), as the reference's groups (_prune_optimizer :438-462).  A split
+sky sample is projected onto the shell and turned back into angles with
+cartesian_to_polar_coord's default radius of 1 (:571-573, as the reference calls it).
 
 Rank consistency: every input of the decisions (parameters, reduced statistics) is
 identical on every rank by construction, and the split's samples come from ``generator``,
@@ -33,9 +34,9 @@ from typing import Dict, Optional
 
 import torch
 
-from .train import FlatParams
-
-FG_GROUPS = ("albedo", "roughness", "metalness")
+from .train import FG_ROW_GROUPS as FG_GROUPS
+from .train import SKY_ROW_GROUPS as SKY_GROUPS
+from .train import FlatParams, SkyLayout, cartesian_to_polar_coord, sky_xyz
 
 
 def build_rotation(r: torch.Tensor) -> torch.Tensor:
@@ -81,13 +82,18 @@ class _Rows:
         self.is_sky = torch.cat([self.is_sky, new_is_sky])
 
     def keep(self, mask: torch.Tensor) -> None:
-        fg_mask = mask[~self.is_sky]
+        fg_mask, sky_mask = mask[~self.is_sky], mask[self.is_sky]
         for name in self.t:
-            if name in self.global_groups:  # embeddings and MLP weights: not per Gaussian
+            if name in self.global_groups:  # embeddings, MLP weights, sky radius: not per Gaussian
                 continue
-            m = fg_mask if name in FG_GROUPS else mask
+            m = fg_mask if name in FG_GROUPS else sky_mask if name in SKY_GROUPS else mask
             self.t[name] = [x[m] for x in self.t[name]]
         self.is_sky = self.is_sky[mask]
+
+    def xyz(self, center: torch.Tensor) -> torch.Tensor:
+        """get_xyz of the current rows (gaussian_model.py:84-93)."""
+        sky = sky_xyz(self.get("sky_angles"), self.get("sky_radius"), center) if bool(self.is_sky.any()) else None
+        return SkyLayout(self.is_sky).xyz(self.get("xyz"), sky)
 
 
 def _reset_stats(scene, P, dev):
@@ -110,9 +116,9 @@ def densify_and_prune(scene, max_grad: float, min_opacity: float, extent: float,
         scaling = torch.exp(rows.get("scaling"))
         sel = (torch.norm(grads, dim=-1) >= max_grad) & (scaling.max(dim=1).values <= percent_dense * extent)
         if bool(sel.any()):
-            sel_fg = sel[~rows.is_sky]
-            new = {"xyz": rows.get("xyz")[sel], "scaling": rows.get("scaling")[sel],
-                   "rotation": rows.get("rotation")[sel], "opacity": rows.get("opacity")[sel]}
+            sel_fg, sel_sky = sel[~rows.is_sky], sel[rows.is_sky]
+            new = {"scaling": rows.get("scaling")[sel], "rotation": rows.get("rotation")[sel],
+                   "opacity": rows.get("opacity")[sel], "sky_angles": rows.get("sky_angles")[sel_sky]}
             new.update({g: rows.get(g)[sel_fg] for g in FG_GROUPS})
             rows.append(new, rows.is_sky[sel])
             # densification_postfix resets the statistics (:540-542)
@@ -128,15 +134,17 @@ def densify_and_prune(scene, max_grad: float, min_opacity: float, extent: float,
             stds = scaling[sel].repeat(N, 1)
             samples = torch.normal(mean=torch.zeros_like(stds), std=stds, generator=generator)
             rots = build_rotation(rows.get("rotation")[sel]).repeat(N, 1, 1)
-            new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + rows.get("xyz")[sel].repeat(N, 1)
+            new_xyz = torch.bmm(rots, samples.unsqueeze(-1)).squeeze(-1) + rows.xyz(scene.sky_center)[sel].repeat(N, 1)
             new_sky = rows.is_sky[sel].repeat(N)
+            new = {"scaling": torch.log(scaling[sel].repeat(N, 1) / (0.8 * N)),
+                   "rotation": rows.get("rotation")[sel].repeat(N, 1), "opacity": rows.get("opacity")[sel].repeat(N, 1)}
             if bool(new_sky.any()):
                 c = scene.sky_center
                 d = new_xyz[new_sky] - c
-                new_xyz[new_sky] = c + scene.sky_radius * d / torch.norm(d, dim=1)[..., None]
-            new = {"xyz": new_xyz, "scaling": torch.log(scaling[sel].repeat(N, 1) / (0.8 * N)),
-                   "rotation": rows.get("rotation")[sel].repeat(N, 1), "opacity": rows.get("opacity")[sel].repeat(N, 1)}
-            new.update({g: rows.get(g)[sel_fg].repeat(N, 1) for g in FG_GROUPS})
+                new_xyz[new_sky] = c + rows.get("sky_radius") * d / torch.norm(d, dim=1)[..., None]
+                new["sky_angles"] = cartesian_to_polar_coord(new_xyz[new_sky], c)
+            new["xyz"] = new_xyz[~new_sky]
+            new.update({g: rows.get(g)[sel_fg].repeat(N, 1) for g in FG_GROUPS if g != "xyz"})
             rows.append(new, new_sky)
             _reset_stats(scene, rows.is_sky.shape[0], dev)
             prune = torch.cat([sel, torch.zeros(N * int(sel.sum()), device=dev, dtype=torch.bool)])
@@ -166,6 +174,5 @@ def _rebuild(scene, rows: _Rows) -> None:
             fp.exp_avg[off:off + n].copy_(m.reshape(-1))
             fp.exp_avg_sq[off:off + n].copy_(s.reshape(-1))
     scene.fp = fp
-    scene.is_sky = rows.is_sky.reshape(-1, 1)
-    scene.P = rows.is_sky.shape[0]
+    scene.set_sky_flags(rows.is_sky)
     scene.step_stats = None

@@ -186,17 +186,24 @@ def consistent_rng(device, group=None):
         yield seed
 
 
-def replica_checksums(tensors: Sequence[torch.Tensor], group=None) -> List[List[float]]:
-    """Per-rank float64 checksums (sum and sum of squares of the bit patterns' values) of
-    ``tensors``, all-gathered: identical rows mean identical replicas (a debug check after
-    densification)."""
-    sums = []
-    for t in tensors:
-        x = t.detach().reshape(-1).double()
-        sums += [float(x.numel()), float(x.sum()), float((x * x).sum())]
-    mine = torch.tensor(sums, dtype=torch.float64)
+def replicas_identical(tensors: Sequence[torch.Tensor], group=None) -> List[bool]:
+    """Whether every rank holds byte-identical ``tensors`` (a debug check after
+    densification): each tensor's bytes are all-gathered (after its shape) and compared with
+    rank 0's by ``torch.equal`` on the raw bytes, so NaN payloads, -0/+0 and any other bit
+    difference count.  Returns one flag per tensor, the same on every rank."""
     if not (dist.is_available() and dist.is_initialized()):
-        return [sums]
-    out = [torch.zeros_like(mine) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(out, mine, group=group)
-    return [o.tolist() for o in out]
+        return [True for _ in tensors]
+    world = dist.get_world_size(group)
+    out = []
+    for t in tensors:
+        b = t.detach().contiguous().reshape(-1).view(torch.uint8)
+        n = torch.tensor([b.numel()], dtype=torch.int64, device=b.device)
+        ns = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(ns, n, group=group)
+        if any(int(x) != int(n) for x in ns):
+            out.append(False)
+            continue
+        bs = [torch.empty_like(b) for _ in range(world)]
+        dist.all_gather(bs, b, group=group)
+        out.append(all(torch.equal(bs[0], x) for x in bs[1:]))
+    return out

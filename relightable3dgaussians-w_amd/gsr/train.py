@@ -25,10 +25,16 @@ envlight (envl_sh_loss), min-scale and sky-depth regularisers with the configure
 (configs/optimizer/optimization_params.yaml).  The embedding table and the MLP weights are
 segments of the same flat buffer, so their gradients cross the ranks in the same all-reduce.
 
-Differences kept on purpose: sky Gaussians keep their xyz in the xyz group (the reference
-stores their (theta, phi) angles on a fixed shell, gaussian_model.py:96-103); the random
-draws (dropout masks, SH noise, envlight directions) come from one device generator per
-scene instead of the global CPU/GPU RNG, so a step is reproducible and synchronisation-free.
+Sky Gaussians are parametrised as the reference's: two angles (theta, phi) per sky Gaussian
+on a shell of learnable radius around a fixed centre (gaussian_model.py:84-103,159-169,
+227-251), so the gradient bucket carries xyz for the foreground and 2 floats per sky
+Gaussian.  The loss terms switch on at the reference's iterations
+(reg_normal_from_iter, reg_sky_gauss_depth_from_iter; train.py:89,113), and the envlight term
+is added unweighted when lambda_envlight > 0 (train.py:99-102: the weight is only a switch).
+
+Difference kept on purpose: the random draws (dropout masks, SH noise, envlight directions)
+come from one device generator per scene instead of the global CPU/GPU RNG, so a step is
+reproducible and synchronisation-free.
 """
 from __future__ import annotations
 
@@ -41,10 +47,14 @@ import torch.nn.functional as F
 
 from . import _lib
 
-# (name, columns, lr) -- configs/optimizer/*.yaml defaults, gaussian_model.py:264-274
-# (xyz and scaling lrs carry the scene's spatial_lr_scale, applied by the caller)
+# (name, columns, lr) -- configs/optimizer/*.yaml defaults, in training_setup's group order
+# (gaussian_model.py:259-274; xyz, scaling and sky_angles lrs carry the scene's spatial_lr_scale)
 GAUSSIAN_GROUPS = (("xyz", 3, 0.00016), ("albedo", 3, 0.0025), ("opacity", 1, 0.05), ("scaling", 3, 0.001),
-                   ("rotation", 4, 0.001), ("roughness", 1, 0.0002), ("metalness", 1, 0.0002))
+                   ("rotation", 4, 0.001), ("roughness", 1, 0.0002), ("metalness", 1, 0.0002),
+                   ("sky_radius", 1, 0.0001), ("sky_angles", 2, 0.00016))
+FG_ROW_GROUPS = ("xyz", "albedo", "roughness", "metalness")  # one row per foreground Gaussian
+SKY_ROW_GROUPS = ("sky_angles",)                             # one row per sky Gaussian
+SCENE_GROUPS = ("sky_radius",)                               # one value per scene
 MLP_LR = 0.0002         # mlp_lr (configs/optimizer/optimization_params.yaml)
 EMBEDDINGS_LR = 0.0002  # embeddings_lr
 EMBEDDING_DIM = 32      # configs/relightable3DG-W.yaml embeddings_dim
@@ -57,6 +67,7 @@ ENV_NOISE_STD = 0.025   # train.py:70
 # loss weights (configs/optimizer/optimization_params.yaml)
 LAMBDA_DSSIM, LAMBDA_SKY_BRDF, LAMBDA_NORMAL = 0.2, 0.5, 0.05
 LAMBDA_ENVLIGHT, LAMBDA_SCALE, LAMBDA_SKY_GAUSS = 100.0, 100.0, 0.05
+REG_NORMAL_FROM_ITER, REG_SKY_GAUSS_DEPTH_FROM_ITER = 15000, 0
 
 
 class FlatParams:
@@ -396,13 +407,14 @@ def depth_loss_gaussians(gaussians, camera, visibility_filter: torch.Tensor, gam
 
 
 def view_regularisers(pc, radii: torch.Tensor, viewmats: torch.Tensor, env_sh: torch.Tensor, dirs: torch.Tensor,
-                      gamma: float = 0.02) -> torch.Tensor:
-    """The three regularisers of train.py:101-118 for V views at once, as [V] losses:
-    LAMBDA_ENVLIGHT envl_sh_loss(env_sh[v]) + LAMBDA_SCALE min_scale_loss(radii[v])
-    + LAMBDA_SKY_GAUSS depth_loss_gaussians(view v), each equal to the single-view function
-    above.  radii [V,P], viewmats [V,4,4] (row-vector world-to-view), env_sh [V,25,3], dirs
-    [V,10,3].  Batched over views, the per-Gaussian work is ~15 [V,P] kernels each way instead
-    of ~15 [P] kernels per view per function."""
+                      gamma: float = 0.02, depth_on: bool = True) -> torch.Tensor:
+    """The three regularisers of train.py:99-118 for V views at once, as [V] losses:
+    envl_sh_loss(env_sh[v]) (unweighted: lambda_envlight only switches it on, :99-102)
+    + LAMBDA_SCALE min_scale_loss(radii[v]) + LAMBDA_SKY_GAUSS depth_loss_gaussians(view v)
+    (when ``depth_on``: iteration > reg_sky_gauss_depth_from_iter, :113), each equal to the
+    single-view function above.  radii [V,P], viewmats [V,4,4] (row-vector world-to-view),
+    env_sh [V,25,3], dirs [V,10,3].  Batched over views, the per-Gaussian work is ~15 [V,P]
+    kernels each way instead of ~15 [P] kernels per view per function."""
     V = radii.shape[0]
 
     def rows(x):  # per-view sums of a [V,P] tensor: V full reductions (PyTorch's reduction
@@ -426,7 +438,71 @@ def view_regularisers(pc, radii: torch.Tensor, viewmats: torch.Tensor, env_sh: t
     neg = (vals < 0).to(vals.dtype)
     n = neg.sum(dim=(1, 2))
     el = torch.where(n > 0, (vals * vals * neg).sum(dim=(1, 2)) / n.clamp(min=1), torch.zeros_like(n))
-    return LAMBDA_ENVLIGHT * el + LAMBDA_SCALE * ms + LAMBDA_SKY_GAUSS * dl
+    total = torch.zeros_like(ms)
+    if LAMBDA_ENVLIGHT > 0:
+        total = total + el
+    if LAMBDA_SCALE > 0:
+        total = total + LAMBDA_SCALE * ms
+    if depth_on and LAMBDA_SKY_GAUSS > 0:
+        total = total + LAMBDA_SKY_GAUSS * dl
+    return total
+
+
+# ---- the sky Gaussians' parametrisation (gaussian_model.py:84-103,159-169) -----------------
+
+def cartesian_to_polar_coord(xyz: torch.Tensor, center: torch.Tensor = None, radius=1.0) -> torch.Tensor:
+    """utils/general_utils.py:295-299: theta = acos(clamp((c_y - y) / radius, -1, 1)),
+    phi = atan2(x - c_x, z - c_z), as [N,2].  ``radius`` defaults to 1.0 as in the reference
+    (densify_and_split calls it without a radius, gaussian_model.py:573)."""
+    if center is None:
+        center = torch.zeros(3, dtype=xyz.dtype, device=xyz.device)
+    theta = torch.acos(torch.clamp((-xyz[..., 1] + center[1]) / radius, -1, 1)).unsqueeze(1)
+    phi = torch.atan2(xyz[..., 0] - center[0], xyz[..., 2] - center[2]).unsqueeze(1)
+    return torch.cat((theta, phi), dim=1)
+
+
+def sky_angles_clamped(a: torch.Tensor) -> torch.Tensor:
+    """get_sky_angles (gaussian_model.py:159-169): theta clamped to [0, pi/2], phi to
+    [-pi/2, pi/2] (zero gradient outside the range)."""
+    tm = (a[..., 0] < 0) | (a[..., 0] > torch.pi / 2)
+    pm = (a[..., 1] < -torch.pi / 2) | (a[..., 1] > torch.pi / 2)
+    th = torch.where(tm, torch.clamp(a[..., 0], 0, torch.pi / 2), a[..., 0])
+    ph = torch.where(pm, torch.clamp(a[..., 1], -torch.pi / 2, torch.pi / 2), a[..., 1])
+    return torch.cat((th.unsqueeze(1), ph.unsqueeze(1)), dim=1)
+
+
+def sky_xyz(angles: torch.Tensor, radius: torch.Tensor, center: torch.Tensor) -> torch.Tensor:
+    """get_sky_xyz (gaussian_model.py:95-103), COLMAP axes: radius (sin t sin p, -cos t,
+    sin t cos p) + center, from the clamped angles."""
+    a = sky_angles_clamped(angles)
+    x = torch.sin(a[..., 0]) * torch.sin(a[..., 1])
+    y = -torch.cos(a[..., 0])
+    z = torch.sin(a[..., 0]) * torch.cos(a[..., 1])
+    return radius * torch.stack([x, y, z], dim=-1) + center.reshape(-1)
+
+
+class SkyLayout:
+    """Where the foreground and sky rows sit among all P Gaussians (get_xyz's scatter by the
+    sky flags, gaussian_model.py:84-93), as index tensors made once per scene layout (boolean
+    indexing would synchronise with the host every iteration).  ``tail``: the sky Gaussians
+    are the last rows, so the scatter is one concatenation."""
+
+    def __init__(self, is_sky: torch.Tensor):
+        m = is_sky.reshape(-1).bool()
+        self.P = int(m.numel())
+        self.n_sky = int(m.sum())
+        self.n_fg = self.P - self.n_sky
+        self.tail = bool(m[self.n_fg:].all()) and not bool(m[:self.n_fg].any())
+        self.fg_idx = torch.nonzero(~m).reshape(-1)
+        self.sky_idx = torch.nonzero(m).reshape(-1)
+
+    def xyz(self, xyz_fg: torch.Tensor, xyz_sky: torch.Tensor) -> torch.Tensor:
+        if self.n_sky == 0:
+            return xyz_fg.view(xyz_fg.shape)
+        if self.tail:
+            return torch.cat([xyz_fg, xyz_sky], dim=0)
+        out = torch.zeros(self.P, 3, dtype=xyz_fg.dtype, device=xyz_fg.device)
+        return out.index_put((self.fg_idx,), xyz_fg).index_put((self.sky_idx,), xyz_sky)
 
 
 def draw_step_randomness(n_views: int, device, generator: torch.Generator = None) -> Dict[str, torch.Tensor]:
@@ -442,27 +518,43 @@ def draw_step_randomness(n_views: int, device, generator: torch.Generator = None
 # ---- the model view render() reads and the step ------------------------------------------
 
 class RelitScene:
-    """A relightable scene on one rank: FlatParams with the Gaussian groups, the per-view
-    embedding table [n_views, 32] (relit3DGW_model.py:66-67) and MLPNet's weights (the
-    ``mlp.*`` groups, PyTorch's default Linear initialisation), and the constant sky flags.  ``model()`` gives the activated attributes as render() reads them
-    (gaussian_model.py:74-180: exp scaling, normalised rotation, sigmoid opacity and
-    materials)."""
+    """A relightable scene on one rank: FlatParams with the Gaussian groups (foreground xyz,
+    sky (theta, phi) angles and the sky shell radius as the reference stores them), the
+    per-view embedding table [n_views, 32] (relit3DGW_model.py:66-67) and MLPNet's weights
+    (the ``mlp.*`` groups, PyTorch's default Linear initialisation), and the constant sky
+    flags.  ``model()`` gives the activated attributes as render() reads them
+    (gaussian_model.py:74-180: get_xyz scattered from the foreground rows and the shell, exp
+    scaling, normalised rotation, sigmoid opacity and materials).
+
+    ``xyz`` [P,3] are all positions; the sky rows become angles on a shell around
+    ``sky_center`` (default: the origin) of radius ``sky_radius`` (default: the sky rows'
+    median distance from the centre), as augment_with_sky_gaussians does (:227-251)."""
 
     def __init__(self, xyz, scaling_raw, rotation_raw, opacity_raw, albedo_raw, rough_raw, metal_raw, is_sky,
-                 n_views, device, spatial_lr_scale=1.0, seed=0):
+                 n_views, device, spatial_lr_scale=1.0, seed=0, sky_center=None, sky_radius=None):
         P, N_fg = xyz.shape[0], albedo_raw.shape[0]
+        m = is_sky.reshape(-1).bool().cpu()
+        if int((~m).sum()) != N_fg:
+            raise ValueError(f"RelitScene: {int((~m).sum())} foreground Gaussians but {N_fg} material rows")
+        self.sky_center = (torch.zeros(3) if sky_center is None else torch.as_tensor(sky_center).float().reshape(3))
+        xyz = xyz.float().cpu()
+        sky_pts = xyz[m]
+        if sky_radius is None:
+            sky_radius = float((sky_pts - self.sky_center).norm(dim=1).median()) if sky_pts.shape[0] else 1.0
         spec = []
         for name, cols, lr in GAUSSIAN_GROUPS:
-            rows = N_fg if name in ("albedo", "roughness", "metalness") else P
-            if name in ("xyz", "scaling"):
+            if name in ("xyz", "scaling", "sky_angles"):
                 lr *= spatial_lr_scale
-            spec.append((name, (rows, cols), lr))
+            rows = N_fg if name in FG_ROW_GROUPS else (P - N_fg) if name in SKY_ROW_GROUPS else P
+            spec.append((name, (1,) if name in SCENE_GROUPS else (rows, cols), lr))
         spec.append(("embeddings", (n_views, EMBEDDING_DIM), EMBEDDINGS_LR))
         for name, fout, fin in MLP_LAYERS:
             spec += [(f"mlp.{name}.weight", (fout, fin), MLP_LR), (f"mlp.{name}.bias", (fout,), MLP_LR)]
         self.fp = FlatParams(spec, device)
-        for name, v in (("xyz", xyz), ("scaling", scaling_raw), ("rotation", rotation_raw), ("opacity", opacity_raw),
-                        ("albedo", albedo_raw), ("roughness", rough_raw), ("metalness", metal_raw)):
+        for name, v in (("xyz", xyz[~m]), ("scaling", scaling_raw), ("rotation", rotation_raw),
+                        ("opacity", opacity_raw), ("albedo", albedo_raw), ("roughness", rough_raw),
+                        ("metalness", metal_raw), ("sky_radius", torch.tensor([float(sky_radius)])),
+                        ("sky_angles", cartesian_to_polar_coord(sky_pts, self.sky_center, float(sky_radius)))):
             self.fp.load(name, v)
         g = torch.Generator().manual_seed(seed)
         # embeddings: unit rows, as initialize_embeddings normalises its encoder's outputs
@@ -475,24 +567,39 @@ class RelitScene:
         self.rng = torch.Generator(device=device)
         self.rng.manual_seed(seed + 12345)
         self.id_cache = {}
-        self.global_groups = {"embeddings"} | {n for n in self.fp.names if n.startswith("mlp.")}
-        self.is_sky = is_sky.to(device).reshape(-1, 1).bool()
-        self.P = P
+        self.global_groups = {"embeddings"} | {n for n in self.fp.names if n.startswith("mlp.")} | set(SCENE_GROUPS)
+        self.sky_center = self.sky_center.to(device)
+        self.set_sky_flags(m.to(device))
         self.stats = {"xyz_gradient_accum": torch.zeros(P, 1, device=device),
                       "denom": torch.zeros(P, 1, device=device),
                       "max_radii2D": torch.zeros(P, device=device)}
         self.step_stats = None
-        # the sky shell split samples are projected onto (gaussian_model.py:566-568)
-        sky_xyz = xyz[is_sky.reshape(-1).bool()].float()
-        self.sky_center = torch.zeros(3, device=device)
-        self.sky_radius = float(sky_xyz.norm(dim=1).median()) if sky_xyz.shape[0] else 1.0
+        self.iteration = 0  # the reference's loop counter of the last step (train.py:55)
 
-    def model(self):
-        p = self.fp.params
-        # xyz goes through a view made on the current (main) stream: the views render on side
-        # streams, and a leaf consumed there would accumulate its gradient off the stream it
-        # lives on (autograd's AccumulateGrad stream-mismatch warning)
-        return types.SimpleNamespace(get_xyz=p["xyz"].view(p["xyz"].shape), get_scaling=torch.exp(p["scaling"]),
+    def set_sky_flags(self, is_sky: torch.Tensor) -> None:
+        self.is_sky = is_sky.reshape(-1, 1).bool()
+        self.layout = SkyLayout(self.is_sky)
+        self.P = self.layout.P
+
+    @property
+    def sky_radius(self) -> torch.Tensor:
+        return self.fp.params["sky_radius"]
+
+    def get_xyz(self, params=None) -> torch.Tensor:
+        """gaussian_model.py:84-93 on the flat parameters (or on ``params``, a dict of leaves
+        with the same names)."""
+        p = self.fp.params if params is None else params
+        sky = None
+        if self.layout.n_sky:
+            sky = sky_xyz(p["sky_angles"], p["sky_radius"], self.sky_center)
+        return self.layout.xyz(p["xyz"], sky)
+
+    def model(self, params=None):
+        p = self.fp.params if params is None else params
+        # get_xyz is made on the current (main) stream: the views render on side streams, and
+        # a leaf consumed there would accumulate its gradient off the stream it lives on
+        # (autograd's AccumulateGrad stream-mismatch warning)
+        return types.SimpleNamespace(get_xyz=self.get_xyz(p), get_scaling=torch.exp(p["scaling"]),
                                      get_rotation=F.normalize(p["rotation"]), get_opacity=torch.sigmoid(p["opacity"]),
                                      get_albedo=torch.sigmoid(p["albedo"]), get_roughness=torch.sigmoid(p["roughness"]),
                                      get_metalness=torch.sigmoid(p["metalness"]), get_is_sky=self.is_sky)
@@ -502,7 +609,8 @@ _BLACK = {}
 
 
 def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
-               world: int = 1, bg=None, streams=None, rand: Dict[str, torch.Tensor] = None) -> torch.Tensor:
+               world: int = 1, bg=None, streams=None, rand: Dict[str, torch.Tensor] = None,
+               iteration: int = None) -> torch.Tensor:
     """One data-parallel iteration: this rank's views rendered and back-propagated, one
     all-reduce of the flat gradient, the densification statistics reduced, one fused Adam
     step with the mean gradient over all ranks' views.  ``streams``: HIP streams the views
@@ -510,12 +618,15 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     optimizer step, so one view's latency-bound geometry passes overlap another's tile
     passes; autograd runs each view's backward on its forward's stream.  ``rand``: the
     iteration's random draws (draw_step_randomness; default: from the scene's generator).
-    Returns this rank's summed loss as a device scalar (no host synchronisation inside the
-    step).
+    ``iteration``: the reference's loop counter (default: the scene's last + 1), which
+    switches the normal term on past reg_normal_from_iter and the sky-depth term past
+    reg_sky_gauss_depth_from_iter.  Returns this rank's summed loss as a device scalar (no
+    host synchronisation inside the step).
 
     Per view (train.py:66-120): envlight_sh, sky_sh = MLPNet(embedding); render() with
-    envlight_sh + noise; loss = reconstruction + sky-BRDF + normal (view_loss)
-    + 100 envl_sh_loss(envlight_sh) + 100 min_scale_loss(radii) + 0.05 depth_loss_gaussians."""
+    envlight_sh + noise; loss = reconstruction + sky-BRDF (+ 0.05 normal once iteration >
+    15000) (view_loss) + envl_sh_loss(envlight_sh) + 100 min_scale_loss(radii)
+    (+ 0.05 depth_loss_gaussians once iteration > 0)."""
     import relit_shade
 
     from . import relit
@@ -523,6 +634,8 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     fp = scene.fp
     fp.zero_grad()
     dev = fp.device
+    scene.iteration = it = scene.iteration + 1 if iteration is None else int(iteration)
+    lam_normal = LAMBDA_NORMAL if (it > REG_NORMAL_FROM_ITER and LAMBDA_NORMAL > 0) else 0.0
     if bg is None:  # one tensor per device: render()'s grey-background check is cached on it
         bg = _BLACK.get(str(dev))
         if bg is None:
@@ -552,7 +665,7 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
             light = relit_shade.EnvironmentLight(env_lit[i], sh_degree=4)
             out = relit.render(view, pc, light, sky_sh[i:i + 1], 1, pipe, bg, debug=False)
             losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask, LAMBDA_DSSIM, LAMBDA_SKY_BRDF,
-                                    LAMBDA_NORMAL))
+                                    lam_normal))
         outs.append(out)
     for s in streams:
         main.wait_stream(s)
@@ -563,7 +676,7 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     for o in outs:
         o["radii"].record_stream(main)
     vms = torch.stack([v.world_view_transform for v in views]).float()
-    reg = view_regularisers(pc, radii, vms, env_sh, rand["dirs"])
+    reg = view_regularisers(pc, radii, vms, env_sh, rand["dirs"], depth_on=it > REG_SKY_GAUSS_DEPTH_FROM_ITER)
     total = torch.stack(losses).sum() + reg.sum()
     total.backward()
     for s in streams:
@@ -603,11 +716,21 @@ def synthetic_relit_scene(P_fg, n_views, W, H, focal, device, seed=0, sky_frac=0
     g = torch.Generator().manual_seed(seed + 1)
     is_sky = torch.zeros(P, dtype=torch.bool)
     is_sky[P_fg:] = True
+    # the sky Gaussians on a shell of radius 30 (the far end of the depth range) around the
+    # origin, in the upper half of the frustum (COLMAP axes: -y is up), at the screen size
+    # they were drawn with
+    xyz, scales = gs["means3D"].clone(), gs["scales"].clone()
+    d = xyz[P_fg:].clone()
+    d[:, 1] = -d[:, 1].abs()
+    r = d.norm(dim=1, keepdim=True)
+    xyz[P_fg:] = 30.0 * d / r
+    scales[P_fg:] *= 30.0 / r
     logit = lambda x: torch.log(x / (1 - x))
-    scene = RelitScene(gs["means3D"], torch.log(gs["scales"]), gs["rotations"], logit(gs["opacities"]),
+    scene = RelitScene(xyz, torch.log(scales), gs["rotations"], logit(gs["opacities"]),
                        logit(torch.rand(P_fg, 3, generator=g) * 0.9 + 0.05),
                        logit(torch.rand(P_fg, 1, generator=g) * 0.9 + 0.05),
-                       logit(torch.rand(P_fg, 1, generator=g) * 0.9 + 0.05), is_sky, n_views, device, seed=seed)
+                       logit(torch.rand(P_fg, 1, generator=g) * 0.9 + 0.05), is_sky, n_views, device, seed=seed,
+                       sky_radius=30.0)
     views, gts = [], []
     for v in range(n_views):
         pos = (torch.rand(3, generator=g) - 0.5).numpy() * 0.4

@@ -156,12 +156,34 @@ def run_densify(rank, world, port, out_path):
         running = stats_run(rank, world)
         scene = densify_run(rank, world)
         fp = scene.fp
-        sums = dp.replica_checksums([fp.flat, fp.exp_avg, fp.exp_avg_sq, scene.is_sky.float()])
+        same = dp.replicas_identical([fp.flat, fp.exp_avg, fp.exp_avg_sq, scene.is_sky.to(torch.uint8),
+                                      torch.tensor([scene.P, fp.t])])
         if rank == 0:
             out = {k: v.numpy() for k, v in running.items()}
-            out.update(checksums=np.array(sums), P=np.array(scene.P), flat=fp.flat.numpy(), m=fp.exp_avg.numpy(),
+            out.update(identical=np.array(same), P=np.array(scene.P), flat=fp.flat.numpy(), m=fp.exp_avg.numpy(),
                        v=fp.exp_avg_sq.numpy(), is_sky=scene.is_sky.numpy(), t=np.array(fp.t))
             np.savez(out_path, **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def run_identical_probe(rank, world, port, out_path):
+    """replicas_identical on tensors that differ on rank 1 by one bit (-0.0 vs +0.0) and on
+    tensors that agree."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsr import dp
+        a = torch.zeros(5)
+        if rank == 1:
+            a[2] = -0.0
+        b = torch.arange(7, dtype=torch.float32)
+        c = torch.ones(3 + rank)  # shapes differ
+        flags = dp.replicas_identical([a, b, c])
+        if rank == 0:
+            np.save(out_path, np.array(flags))
         dist.barrier()
     finally:
         dist.destroy_process_group()

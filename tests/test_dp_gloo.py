@@ -73,8 +73,8 @@ def test_multi_step_stats_and_rank_consistent_densify(tmp_path):
     assert float(ref["denom"].max()) > dp_worker.N_STEPS  # several views per step, several steps
     assert np.array_equal(got["max_radii2D"], ref["max_radii2D"].numpy())
     np.testing.assert_allclose(got["xyz_gradient_accum"], ref["xyz_gradient_accum"].numpy(), rtol=1e-6, atol=1e-7)
-    sums = got["checksums"]
-    assert sums.shape[0] == 2 and np.array_equal(sums[0], sums[1]), sums
+    same = got["identical"]  # parameters, both moments, sky flags, (P, t): byte-equal on both ranks
+    assert same.shape == (5,) and same.all(), same
     P0 = dp_worker.small_scene().P
     assert int(got["P"]) != P0  # the surgery did something
     assert int(got["t"]) == 7
@@ -90,3 +90,10 @@ def test_densify_matches_sequential_with_same_seed():
     assert a.P != base.P
     # the Adam moments of appended rows are zero; kept rows carry theirs
     assert a.fp.exp_avg.abs().sum() > 0
+
+
+def test_replicas_identical_sees_one_bit(tmp_path):
+    """The replica check compares bytes: -0.0 against +0.0 and a shape difference are caught."""
+    out = str(tmp_path / "flags.npy")
+    mp.spawn(dp_worker.run_identical_probe, args=(2, free_port(), out), nprocs=2, join=True)
+    assert np.load(out).tolist() == [False, True, False]

@@ -58,7 +58,11 @@ def test_adam_rejects_bad_arguments():
 
 @pytest.mark.parametrize("nstreams", [1, 2])
 def test_train_step_matches_plain_autograd_and_adam(nstreams):
-    """... with the views on one stream or alternating over two (the bench's cfg4 layout)."""
+    """... with the views on one stream or alternating over two (the bench's cfg4 layout).
+    The two iterations are 15000 and 15001, the two sides of reg_normal_from_iter: the
+    normal-consistency term is off in the first and on in the second (train.py:89).  The
+    envlight term is unweighted (train.py:99-102); sky positions come from the (theta, phi)
+    leaves on the shell (gaussian_model.py:84-103)."""
     import types
 
     import torch.nn.functional as F
@@ -68,6 +72,7 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
     dev = torch.device("cuda")
     streams = None if nstreams == 1 else [torch.cuda.Stream() for _ in range(nstreams)]
     scene, views, gts = train.synthetic_relit_scene(3000, 2, 160, 96, 120.0, dev, seed=3)
+    scene.iteration = train.REG_NORMAL_FROM_ITER - 1
     fp = scene.fp
     gen = torch.Generator(device=dev)
     gen.manual_seed(11)
@@ -77,20 +82,22 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
                            eps=1e-15)
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
     bg = torch.zeros(3, device=dev)
-    for it in range(2):
+    for it in (train.REG_NORMAL_FROM_ITER, train.REG_NORMAL_FROM_ITER + 1):
+        lam_normal = 0.05 if it > 15000 else 0.0
         opt.zero_grad(set_to_none=True)
         rand = train.draw_step_randomness(2, dev, gen)
         env_sh, sky_sh = train.mlp_forward(leaves, leaves["embeddings"][[0, 1]], rand["dropout"])
         for vid, (view, gt) in enumerate(zip(views, gts)):
             pc = types.SimpleNamespace(
-                get_xyz=leaves["xyz"], get_scaling=torch.exp(leaves["scaling"]),
+                get_xyz=scene.get_xyz(leaves), get_scaling=torch.exp(leaves["scaling"]),
                 get_rotation=F.normalize(leaves["rotation"]), get_opacity=torch.sigmoid(leaves["opacity"]),
                 get_albedo=torch.sigmoid(leaves["albedo"]), get_roughness=torch.sigmoid(leaves["roughness"]),
                 get_metalness=torch.sigmoid(leaves["metalness"]), get_is_sky=scene.is_sky)
             light = relit_shade.EnvironmentLight(env_sh[vid] + rand["noise"][vid], sh_degree=4)
             out = relit.render(view, pc, light, sky_sh[vid:vid + 1], 1, pipe, bg, debug=False)
-            loss = train.view_loss(out, gt, view.sky_mask.expand_as(gt), view.occluders_mask.expand_as(gt))
-            loss = loss + 100.0 * train.envl_sh_loss(env_sh[vid:vid + 1], 4, dirs=rand["dirs"][vid])
+            loss = train.view_loss(out, gt, view.sky_mask.expand_as(gt), view.occluders_mask.expand_as(gt),
+                                   lambda_normal=lam_normal)
+            loss = loss + train.envl_sh_loss(env_sh[vid:vid + 1], 4, dirs=rand["dirs"][vid])
             loss = loss + 100.0 * train.min_scale_loss(out["radii"], pc)
             loss = loss + 0.05 * train.depth_loss_gaussians(pc, view, out["radii"] > 0)
             loss.backward(retain_graph=vid == 0)
@@ -98,12 +105,14 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
             p.grad /= len(views)
         opt.step()
         loss_flat = train.train_step(scene, views, [0, 1], gts, streams=streams, rand=rand)
+        assert scene.iteration == it
     torch.cuda.synchronize()
     assert torch.isfinite(loss_flat)
     for n in fp.names:
         e = rel_l2(fp.params[n].detach().cpu().numpy(), leaves[n].detach().cpu().numpy())
         assert e < 1e-4, (n, e)
-    for n in ("embeddings", "mlp.base.0.weight", "mlp.sh_envl_outlayer.bias", "mlp.sh_sky_outlayer.weight"):
+    for n in ("embeddings", "mlp.base.0.weight", "mlp.sh_envl_outlayer.bias", "mlp.sh_sky_outlayer.weight",
+              "sky_angles", "sky_radius"):
         assert float(fp.grad[fp.offsets[fp.names.index(n)]:fp.ends[fp.names.index(n)]].abs().sum()) > 0, n
     assert float(scene.stats["denom"].max()) == 4.0  # 2 views x 2 iterations
     assert float(scene.stats["xyz_gradient_accum"].sum()) > 0

@@ -99,9 +99,12 @@ def test_min_scale_and_sky_depth_losses(gold):
     assert rel_l2(dx.numpy(), gold["reg/d_xyz"]) < 1e-5
 
 
-def test_view_regularisers_batched_equal_single_view():
+@pytest.mark.parametrize("depth_on", [True, False])
+def test_view_regularisers_batched_equal_single_view(depth_on):
     """view_regularisers (all views at once, as train_step runs them) equals the single-view
-    reference functions summed with the configured weights."""
+    reference functions summed as train.py:99-118 adds them: envl_sh_loss unweighted
+    (lambda_envlight is a switch), lambda_scale x min_scale_loss, lambda_sky_gauss x
+    depth_loss_gaussians only past reg_sky_gauss_depth_from_iter."""
     from gsr import train
     g = torch.Generator().manual_seed(3)
     P, V = 500, 3
@@ -115,14 +118,17 @@ def test_view_regularisers_batched_equal_single_view():
     vms[:, :3, :3] = torch.linalg.qr(torch.randn(V, 3, 3, generator=g))[0]
     env = (torch.randn(V, 25, 3, generator=g) * 0.8).requires_grad_(True)
     dirs = torch.rand(V, 10, 3, generator=g) * 2 - 1
-    got = train.view_regularisers(pc, radii, vms, env, dirs)
+    got = train.view_regularisers(pc, radii, vms, env, dirs, depth_on=depth_on)
+    assert train.LAMBDA_ENVLIGHT > 0 and train.LAMBDA_SCALE > 0 and train.LAMBDA_SKY_GAUSS > 0
     want = torch.stack([
-        train.LAMBDA_ENVLIGHT * train.envl_sh_loss(env[v:v + 1], 4, dirs=dirs[v])
+        train.envl_sh_loss(env[v:v + 1], 4, dirs=dirs[v])
         + train.LAMBDA_SCALE * train.min_scale_loss(radii[v], pc)
-        + train.LAMBDA_SKY_GAUSS * train.depth_loss_gaussians(pc, types.SimpleNamespace(world_view_transform=vms[v]),
-                                                              radii[v] > 0) for v in range(V)])
+        + (train.LAMBDA_SKY_GAUSS * train.depth_loss_gaussians(
+            pc, types.SimpleNamespace(world_view_transform=vms[v]), radii[v] > 0) if depth_on else 0.0)
+        for v in range(V)])
     assert torch.allclose(got, want, rtol=1e-5, atol=1e-7)
-    ga = torch.autograd.grad(got.sum(), [scaling, xyz, env])
-    gb = torch.autograd.grad(want.sum(), [scaling, xyz, env])
+    ins = [scaling, xyz, env] if depth_on else [scaling, env]  # xyz enters only the depth term
+    ga = torch.autograd.grad(got.sum(), ins)
+    gb = torch.autograd.grad(want.sum(), ins)
     for a, b in zip(ga, gb):
         assert rel_l2(a.numpy(), b.numpy()) < 1e-5

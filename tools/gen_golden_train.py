@@ -13,6 +13,17 @@ Pinned by these fixtures:
                           from the same seeded CPU generator and stored)
   min_scale_loss          utils/loss_utils.py:210-220
   depth_loss_gaussians    utils/loss_utils.py:140-148 (+ GaussianModel.get_depth :125-130)
+
+and tests/golden/train_sky.npz:
+  get_xyz / get_sky_xyz / get_sky_angles   scene/gaussian_model.py:84-103,159-169 (sky
+                          Gaussians as clamped (theta, phi) on a shell of learnable radius,
+                          interleaved with the foreground rows) + autograd gradients
+  cartesian_to_polar_coord utils/general_utils.py:295-299 (default and explicit radius)
+  densify_and_prune       scene/gaussian_model.py:438-625 on a GaussianModel with an Adam
+                          state (one torch.optim.Adam step first): clone, split (sky samples
+                          projected onto the shell, angles back with the default radius),
+                          prune; every group's rows and moments before and after, under a
+                          fixed torch.manual_seed for the split's torch.normal
 """
 import os
 import sys
@@ -108,6 +119,104 @@ def main():
                "reg/depth_loss": np.array(float(dl), np.float32), "reg/d_xyz": d_xyz.numpy()})
     np.savez_compressed(os.path.join(OUT, "train_step.npz"), **fx)
     print("wrote", os.path.join(OUT, "train_step.npz"))
+    sky_and_densify(GaussianModel)
+
+
+GROUPS = ("xyz", "albedo", "opacity", "scaling", "rotation", "roughness", "metalness", "sky_radius", "sky_angles")
+
+
+def sky_and_densify(GaussianModel):
+    from torch import nn
+
+    from utils import general_utils as gu
+    rng = np.random.default_rng(777)
+    fx = {}
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32)
+
+    # ---------------- get_xyz with sky angles (interleaved rows, out-of-range angles) -----
+    P, n_sky = 240, 60
+    is_sky = np.zeros((P, 1), bool)
+    is_sky[rng.choice(P, n_sky, replace=False)] = True
+    gm = GaussianModel()
+    gm._xyz = nn.Parameter(t(rng.normal(0, 2, (P - n_sky, 3))))
+    ang = np.stack([rng.uniform(-0.3, np.pi / 2 + 0.3, n_sky), rng.uniform(-np.pi / 2 - 0.3, np.pi / 2 + 0.3, n_sky)], 1)
+    gm._sky_angles = nn.Parameter(t(ang))
+    gm._sky_radius = nn.Parameter(torch.tensor(7.5))
+    gm._sky_gauss_center = t([[0.3, -0.2, 1.0]])
+    gm._is_sky = torch.tensor(is_sky)
+    xyz = gm.get_xyz
+    g = t(rng.normal(0, 1, (P, 3)))
+    d_xyz, d_ang, d_rad = torch.autograd.grad(xyz, [gm._xyz, gm._sky_angles, gm._sky_radius], g)
+    fx.update({"sky/is_sky": is_sky, "sky/xyz_fg": gm._xyz.detach().numpy(), "sky/angles": ang.astype(np.float32),
+               "sky/radius": np.float32(7.5), "sky/center": np.float32([0.3, -0.2, 1.0]),
+               "sky/get_xyz": xyz.detach().numpy(), "sky/g": g.numpy(), "sky/d_xyz_fg": d_xyz.numpy(),
+               "sky/d_angles": d_ang.numpy(), "sky/d_radius": np.float32(d_rad)})
+    pts = t(rng.normal(0, 5, (50, 3)))
+    c = t([0.3, -0.2, 1.0])
+    fx["c2p/pts"] = pts.numpy()
+    fx["c2p/center"] = c.numpy()
+    fx["c2p/default_radius"] = gu.cartesian_to_polar_coord(pts, c).numpy()
+    fx["c2p/radius_7_5"] = gu.cartesian_to_polar_coord(pts, c, 7.5).numpy()
+
+    # ---------------- densify_and_prune with an Adam state ---------------------------------
+    P, n_sky = 400, 80
+    is_sky = np.zeros((P, 1), bool)
+    is_sky[rng.choice(P, n_sky, replace=False)] = True
+    n_fg = P - n_sky
+    gm = GaussianModel()
+    gm.percent_dense = 0.01
+    center = t([[0.1, 0.0, 0.5]])
+    radius = 6.0
+    sky_dirs = rng.normal(0, 1, (n_sky, 3))
+    sky_dirs[:, 1] = -np.abs(sky_dirs[:, 1])
+    sky_dirs[:, 2] = np.abs(sky_dirs[:, 2])
+    sky_pts = center + radius * t(sky_dirs / np.linalg.norm(sky_dirs, axis=1, keepdims=True))
+    gm._xyz = nn.Parameter(t(rng.normal(0, 1.5, (n_fg, 3))))
+    gm._sky_gauss_center = center
+    gm._sky_radius = nn.Parameter(torch.tensor(radius))
+    gm._sky_angles = nn.Parameter(gu.cartesian_to_polar_coord(sky_pts, center.squeeze(), gm._sky_radius).detach())
+    # scales straddling percent_dense * extent (extent 4 -> 0.04): clones below, splits above
+    gm._scaling = nn.Parameter(t(np.log(np.exp(rng.normal(np.log(0.04), 0.8, (P, 3))))))
+    gm._rotation = nn.Parameter(t(rng.normal(0, 1, (P, 4))))
+    gm._opacity = nn.Parameter(t(rng.normal(0, 2, (P, 1))))
+    gm._albedo = nn.Parameter(t(rng.normal(0, 1, (n_fg, 3))))
+    gm._roughness = nn.Parameter(t(rng.normal(0, 1, (n_fg, 1))))
+    gm._metalness = nn.Parameter(t(rng.normal(0, 1, (n_fg, 1))))
+    gm._is_sky = torch.tensor(is_sky)
+    params = {n: getattr(gm, "_" + n) for n in GROUPS}
+    lrs = {"xyz": 1e-3, "albedo": 2.5e-3, "opacity": 0.05, "scaling": 1e-3, "rotation": 1e-3, "roughness": 2e-4,
+           "metalness": 2e-4, "sky_radius": 1e-4, "sky_angles": 1e-3}
+    gm.optimizer = torch.optim.Adam([{"params": [params[n]], "lr": lrs[n], "name": n} for n in GROUPS], lr=0.0,
+                                    eps=1e-15)
+    for n in GROUPS:  # one step with fixed gradients: every group gets an Adam state
+        params[n].grad = t(rng.normal(0, 1e-2, tuple(params[n].shape)))
+    gm.optimizer.step()
+    accum = np.abs(rng.normal(0, 1, (P, 1))) * 2e-4
+    denom = rng.integers(0, 3, (P, 1)).astype(np.float32)
+    gm.xyz_gradient_accum = t(accum)
+    gm.denom = t(denom)
+    gm.max_radii2D = t(rng.integers(0, 30, P))
+    for n in GROUPS:
+        st = gm.optimizer.state[params[n]]
+        fx[f"dens/before/{n}"] = params[n].detach().numpy()
+        fx[f"dens/before/m/{n}"] = st["exp_avg"].numpy()
+        fx[f"dens/before/v/{n}"] = st["exp_avg_sq"].numpy()
+    fx.update({"dens/before/is_sky": is_sky, "dens/center": center.numpy().reshape(3),
+               "dens/accum": accum.astype(np.float32), "dens/denom": denom,
+               "dens/max_radii2D": gm.max_radii2D.numpy(), "dens/seed": np.int64(2024),
+               "dens/args": np.float32([1e-4, 0.1, 4.0, 20.0])})  # max_grad, min_opacity, extent, max_screen_size
+    torch.manual_seed(2024)
+    gm.densify_and_prune(1e-4, 0.1, 4.0, 20.0, None)
+    for n in GROUPS:
+        p = gm.optimizer.param_groups[[gr["name"] for gr in gm.optimizer.param_groups].index(n)]["params"][0]
+        st = gm.optimizer.state[p]
+        fx[f"dens/after/{n}"] = p.detach().numpy()
+        fx[f"dens/after/m/{n}"] = st["exp_avg"].numpy()
+        fx[f"dens/after/v/{n}"] = st["exp_avg_sq"].numpy()
+    fx["dens/after/is_sky"] = gm._is_sky.numpy()
+    fx["dens/after/get_xyz"] = gm.get_xyz.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "train_sky.npz"), **fx)
+    print("wrote", os.path.join(OUT, "train_sky.npz"), {k: v.shape for k, v in fx.items() if k.startswith("dens/a")})
 
 
 if __name__ == "__main__":

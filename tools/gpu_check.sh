@@ -14,6 +14,6 @@ rc=$?; tail -1 gpurun_out/b.log | cut -c1-600; [ $rc -eq 0 ] || exit $rc
 export TMPDIR=/tmp
 rm -rf gpurun_out/tl
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -- python3 bench.py --steps 10 --warmup 3 \
-  --no-minibatch --no-refalgo --no-cpu-baseline > gpurun_out/tl.log 2>&1
+  --no-minibatch --no-refalgo --no-cpu-baseline --no-train > gpurun_out/tl.log 2>&1
 rc=$?; [ $rc -eq 0 ] || exit $rc
 python3 tools/timeline.py gpurun_out/tl > gpurun_out/timeline.txt; cat gpurun_out/timeline.txt

@@ -12,7 +12,7 @@ for CT in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_B
           "SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $CT --kernel-include-regex "$KRE" --output-format csv \
-    -d "$R/gpurun_out/${TAG}_$i" -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline \
+    -d "$R/gpurun_out/${TAG}_$i" -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-train \
     > "$R/gpurun_out/${TAG}_$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 "$R/gpurun_out/${TAG}_$i.log"; exit $rc; }
 done
