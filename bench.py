@@ -177,7 +177,7 @@ def bench_relight(args, dev):
 
     import diff_gaussian_rasterization as dgr
     import relit_shade
-    from gsr import relit, scenes
+    from gsr import relit, scenes, shrot
     stress = args.config == "cfg5-relit"  # cfg5: 5M Gaussians at 3840x2160, relit render with backward
     P_fg = args.P or (4_545_455 if stress else 1_000_000)
     P = P_fg + P_fg // 10  # + 10 % sky Gaussians
@@ -191,9 +191,13 @@ def bench_relight(args, dev):
               "metalness": torch.rand(P_fg, 1, generator=gen)}
     leaves = {k: v.to(dev) for k, v in leaves.items()}
     scaling = gs["scales"].to(dev)
-    base = (torch.randn(25, 3, generator=gen) * 0.3).to(dev)
+    base = torch.randn(25, 3, generator=gen) * 0.3
     base[0] = 1.0
-    sky_sh = (torch.randn(1, 4, 3, generator=gen) * 0.3).to(dev)
+    # the reference's relight sequence (relit_novel_view.py:131-152): the environment SH
+    # rotated about y by 30 angles over [0, 6.28], one view per angle, fix_sky=True with a
+    # zero sky SH
+    bases = [b.to(dev) for b in shrot.rotated_sequence(base)]
+    sky_sh = torch.zeros(1, 4, 3, device=dev)
     view = types.SimpleNamespace(image_width=W, image_height=H, FoVx=cam.FoVx, FoVy=cam.FoVy,
                                  world_view_transform=cam.world_view_transform.to(dev),
                                  full_proj_transform=cam.full_proj_transform.to(dev),
@@ -213,16 +217,18 @@ def bench_relight(args, dev):
     counter = [0]
 
     def step(fn):
-        s = rstreams[counter[0] % len(rstreams)]
+        k = counter[0]
+        s = rstreams[k % len(rstreams)]
         counter[0] += 1
         s.wait_stream(main_s)
         with torch.cuda.stream(s):
-            t = {k: v.detach().requires_grad_(True) for k, v in leaves.items()}
-            light = relit_shade.EnvironmentLight(base.detach().clone().requires_grad_(True), sh_degree=4)
+            t = {k_: v.detach().requires_grad_(True) for k_, v in leaves.items()}
+            light = relit_shade.EnvironmentLight(bases[k % len(bases)].detach().clone().requires_grad_(True),
+                                                 sh_degree=4)
             pc = _RelitModel(get_xyz=t["xyz"], get_rotation=t["rotation"], get_scaling=scaling,
                              get_opacity=t["opacity"], get_is_sky=is_sky_dev, get_albedo=t["albedo"],
                              get_roughness=t["roughness"], get_metalness=t["metalness"])
-            out = fn(view, pc, light, sky_sh, 1, pipe, bg, debug=False)
+            out = fn(view, pc, light, sky_sh, 1, pipe, bg, debug=False, fix_sky=True)
             loss = sum((out[k] * dweights[k]).sum() for k in names)
             loss.backward()
 
@@ -248,7 +254,8 @@ def bench_relight(args, dev):
         "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{'cfg5 (relit stress)' if stress else 'cfg3'}: {P_fg} foreground + {P - P_fg} sky "
-                               f"Gaussians, {W}x{H}, env SH deg 4, sky SH deg 1, debug=False", "gaussians": P,
+                               f"Gaussians, {W}x{H}, env SH deg 4 rotated about y over the reference's 30 relight "
+                               "angles (one per view), fix_sky=True, debug=False", "gaussians": P,
                    "width": W, "height": H},
         "mpix_per_s": round(W * H / (ms * 1e-3) / 1e6, 3),
         "implementation": f"gsr.relit.render: fused relit features + one 14-channel composite; views on {nsr} "

@@ -238,21 +238,28 @@ thread_local Scratch g_scratch2;  // list materialisation, debug checks
 // Wait until the device has stored the four totals of call `seq` (frame_totals: each word is
 // value << 16 | seq mod 2^16) and unpack them into out[0..3].  Spins on the coherent
 // host-mapped words; every 256 polls the stream is queried, so a failed or finished stream
-// ends the wait (a finished stream must have stored them).
+// ends the wait (a finished stream must have stored them: the words are read once more after
+// the query, since they may have landed between the last read and the query).
 int wait_totals(const unsigned long long* p, unsigned long long seq, hipStream_t s, unsigned long long* out) {
     const unsigned long long tag = seq & 0xFFFFull;
-    for (unsigned it = 1;; it++) {
+    auto read = [&]() {
         bool ok = true;
         for (int k = 0; k < 4; k++) {
             const unsigned long long w = __atomic_load_n(p + k, __ATOMIC_ACQUIRE);
             ok = ok && (w & 0xFFFFull) == tag;
             out[k] = w >> 16;
         }
-        if (ok) return 0;
+        return ok;
+    };
+    for (unsigned it = 1;; it++) {
+        if (read()) return 0;
         if ((it & 255u) == 0) {
             const hipError_t q = hipStreamQuery(s);
             if (q != hipSuccess && q != hipErrorNotReady) return gsr_fail_hip(q, __LINE__);
-            if (q == hipSuccess && (it & 511u) == 0) return gsr_fail_hip(hipErrorUnknown, __LINE__);  // done, no totals
+            if (q == hipSuccess) {
+                if (read()) return 0;
+                return gsr_fail_hip(hipErrorUnknown, __LINE__);  // the stream is done and stored no totals
+            }
         }
 #if defined(__x86_64__)
         __builtin_ia32_pause();
@@ -823,10 +830,11 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
         gsr::launch_recolor(P, src_radii, reinterpret_cast<const gsr::Rec*>(src + gl.rec), colors_precomp,
                             at<gsr::Rec>(geom, gl.rec), radii, s);
     }
-    if (det_on()) {  // the deterministic backward's gather reads this call's rects and depth keys
-        HIP_OK(hipMemcpyAsync(geom + gl.depth_key, src + gl.depth_key, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
-        HIP_OK(hipMemcpyAsync(geom + gl.rect, src + gl.rect, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
-    }
+    // the deterministic backward's gather reads this call's rects and depth keys; copied
+    // always (12 B per Gaussian), so deterministic mode may be switched on between a cached
+    // forward and its backward
+    HIP_OK(hipMemcpyAsync(geom + gl.depth_key, src + gl.depth_key, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
+    HIP_OK(hipMemcpyAsync(geom + gl.rect, src + gl.rect, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
     GSR_LAUNCH_CHECK();
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
     gsr::RenderFwdArgs ra;  // with R == 0 every super-tile list is empty: background everywhere

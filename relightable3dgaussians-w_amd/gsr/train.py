@@ -610,7 +610,7 @@ _BLACK = {}
 
 def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[torch.Tensor], group=None,
                world: int = 1, bg=None, streams=None, rand: Dict[str, torch.Tensor] = None,
-               iteration: int = None) -> torch.Tensor:
+               iteration: int = None, render_fn=None, optimizer_step: bool = True) -> torch.Tensor:
     """One data-parallel iteration: this rank's views rendered and back-propagated, one
     all-reduce of the flat gradient, the densification statistics reduced, one fused Adam
     step with the mean gradient over all ranks' views.  ``streams``: HIP streams the views
@@ -621,7 +621,10 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     ``iteration``: the reference's loop counter (default: the scene's last + 1), which
     switches the normal term on past reg_normal_from_iter and the sky-depth term past
     reg_sky_gauss_depth_from_iter.  Returns this rank's summed loss as a device scalar (no
-    host synchronisation inside the step).
+    host synchronisation inside the step).  ``render_fn``: render()'s implementation (default
+    the fused gsr.relit.render; gsr.relit.render_calls is render()'s own call sequence).
+    ``optimizer_step=False`` stops after the gradient exchange (fp.grad holds the summed
+    gradient; tests).
 
     Per view (train.py:66-120): envlight_sh, sky_sh = MLPNet(embedding); render() with
     envlight_sh + noise; loss = reconstruction + sky-BRDF (+ 0.05 normal once iteration >
@@ -663,7 +666,7 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         s.wait_stream(main)
         with torch.cuda.stream(s):
             light = relit_shade.EnvironmentLight(env_lit[i], sh_degree=4)
-            out = relit.render(view, pc, light, sky_sh[i:i + 1], 1, pipe, bg, debug=False)
+            out = (render_fn or relit.render)(view, pc, light, sky_sh[i:i + 1], 1, pipe, bg, debug=False)
             losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask, LAMBDA_DSSIM, LAMBDA_SKY_BRDF,
                                     lam_normal))
         outs.append(out)
@@ -698,7 +701,8 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=group)
         n_views *= world
     scene.step_stats.commit(scene.stats, group=group, world=world)
-    fp.step(grad_scale=1.0 / n_views)
+    if optimizer_step:
+        fp.step(grad_scale=1.0 / n_views)
     return total.detach()
 
 

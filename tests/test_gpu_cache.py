@@ -130,3 +130,39 @@ def test_cache_is_keyed_on_the_stream():
     assert cache.hits == h0 + 1
     torch.cuda.synchronize()
     assert torch.equal(a, b) and torch.equal(a, c) and torch.equal(a, d)
+
+
+def test_deterministic_backward_after_cached_forward():
+    """deterministic mode switched on between cached forwards (gsr_forward_reuse)
+    and their backward: the gather needs every call's rects and depth keys, which the reuse
+    path copies whatever the mode at forward time.  The gradients match the atomic backward
+    of the same calls (1e-5, summation order)."""
+    from gsr import _lib
+    dgr, g, settings = _setup(P=3000, W=128, H=96)
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    colors = [torch.rand(g["means3D"].shape[0], 3, device="cuda", generator=gen) for _ in range(3)]
+    bgs = [(0.0, 0.0, 0.0)] * 3
+
+    def run(det_at_backward):
+        dgr.geometry_cache(True)
+        means3D = g["means3D"].clone().requires_grad_(True)
+        cols = [c.clone().requires_grad_(True) for c in colors]
+        s = settings(bgs[0])
+        imgs = [dgr.GaussianRasterizer(s)(means3D=means3D, means2D=torch.zeros_like(means3D), opacities=g["opacities"],
+                                          colors_precomp=c, scales=g["scales"], rotations=g["rotations"])[0]
+                for c in cols]
+        w = torch.Generator(device="cuda").manual_seed(6)
+        loss = sum((torch.randn(i.shape, device="cuda", generator=w) * i).sum() for i in imgs)
+        _lib.set_deterministic(det_at_backward)
+        try:
+            loss.backward()
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_deterministic(False)
+        return [means3D.grad.cpu()] + [c.grad.cpu() for c in cols]
+
+    a, d = run(False), run(True)
+    for x, y in zip(a, d):
+        assert torch.isfinite(y).all()
+        e = torch.linalg.norm((x - y).double()) / torch.linalg.norm(x.double()).clamp_min(1e-30)
+        assert e < 1e-5, e

@@ -249,22 +249,15 @@ def test_cfg1_exact_size_forward_backward():
         assert rel_l2(mine.detach().cpu().numpy().reshape(r.shape), r) <= 1e-4, n
 
 
-def test_cfg5_relit_render_fused_matches_calls():
-    """cfg5's relight render with backward at 3840x2160 (400k foreground + 40k sky
-    Gaussians): the fused gsr.relit.render (14-channel composite at 4K) against render()'s
-    own call sequence on the drop-in rasterizer, every image and every parameter gradient."""
+def _fused_vs_calls(scene, view, light_leaves, bg, fix_sky=False):
+    """Run the fused gsr.relit.render and render()'s own call sequence (gsr.relit.render_calls)
+    on the same scene and light, a random-weighted loss over every image, backward.  Returns
+    the per-image relative errors, the per-parameter gradient errors and the same gradient
+    errors with normal_ref out of the loss, plus the fused outputs."""
     import types
     import relit_shade
-    from gsr import relit, train
-    scene, views, _ = train.synthetic_relit_scene(400_000, 1, 3840, 2160, 2800.0, "cuda", seed=2)
-    view = views[0]
+    from gsr import relit
     pipe = types.SimpleNamespace(compute_cov3D_python=False)
-    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
-    g = torch.Generator().manual_seed(2)  # the lighting: env SH deg 4 (DC 1) and sky SH deg 1
-    env0 = torch.randn(25, 3, generator=g) * 0.3
-    env0[0] = 1.0
-    sky0 = torch.randn(1, 4, 3, generator=g) * 0.3
-    light_leaves = {"env_sh": env0.cuda().requires_grad_(True), "sky_sh": sky0.cuda().requires_grad_(True)}
 
     def run(fn, skip=()):
         scene.fp.zero_grad()
@@ -272,13 +265,15 @@ def test_cfg5_relit_render_fused_matches_calls():
             t.grad = None
         pc = scene.model()
         light = relit_shade.EnvironmentLight(light_leaves["env_sh"], sh_degree=4)
-        out = fn(view, pc, light, light_leaves["sky_sh"], 1, pipe, bg, debug=False)
+        out = fn(view, pc, light, light_leaves["sky_sh"], 1, pipe, bg, debug=False, fix_sky=fix_sky)
         keys = sorted(k for k in out if k not in ("viewspace_points", "visibility_filter", "radii"))
         gen = torch.Generator(device="cuda").manual_seed(6)
         loss = sum((out[k] * torch.randn(out[k].shape, device="cuda", generator=gen)).sum()
                    for k in keys if k not in skip)
         loss.backward()
-        grads = torch.cat([scene.fp.grad] + [light_leaves[k].grad.reshape(-1) for k in ("env_sh", "sky_sh")])
+        lg = [torch.zeros_like(light_leaves[k]).reshape(-1) if light_leaves[k].grad is None
+              else light_leaves[k].grad.reshape(-1) for k in ("env_sh", "sky_sh")]
+        grads = torch.cat([scene.fp.grad] + lg)
         return {k: out[k].detach() for k in keys}, out["radii"], grads, out["viewspace_points"].grad.clone()
 
     def grad_errs(g_f, g_r):
@@ -304,6 +299,84 @@ def test_cfg5_relit_render_fused_matches_calls():
     errs2 = grad_errs(g_f2, g_r2)
     errs2["means2D"] = float(torch.linalg.norm((m_f2 - m_r2).double()) / torch.linalg.norm(m_r2.double()))
     print("images", img_errs, "\ngradients", errs, "\ngradients without normal_ref", errs2)
+    return img_errs, errs, errs2, o_f
+
+
+def test_cfg3_relit_render_at_size():
+    """cfg3 at its size (1M foreground + 100k sky Gaussians, 1920x1080) under the
+    reference's relight sequence (relit_novel_view.py:131-152: the env SH rotated about y,
+    fix_sky=True, zero sky SH; view 7 of the 30 angles):
+      * the fused render's image channel equals one drop-in rasterizer call with its relit
+        colours, bit for bit, and that call matches the C oracle on 32 sampled tiles (colour
+        1e-6, n_contrib exact, final T 1e-6) from its own lists and records;
+      * every image and gradient of the fused render matches render()'s call sequence
+        (images 1e-5, gradients 1e-4)."""
+    import math
+    import types
+
+    import relit_shade
+    from gsr import shrot, train
+    scene, views, _ = train.synthetic_relit_scene(1_000_000, 1, 1920, 1080, 1400.0, "cuda", seed=4)
+    assert scene.P == 1_100_000
+    view = views[0]
+    g = torch.Generator().manual_seed(3)
+    env0 = torch.randn(25, 3, generator=g) * 0.3
+    env0[0] = 1.0
+    env = shrot.rotate_sh(env0, shrot.rotation_y(float(shrot.reference_angles()[7])))
+    light_leaves = {"env_sh": env.cuda().requires_grad_(True), "sky_sh": torch.zeros(1, 4, 3, device="cuda")}
+    bg = torch.zeros(3, device="cuda")
+    W, H = 1920, 1080
+    # the image channel against one drop-in call and the oracle
+    with torch.no_grad():
+        pc = scene.model()
+        feat = relit_shade.relit_features(pc.get_xyz, pc.get_rotation, pc.get_scaling, pc.get_is_sky.squeeze(),
+                                          pc.get_albedo, pc.get_roughness, pc.get_metalness,
+                                          relit_shade.EnvironmentLight(light_leaves["env_sh"], sh_degree=4),
+                                          view.camera_center, view.world_view_transform, light_leaves["sky_sh"], 1,
+                                          True, True)
+    cam = types.SimpleNamespace(image_width=W, image_height=H, tanfovx=math.tan(view.FoVx * 0.5),
+                                tanfovy=math.tan(view.FoVy * 0.5), world_view_transform=view.world_view_transform,
+                                full_proj_transform=view.full_proj_transform, camera_center=view.camera_center)
+    gs = {"means3D": pc.get_xyz.float().contiguous(), "colors": feat[:, 0:3].contiguous(),
+          "opacities": pc.get_opacity.contiguous(), "scales": pc.get_scaling.contiguous(),
+          "rotations": pc.get_rotation.contiguous()}
+    st = run_gpu(cam, gs, mode="colors")
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    tiles = _sample_tiles(gx, gy, seed=8)
+    rec = st["rec"]
+    out, fT, nc = orc.render_fwd(st["ranges"], st["point_list"], rec[:, 0:2], rec[:, 6:9], rec[:, 2:6],
+                                 np.zeros(3, np.float32), W, H, tiles=tiles)
+    m = _tile_mask(tiles, gx, W, H)
+    color = st["color"].cpu().numpy()
+    assert np.abs(out[:, m]).max() > 0.05  # the sampled tiles are lit
+    assert rel_l2(color[:, m], out[:, m]) <= 1e-6
+    np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
+    assert np.abs(color[:, m] - out[:, m]).max() <= 1e-6
+    assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
+    del st
+    img_errs, errs, errs2, o_f = _fused_vs_calls(scene, view, light_leaves, bg, fix_sky=True)
+    assert torch.equal(o_f["render"], torch.as_tensor(color, device="cuda"))
+    for k, e in img_errs.items():
+        assert e < 1e-5, (k, e)
+    for k, e in errs.items():
+        assert e < 1e-4, (k, e)
+    assert "sky_sh" not in errs  # fix_sky: the sky SH gets no gradient
+
+
+def test_cfg5_relit_render_fused_matches_calls():
+    """cfg5's relight render with backward at 3840x2160 (400k foreground + 40k sky
+    Gaussians): the fused gsr.relit.render (14-channel composite at 4K) against render()'s
+    own call sequence on the drop-in rasterizer, every image and every parameter gradient."""
+    from gsr import train
+    scene, views, _ = train.synthetic_relit_scene(400_000, 1, 3840, 2160, 2800.0, "cuda", seed=2)
+    view = views[0]
+    bg = torch.tensor([0.1, 0.2, 0.3], device="cuda")
+    g = torch.Generator().manual_seed(2)  # the lighting: env SH deg 4 (DC 1) and sky SH deg 1
+    env0 = torch.randn(25, 3, generator=g) * 0.3
+    env0[0] = 1.0
+    sky0 = torch.randn(1, 4, 3, generator=g) * 0.3
+    light_leaves = {"env_sh": env0.cuda().requires_grad_(True), "sky_sh": sky0.cuda().requires_grad_(True)}
+    img_errs, errs, errs2, _ = _fused_vs_calls(scene, view, light_leaves, bg)
     for k, e in img_errs.items():
         # normal_ref is a cross product of one-pixel depth differences: at 4K those are ~1e-4
         # of the depth, so float rounding of the back-projection (the epilogue kernel vs

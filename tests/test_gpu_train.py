@@ -116,3 +116,47 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
         assert float(fp.grad[fp.offsets[fp.names.index(n)]:fp.ends[fp.names.index(n)]].abs().sum()) > 0, n
     assert float(scene.stats["denom"].max()) == 4.0  # 2 views x 2 iterations
     assert float(scene.stats["xyz_gradient_accum"].sum()) > 0
+
+
+def test_full_size_step_properties():
+    """cfg4's iteration at its full size (1.5M Gaussians: 1.36M foreground + 10 % sky on the
+    shell, 1920x1080, 4 views, every loss term on): the summed gradient of the fused 4-view
+    step equals the sum of four single-view steps through render()'s own call sequence on the
+    drop-in rasterizer (gsr.relit.render_calls), segment by segment; everything finite; the
+    Adam step moves every Gaussian group and leaves the parameters finite."""
+    from gsr import relit, train
+    dev = torch.device("cuda")
+    scene, views, gts = train.synthetic_relit_scene(1_363_637, 4, 1920, 1080, 1400.0, dev, seed=0)
+    assert scene.P == 1_500_000
+    fp = scene.fp
+    it = train.REG_NORMAL_FROM_ITER + 1
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    rand = train.draw_step_randomness(4, dev, gen)
+    train.train_step(scene, views, [0, 1, 2, 3], gts, rand=rand, iteration=it, optimizer_step=False)
+    g4 = fp.grad.clone()
+    acc = torch.zeros_like(g4)
+    for v in range(4):
+        r1 = {k: t[v:v + 1] for k, t in rand.items()}
+        train.train_step(scene, [views[v]], [v], [gts[v]], rand=r1, iteration=it, render_fn=relit.render_calls,
+                         optimizer_step=False)
+        acc += fp.grad
+    torch.cuda.synchronize()
+    assert torch.isfinite(g4).all() and torch.isfinite(acc).all()
+    errs = {}
+    for name, off, end in zip(fp.names, fp.offsets, fp.ends):
+        a, b = g4[off:end].double(), acc[off:end].double()
+        if b.any():
+            errs[name] = float(torch.linalg.norm(a - b) / torch.linalg.norm(b))
+    print("fused 4-view step vs 4 render_calls steps:", errs)
+    assert set(errs) >= {"xyz", "opacity", "scaling", "rotation", "albedo", "roughness", "metalness", "sky_angles",
+                         "sky_radius", "embeddings"}
+    for name, e in errs.items():
+        assert e < 2e-4, (name, e)
+    before = fp.flat.clone()
+    train.train_step(scene, views, [0, 1, 2, 3], gts, rand=rand, iteration=it)
+    torch.cuda.synchronize()
+    assert torch.isfinite(fp.flat).all()
+    for name, off, end in zip(fp.names, fp.offsets, fp.ends):
+        if name in ("xyz", "opacity", "scaling", "rotation", "albedo", "sky_angles"):
+            assert (fp.flat[off:end] != before[off:end]).float().mean() > 0.5, name
