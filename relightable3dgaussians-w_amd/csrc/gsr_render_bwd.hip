@@ -19,6 +19,7 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
+
 namespace gsr {
 
 #ifdef GSR_RENDER_STATS
@@ -231,8 +232,12 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
 // whole tile.
+#ifndef GSR_BWD_WAVES
+#define GSR_BWD_WAVES 4
+#endif
 template <bool DET>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 4))) k_render_bwd(RenderBwdArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
+k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row

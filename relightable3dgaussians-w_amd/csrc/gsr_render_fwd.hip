@@ -17,6 +17,10 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
+#ifndef GSR_FWD_WAVES
+#define GSR_FWD_WAVES 6
+#endif
+
 namespace gsr {
 
 #ifdef GSR_RENDER_STATS
@@ -202,7 +206,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
 // whole tile.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(6, 6))) k_render_fwd(RenderFwdArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, GSR_FWD_WAVES)))
+k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;

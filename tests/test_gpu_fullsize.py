@@ -310,7 +310,7 @@ def test_cfg3_relit_render_at_size():
         colours, bit for bit, and that call matches the C oracle on 32 sampled tiles (colour
         1e-6, n_contrib exact, final T 1e-6) from its own lists and records;
       * every image and gradient of the fused render matches render()'s call sequence
-        (images 1e-5, gradients 1e-4)."""
+        (images 1e-5, normal_ref 1e-4; gradients 1e-4, 2e-4 through normal_ref)."""
     import math
     import types
 
@@ -357,9 +357,13 @@ def test_cfg3_relit_render_at_size():
     img_errs, errs, errs2, o_f = _fused_vs_calls(scene, view, light_leaves, bg, fix_sky=True)
     assert torch.equal(o_f["render"], torch.as_tensor(color, device="cuda"))
     for k, e in img_errs.items():
-        assert e < 1e-5, (k, e)
-    for k, e in errs.items():
-        assert e < 1e-4, (k, e)
+        # normal_ref: central differences of the depth image amplify float rounding (the
+        # epilogue kernel vs PyTorch's back-projection; measured 2.5e-5 at 1080p, 4.3e-5 at 4K)
+        assert e < (1e-4 if k == "normal_ref" else 1e-5), (k, e)
+    for k, e in errs2.items():  # without normal_ref in the loss: measured <= 7.3e-6
+        assert e < 1e-4, ("without normal_ref", k, e)
+    for k, e in errs.items():  # through normal_ref's backward: measured <= 6.5e-5
+        assert e < 2e-4, (k, e)
     assert "sky_sh" not in errs  # fix_sky: the sky SH gets no gradient
 
 
