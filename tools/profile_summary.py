@@ -73,11 +73,13 @@ def main(tag="r01"):
                 bench = json.loads(line)
     json.dump(dict(tag=tag, correction="traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch (gfx950)",
                    command="rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
-                           "--no-cpu-baseline; separate --pmc FETCH_SIZE and --pmc WRITE_SIZE passes",
+                           "--no-cpu-baseline --no-refalgo --no-train [--no-minibatch] <workload args>; separate "
+                           "--pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES passes",
                    kernels=res, bench_under_profiler=bench),
               open(os.path.join(out_dir, f"{tag}_hbm_traffic.json"), "w"), indent=1)
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
-        f.write(f"# rocprofv3 summary {tag}\n\nbench.py cfg2 (1.5M Gaussians, SH3, 1920x1080) under rocprofv3; "
+        wl = ((bench or {}).get("config") or {}).get("workload", "bench.py's default workload")
+        f.write(f"# rocprofv3 summary {tag}\n\nbench.py under rocprofv3, workload: {wl}; "
                 "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch.\n\n")
         f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s | VALU Minst/launch "
                 "| SALU Minst/launch |\n|---|---|---|---|---|---|---|---|---|---|\n")

@@ -16,4 +16,3 @@ GSR_DIST_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --war
   > gpurun_out/r3_n2.log 2>&1
 rc=$?; echo "n2 rc=$rc"; tail -3 gpurun_out/r3_n2.log; [ $rc -eq 0 ] || exit $rc
 bash tools/profile_round.sh r3b_cfg5 --config cfg5 || exit $?
-STEPS=30 bash tools/variants.sh base v5=relightable3dgaussians-w_amd/lib/v5/libgsr.so base v5=relightable3dgaussians-w_amd/lib/v5/libgsr.so
