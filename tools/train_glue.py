@@ -21,6 +21,7 @@ def main():
     rows = int(sys.argv[2]) if len(sys.argv) > 2 else 40
     dev = torch.device("cuda", 0)
     scene, views, gts = train.synthetic_relit_scene(P_fg, 4, 1920, 1080, 1400.0, dev, seed=0)
+    scene.iteration = train.REG_NORMAL_FROM_ITER  # every loss term on, as bench.py's train leg
     ids = list(range(4))
     for _ in range(3):
         train.train_step(scene, views, ids, gts)
@@ -29,8 +30,9 @@ def main():
         for _ in range(3):
             train.train_step(scene, views, ids, gts)
         torch.cuda.synchronize()
-    print(prof.key_averages(group_by_stack_n=4).table(sort_by="device_time_total", row_limit=rows,
-                                                      max_name_column_width=40, max_src_column_width=90))
+    print(prof.key_averages().table(sort_by="device_time_total", row_limit=rows, max_name_column_width=60))
+    print(prof.key_averages(group_by_stack_n=5).table(sort_by="device_time_total", row_limit=rows,
+                                                      max_name_column_width=40, max_src_column_width=110))
 
 
 if __name__ == "__main__":
