@@ -27,6 +27,14 @@
  *   gsr_view_loss_forward / gsr_view_loss_backward
  *                      the pointwise loss terms of train.py:77-99 (masked L1, sky-BRDF,
  *                      normal consistency) fused into one kernel each way
+ *   gsr_view_regularisers_forward / _backward, gsr_densify_stats
+ *                      the per-Gaussian view regularisers (utils/loss_utils.py:140-148,
+ *                      210-220) and densification statistics (gaussian_model.py:627-629)
+ *                      of V views in one pass each
+ *   gsr_sh_basis       utils/sh_utils.py:81-151 eval_sh's basis at directions (envlight
+ *                      regulariser, train.py:96)
+ *   gsr_sky_xyz_forward / _backward
+ *                      the sky Gaussians' shell positions (gaussian_model.py:95-103,159-169)
  *   gsr_ssim_forward / gsr_ssim_backward
  *                      the training loss's SSIM (utils/loss_utils.py:53-96, train.py:78)
  *                      as one fused stencil kernel each way
@@ -214,6 +222,35 @@ int gsr_view_loss_forward(int npix, const float* img, const float* gt, const flo
 int gsr_view_loss_backward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
                            const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
                            float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, void* stream);
+
+/* Training-step bookkeeping over V <= 8 views at once (csrc/gsr_trainaux.hip).
+ * radii / grad_means2D: arrays of V device pointers (host arrays) to each view's [P] int32
+ * radii and [P,3] means2D gradient.  depth_cols [V][4] (device): the view's depth column,
+ * depth = xyz . c[0:3] + c[3].  Forward: gsr_view_regularisers_partials(P) x 5V partial sums
+ * per view v: [0] #visible foreground, [1] #visible sky, [2] sum min-scale over visible
+ * foreground, [3] sum depth over visible sky, [4] sum depth over visible foreground.
+ * Backward: grad_sums [5V] (device) are the sums' upstream gradients; d_xyz / d_scaling
+ * (either may be null) are overwritten.  gsr_densify_stats updates accum / denom /
+ * max_radii [P] in place over the views in order. */
+int gsr_view_regularisers_partials(int P);
+int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* scaling, const int* const* radii,
+                                  const unsigned char* is_sky, const float* depth_cols, float* partials,
+                                  void* stream);
+int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int* const* radii,
+                                   const unsigned char* is_sky, const float* depth_cols, const float* grad_sums,
+                                   float* d_xyz, float* d_scaling, void* stream);
+int gsr_densify_stats(int P, int V, const float* const* grad_means2D, const int* const* radii, float* accum,
+                      float* denom, float* max_radii, void* stream);
+/* Real SH basis [N][(deg+1)^2] at the normalised directions dirs [N,3], deg 0..4. */
+int gsr_sh_basis(int N, int deg, const float* dirs, float* out, void* stream);
+/* Sky shell: angles [N,2] (theta, phi; clamped to [0,pi/2] and [-pi/2,pi/2]), radius [1],
+ * center [3] (device) -> xyz [N,3] = r (sin t sin p, -cos t, sin t cos p) + center.
+ * Backward writes d_angles [N,2] and gsr_sky_xyz_partials(N) partial sums of d radius. */
+int gsr_sky_xyz_partials(int N);
+int gsr_sky_xyz_forward(int N, const float* angles, const float* radius, const float* center, float* xyz,
+                        void* stream);
+int gsr_sky_xyz_backward(int N, const float* angles, const float* radius, const float* grad_xyz, float* d_angles,
+                         float* d_radius_partials, void* stream);
 
 /* 2D texture lookups with nvdiffrast.torch.texture semantics (csrc/gsr_texture.hip).
  * tex [tex_nb][tex_h][tex_w][C] (tex_nb == 1 broadcasts over the minibatch, else == nb);

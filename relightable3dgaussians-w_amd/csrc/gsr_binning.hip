@@ -152,7 +152,10 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
-constexpr int ST_G = 1024;  // Gaussians per block
+#ifndef GSR_ST_G
+#define GSR_ST_G 1024
+#endif
+constexpr int ST_G = GSR_ST_G;  // Gaussians per block
 // waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
 // per-wave LDS state of 8 waves would not fit (st_waves)
 

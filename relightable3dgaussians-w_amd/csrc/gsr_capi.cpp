@@ -1334,4 +1334,99 @@ int gsr_view_loss_backward(int npix, const float* img, const float* gt, const fl
     return GSR_OK;
 }
 
+/* ---- training-step bookkeeping (csrc/gsr_trainaux.hip) ---- */
+static int view_ptrs_int(int V, const int* const* src, gsr::ViewPtrs<int>& dst) {
+    for (int v = 0; v < gsr::REG_MAXV; v++) dst.p[v] = nullptr;
+    for (int v = 0; v < V; v++) {
+        if (!src[v]) return 0;
+        dst.p[v] = src[v];
+    }
+    return 1;
+}
+
+int gsr_view_regularisers_partials(int P) { return P <= 0 ? 0 : gsr::view_regs_blocks(P); }
+
+int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* scaling, const int* const* radii,
+                                  const unsigned char* is_sky, const float* depth_cols, float* partials,
+                                  void* stream_) {
+    if (P <= 0 || V <= 0 || V > gsr::REG_MAXV)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_forward: bad P=%d V=%d (1..%d views)", P, V, gsr::REG_MAXV);
+    if (!xyz || !scaling || !radii || !is_sky || !depth_cols || !partials)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_forward: missing buffers");
+    gsr::ViewPtrs<int> rp;
+    if (!view_ptrs_int(V, radii, rp)) return fail(GSR_E_ARG, "gsr_view_regularisers_forward: missing radii");
+    gsr::launch_view_regs_fwd(P, V, xyz, scaling, rp, is_sky, depth_cols, partials,
+                              reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int* const* radii,
+                                   const unsigned char* is_sky, const float* depth_cols, const float* grad_sums,
+                                   float* d_xyz, float* d_scaling, void* stream_) {
+    if (P <= 0 || V <= 0 || V > gsr::REG_MAXV)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_backward: bad P=%d V=%d (1..%d views)", P, V, gsr::REG_MAXV);
+    if (!scaling || !radii || !is_sky || !depth_cols || !grad_sums)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_backward: missing buffers");
+    gsr::ViewPtrs<int> rp;
+    if (!view_ptrs_int(V, radii, rp)) return fail(GSR_E_ARG, "gsr_view_regularisers_backward: missing radii");
+    gsr::launch_view_regs_bwd(P, V, scaling, rp, is_sky, depth_cols, grad_sums, d_xyz, d_scaling,
+                              reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_densify_stats(int P, int V, const float* const* grad_means2D, const int* const* radii, float* accum,
+                      float* denom, float* max_radii, void* stream_) {
+    if (P < 0 || V <= 0 || V > gsr::REG_MAXV)
+        return fail(GSR_E_ARG, "gsr_densify_stats: bad P=%d V=%d (1..%d views)", P, V, gsr::REG_MAXV);
+    if (P == 0) return GSR_OK;
+    if (!grad_means2D || !radii || !accum || !denom || !max_radii)
+        return fail(GSR_E_ARG, "gsr_densify_stats: missing buffers");
+    gsr::ViewPtrs<int> rp;
+    gsr::ViewPtrs<float> gp;
+    if (!view_ptrs_int(V, radii, rp)) return fail(GSR_E_ARG, "gsr_densify_stats: missing radii");
+    for (int v = 0; v < gsr::REG_MAXV; v++) gp.p[v] = nullptr;
+    for (int v = 0; v < V; v++) {
+        if (!grad_means2D[v]) return fail(GSR_E_ARG, "gsr_densify_stats: missing means2D gradient");
+        gp.p[v] = grad_means2D[v];
+    }
+    gsr::launch_densify_stats(P, V, gp, rp, accum, denom, max_radii, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_sh_basis(int N, int deg, const float* dirs, float* out, void* stream_) {
+    if (N < 0 || deg < 0 || deg > 4) return fail(GSR_E_ARG, "gsr_sh_basis: bad N=%d deg=%d (0..4)", N, deg);
+    if (N == 0) return GSR_OK;
+    if (!dirs || !out) return fail(GSR_E_ARG, "gsr_sh_basis: missing buffers");
+    gsr::launch_sh_basis(N, deg, dirs, out, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_sky_xyz_partials(int N) { return N <= 0 ? 0 : gsr::sky_blocks(N); }
+
+int gsr_sky_xyz_forward(int N, const float* angles, const float* radius, const float* center, float* xyz,
+                        void* stream_) {
+    if (N < 0) return fail(GSR_E_ARG, "gsr_sky_xyz_forward: bad N");
+    if (N == 0) return GSR_OK;
+    if (!angles || !radius || !center || !xyz) return fail(GSR_E_ARG, "gsr_sky_xyz_forward: missing buffers");
+    gsr::launch_sky_xyz_fwd(N, angles, radius, center, xyz, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_sky_xyz_backward(int N, const float* angles, const float* radius, const float* grad_xyz, float* d_angles,
+                         float* d_radius_partials, void* stream_) {
+    if (N < 0) return fail(GSR_E_ARG, "gsr_sky_xyz_backward: bad N");
+    if (N == 0) return GSR_OK;
+    if (!angles || !radius || !grad_xyz || !d_angles || !d_radius_partials)
+        return fail(GSR_E_ARG, "gsr_sky_xyz_backward: missing buffers");
+    gsr::launch_sky_xyz_bwd(N, angles, radius, grad_xyz, d_angles, d_radius_partials,
+                            reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

@@ -369,4 +369,23 @@ void launch_texture_fwd(int nb, int npix, int tex_nb, int h, int w, int C, const
 void launch_texture_bwd(int nb, int npix, int tex_nb, int h, int w, int C, const float* tex, const float* uv,
                         int filter, int boundary, const float* dout, float* d_uv, float* d_tex, hipStream_t s);
 
+// ---- training-step bookkeeping over V views at once (gsr_trainaux.hip) ------------------
+constexpr int REG_MAXV = 8;  // views per launch
+template <typename T>
+struct ViewPtrs {  // one device pointer per view, passed by value in the kernel arguments
+    const T* p[REG_MAXV];
+};
+int view_regs_blocks(int P);
+void launch_view_regs_fwd(int P, int V, const float* xyz, const float* scaling, const ViewPtrs<int>& radii,
+                          const unsigned char* is_sky, const float* dcol, float* partials, hipStream_t s);
+void launch_view_regs_bwd(int P, int V, const float* scaling, const ViewPtrs<int>& radii, const unsigned char* is_sky,
+                          const float* dcol, const float* g, float* d_xyz, float* d_scaling, hipStream_t s);
+void launch_densify_stats(int P, int V, const ViewPtrs<float>& g2d, const ViewPtrs<int>& radii, float* accum,
+                          float* denom, float* maxr, hipStream_t s);
+void launch_sh_basis(int N, int deg, const float* dirs, float* out, hipStream_t s);
+int sky_blocks(int N);
+void launch_sky_xyz_fwd(int N, const float* ang, const float* radius, const float* center, float* out, hipStream_t s);
+void launch_sky_xyz_bwd(int N, const float* ang, const float* radius, const float* g, float* d_ang, float* d_rad_part,
+                        hipStream_t s);
+
 }  // namespace gsr

@@ -69,6 +69,15 @@ def _declare(lib):
     lib.gsr_view_loss_partials.argtypes = [i]
     lib.gsr_view_loss_forward.argtypes = [i] + [vp] * 9 + [vp]
     lib.gsr_view_loss_backward.argtypes = [i] + [vp] * 9 + [vp] * 5 + [vp]
+    pa = C.POINTER(C.c_void_p)  # host array of device pointers, one per view
+    lib.gsr_view_regularisers_partials.argtypes = [i]
+    lib.gsr_view_regularisers_forward.argtypes = [i, i, vp, vp, pa, vp, vp, vp, vp]
+    lib.gsr_view_regularisers_backward.argtypes = [i, i, vp, pa, vp, vp, vp, vp, vp, vp]
+    lib.gsr_densify_stats.argtypes = [i, i, pa, pa, vp, vp, vp, vp]
+    lib.gsr_sh_basis.argtypes = [i, i, vp, vp, vp]
+    lib.gsr_sky_xyz_partials.argtypes = [i]
+    lib.gsr_sky_xyz_forward.argtypes = [i, vp, vp, vp, vp, vp]
+    lib.gsr_sky_xyz_backward.argtypes = [i, vp, vp, vp, vp, vp, vp]
     lib.gsr_ssim_partials.argtypes = [i, i, i]
     lib.gsr_ssim_partials.restype = C.c_longlong
     lib.gsr_ssim_forward.argtypes = [i, i, i, vp, vp, vp, C.c_longlong, C.POINTER(C.c_float), vp, vp, vp]
@@ -91,7 +100,9 @@ def _declare(lib):
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
-               "gsr_view_loss_forward", "gsr_view_loss_backward",
+               "gsr_view_loss_forward", "gsr_view_loss_backward", "gsr_view_regularisers_forward",
+               "gsr_view_regularisers_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
+               "gsr_sky_xyz_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
                "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
@@ -133,6 +144,15 @@ def fptr(t):
     if not t.is_contiguous():
         raise RuntimeError("internal: pointer of a non-contiguous tensor")
     return t.data_ptr()
+
+
+def ptr_array(ts):
+    """A host array of the device pointers of ``ts`` (contiguous tensors), for the C ABI's
+    per-view pointer-table arguments."""
+    for t in ts:
+        if not t.is_contiguous():
+            raise RuntimeError("internal: pointer of a non-contiguous tensor")
+    return (C.c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
 
 def stream_of(device):

@@ -173,11 +173,9 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     import diff_gaussian_rasterization as dgr
     import relit_shade
 
-    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True) + 0
-    try:
-        screenspace_points.retain_grad()
-    except Exception:
-        pass
+    # a leaf (the reference adds 0 to make it a non-leaf and retains its gradient: the same
+    # .grad after backward, without a full-size add kernel per view)
+    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True)
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
     settings = dgr.GaussianRasterizationSettings(
@@ -237,12 +235,15 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     H, W = settings.image_height, settings.image_width
     parts = _SplitChannels.apply(image, tuple(widths))
     imgs = {name: (v.expand(3, H, W) if k == 1 else v) for (name, _, _), k, v in zip(chans, widths, parts)}
+    # the depth plane the epilogue reads: a view of a one-channel part (no select of the
+    # expanded image, whose backward is a full-size zero tensor + copy + sum)
+    planes = {name: (v.view(H, W) if k == 1 else v[0]) for (name, _, _), k, v in zip(chans, widths, parts)}
     out = {"render": imgs["render"], "viewspace_points": screenspace_points, "visibility_filter": radii > 0,
            "radii": radii}
     extras = {k: v for k, v in imgs.items() if k != "render"}
     # normal remap + sky mask and normal_ref from the depth image in one kernel each way
     extras["normal"], extras["normal_ref"] = _Epilogue.apply(
-        extras["normal"], extras["depth"][0], extras["alpha"][0].detach(), sky_mask.float(),
+        extras["normal"], planes["depth"], planes["alpha"].detach(), sky_mask.float(),
         _epilogue_camera(viewpoint_camera), bool(normal_view))
     out.update(extras)
     return out

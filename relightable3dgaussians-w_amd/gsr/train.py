@@ -406,35 +406,101 @@ def depth_loss_gaussians(gaussians, camera, visibility_filter: torch.Tensor, gam
     return torch.exp(-gamma * (avg_sky - avg_fg))
 
 
-def view_regularisers(pc, radii: torch.Tensor, viewmats: torch.Tensor, env_sh: torch.Tensor, dirs: torch.Tensor,
-                      gamma: float = 0.02, depth_on: bool = True) -> torch.Tensor:
+class _FusedViewRegs(torch.autograd.Function):
+    """The per-Gaussian half of view_regularisers as one HIP pass each way
+    (csrc/gsr_trainaux.hip): sums [V,5] per view = (#visible foreground, #visible sky,
+    sum min-scale over visible foreground, sum depth over visible sky, sum depth over visible
+    foreground), differentiable in xyz and scaling."""
+
+    @staticmethod
+    def forward(ctx, xyz, scaling, dcol, radii, is_sky):
+        P, V = xyz.shape[0], len(radii)
+        L = _lib.lib()
+        parts = torch.empty(L.gsr_view_regularisers_partials(P), 5 * V, device=xyz.device)
+        rp = _lib.ptr_array(radii)
+        _lib.check(L.gsr_view_regularisers_forward(P, V, xyz.data_ptr(), scaling.data_ptr(), rp, is_sky.data_ptr(),
+                                                   dcol.data_ptr(), parts.data_ptr(), _lib.stream_of(xyz.device)),
+                   "gsr_view_regularisers_forward")
+        ctx.save_for_backward(scaling, dcol, is_sky, *radii)
+        ctx.P, ctx.V = P, V
+        return parts.sum(0).view(V, 5)
+
+    @staticmethod
+    def backward(ctx, g):
+        scaling, dcol, is_sky, *radii = ctx.saved_tensors
+        dx = torch.empty(ctx.P, 3, device=scaling.device) if ctx.needs_input_grad[0] else None
+        ds = torch.empty_like(scaling) if ctx.needs_input_grad[1] else None
+        if dx is None and ds is None:
+            return None, None, None, None, None
+        ptr = lambda t: None if t is None else t.data_ptr()
+        _lib.check(_lib.lib().gsr_view_regularisers_backward(ctx.P, ctx.V, scaling.data_ptr(), _lib.ptr_array(radii),
+                                                             is_sky.data_ptr(), dcol.data_ptr(),
+                                                             g.contiguous().data_ptr(), ptr(dx), ptr(ds),
+                                                             _lib.stream_of(scaling.device)),
+                   "gsr_view_regularisers_backward")
+        return dx, ds, None, None, None
+
+
+def sh_basis_fused(deg: int, dirs: torch.Tensor) -> torch.Tensor:
+    """sh_basis(deg, dirs / |dirs|) as one HIP launch (gsr_sh_basis); no gradient (the
+    directions are random draws)."""
+    N = dirs.shape[0]
+    d = dirs.detach().float().contiguous()
+    out = torch.empty(N, (deg + 1) ** 2, device=dirs.device)
+    _lib.check(_lib.lib().gsr_sh_basis(N, deg, d.data_ptr(), out.data_ptr(), _lib.stream_of(dirs.device)),
+               "gsr_sh_basis")
+    return out
+
+
+def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, dirs: torch.Tensor,
+                      gamma: float = 0.02, depth_on: bool = True, fused: bool = None) -> torch.Tensor:
     """The three regularisers of train.py:99-118 for V views at once, as [V] losses:
     envl_sh_loss(env_sh[v]) (unweighted: lambda_envlight only switches it on, :99-102)
     + LAMBDA_SCALE min_scale_loss(radii[v]) + LAMBDA_SKY_GAUSS depth_loss_gaussians(view v)
     (when ``depth_on``: iteration > reg_sky_gauss_depth_from_iter, :113), each equal to the
-    single-view function above.  radii [V,P], viewmats [V,4,4] (row-vector world-to-view),
-    env_sh [V,25,3], dirs [V,10,3].  Batched over views, the per-Gaussian work is ~15 [V,P]
-    kernels each way instead of ~15 [P] kernels per view per function."""
-    V = radii.shape[0]
+    single-view function above.  radii [V,P] or a list of V [P] tensors, viewmats [V,4,4]
+    (row-vector world-to-view), env_sh [V,25,3], dirs [V,10,3].
 
-    def rows(x):  # per-view sums of a [V,P] tensor: V full reductions (PyTorch's reduction
-        # over the inner axis of a [4, 1.5M] tensor runs at ~0.2 TB/s: 114 us per call)
-        return torch.stack([x[v].sum() for v in range(V)])
-    sky = pc.get_is_sky.reshape(-1)
-    vis = radii > 0
-    wf = (vis & ~sky).to(torch.float32)                        # visible foreground
-    ws = (vis & sky).to(torch.float32)                         # visible sky
-    nf, ns = rows(wf), rows(ws)
-    smin = pc.get_scaling.min(dim=-1).values                   # [P]
-    ms = rows(wf * smin) / nf
+    ``fused`` (default: on GPU tensors): the per-Gaussian sums of all V views in one HIP pass
+    each way and the SH basis in one launch (csrc/gsr_trainaux.hip); otherwise the PyTorch
+    composition below (~15 [V,P] kernels each way plus V x 5 reductions), which is also the
+    fused path's test reference."""
+    V = len(radii)
     x = pc.get_xyz
+    if fused is None:
+        fused = x.is_cuda
     c = viewmats[:, :, 2]                                      # [V,4]: the depth column
-    depth = x[:, 0] * c[:, 0:1] + x[:, 1] * c[:, 1:2] + x[:, 2] * c[:, 2:3] + c[:, 3:4]   # [V,P]
-    avg_sky = rows(depth * ws) / ns
-    avg_fg = (rows(depth * wf) / nf).detach()
+    if fused:
+        rl = [r.contiguous() for r in radii] if isinstance(radii, (list, tuple)) else list(radii.contiguous())
+        sky_u8 = pc.get_is_sky.reshape(-1).contiguous()
+        sums = _FusedViewRegs.apply((x if depth_on else x.detach()).contiguous(), pc.get_scaling.contiguous(), c.float().contiguous(), rl,
+                                    sky_u8)
+        nf, ns = sums[:, 0], sums[:, 1]
+        ms = sums[:, 2] / nf
+        avg_sky = sums[:, 3] / ns
+        avg_fg = (sums[:, 4] / nf).detach()
+    else:
+        radii = torch.stack(list(radii)) if isinstance(radii, (list, tuple)) else radii
+
+        def rows(t):  # per-view sums of a [V,P] tensor
+            return torch.stack([t[v].sum() for v in range(V)])
+        sky = pc.get_is_sky.reshape(-1)
+        vis = radii > 0
+        wf = (vis & ~sky).to(torch.float32)                        # visible foreground
+        ws = (vis & sky).to(torch.float32)                         # visible sky
+        nf, ns = rows(wf), rows(ws)
+        smin = pc.get_scaling.min(dim=-1).values                   # [P]
+        ms = rows(wf * smin) / nf
+        depth = x[:, 0] * c[:, 0:1] + x[:, 1] * c[:, 1:2] + x[:, 2] * c[:, 2:3] + c[:, 3:4]   # [V,P]
+        avg_sky = rows(depth * ws) / ns
+        avg_fg = (rows(depth * wf) / nf).detach()
     dl = torch.exp(-gamma * (avg_sky - avg_fg))
-    d = dirs / dirs.norm(dim=-1, keepdim=True)
-    vals = torch.bmm(sh_basis(4, d.reshape(-1, 3)).reshape(V, -1, 25), env_sh.reshape(V, 25, 3))  # [V,10,3]
+    if fused:
+        basis = sh_basis_fused(4, dirs.reshape(-1, 3))
+    else:
+        d = dirs / dirs.norm(dim=-1, keepdim=True)
+        basis = sh_basis(4, d.reshape(-1, 3))
+    vals = torch.bmm(basis.reshape(V, -1, 25), env_sh.reshape(V, 25, 3))  # [V,10,3]
     neg = (vals < 0).to(vals.dtype)
     n = neg.sum(dim=(1, 2))
     el = torch.where(n > 0, (vals * vals * neg).sum(dim=(1, 2)) / n.clamp(min=1), torch.zeros_like(n))
@@ -471,9 +537,40 @@ def sky_angles_clamped(a: torch.Tensor) -> torch.Tensor:
     return torch.cat((th.unsqueeze(1), ph.unsqueeze(1)), dim=1)
 
 
-def sky_xyz(angles: torch.Tensor, radius: torch.Tensor, center: torch.Tensor) -> torch.Tensor:
+class _FusedSkyXYZ(torch.autograd.Function):
+    """sky_xyz as one HIP pass each way (gsr_sky_xyz_forward/backward); differentiable in
+    the angles and the radius (the centre is a constant of the scene)."""
+
+    @staticmethod
+    def forward(ctx, angles, radius, center):
+        N = angles.shape[0]
+        out = torch.empty(N, 3, device=angles.device)
+        _lib.check(_lib.lib().gsr_sky_xyz_forward(N, angles.data_ptr(), radius.data_ptr(), center.data_ptr(),
+                                                  out.data_ptr(), _lib.stream_of(angles.device)), "gsr_sky_xyz_forward")
+        ctx.save_for_backward(angles, radius)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        angles, radius = ctx.saved_tensors
+        N = angles.shape[0]
+        L = _lib.lib()
+        da = torch.empty_like(angles)
+        dr = torch.empty(L.gsr_sky_xyz_partials(N), device=angles.device)
+        _lib.check(L.gsr_sky_xyz_backward(N, angles.data_ptr(), radius.data_ptr(), g.contiguous().data_ptr(),
+                                          da.data_ptr(), dr.data_ptr(), _lib.stream_of(angles.device)),
+                   "gsr_sky_xyz_backward")
+        return da, dr.sum().reshape(radius.shape), None
+
+
+def sky_xyz(angles: torch.Tensor, radius: torch.Tensor, center: torch.Tensor, fused: bool = None) -> torch.Tensor:
     """get_sky_xyz (gaussian_model.py:95-103), COLMAP axes: radius (sin t sin p, -cos t,
-    sin t cos p) + center, from the clamped angles."""
+    sin t cos p) + center, from the clamped angles.  ``fused`` (default: on GPU tensors):
+    one HIP pass each way instead of ~20 elementwise kernels."""
+    if fused is None:
+        fused = angles.is_cuda
+    if fused and angles.shape[0]:
+        return _FusedSkyXYZ.apply(angles.contiguous(), radius.contiguous(), center.float().contiguous())
     a = sky_angles_clamped(angles)
     x = torch.sin(a[..., 0]) * torch.sin(a[..., 1])
     y = -torch.cos(a[..., 0])
@@ -675,9 +772,9 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     for t in losses:
         t.record_stream(main)
     # envlight, min-scale and sky-depth regularisers of every view at once, on the main stream
-    radii = torch.stack([o["radii"] for o in outs])
-    for o in outs:
-        o["radii"].record_stream(main)
+    radii = [o["radii"] for o in outs]
+    for r in radii:
+        r.record_stream(main)
     vms = torch.stack([v.world_view_transform for v in views]).float()
     reg = view_regularisers(pc, radii, vms, env_sh, rand["dirs"], depth_on=it > REG_SKY_GAUSS_DEPTH_FROM_ITER)
     total = torch.stack(losses).sum() + reg.sum()
@@ -689,10 +786,8 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         scene.step_stats = gdp.StepStats(scene.P, dev)
     scene.step_stats.zero()
     for out in outs:
-        g, r = out["viewspace_points"].grad, out["radii"]
-        g.record_stream(main)
-        r.record_stream(main)
-        scene.step_stats.add_view(g, r)
+        out["viewspace_points"].grad.record_stream(main)
+    scene.step_stats.add_views([o["viewspace_points"].grad for o in outs], radii)
     del outs
     fp.check_grads_in_place()
     n_views = len(views)

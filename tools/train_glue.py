@@ -26,13 +26,18 @@ def main():
     for _ in range(3):
         train.train_step(scene, views, ids, gts)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         for _ in range(3):
             train.train_step(scene, views, ids, gts)
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="device_time_total", row_limit=rows, max_name_column_width=60))
-    print(prof.key_averages(group_by_stack_n=5).table(sort_by="device_time_total", row_limit=rows,
-                                                      max_name_column_width=40, max_src_column_width=110))
+    # the PyTorch glue by input shapes (which tensors the copies, products, sums and fills run on)
+    ka = prof.key_averages(group_by_input_shape=True)
+    glue = [e for e in ka if e.key.startswith("aten::") and e.device_time_total > 0]
+    glue.sort(key=lambda e: -e.device_time_total)
+    print("\n%-28s %10s %6s  %s" % ("op", "device us", "calls", "input shapes"))
+    for e in glue[:rows]:
+        print("%-28s %10.1f %6d  %s" % (e.key, e.device_time_total, e.count, str(e.input_shapes)[:150]))
 
 
 if __name__ == "__main__":
