@@ -35,6 +35,7 @@
  *                      regulariser, train.py:96)
  *   gsr_sky_xyz_forward / _backward
  *                      the sky Gaussians' shell positions (gaussian_model.py:95-103,159-169)
+ *   gsr_view_objective the view's loss and backward coefficients from both partials
  *   gsr_ssim_forward / gsr_ssim_backward
  *                      the training loss's SSIM (utils/loss_utils.py:53-96, train.py:78)
  *                      as one fused stencil kernel each way
@@ -203,12 +204,13 @@ int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double*
  * block_sums: 2 * gsr_ssim_partials(C,H,W) floats, per workgroup a fixed-order partial of
  * sum(map * mask) and of #(mask == 1) (the caller adds them).  dmaps: null (no backward) or 3*C*H*W floats kept for the backward.
  * The backward writes dL/dimg1 = gscale[0] * (window^T applied to dmaps) (img2 gets none:
- * it is the ground truth); gscale is a device scalar, dL/dloss / #mask. */
+ * it is the ground truth), or adds it to dimg1 when `accumulate` is non-zero; gscale is a
+ * device scalar, dL/dloss / #mask. */
 long long gsr_ssim_partials(int C, int height, int width);
 int gsr_ssim_forward(int C, int height, int width, const float* img1, const float* img2, const float* mask,
                      long long mask_cstride, const float* window, float* block_sums, float* dmaps, void* stream);
 int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
-                      const float* gscale, const float* window, float* dimg1, void* stream);
+                      const float* gscale, const float* window, float* dimg1, int accumulate, void* stream);
 
 /* The pointwise terms of the training loss (train.py:77-99) over one view: images img, gt,
  * diff, spec, nrm, nref are [3,H,W] (npix = H*W), the sky and occluder masks [H,W].
@@ -216,6 +218,14 @@ int gsr_ssim_backward(int C, int height, int width, const float* img1, const flo
  * caller adds.  Backward: coef (device) = (k_img, k_brdf, k_normal); any gradient pointer
  * may be null. */
 int gsr_view_loss_partials(int npix);
+/* One view's training objective from the partial sums of gsr_view_loss_forward and
+ * gsr_ssim_forward (with the occluder mask): loss[0] = the pointwise terms +
+ * lambda_dssim (1 - SSIM) (train.py:77-99), and coef[4] = the backward coefficients before the
+ * upstream gradient: (k_img, k_brdf, k_normal) for gsr_view_loss_backward and the SSIM map
+ * sum's for gsr_ssim_backward.  One workgroup; sums in double (counts exact at 4K). */
+int gsr_view_objective(int n_loss_partials, const float* loss_partials, long long n_ssim_partials,
+                       const float* ssim_partials, int npix, double lambda_dssim, double lambda_sky,
+                       double lambda_normal, float* loss, float* coef, void* stream);
 int gsr_view_loss_forward(int npix, const float* img, const float* gt, const float* diff, const float* spec,
                           const float* nrm, const float* nref, const float* sky, const float* occ, float* partials,
                           void* stream);

@@ -17,6 +17,8 @@
 //      point_list directly, in coalesced runs.
 // Every step is stable, so each tile's list is exactly the reference's order
 // (depth-bits ascending, Gaussian index ascending on ties), bit-exact.
+#include <type_traits>
+
 #include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
@@ -24,20 +26,24 @@
 
 namespace gsr {
 
-// Local tile rect of a Gaussian inside super-tile (sx, sy): cx0 | (cx1-1) << 3 | cy0 << 6 |
-// (cy1-1) << 8, where [cx0, cx1) x [cy0, cy1) are tile offsets within the 8x4 super-tile.
+// Local tile rect of a Gaussian inside super-tile (sx, sy) (gsr_common.hpp's code layout).
 __device__ __forceinline__ uint32_t local_rect_code(uint2 r, uint32_t sx, uint32_t sy) {
     const int tx0 = (int)(sx * GSR_ST_W), ty0 = (int)(sy * GSR_ST_H);
     const int cx0 = max((int)(r.x & 0xffffu) - tx0, 0), cx1 = min((int)(r.x >> 16) - tx0, (int)GSR_ST_W);
     const int cy0 = max((int)(r.y & 0xffffu) - ty0, 0), cy1 = min((int)(r.y >> 16) - ty0, (int)GSR_ST_H);
-    return (uint32_t)cx0 | ((uint32_t)(cx1 - 1) << 3) | ((uint32_t)cy0 << 6) | ((uint32_t)(cy1 - 1) << 8);
+    return (uint32_t)cx0 | ((uint32_t)(cx1 - 1) << ST_XB) | ((uint32_t)cy0 << (2 * ST_XB)) |
+           ((uint32_t)(cy1 - 1) << (2 * ST_XB + ST_YB));
 }
-__device__ __forceinline__ uint32_t local_rect_mask(uint32_t code) {
-    const uint32_t cx0 = code & 7u, cx1 = ((code >> 3) & 7u) + 1u, cy0 = (code >> 6) & 3u, cy1 = ((code >> 8) & 3u) + 1u;
-    const uint32_t row = ((1u << cx1) - 1u) & ~((1u << cx0) - 1u);
-    uint32_t m = 0;
+// the super-tile's tiles a code covers: bit t = tile (t % ST_W, t / ST_W)
+using st_mask_t = typename std::conditional<GSR_ST_W * GSR_ST_H <= 32u, uint32_t, uint64_t>::type;
+__device__ __forceinline__ st_mask_t local_rect_mask(uint32_t code) {
+    constexpr uint32_t XM = GSR_ST_W - 1u, YM = GSR_ST_H - 1u;
+    const uint32_t cx0 = code & XM, cx1 = ((code >> ST_XB) & XM) + 1u, cy0 = (code >> (2 * ST_XB)) & YM,
+                   cy1 = ((code >> (2 * ST_XB + ST_YB)) & YM) + 1u;
+    const st_mask_t row = (((st_mask_t)1 << cx1) - 1u) & ~(((st_mask_t)1 << cx0) - 1u);
+    st_mask_t m = 0;
 #pragma unroll
-    for (uint32_t y = 0; y < GSR_ST_H; y++) m |= (y >= cy0 && y < cy1) ? row << (GSR_ST_W * y) : 0u;
+    for (uint32_t y = 0; y < GSR_ST_H; y++) m |= (y >= cy0 && y < cy1) ? row << (GSR_ST_W * y) : (st_mask_t)0;
     return m;
 }
 
@@ -152,6 +158,9 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
+#ifndef GSR_EXP_STWRITE
+#define GSR_EXP_STWRITE 0
+#endif
 #ifndef GSR_ST_G
 #define GSR_ST_G 1024
 #endif
@@ -204,7 +213,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
 // Segment table of the materialised tile lists (SEG entries per segment, see k_seg_lists),
 // in the materialisation scratch (seg_layout).
 constexpr uint32_t SEG = 1024;
-constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32
+constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32 (8 x 4)
 struct SegTable {
     uint32_t *seg_st, *seg_e0, *st_seg0, *nseg_total, *seg_cnt;
     uint32_t gcap;  // capacity of the table (segments)
@@ -264,8 +273,17 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
                 const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
+#if GSR_EXP_STWRITE == 1  // timing experiment: each lane's entries at consecutive slots (wrong order)
+                {
+                    const uint32_t dpos = (uint32_t)(((unsigned long long)(c0 + lane) * 6u + (sy - sy0) * 8u + (sx - sx0)) % cap);
+                    ent[dpos] = make_uint2(sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS), gid + (pos & 0u));
+                }
+#elif GSR_EXP_STWRITE == 2  // timing experiment: no entry store
+                asm volatile("" ::"v"(pos), "v"(local_rect_code(r, sx, sy)));
+#else
                 if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
                     ent[pos] = make_uint2(sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS), gid);
+#endif
             }
         lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
@@ -330,7 +348,11 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) header[0] = min(carry, cap);
     __syncthreads();
+#if GSR_EXP_STWRITE == 3  // timing experiment: the block set-up alone
+    if (p0 < 0) st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
+#else
     st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
+#endif
 }
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
@@ -363,6 +385,9 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
     const int W = st_waves(NS);
+#if GSR_EXP_STWRITE
+    (void)hipMemsetAsync(ent, 0, sizeof(uint2) * (size_t)cap, s);  // the experiments leave entries unwritten
+#endif
     char* t = reinterpret_cast<char*>(temp);
     auto take = [&](size_t bytes) {
         char* p = t;
@@ -506,9 +531,10 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
         const uint32_t b = e0 + 256u * j;
         if (b >= e1) break;  // block-uniform
         const uint32_t e = b + tid;
-        uint32_t id = 0, mask = 0;
+        uint32_t id = 0;
+        st_mask_t mask = 0;
         if (e < e1) {
-            // local tile coverage mask (bit t = (t / 8) row, (t % 8) column)
+            // local tile coverage mask (bit t = tile (t % ST_W, t / ST_W))
             mask = local_rect_mask(kb[j] >> ST_KEY_BITS);
             if (WRITE) id = vb[j];
         }
@@ -516,7 +542,7 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
         uint32_t mine = 0;
 #pragma unroll
         for (int t = 0; t < ST_TILES; t++) {
-            bal[t] = __ballot((mask >> t) & 1u);
+            bal[t] = __ballot((uint32_t)(mask >> t) & 1u);
             mine = lane == t ? (uint32_t)__popcll(bal[t]) : mine;
         }
         if (lane < ST_TILES) s_wc[wave][lane] = mine;
@@ -532,7 +558,7 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
             const uint32_t wbase = run + (wave > 0 ? c0 : 0u) + (wave > 1 ? c1 : 0u) + (wave > 2 ? c2 : 0u);
 #pragma unroll
             for (int t = 0; t < ST_TILES; t++) {
-                if ((mask >> t) & 1u) {
+                if ((uint32_t)(mask >> t) & 1u) {
                     const uint32_t lo = (uint32_t)bal[t], hi = (uint32_t)(bal[t] >> 32);
                     const uint32_t r = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
                     const uint32_t pos = bcast(wbase, t) + r;

@@ -1298,12 +1298,25 @@ int gsr_ssim_forward(int C, int height, int width, const float* img1, const floa
 }
 
 int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
-                      const float* gscale, const float* window, float* dimg1, void* stream_) {
+                      const float* gscale, const float* window, float* dimg1, int accumulate, void* stream_) {
     if (C <= 0 || C > 65535 || height <= 0 || width <= 0) return fail(GSR_E_ARG, "gsr_ssim_backward: bad sizes");
     gsr::SsimWindow w;
     if (!img1 || !img2 || !dmaps || !gscale || !dimg1 || !ssim_window(window, w))
         return fail(GSR_E_ARG, "gsr_ssim_backward: missing buffers");
-    gsr::launch_ssim_bwd(C, height, width, img1, img2, dmaps, gscale, w, dimg1, reinterpret_cast<hipStream_t>(stream_));
+    gsr::launch_ssim_bwd(C, height, width, img1, img2, dmaps, gscale, w, dimg1, accumulate ? 1 : 0,
+                         reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_view_objective(int n_loss_partials, const float* loss_partials, long long n_ssim_partials,
+                       const float* ssim_partials, int npix, double lambda_dssim, double lambda_sky,
+                       double lambda_normal, float* loss, float* coef, void* stream_) {
+    if (n_loss_partials <= 0 || n_ssim_partials <= 0 || n_ssim_partials > 0x7fffffffLL || npix <= 0)
+        return fail(GSR_E_ARG, "gsr_view_objective: bad sizes");
+    if (!loss_partials || !ssim_partials || !loss || !coef) return fail(GSR_E_ARG, "gsr_view_objective: missing buffers");
+    gsr::launch_view_objective(n_loss_partials, loss_partials, (int)n_ssim_partials, ssim_partials, npix, lambda_dssim,
+                               lambda_sky, lambda_normal, loss, coef, reinterpret_cast<hipStream_t>(stream_));
     GSR_LAUNCH_CHECK();
     return GSR_OK;
 }

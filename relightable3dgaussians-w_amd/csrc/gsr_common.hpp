@@ -11,11 +11,24 @@
 #define GSR_BLOCK_X 16
 #define GSR_BLOCK_Y 16
 #define GSR_TILE_PIX 256
-// super-tile (binning granularity) in tiles
+// super-tile (binning granularity) in tiles: powers of two, at most 64 tiles
+#ifndef GSR_ST_W
 #define GSR_ST_W 8u
+#endif
+#ifndef GSR_ST_H
 #define GSR_ST_H 4u
+#endif
 
 namespace gsr {
+
+// A super-tile entry's local tile rect (the tiles of its super-tile the Gaussian's rect
+// covers): cx0 | (cx1 - 1) << ST_XB | cy0 << 2 ST_XB | (cy1 - 1) << (2 ST_XB + ST_YB), with
+// [cx0, cx1) x [cy0, cy1) tile offsets inside the super-tile.
+constexpr uint32_t st_log2(uint32_t v) { return v <= 1u ? 0u : 1u + st_log2(v >> 1); }
+constexpr uint32_t ST_XB = st_log2(GSR_ST_W), ST_YB = st_log2(GSR_ST_H);
+static_assert((1u << ST_XB) == GSR_ST_W && (1u << ST_YB) == GSR_ST_H, "super-tile sides must be powers of two");
+static_assert(GSR_ST_W * GSR_ST_H <= 64u, "at most 64 tiles per super-tile (one lane each)");
+constexpr uint32_t ST_CODE_BITS = 2u * (ST_XB + ST_YB);
 
 // auxiliary.h:22-39 (same decimal literals as the reference)
 __device__ constexpr float SH_C0 = 0.28209479177387814f;

@@ -135,6 +135,7 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s);
 // Super-tile keys: id in bits [0, ST_KEY_BITS), the entry's local tile rect above (so at
 // most 2^20 super-tiles; the sort orders only the id bits).
 constexpr int ST_KEY_BITS = 20;
+static_assert(ST_KEY_BITS + ST_CODE_BITS <= 32, "super-tile key + local rect code must fit 32 bits");
 constexpr uint32_t ST_KEY_MASK = (1u << ST_KEY_BITS) - 1u;
 // Super-tile entries of the P_v depth-sorted Gaussians, emitted directly in super-tile
 // order, plus the super-tile ranges and header[0] = S.  NS <= 1365.
@@ -313,13 +314,15 @@ void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, 
                      long long mask_cstride, const SsimWindow& win, float C1, float C2, float* block_sums,
                      float* dmaps, hipStream_t s);
 void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
-                     const float* gscale, const SsimWindow& win, float* dimg1, hipStream_t s);
+                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s);
 
 // ---- fused pointwise training-loss terms (gsr_loss.hip) ---------------------------------
 int view_loss_blocks(int npix);
 void launch_view_loss_fwd(int npix, const float* img, const float* gt, const float* diff, const float* spec,
                           const float* nrm, const float* nref, const float* sky, const float* occ, float* partials,
                           hipStream_t s);
+void launch_view_objective(int nvl, const float* vl, int nss, const float* ss, int npix, double l_dssim, double l_sky,
+                           double l_normal, float* loss, float* coef, hipStream_t s);
 void launch_view_loss_bwd(int npix, const float* img, const float* gt, const float* diff, const float* spec,
                           const float* nrm, const float* nref, const float* sky, const float* occ, const float* coef,
                           float* d_img, float* d_diff, float* d_spec, float* d_nrm, float* d_nref, hipStream_t s);

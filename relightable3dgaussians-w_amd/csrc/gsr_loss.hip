@@ -19,6 +19,9 @@
 //               d n_c  = k4 nr_c (o s)^2,      d nr_c = k4 n_c (o s)^2
 //             (torch's abs backward: sign(0) = 0).
 // HBM-bound: 6 three-channel images + 2 masks in; 5 gradients out.
+//   objective one workgroup turns the pointwise partials and the SSIM partials into the
+//             view's loss and the backward's four coefficients on the device (the ~25 scalar
+//             PyTorch ops of the wrapper, one launch).
 #include "gsr_kernels.hpp"
 
 namespace gsr {
@@ -79,6 +82,58 @@ __global__ void __launch_bounds__(256) k_view_loss_bwd(int npix, const float* __
             if (d_nref) d_nref[i] = k4 * a * os2;
         }
     }
+}
+
+// loss = pw + l_dssim (1 - ssim) as gsr/train.py composes it in PyTorch:
+//   S = sum of the pointwise partials (double), k0 = (1 - l_dssim) / S1 (0 if S1 == 0),
+//   k2 = l_sky / S3 (0 if S3 == 0), pw = (float)(k0 S0 + k2 S2 + l_normal (1 - S4 / npix));
+//   value = (float) sum of the SSIM map partials, N = the mask count (double),
+//   ssim = N > 0 ? (float)(value / N) : 1, loss = pw + (float)l_dssim * (1 - ssim) in float.
+// coef = (k0, k2, -l_normal / npix, -(float)l_dssim / N (0 if N == 0)): the gradient
+// coefficients of the pointwise terms and of the SSIM map sum, before the upstream gradient.
+__global__ void __launch_bounds__(256) k_view_objective(int nvl, const float* __restrict__ vl, int nss,
+                                                        const float* __restrict__ ss, int npix, double l_dssim,
+                                                        double l_sky, double l_normal, float* __restrict__ loss,
+                                                        float* __restrict__ coef) {
+#pragma clang fp contract(off)
+    __shared__ double red[7][4];
+    double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int i = threadIdx.x; i < nvl; i += 256) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) a[k] += (double)vl[(size_t)i * 5 + k];
+    }
+    for (int i = threadIdx.x; i < nss; i += 256) {
+        a[5] += (double)ss[(size_t)i * 2];
+        a[6] += (double)ss[(size_t)i * 2 + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) a[k] += __shfl_xor(a[k], o, 64);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = a[k];
+    }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    double S[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) S[k] = (red[k][0] + red[k][1]) + (red[k][2] + red[k][3]);
+    const double k0 = S[1] > 0.0 ? (1.0 - l_dssim) / S[1] : 0.0;
+    const double k2 = S[3] > 0.0 ? l_sky / S[3] : 0.0;
+    const float pw = (float)(k0 * S[0] + k2 * S[2] + l_normal * (1.0 - S[4] / (double)npix));
+    const float value = (float)S[5];
+    const float ssim = S[6] > 0.0 ? (float)((double)value / S[6]) : 1.f;
+    const float ld = (float)l_dssim;
+    loss[0] = pw + ld * (1.f - ssim);
+    coef[0] = (float)k0;
+    coef[1] = (float)k2;
+    coef[2] = (float)(0.0 - l_normal / (double)npix);
+    coef[3] = S[6] > 0.0 ? (float)(-(double)ld / S[6]) : 0.f;
+}
+
+void launch_view_objective(int nvl, const float* vl, int nss, const float* ss, int npix, double l_dssim, double l_sky,
+                           double l_normal, float* loss, float* coef, hipStream_t s) {
+    hipLaunchKernelGGL(k_view_objective, dim3(1), dim3(256), 0, s, nvl, vl, nss, ss, npix, l_dssim, l_sky, l_normal,
+                       loss, coef);
 }
 
 int view_loss_blocks(int npix) {

@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
 __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
                                                   const float* __restrict__ img2, const float* __restrict__ dmaps,
                                                   const float* __restrict__ gscale, SsimWindow win,
-                                                  float* __restrict__ dimg1) {
+                                                  float* __restrict__ dimg1, int accumulate) {
     __shared__ float s[3][SS_LH][SS_LW];
     __shared__ float hm[3][SS_LH][SS_TW + 1];
     const int c = blockIdx.z;
@@ -214,7 +214,8 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
             q2 += g * col[2][o + k];
         }
         const size_t oo = c * plane + (size_t)y * W + x;
-        dimg1[oo] = sc * (q0 + 2.f * img1[oo] * q1 + img2[oo] * q2);
+        const float d = sc * (q0 + 2.f * img1[oo] * q1 + img2[oo] * q2);
+        dimg1[oo] = accumulate ? dimg1[oo] + d : d;  // accumulate: onto the pointwise terms' gradient
     }
 }
 
@@ -228,8 +229,9 @@ void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, 
 }
 
 void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
-                     const float* gscale, const SsimWindow& win, float* dimg1, hipStream_t s) {
-    hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(256), 0, s, H, W, img1, img2, dmaps, gscale, win, dimg1);
+                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s) {
+    hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(256), 0, s, H, W, img1, img2, dmaps, gscale, win, dimg1,
+                       accumulate);
 }
 
 }  // namespace gsr

@@ -133,8 +133,9 @@ struct TileList {
         nx2 = load_step(step_after(e));
     }
     __device__ __forceinline__ bool covers(uint32_t key) const {
-        const uint32_t code = key >> 20, cx0 = code & 7u, cx1 = (code >> 3) & 7u, cy0 = (code >> 6) & 3u,
-                       cy1 = (code >> 8) & 3u;  // inclusive maxima
+        constexpr uint32_t XM = GSR_ST_W - 1u, YM = GSR_ST_H - 1u;
+        const uint32_t code = key >> 20, cx0 = code & XM, cx1 = (code >> ST_XB) & XM, cy0 = (code >> (2 * ST_XB)) & YM,
+                       cy1 = (code >> (2 * ST_XB + ST_YB)) & YM;  // inclusive maxima
         return (lx - cx0) <= (cx1 - cx0) && (ly - cy0) <= (cy1 - cy0);  // unsigned: also lx >= cx0
     }
     __device__ __forceinline__ bool more() const { return FWD ? e < lim : e > lim; }

@@ -80,7 +80,7 @@ class _Epilogue(torch.autograd.Function):
     [H,W], alpha [H,W] (detached), sky [H,W]) -> (normal, normal_ref), both [3,H,W]."""
 
     @staticmethod
-    def forward(ctx, n01, depth, alpha, sky, cam12, normal_view):
+    def forward(ctx, n01, depth, alpha, sky, cam12, normal_view, dest=None):
         from . import _lib
         H, W = depth.shape
         n01, depth, alpha, sky = (t.float().contiguous() for t in (n01, depth, alpha, sky))
@@ -92,6 +92,7 @@ class _Epilogue(torch.autograd.Function):
                    "gsr_relit_epilogue")
         ctx.save_for_backward(depth, alpha, sky, cam12)
         ctx.normal_view = normal_view
+        ctx.dest = dest  # (n01's, depth's) composite groups: their gradients go to its GradSlab
         return normal, nref
 
     @staticmethod
@@ -101,15 +102,21 @@ class _Epilogue(torch.autograd.Function):
         H, W = depth.shape
         c = lambda t: None if t is None else t.float().contiguous()
         g_normal, g_nref = c(g_normal), c(g_nref)
-        d_n01 = torch.empty((3, H, W), dtype=torch.float32, device=depth.device) if ctx.needs_input_grad[0] else None
-        d_depth = torch.empty_like(depth) if ctx.needs_input_grad[1] else None
+        d_n01 = d_depth = None
+        if ctx.needs_input_grad[0]:
+            d_n01 = slab_take(ctx.dest[0]) if ctx.dest else None
+            if d_n01 is None or d_n01.shape != (3, H, W):
+                d_n01 = torch.empty((3, H, W), dtype=torch.float32, device=depth.device)
+        if ctx.needs_input_grad[1]:
+            d_depth = slab_take(ctx.dest[1]) if ctx.dest else None
+            d_depth = torch.empty_like(depth) if d_depth is None or d_depth.numel() != H * W else d_depth.view(H, W)
         ptr = lambda t: None if t is None else t.data_ptr()
         if d_n01 is not None or d_depth is not None:
             _lib.check(_lib.lib().gsr_relit_epilogue_backward(
                 W, H, cam12.data_ptr(), depth.data_ptr(), alpha.data_ptr(), sky.data_ptr(), int(ctx.normal_view),
                 ptr(g_normal), ptr(g_nref), ptr(d_n01), ptr(d_depth), _lib.stream_of(depth.device)),
                 "gsr_relit_epilogue_backward")
-        return d_n01, d_depth, None, None, None, None
+        return d_n01, d_depth, None, None, None, None, None
 
 
 _GREY = {}
@@ -131,15 +138,54 @@ def _is_grey(bg_color):
     return grey
 
 
+class GradSlab:
+    """The gradient image of one composite [C,H,W], handed out in channel groups: a consumer
+    of a group (the fused view objective, the epilogue) writes its gradient straight into
+    the group's rows instead of a tensor of its own that the split's backward would then
+    copy.  Each group is handed out once (a second consumer, or a second backward over the
+    same graph, gets None and allocates as usual; the split then copies)."""
+
+    def __init__(self, shape, device):
+        self.shape, self.device = tuple(shape), device
+        self.t = None
+        self.taken = set()
+
+    def take(self, c0: int, k: int):
+        if c0 in self.taken:
+            return None
+        self.taken.add(c0)
+        if self.t is None:
+            self.t = torch.empty(self.shape, dtype=torch.float32, device=self.device)
+        return self.t[c0:c0 + k]
+
+    def holds(self, g, c0: int) -> bool:
+        return (self.t is not None and c0 in self.taken and g.dtype == torch.float32 and g.is_contiguous()
+                and g.data_ptr() == self.t[c0].data_ptr())
+
+
+def slab_take(t, k=None):
+    """The GradSlab rows reserved for tensor ``t`` (a group of a composite split by render()),
+    or None."""
+    tag = getattr(t, "_gsr_slab", None)
+    if tag is None:
+        return None
+    slab, c0, kk = tag
+    return slab.take(c0, kk if k is None else k)
+
+
 class _SplitChannels(torch.autograd.Function):
     """The composite image [C,H,W] split into consecutive channel groups (views).  The
-    backward writes each group's gradient into one [C,H,W] tensor (zeros only where a group
-    has none) instead of autograd's full-size zero tensor + add per slice."""
+    backward returns the GradSlab its consumers wrote into when every group's gradient is
+    its slab rows (zeroing the groups with none); otherwise it writes each group's gradient
+    into one [C,H,W] tensor (zeros only where a group has none) instead of autograd's
+    full-size zero tensor + add per slice."""
 
     @staticmethod
-    def forward(ctx, image, widths):
+    def forward(ctx, image, widths, slab):
+        ctx.set_materialize_grads(False)  # groups without a gradient arrive as None, not zeros
         ctx.widths = widths
         ctx.shape = image.shape
+        ctx.slab = slab
         out, c = [], 0
         for k in widths:
             out.append(image[c:c + k])
@@ -148,20 +194,31 @@ class _SplitChannels(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
+        slab, offs, c = ctx.slab, [], 0
+        for k in ctx.widths:
+            offs.append(c)
+            c += k
+        if slab is not None and slab.t is not None and all(t is None or slab.holds(t, c0)
+                                                           for t, c0 in zip(grads, offs)):
+            g = slab.t
+            for k, t, c0 in zip(ctx.widths, grads, offs):
+                if t is None:
+                    g[c0:c0 + k].zero_()
+            if c < g.shape[0]:
+                g[c:].zero_()
+            return g, None, None
         g = torch.empty(ctx.shape, dtype=torch.float32, device=next(t for t in grads if t is not None).device) \
             if any(t is not None for t in grads) else None
         if g is None:
-            return None, None
-        c = 0
-        for k, t in zip(ctx.widths, grads):
+            return None, None, None
+        for k, t, c0 in zip(ctx.widths, grads, offs):
             if t is None:
-                g[c:c + k].zero_()
+                g[c0:c0 + k].zero_()
             else:
-                g[c:c + k].copy_(t)
-            c += k
+                g[c0:c0 + k].copy_(t)
         if c < g.shape[0]:
             g[c:].zero_()
-        return g, None
+        return g, None, None
 
 
 def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color, scaling_modifier=1.0, debug=True,
@@ -233,7 +290,12 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     image, radii = dgr.rasterize_channels(means3D, screenspace_points, features, opacity, scales, rotations,
                                           cov3D_precomp, torch.cat(bgs), settings, nch=nch)
     H, W = settings.image_height, settings.image_width
-    parts = _SplitChannels.apply(image, tuple(widths))
+    slab = GradSlab(image.shape, image.device)
+    parts = _SplitChannels.apply(image, tuple(widths), slab)
+    c0 = 0
+    for v, k in zip(parts, widths):  # where each group's gradient goes (slab_take)
+        v._gsr_slab = (slab, c0, k)
+        c0 += k
     imgs = {name: (v.expand(3, H, W) if k == 1 else v) for (name, _, _), k, v in zip(chans, widths, parts)}
     # the depth plane the epilogue reads: a view of a one-channel part (no select of the
     # expanded image, whose backward is a full-size zero tensor + copy + sum)
@@ -242,9 +304,10 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
            "radii": radii}
     extras = {k: v for k, v in imgs.items() if k != "render"}
     # normal remap + sky mask and normal_ref from the depth image in one kernel each way
+    grp = {name: v for (name, _, _), v in zip(chans, parts)}
     extras["normal"], extras["normal_ref"] = _Epilogue.apply(
         extras["normal"], planes["depth"], planes["alpha"].detach(), sky_mask.float(),
-        _epilogue_camera(viewpoint_camera), bool(normal_view))
+        _epilogue_camera(viewpoint_camera), bool(normal_view), (grp["normal"], grp["depth"]))
     out.update(extras)
     return out
 

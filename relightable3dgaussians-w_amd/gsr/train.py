@@ -211,7 +211,7 @@ class _FusedSSIM(torch.autograd.Function):
         gs = g.reshape(1).float().contiguous()
         d = torch.empty_like(img1)
         _lib.check(_lib.lib().gsr_ssim_backward(Cn, H, W, img1.data_ptr(), img2.data_ptr(), dmaps.data_ptr(),
-                                                gs.data_ptr(), _WIN11, d.data_ptr(), _lib.stream_of(img1.device)),
+                                                gs.data_ptr(), _WIN11, d.data_ptr(), 0, _lib.stream_of(img1.device)),
                    "gsr_ssim_backward")
         return d, None, None
 
@@ -289,10 +289,87 @@ def _plane(mask, H, W):
     return m
 
 
+class _FusedViewObjective(torch.autograd.Function):
+    """The whole per-view objective of train.py:77-99 (pointwise terms + lambda_dssim
+    (1 - SSIM(img, gt; occ))) in four launches forward (pointwise partials, SSIM partials
+    and maps, gsr_view_objective for the scalar tail) and three backward (the coefficients
+    times the upstream gradient, the pointwise gradients, the SSIM gradient added onto the
+    image's), with no PyTorch scalar ops in between; equal to _FusedViewLoss + ssim()."""
+
+    @staticmethod
+    def forward(ctx, img, diff, spec, nrm, nref, gt, sky, occ, lam):
+        import ctypes as C
+        global _WIN11
+        if _WIN11 is None:
+            _WIN11 = (C.c_float * 11)(*gaussian_1d(11).tolist())
+        H, W = sky.shape
+        npix = H * W
+        ts = [t.float().contiguous() for t in (img, gt, diff, spec, nrm, nref, sky, occ)]
+        L = _lib.lib()
+        dev = img.device
+        st = _lib.stream_of(dev)
+        nvl = L.gsr_view_loss_partials(npix)
+        nss = L.gsr_ssim_partials(3, H, W)
+        parts = torch.empty(5 * nvl + 2 * nss + 5, device=dev)
+        vl, ss, loss, coef = parts[:5 * nvl], parts[5 * nvl:5 * nvl + 2 * nss], parts[-5:-4], parts[-4:]
+        _lib.check(L.gsr_view_loss_forward(npix, *[t.data_ptr() for t in ts], vl.data_ptr(), st),
+                   "gsr_view_loss_forward")
+        dmaps = torch.empty((3, 3, H, W), device=dev) if ctx.needs_input_grad[0] else None
+        _lib.check(L.gsr_ssim_forward(3, H, W, ts[0].data_ptr(), ts[1].data_ptr(), ts[7].data_ptr(), 0, _WIN11,
+                                      ss.data_ptr(), None if dmaps is None else dmaps.data_ptr(), st),
+                   "gsr_ssim_forward")
+        _lib.check(L.gsr_view_objective(nvl, vl.data_ptr(), nss, ss.data_ptr(), npix, *[float(x) for x in lam],
+                                        loss.data_ptr(), coef.data_ptr(), st), "gsr_view_objective")
+        ctx.coef = coef
+        ctx.dmaps = dmaps
+        ctx.dest = (img, diff, spec)  # render()'s composite groups write into its GradSlab
+        ctx.save_for_backward(*ts)
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g):
+        ts = ctx.saved_tensors
+        H, W = ts[6].shape
+        cg = (ctx.coef * g.float()).contiguous()  # (k_img, k_brdf, k_normal, k_ssim) x dL/dloss
+        from .relit import slab_take
+        need = ctx.needs_input_grad
+        outs = []
+        for k in range(5):
+            d = None
+            if need[k]:
+                d = slab_take(ctx.dest[k]) if k < 3 else None
+                if d is None or d.shape != ts[0].shape:
+                    d = torch.empty_like(ts[0])
+            outs.append(d)
+        ptr = lambda t: None if t is None else t.data_ptr()
+        st = _lib.stream_of(ts[0].device)
+        _lib.check(_lib.lib().gsr_view_loss_backward(H * W, *[t.data_ptr() for t in ts], cg.data_ptr(),
+                                                     *[ptr(t) for t in outs], st), "gsr_view_loss_backward")
+        if outs[0] is not None:  # the SSIM term's image gradient, added in place
+            _lib.check(_lib.lib().gsr_ssim_backward(3, H, W, ts[0].data_ptr(), ts[1].data_ptr(), ctx.dmaps.data_ptr(),
+                                                    cg.data_ptr() + 12, _WIN11, outs[0].data_ptr(), 1, st),
+                       "gsr_ssim_backward")
+        return (*outs, None, None, None, None)
+
+
 def view_loss(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):
-    """train.py:77-99: reconstruction (L1 + D-SSIM), sky-BRDF and normal-consistency terms.
-    The pointwise terms run as one fused kernel each way (gsr_view_loss_*), the SSIM on
-    gsr_ssim_*.  Masks: [H,W], [1,H,W] or their channel expansion."""
+    """train.py:77-99: reconstruction (L1 + D-SSIM), sky-BRDF and normal-consistency terms,
+    fused (_FusedViewObjective: gsr_view_loss_*, gsr_ssim_*, gsr_view_objective).  Masks:
+    [H,W], [1,H,W] or their channel expansion."""
+    img = out["render"]
+    H, W = img.shape[-2:]
+    sky, occ = _plane(sky_mask, H, W), _plane(occ_mask, H, W)
+    _lib.require_gpu_tensor(img, "render")
+    if img.dim() != 3 or img.shape[0] != 3 or gt.shape != img.shape:
+        raise ValueError(f"view_loss: render and gt must both be [3,H,W], got {tuple(img.shape)}, {tuple(gt.shape)}")
+    return _FusedViewObjective.apply(img, out["diffuse_color"], out["specular_color"], out["normal"],
+                                     out["normal_ref"], gt.detach(), sky, occ,
+                                     (float(lambda_dssim), float(lambda_sky_brdf), float(lambda_normal)))
+
+
+def view_loss_unfused(out, gt, sky_mask, occ_mask, lambda_dssim=0.2, lambda_sky_brdf=0.5, lambda_normal=0.05):
+    """view_loss with the scalar tail in PyTorch (_FusedViewLoss + ssim()): the fused
+    objective's test reference."""
     img = out["render"]
     H, W = img.shape[-2:]
     sky, occ = _plane(sky_mask, H, W), _plane(occ_mask, H, W)
@@ -756,14 +833,17 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     if ids is None:  # one host-to-device copy per view set, not per iteration
         ids = scene.id_cache[key] = torch.as_tensor(key, device=dev, dtype=torch.long)
     env_sh, sky_sh = mlp_forward(fp.params, fp.params["embeddings"][ids], rand["dropout"])
-    env_lit = env_sh + rand["noise"]
+    # one view of each per-view row (unbind: one stacking kernel in the backward, where
+    # indexing gives a zero tensor + copy per view)
+    env_lit = (env_sh + rand["noise"]).unbind(0)
+    sky_rows = sky_sh.unbind(0)
     losses, outs = [], []
     for i, (view, gt) in enumerate(zip(views, gts)):
         s = streams[i % len(streams)]
         s.wait_stream(main)
         with torch.cuda.stream(s):
             light = relit_shade.EnvironmentLight(env_lit[i], sh_degree=4)
-            out = (render_fn or relit.render)(view, pc, light, sky_sh[i:i + 1], 1, pipe, bg, debug=False)
+            out = (render_fn or relit.render)(view, pc, light, sky_rows[i][None], 1, pipe, bg, debug=False)
             losses.append(view_loss(out, gt, view.sky_mask, view.occluders_mask, LAMBDA_DSSIM, LAMBDA_SKY_BRDF,
                                     lam_normal))
         outs.append(out)

@@ -73,3 +73,41 @@ def test_fused_view_loss_matches_torch(H, W, empty_sky):
     for k in names:
         e = rel_l2(a[k].grad.cpu().numpy(), b[k].grad.cpu().numpy())
         assert e < 1e-5 or (b[k].grad.abs().max() == 0 and a[k].grad.abs().max() == 0), (k, e)
+
+
+@pytest.mark.parametrize("H,W,case", [(64, 96, "plain"), (1080, 1920, "plain"), (40, 40, "empty_occ"),
+                                      (33, 47, "empty_sky")])
+def test_fused_objective_matches_scalar_tail(H, W, case):
+    """The objective's scalar tail on the device (gsr_view_objective) and the SSIM gradient
+    added onto the pointwise one against the same kernels with the tail in PyTorch
+    (train.view_loss_unfused): value and gradients to 1e-6, including an empty occluder mask
+    (SSIM 1, no reconstruction gradient) and no non-sky pixel."""
+    from gsr import train
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(21)
+    names = ["render", "diffuse_color", "specular_color", "normal", "normal_ref"]
+    base = {k: torch.rand(3, H, W, generator=g) for k in names}
+    gt = torch.rand(3, H, W, generator=g).to(dev)
+    sky = (torch.rand(H, W, generator=g) > 0.3).float()
+    occ = (torch.rand(H, W, generator=g) > 0.1).float()
+    if case == "empty_occ":
+        occ.zero_()
+    if case == "empty_sky":
+        sky.fill_(1.0)
+    sky, occ = sky.to(dev), occ.to(dev)
+    a = {k: v.to(dev).requires_grad_(True) for k, v in base.items()}
+    b = {k: v.to(dev).requires_grad_(True) for k, v in base.items()}
+    la = train.view_loss(a, gt, sky, occ)
+    lb = train.view_loss_unfused(b, gt, sky, occ)
+    assert la.dim() == 0 and la.dtype == torch.float32
+    (3.0 * la).backward()
+    (3.0 * lb).backward()
+    torch.cuda.synchronize()
+    fa, fb = float(la.detach()), float(lb.detach())
+    assert abs(fa - fb) <= 1e-6 * abs(fb) + 1e-7, (fa, fb)
+    for k in names:
+        ga, gb = a[k].grad, b[k].grad
+        if float(gb.abs().max()) == 0:
+            assert float(ga.abs().max()) == 0, k
+            continue
+        assert rel_l2(ga.cpu().numpy(), gb.cpu().numpy()) < 1e-6, k

@@ -38,6 +38,24 @@ def main():
     print("\n%-28s %10s %6s  %s" % ("op", "device us", "calls", "input shapes"))
     for e in glue[:rows]:
         print("%-28s %10.1f %6d  %s" % (e.key, e.device_time_total, e.count, str(e.input_shapes)[:150]))
+    # ... and by Python call site (the innermost frames in this repository)
+    ks = prof.key_averages(group_by_stack_n=8)
+    sites = {}
+    top = sorted([e for e in ks if e.key.startswith("aten::")], key=lambda e: -e.device_time_total)[:2]
+    for e in top:
+        print("stack sample:", e.key, e.stack[:10])
+    for e in ks:
+        if not e.key.startswith("aten::") or e.device_time_total <= 0:
+            continue
+        fr = [f for f in (e.stack or []) if "relightable3dgaussians-w_amd" in f or "/repo/" in f]
+        site = " < ".join(f.split("/")[-1] for f in fr[:3]) or "?"
+        d = sites.setdefault(site, [0.0, 0, set()])
+        d[0] += e.device_time_total
+        d[1] += e.count
+        d[2].add(e.key)
+    print("\n%10s %6s  %s" % ("device us", "calls", "call site (ops)"))
+    for site, (t, n, ops) in sorted(sites.items(), key=lambda kv: -kv[1][0])[:rows]:
+        print("%10.1f %6d  %s  (%s)" % (t, n, site[:160], ",".join(sorted(o[6:] for o in ops))[:80]))
 
 
 if __name__ == "__main__":
