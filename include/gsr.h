@@ -341,7 +341,7 @@ int gsr_get_deterministic(void);
  * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a
  * stream synchronisation, and fails with GSR_E_DEVICE_CHECK naming the first violation. */
 int gsr_debug_build(void);
-/* The binning buffer holds super-tile lists: every (visible Gaussian, 8x4-tile super-tile its
+/* The binning buffer holds super-tile lists: every (visible Gaussian, super-tile (8x4 tiles; 8x8 in large frames) its
  * rect touches) entry, per super-tile in (depth, index) order with the entry's local tile rect;
  * the tile passes filter a tile's list from them.  This writes the reference's point_list [R]
  * (binningState.point_list after the sort, rasterizer_impl.cu:79-99,303-308) and the tile

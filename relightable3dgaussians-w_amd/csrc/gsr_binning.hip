@@ -3,7 +3,7 @@
 // The reference emits one 64-bit key (tile << 32 | depth) per (Gaussian, tile) pair --
 // R of them, ~28M at 1.5M Gaussians/1080p -- and radix-sorts all R on 32+13 bits.  Here:
 //   1. the P_v visible Gaussians are sorted once by depth (gsr_sort.hip);
-//   2. in that order every Gaussian emits one entry per SUPER-TILE (8x4 tiles) its rect
+//   2. in that order every Gaussian emits one entry per SUPER-TILE (8x4 tiles, 8x8 for large frames: st_sth) its rect
 //      touches (k_st_emit: S ~ 1.3 P_v entries instead of R);
 //   3. the S entries are stably sorted by super-tile id (one 8-bit pass at 1080p);
 //   4. each super-tile list is cut into 1024-entry segments (k_seg_table); one workgroup
@@ -26,25 +26,31 @@
 
 namespace gsr {
 
-// Local tile rect of a Gaussian inside super-tile (sx, sy) (gsr_common.hpp's code layout).
-__device__ __forceinline__ uint32_t local_rect_code(uint2 r, uint32_t sx, uint32_t sy) {
-    const int tx0 = (int)(sx * GSR_ST_W), ty0 = (int)(sy * GSR_ST_H);
+// Local tile rect of a Gaussian inside super-tile (sx, sy) of height 2^sth tiles
+// (gsr_common.hpp's code layout).
+__device__ __forceinline__ uint32_t local_rect_code(uint2 r, uint32_t sx, uint32_t sy, uint32_t sth) {
+    const int tx0 = (int)(sx * GSR_ST_W), ty0 = (int)(sy << sth);
     const int cx0 = max((int)(r.x & 0xffffu) - tx0, 0), cx1 = min((int)(r.x >> 16) - tx0, (int)GSR_ST_W);
-    const int cy0 = max((int)(r.y & 0xffffu) - ty0, 0), cy1 = min((int)(r.y >> 16) - ty0, (int)GSR_ST_H);
+    const int cy0 = max((int)(r.y & 0xffffu) - ty0, 0), cy1 = min((int)(r.y >> 16) - ty0, 1 << sth);
     return (uint32_t)cx0 | ((uint32_t)(cx1 - 1) << ST_XB) | ((uint32_t)cy0 << (2 * ST_XB)) |
            ((uint32_t)(cy1 - 1) << (2 * ST_XB + ST_YB));
 }
 // the super-tile's tiles a code covers: bit t = tile (t % ST_W, t / ST_W)
-using st_mask_t = typename std::conditional<GSR_ST_W * GSR_ST_H <= 32u, uint32_t, uint64_t>::type;
-__device__ __forceinline__ st_mask_t local_rect_mask(uint32_t code) {
-    constexpr uint32_t XM = GSR_ST_W - 1u, YM = GSR_ST_H - 1u;
+__device__ __forceinline__ uint64_t local_rect_mask(uint32_t code) {
+    constexpr uint32_t XM = (1u << ST_XB) - 1u, YM = (1u << ST_YB) - 1u;
     const uint32_t cx0 = code & XM, cx1 = ((code >> ST_XB) & XM) + 1u, cy0 = (code >> (2 * ST_XB)) & YM,
                    cy1 = ((code >> (2 * ST_XB + ST_YB)) & YM) + 1u;
-    const st_mask_t row = (((st_mask_t)1 << cx1) - 1u) & ~(((st_mask_t)1 << cx0) - 1u);
-    st_mask_t m = 0;
+    const uint64_t row = ((1ull << cx1) - 1ull) & ~((1ull << cx0) - 1ull);
+    uint64_t m = 0;
 #pragma unroll
-    for (uint32_t y = 0; y < GSR_ST_H; y++) m |= (y >= cy0 && y < cy1) ? row << (GSR_ST_W * y) : (st_mask_t)0;
+    for (uint32_t y = 0; y < (1u << ST_YB); y++) m |= (y >= cy0 && y < cy1) ? row << (GSR_ST_W * y) : 0ull;
     return m;
+}
+// the super-tile rect [sx0, sx1) x [sy0, sy1) of a tile rect, packed as the tile rects are
+__device__ __forceinline__ uint2 st_rect_of(uint2 r, uint32_t sth) {
+    const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
+    const uint32_t sy0 = (r.y & 0xffffu) >> sth, sy1 = ((r.y >> 16) + (1u << sth) - 1u) >> sth;
+    return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
 }
 
 // ---- 2. super-tile emission -----------------------------------------------------------
@@ -52,7 +58,7 @@ __device__ __forceinline__ st_mask_t local_rect_mask(uint32_t code) {
 // run: lane i writes entry i, i+64, ... (coalesced), locating its Gaussian by binary
 // search over the wave's inclusive count prefix in LDS.
 __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets,
-                                                  const uint2* rect, unsigned gsx, uint32_t* st_keys,
+                                                  const uint2* rect, unsigned gsx, unsigned sth, uint32_t* st_keys,
                                                   uint32_t* st_vals) {
     __shared__ uint32_t s_inc[4][64];
     __shared__ uint32_t s_id[4][64];
@@ -65,10 +71,8 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
     if (s < Pv) {
         idx = sorted_ids[s];
         r = rect[idx];
-        const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
-        const uint32_t sy0 = (r.y & 0xffffu) / GSR_ST_H, sy1 = ((r.y >> 16) + GSR_ST_H - 1) / GSR_ST_H;
-        sr = make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
-        cnt = (sx1 - sx0) * (sy1 - sy0);
+        sr = st_rect_of(r, sth);
+        cnt = ((sr.x >> 16) - (sr.x & 0xffffu)) * ((sr.y >> 16) - (sr.y & 0xffffu));
     }
     uint32_t inc = cnt;
 #pragma unroll
@@ -96,7 +100,7 @@ __global__ void __launch_bounds__(256) k_st_emit(int Pv, const uint32_t* sorted_
         const uint32_t x0 = rr.x & 0xffffu, w = (rr.x >> 16) - x0, y0 = rr.y & 0xffffu;
         const uint32_t yy = k / w, xx = k - yy * w;
         const uint32_t sx = x0 + xx, sy = y0 + yy;
-        st_keys[base + i] = (sy * gsx + sx) | (local_rect_code(s_rect[wave][lo], sx, sy) << ST_KEY_BITS);
+        st_keys[base + i] = (sy * gsx + sx) | (local_rect_code(s_rect[wave][lo], sx, sy, sth) << ST_KEY_BITS);
         st_vals[base + i] = s_id[wave][lo];
     }
 }
@@ -158,9 +162,6 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
-#ifndef GSR_EXP_STWRITE
-#define GSR_EXP_STWRITE 0
-#endif
 #ifndef GSR_ST_G
 #define GSR_ST_G 1024
 #endif
@@ -168,11 +169,6 @@ constexpr int ST_G = GSR_ST_G;  // Gaussians per block
 // waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
 // per-wave LDS state of 8 waves would not fit (st_waves)
 
-__device__ __forceinline__ uint2 st_rect_of(uint2 r) {
-    const uint32_t sx0 = (r.x & 0xffffu) / GSR_ST_W, sx1 = ((r.x >> 16) + GSR_ST_W - 1) / GSR_ST_W;
-    const uint32_t sy0 = (r.y & 0xffffu) / GSR_ST_H, sy1 = ((r.y >> 16) + GSR_ST_H - 1) / GSR_ST_H;
-    return make_uint2(sx0 | (sx1 << 16), sy0 | (sy1 << 16));
-}
 
 // P_v from the depth sort's last pass (depth_sort's pv_out).  The forward launches the binning before its one host synchronisation (the
 // binning buffer is sized from the previous call's counts, see gsr_capi.cpp), so these
@@ -183,7 +179,7 @@ __device__ __forceinline__ int block_visible(int pv_host, const unsigned long lo
 }
 
 template <int ST_W>
-__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const uint2* rect_sorted, unsigned gsx,
+__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const uint2* rect_sorted, unsigned gsx, unsigned sth,
                                                   int NS, int nb, uint32_t* table, uint32_t* wcounts) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
@@ -195,7 +191,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
     uint32_t* wh = hist + wave * NS;
     for (int p = p0 + lane; p < p1; p += 64) {
-        const uint2 sr = st_rect_of(rect_sorted[p]);
+        const uint2 sr = st_rect_of(rect_sorted[p], sth);
         for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
             for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
     }
@@ -213,7 +209,6 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
 // Segment table of the materialised tile lists (SEG entries per segment, see k_seg_lists),
 // in the materialisation scratch (seg_layout).
 constexpr uint32_t SEG = 1024;
-constexpr int ST_TILES = GSR_ST_W * GSR_ST_H;  // 32 (8 x 4)
 struct SegTable {
     uint32_t *seg_st, *seg_e0, *st_seg0, *nseg_total, *seg_cnt;
     uint32_t gcap;  // capacity of the table (segments)
@@ -246,7 +241,7 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 // the run and clears the mask.  Order-independent atomics only, so the output is
 // deterministic, and each super-tile's entries come out in depth order.
 __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                                        unsigned gsx, uint32_t* wcnt, unsigned long long* wmask, uint2* ent,
+                                        unsigned gsx, unsigned sth, uint32_t* wcnt, unsigned long long* wmask, uint2* ent,
                                         uint32_t cap) {
     const int lane = threadIdx.x & 63;
     const unsigned long long bit = 1ull << lane, lt = bit - 1ull;
@@ -260,7 +255,7 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
     for (int c0 = p0; c0 < p1; c0 += 64) {
         const uint2 r = r_nx;
         const uint32_t gid = gid_nx;
-        const uint2 sr = (c0 + lane < p1) ? st_rect_of(r) : make_uint2(0u, 0u);
+        const uint2 sr = (c0 + lane < p1) ? st_rect_of(r, sth) : make_uint2(0u, 0u);
         if (c0 + 64 + lane < p1) {
             r_nx = rect_sorted[c0 + 64 + lane];
             gid_nx = sorted_ids[c0 + 64 + lane];
@@ -273,17 +268,8 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
             for (uint32_t sx = sx0; sx < sx1; sx++) {
                 const uint32_t sid = sy * gsx + sx;
                 const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
-#if GSR_EXP_STWRITE == 1  // timing experiment: each lane's entries at consecutive slots (wrong order)
-                {
-                    const uint32_t dpos = (uint32_t)(((unsigned long long)(c0 + lane) * 6u + (sy - sy0) * 8u + (sx - sx0)) % cap);
-                    ent[dpos] = make_uint2(sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS), gid + (pos & 0u));
-                }
-#elif GSR_EXP_STWRITE == 2  // timing experiment: no entry store
-                asm volatile("" ::"v"(pos), "v"(local_rect_code(r, sx, sy)));
-#else
-                if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
-                    ent[pos] = make_uint2(sid | (local_rect_code(r, sx, sy) << ST_KEY_BITS), gid);
-#endif
+if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
+                    ent[pos] = make_uint2(sid | (local_rect_code(r, sx, sy, sth) << ST_KEY_BITS), gid);
             }
         lds_order();
         for (uint32_t sy = sy0; sy < sy1; sy++)
@@ -305,7 +291,7 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
 // the super-tile bases itself (block 0 also writes the ranges and header[0] = S).
 template <int ST_W>
 __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
-                                                     const uint2* rect_sorted, unsigned gsx, int NS, int nb,
+                                                     const uint2* rect_sorted, unsigned gsx, unsigned sth, int NS, int nb,
                                                      const uint32_t* table, const uint32_t* wcounts,
                                                      const uint32_t* tot, uint2* st_ranges, unsigned long long* header,
                                                      uint2* ent, uint32_t cap, FrameTotals ft, TileOrderArgs ord) {
@@ -348,11 +334,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) header[0] = min(carry, cap);
     __syncthreads();
-#if GSR_EXP_STWRITE == 3  // timing experiment: the block set-up alone
-    if (p0 < 0) st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
-#else
-    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
-#endif
+    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, sth, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
 }
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
@@ -366,7 +348,7 @@ size_t st_bin_temp_bytes(long long Pv, int NS) {
 bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
 void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
+                   unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
                    uint32_t cap, hipStream_t s, const FrameTotals* ftp, const TileOrderArgs* ordp) {
     FrameTotals ft{};
     if (ftp) ft = *ftp;
@@ -385,9 +367,6 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     }
     const int nb = (Pv + ST_G - 1) / ST_G;
     const int W = st_waves(NS);
-#if GSR_EXP_STWRITE
-    (void)hipMemsetAsync(ent, 0, sizeof(uint2) * (size_t)cap, s);  // the experiments leave entries unwritten
-#endif
     char* t = reinterpret_cast<char*>(temp);
     auto take = [&](size_t bytes) {
         char* p = t;
@@ -398,20 +377,20 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
     if (W == 8)
-        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
+        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, totals, rect_sorted, gsx, sth, NS, nb,
                            table, wcounts);
     else
-        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, NS, nb,
+        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, sth, NS, nb,
                            table, wcounts);
     launch_digit_scan(NS, table, nb, tot, s);
     if (ordp) ord.st_tot = tot;
     const dim3 grid(nb + (ftp ? 1 : 0) + (ordp && ord.ntile ? 8 : 0));
     if (W == 8)
         hipLaunchKernelGGL(k_st_scatter<8>, grid, dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
+                           gsx, sth, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
     else
         hipLaunchKernelGGL(k_st_scatter<4>, grid, dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
+                           gsx, sth, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)
@@ -448,9 +427,10 @@ struct StGeom {
 __device__ __forceinline__ StGeom st_geom(unsigned st, unsigned gsx, unsigned gx, unsigned gy) {
     StGeom g;
     g.tx0 = (st % gsx) * GSR_ST_W;
-    g.ty0 = (st / gsx) * GSR_ST_H;
+    const unsigned sth = st_sth(gx, gy);
+    g.ty0 = (st / gsx) << sth;
     g.nx = min(GSR_ST_W, gx - g.tx0);
-    g.ny = min(GSR_ST_H, gy - g.ty0);
+    g.ny = min(1u << sth, gy - g.ty0);
     return g;
 }
 
@@ -532,7 +512,7 @@ __global__ void __launch_bounds__(256) k_seg_lists(const uint32_t* nseg_total, c
         if (b >= e1) break;  // block-uniform
         const uint32_t e = b + tid;
         uint32_t id = 0;
-        st_mask_t mask = 0;
+        uint64_t mask = 0;
         if (e < e1) {
             // local tile coverage mask (bit t = tile (t % ST_W, t / ST_W))
             mask = local_rect_mask(kb[j] >> ST_KEY_BITS);
@@ -655,10 +635,10 @@ __global__ void __launch_bounds__(1024) k_tile_scan(int T, const uint32_t* cnt, 
 
 // ---- host launchers ---------------------------------------------------------------------
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
-                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s) {
+                    unsigned sth, uint32_t* st_keys, uint32_t* st_vals, hipStream_t s) {
     if (Pv == 0) return;
-    hipLaunchKernelGGL(k_st_emit, dim3((Pv + 255) / 256), dim3(256), 0, s, Pv, sorted_ids, offsets, rect, gsx, st_keys,
-                       st_vals);
+    hipLaunchKernelGGL(k_st_emit, dim3((Pv + 255) / 256), dim3(256), 0, s, Pv, sorted_ids, offsets, rect, gsx, sth,
+                       st_keys, st_vals);
 }
 
 void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, const uint32_t* sorted_vals, uint2* ranges,

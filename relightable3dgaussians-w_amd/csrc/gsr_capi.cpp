@@ -119,13 +119,17 @@ ImgLayout img_layout(int W, int H) {
 }
 
 unsigned st_x(int W) { return (tiles_x(W) + GSR_ST_W - 1) / GSR_ST_W; }
-unsigned st_y(int H) { return (tiles_y(H) + GSR_ST_H - 1) / GSR_ST_H; }
+unsigned st_h(int W, int H) { return gsr::st_sth(tiles_x(W), tiles_y(H)); }  // log2 super-tile height
+unsigned st_y(int W, int H) {
+    const unsigned sth = st_h(W, H);
+    return (tiles_y(H) + (1u << sth) - 1) >> sth;
+}
 
 // capS: the entry capacity (0: the fixed part only, as the backward computes it)
 BinLayout bin_layout(long long capS, int W, int H, long long Pv) {
     Carver c;
     BinLayout L;
-    const size_t NS = (size_t)st_x(W) * st_y(H);
+    const size_t NS = (size_t)st_x(W) * st_y(W, H);
     const bool fused = gsr::st_bin_supported((int)NS);
     L.header = c.take(16);
     L.st_ranges = c.take(8 * NS);
@@ -338,7 +342,7 @@ int materialize_lists(long long R, int W, int H, const char* bin, uint32_t* out_
     HIP_OK(hipMemcpyAsync(&S, bin + bl.header, 8, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
     const unsigned gx = tiles_x(W), gy = tiles_y(H), gsx = st_x(W);
-    const int NS = (int)(st_x(W) * st_y(H)), T = (int)(gx * gy);
+    const int NS = (int)(st_x(W) * st_y(W, H)), T = (int)(gx * gy);
     void* tmp = g_scratch2.get(gsr::materialize_temp_bytes((long long)S, NS, T));
     if (!tmp) return fail(GSR_E_ALLOC, "list materialisation: scratch allocation failed");
     gsr::launch_materialize((long long)S, NS, reinterpret_cast<const uint2*>(bin + bl.st_ranges),
@@ -534,7 +538,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     if (!cov3D_precomp && (!scales || !rotations) && P > 0)
         return fail(GSR_E_ARG, "gsr_forward: need scales+rotations or cov3D_precomp");
     if (tiles_x(width) > 65535u || tiles_y(height) > 65535u ||
-        (unsigned long long)st_x(width) * st_y(height) >= (1ull << gsr::ST_KEY_BITS))
+        (unsigned long long)st_x(width) * st_y(width, height) >= (1ull << gsr::ST_KEY_BITS))
         return fail(GSR_E_ARG, "gsr_forward: image too large");
 
     // rasterizer_impl.cu:221-222 (host float arithmetic == device float arithmetic)
@@ -598,7 +602,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     }
     const unsigned long long seq = ++g_pinned.seq;
     const gsr::FrameTotals ft{pa.blk_tot, gsr::pre_blocks(P), g_pinned.p_dev, seq};
-    const unsigned gsx = st_x(width), gsy = st_y(height);
+    const unsigned gsx = st_x(width), gsy = st_y(width, height);
     const int NS = (int)(gsx * gsy);
     const bool fused_bin = gsr::st_bin_supported(NS);
     const bool speculate = fused_bin && g_hint.P == P && g_hint.W == width && g_hint.H == height;
@@ -656,7 +660,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
-            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, NS,
+            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, st_h(width, height), NS,
                                at<void>(bin, bl.st_bin_tmp), ent, st_ranges, header, (uint32_t)capS, s,
                                dev ? &ft : nullptr, &ord);
             GSR_LAUNCH_CHECK();
@@ -672,7 +676,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
             }
             {
                 GSR_STAGE(ST_DUPLICATE);
-                gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, stk, stv, s);
+                gsr::launch_st_emit((int)Pv, sorted_ids, offsets, pa.rect, gsx, st_h(width, height), stk, stv, s);
             }
             int flip2;
             {

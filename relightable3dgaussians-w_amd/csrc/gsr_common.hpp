@@ -11,24 +11,37 @@
 #define GSR_BLOCK_X 16
 #define GSR_BLOCK_Y 16
 #define GSR_TILE_PIX 256
-// super-tile (binning granularity) in tiles: powers of two, at most 64 tiles
-#ifndef GSR_ST_W
+// super-tile (binning granularity): GSR_ST_W tiles wide and 2^sth tiles high, sth chosen per
+// frame by st_sth (below)
 #define GSR_ST_W 8u
-#endif
-#ifndef GSR_ST_H
-#define GSR_ST_H 4u
-#endif
 
 namespace gsr {
 
 // A super-tile entry's local tile rect (the tiles of its super-tile the Gaussian's rect
 // covers): cx0 | (cx1 - 1) << ST_XB | cy0 << 2 ST_XB | (cy1 - 1) << (2 ST_XB + ST_YB), with
-// [cx0, cx1) x [cy0, cy1) tile offsets inside the super-tile.
-constexpr uint32_t st_log2(uint32_t v) { return v <= 1u ? 0u : 1u + st_log2(v >> 1); }
-constexpr uint32_t ST_XB = st_log2(GSR_ST_W), ST_YB = st_log2(GSR_ST_H);
-static_assert((1u << ST_XB) == GSR_ST_W && (1u << ST_YB) == GSR_ST_H, "super-tile sides must be powers of two");
-static_assert(GSR_ST_W * GSR_ST_H <= 64u, "at most 64 tiles per super-tile (one lane each)");
+// [cx0, cx1) x [cy0, cy1) tile offsets inside the super-tile (fields sized for the tallest
+// super-tile).
+constexpr uint32_t ST_XB = 3u, ST_YB = 3u;
+static_assert((1u << ST_XB) == GSR_ST_W, "super-tile width");
 constexpr uint32_t ST_CODE_BITS = 2u * (ST_XB + ST_YB);
+constexpr int ST_TILES = 64;  // tiles of the tallest super-tile (8 x 8), one lane each
+// Super-tile height: 8x4 tiles (sth = 2) while the frame has at most ST_SMALL_MAX of them, the
+// binning scatter's limit for 8 waves per workgroup in 64 KiB of LDS (st_waves); larger
+// frames (4K: 1020 8x4 super-tiles) take 8x8 (sth = 3): fewer entries per Gaussian (cfg5:
+// 3.2 instead of 4.7) and half the per-wave scatter state, for a little more filtering in
+// the tile passes.  A pure function of the tile grid, evaluated on the host and in the
+// kernels alike.  GSR_ST_STH forces one height (experiments).
+constexpr unsigned ST_SMALL_MAX = 682;
+__host__ __device__ __forceinline__ unsigned st_sth(unsigned gx, unsigned gy) {
+#ifdef GSR_ST_STH
+    (void)gx;
+    (void)gy;
+    return GSR_ST_STH;
+#else
+    const unsigned long long ns4 = (unsigned long long)((gx + GSR_ST_W - 1u) / GSR_ST_W) * ((gy + 3u) / 4u);
+    return ns4 > ST_SMALL_MAX ? 3u : 2u;
+#endif
+}
 
 // auxiliary.h:22-39 (same decimal literals as the reference)
 __device__ constexpr float SH_C0 = 0.28209479177387814f;

@@ -125,7 +125,7 @@ struct FrameTotals {
 void launch_frame_totals(const FrameTotals& ft, hipStream_t s);
 
 // ---- binning (gsr_binning.hip) ----------------------------------------------------------
-// The binning stops at SUPER-TILE lists: one entry per (visible Gaussian, 8x4-tile super-tile
+// The binning stops at SUPER-TILE lists: one entry per (visible Gaussian, super-tile (8x4 tiles, 8x8 past ST_SMALL_MAX: st_sth)
 // its rect touches), entry = (local tile rect code << ST_KEY_BITS | super-tile id, Gaussian
 // id), every super-tile's entries contiguous and in (depth, index) order.  A tile's list (the
 // reference's point_list range) is the subsequence of its super-tile's entries whose local
@@ -147,13 +147,13 @@ bool st_bin_supported(int NS);
 // positions >= cap are not written (the speculative forward detects the overflow and redoes
 // the binning).  ft (optional): the frame totals run as one extra workgroup of the scatter.
 void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
+                   unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
                    uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr, const TileOrderArgs* order = nullptr);
 // Large images (NS > 1365): in depth order, every visible Gaussian emits one (super-tile,
 // gaussian) pair per super-tile its rect touches, at offsets[s] (exclusive scan of st_count
 // in depth order); the pairs are then radix-sorted by super-tile and packed into entries.
 void launch_st_emit(int Pv, const uint32_t* sorted_ids, const uint32_t* offsets, const uint2* rect, unsigned gsx,
-                    uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
+                    unsigned sth, uint32_t* st_keys, uint32_t* st_vals, hipStream_t s);
 // ranges[k] = [first, last+1) of super-tile k in the sorted pairs ((0, 0) when absent), the
 // pairs packed into ent, header[0] = n.
 void launch_seg_ranges(long long n, int nseg, const uint32_t* sorted_keys, const uint32_t* sorted_vals, uint2* ranges,

@@ -11,7 +11,7 @@ namespace gsr {
 __device__ __forceinline__ uint32_t tile_cost(unsigned t, const TileOrderArgs& a) {
     if (a.cost) return a.cost[t];
     if (a.st_tot || a.st_ranges) {
-        const unsigned st = (t / a.gx) / GSR_ST_H * a.gsx + (t % a.gx) / GSR_ST_W;
+        const unsigned st = ((t / a.gx) >> st_sth(a.gx, a.ntile / a.gx)) * a.gsx + (t % a.gx) / GSR_ST_W;
         if (a.st_tot) return a.st_tot[st];
         const uint2 r = a.st_ranges[st];
         return r.y - r.x;

@@ -117,8 +117,9 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
         key = __float_as_uint(p_view.z);
         irad = r_;
         tiles = area;
+        const unsigned sth = st_sth(a.grid_x, a.grid_y);
         stc = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
-              ((rmax.y + GSR_ST_H - 1) / GSR_ST_H - rmin.y / GSR_ST_H);
+              (((rmax.y + (1u << sth) - 1) >> sth) - (rmin.y >> sth));
     } while (false);
     a.depth_key[idx] = key;
     key_out = key;

@@ -88,10 +88,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 #endif
     // the tile's list back to front from its last contributor (the forward's tile_emax and
     // tile_nmax: the entry and, over the whole tile, its list position + 1)
-    const unsigned sti = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sth = st_sth(a.grid_x, a.grid_y);
+    const unsigned sti = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<false> tl;
-    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
         tl.fill(s_list);

@@ -39,10 +39,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const unsigned sti = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sth = st_sth(a.grid_x, a.grid_y);
+    const unsigned sti = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<true> tl;
-    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, 0u, 0u);
+    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, sth, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];

@@ -30,10 +30,11 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
-    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sth = st_sth(a.grid_x, a.grid_y);
+    const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<true> tl;
-    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, 0u, 0u);
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
@@ -202,10 +203,11 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
 
     // back to front from the tile's last contributor (as gsr_render_bwd.hip)
-    const unsigned st = (tile / a.grid_x) / GSR_ST_H * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    const unsigned sth = st_sth(a.grid_x, a.grid_y);
+    const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<false> tl;
-    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
     for (;;) {
         tl.fill(s_list);

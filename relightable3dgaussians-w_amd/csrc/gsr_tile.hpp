@@ -73,7 +73,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // ---- a tile's list, read from its super-tile's entries -------------------------------------
 // The binning stops at super-tile lists (gsr_binning.hip): the entries of every Gaussian that
-// touches an 8x4-tile super-tile, in (depth, index) order, each carrying its local tile rect.
+// touches a super-tile (8x4 or 8x8 tiles, st_sth), in (depth, index) order, each carrying its local tile rect.
 // A tile's list -- the reference's point_list range, entry for entry -- is the subsequence of
 // its super-tile's entries whose local rect covers the tile.  TileList filters 64 entries per
 // step (one 8-B load per lane, prefetched a step ahead; a rect test; a ballot) and appends the
@@ -113,12 +113,13 @@ struct TileList {
     }
     // st_range: the super-tile's entries [first, last); BWD: start below `top`, whose covering
     // predecessors number pos0
-    __device__ __forceinline__ void init(const uint2* ent_, uint2 st_range, unsigned tile, unsigned gx, uint32_t top,
-                                         uint32_t pos0) {
+    // sth: the super-tile height's log2 (st_sth)
+    __device__ __forceinline__ void init(const uint2* ent_, uint2 st_range, unsigned tile, unsigned gx, unsigned sth,
+                                         uint32_t top, uint32_t pos0) {
         ent = ent_;
         const unsigned tx = tile % gx, ty = tile / gx;
         lx = tx % GSR_ST_W;
-        ly = ty % GSR_ST_H;
+        ly = ty & ((1u << sth) - 1u);
         head = tail = 0;
         if (FWD) {
             e = st_range.x;
@@ -133,7 +134,7 @@ struct TileList {
         nx2 = load_step(step_after(e));
     }
     __device__ __forceinline__ bool covers(uint32_t key) const {
-        constexpr uint32_t XM = GSR_ST_W - 1u, YM = GSR_ST_H - 1u;
+        constexpr uint32_t XM = (1u << ST_XB) - 1u, YM = (1u << ST_YB) - 1u;
         const uint32_t code = key >> 20, cx0 = code & XM, cx1 = (code >> ST_XB) & XM, cy0 = (code >> (2 * ST_XB)) & YM,
                        cy1 = (code >> (2 * ST_XB + ST_YB)) & YM;  // inclusive maxima
         return (lx - cx0) <= (cx1 - cx0) && (ly - cy0) <= (cy1 - cy0);  // unsigned: also lx >= cx0

@@ -201,13 +201,15 @@ def test_forward_is_deterministic(cfg2):
     np.testing.assert_array_equal(st["n_contrib"], st2["n_contrib"])
 
 
-@pytest.mark.parametrize("W,H,P", [(3840, 2160, 100_000), (5120, 2880, 60_000)])
+@pytest.mark.parametrize("W,H,P", [(2560, 1440, 100_000), (3840, 2160, 100_000), (5120, 2880, 60_000),
+                                   (8192, 4320, 40_000)])
 def test_large_frame_binning_exact(W, H, P):
-    """cfg5's 3840x2160 frame: 30 x 34 = 1020 super-tiles run the fused
-    super-tile binning with four waves per workgroup (eight would exceed its LDS budget);
-    5120x2880 (1800 super-tiles) exceeds that too and runs the emit + offsets scan +
-    one-pass sort path.  Both must reproduce the oracle's (tile, depth, index) lists and
-    tile ranges bit for bit."""
+    """Large frames (SURVEY §8d cfg5): 2560x1440 keeps 8x4-tile super-tiles (460);
+    cfg5's 3840x2160 would need 1020 of them, past the 8-wave scatter's LDS budget, so it
+    takes 8x8-tile super-tiles (510, st_sth); 5120x2880 has 920 of those (fused binning,
+    8 waves); 8192x4320 (2176) exceeds the fused binning and runs the emit + offsets scan +
+    one-pass sort path.  All must reproduce the oracle's (tile, depth, index) lists and tile
+    ranges bit for bit."""
     from gsr import scenes
     cam, gs, c = scenes.build_config("cfg5", device="cpu", seed=1, P=P, W=W, H=H)
     st = run_gpu(cam, gs, mode="sh", sh_degree=c["sh_degree"])
