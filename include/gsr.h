@@ -36,6 +36,9 @@
  *   gsr_sky_xyz_forward / _backward
  *                      the sky Gaussians' shell positions (gaussian_model.py:95-103,159-169)
  *   gsr_view_objective the view's loss and backward coefficients from both partials
+ *   gsr_activations_forward / _backward
+ *                      the model's activations (gaussian_model.py:69-103) in one pass each
+ *                      way, the backward into the optimizer's flat gradient
  *   gsr_ssim_forward / gsr_ssim_backward
  *                      the training loss's SSIM (utils/loss_utils.py:53-96, train.py:78)
  *                      as one fused stencil kernel each way
@@ -261,6 +264,30 @@ int gsr_sky_xyz_forward(int N, const float* angles, const float* radius, const f
                         void* stream);
 int gsr_sky_xyz_backward(int N, const float* angles, const float* radius, const float* grad_xyz, float* d_angles,
                          float* d_radius_partials, void* stream);
+
+/* The model's activations (gaussian_model.py:69-103) over P = n_fg + n_sky Gaussians:
+ * xyz [P,3] = the foreground rows xyz_fg [n_fg,3] and the sky shell points from angles
+ * [n_sky,2], radius [1], center [3] (gsr_sky_xyz_forward), placed by src [P] (the foreground
+ * row >= 0, or -1 - the sky row; null: the first n_fg rows are the foreground); scale =
+ * exp(scale_raw), rot = rot_raw / max(|rot_raw|, 1e-12), op = sigmoid(op_raw) [P]; alb, rough,
+ * metal = sigmoid of the raw [n_fg] rows.  The backward writes (not adds) the raw parameters'
+ * gradients from the activations' upstream gradients (any g_* may be null: zero);
+ * radius_partials: gsr_activations_partials(P, n_fg) floats of scratch. */
+int gsr_activations_partials(int P, int n_fg);
+int gsr_activations_forward(int P, int n_fg, int n_sky, const int* src, const float* xyz_fg, const float* angles,
+                            const float* radius, const float* center, const float* scale_raw, const float* rot_raw,
+                            const float* op_raw, const float* alb_raw, const float* rough_raw, const float* metal_raw,
+                            float* xyz, float* scale, float* rot, float* op, float* alb, float* rough, float* metal,
+                            void* stream);
+int gsr_activations_backward(int P, int n_fg, int n_sky, const int* src, const float* xyz_fg, const float* angles,
+                             const float* radius, const float* center, const float* scale_raw, const float* rot_raw,
+                             const float* op_raw, const float* alb_raw, const float* rough_raw, const float* metal_raw,
+                             const float* scale, const float* rot, const float* op, const float* alb,
+                             const float* rough, const float* metal, const float* g_xyz, const float* g_scale,
+                             const float* g_rot, const float* g_op, const float* g_alb, const float* g_rough,
+                             const float* g_metal, float* d_xyz_fg, float* d_angles, float* d_radius,
+                             float* radius_partials, float* d_scale_raw, float* d_rot_raw, float* d_op_raw,
+                             float* d_alb_raw, float* d_rough_raw, float* d_metal_raw, void* stream);
 
 /* 2D texture lookups with nvdiffrast.torch.texture semantics (csrc/gsr_texture.hip).
  * tex [tex_nb][tex_h][tex_w][C] (tex_nb == 1 broadcasts over the minibatch, else == nb);

@@ -1446,4 +1446,70 @@ int gsr_sky_xyz_backward(int N, const float* angles, const float* radius, const 
     return GSR_OK;
 }
 
+/* ---- the model's activations (csrc/gsr_trainaux.hip) ---- */
+static int act_args(int P, int n_fg, int n_sky, const int* src, const float* xyz_fg, const float* angles,
+                    const float* radius, const float* center, const float* scale_raw, const float* rot_raw,
+                    const float* op_raw, const float* alb_raw, const float* rough_raw, const float* metal_raw,
+                    gsr::ActArgs& a) {
+    if (P < 0 || n_fg < 0 || n_sky < 0 || n_fg + n_sky != P) return 0;
+    if (P && (!scale_raw || !rot_raw || !op_raw)) return 0;
+    if (n_fg && (!xyz_fg || !alb_raw || !rough_raw || !metal_raw)) return 0;
+    if (n_sky && (!angles || !radius || !center)) return 0;
+    a = gsr::ActArgs{P, n_fg, n_sky, src, xyz_fg, angles, radius, center, scale_raw, rot_raw, op_raw, alb_raw, rough_raw,
+                     metal_raw};
+    return 1;
+}
+
+int gsr_activations_partials(int P, int n_fg) {
+    gsr::ActArgs a{};
+    a.P = P;
+    a.Nfg = n_fg;
+    return (P <= 0 && n_fg <= 0) ? 0 : gsr::activation_blocks(a);
+}
+
+int gsr_activations_forward(int P, int n_fg, int n_sky, const int* src, const float* xyz_fg, const float* angles,
+                            const float* radius, const float* center, const float* scale_raw, const float* rot_raw,
+                            const float* op_raw, const float* alb_raw, const float* rough_raw, const float* metal_raw,
+                            float* xyz, float* scale, float* rot, float* op, float* alb, float* rough, float* metal,
+                            void* stream_) {
+    gsr::ActArgs a;
+    if (!act_args(P, n_fg, n_sky, src, xyz_fg, angles, radius, center, scale_raw, rot_raw, op_raw, alb_raw, rough_raw,
+                  metal_raw, a))
+        return fail(GSR_E_ARG, "gsr_activations_forward: bad sizes (P=%d fg=%d sky=%d) or missing inputs", P, n_fg, n_sky);
+    if (P + n_fg == 0) return GSR_OK;
+    if ((P && (!xyz || !scale || !rot || !op)) || (n_fg && (!alb || !rough || !metal)))
+        return fail(GSR_E_ARG, "gsr_activations_forward: missing outputs");
+    gsr::launch_activations_fwd(a, gsr::ActOutW{xyz, scale, rot, op, alb, rough, metal},
+                                reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_activations_backward(int P, int n_fg, int n_sky, const int* src, const float* xyz_fg, const float* angles,
+                             const float* radius, const float* center, const float* scale_raw, const float* rot_raw,
+                             const float* op_raw, const float* alb_raw, const float* rough_raw, const float* metal_raw,
+                             const float* scale, const float* rot, const float* op, const float* alb,
+                             const float* rough, const float* metal, const float* g_xyz, const float* g_scale,
+                             const float* g_rot, const float* g_op, const float* g_alb, const float* g_rough,
+                             const float* g_metal, float* d_xyz_fg, float* d_angles, float* d_radius,
+                             float* radius_partials, float* d_scale_raw, float* d_rot_raw, float* d_op_raw,
+                             float* d_alb_raw, float* d_rough_raw, float* d_metal_raw, void* stream_) {
+    gsr::ActArgs a;
+    if (!act_args(P, n_fg, n_sky, src, xyz_fg, angles, radius, center, scale_raw, rot_raw, op_raw, alb_raw, rough_raw,
+                  metal_raw, a))
+        return fail(GSR_E_ARG, "gsr_activations_backward: bad sizes (P=%d fg=%d sky=%d) or missing inputs", P, n_fg, n_sky);
+    if (P + n_fg == 0) return GSR_OK;
+    if ((P && (!scale || !rot || !op || !d_scale_raw || !d_rot_raw || !d_op_raw)) ||
+        (n_fg && (!alb || !rough || !metal || !d_xyz_fg || !d_alb_raw || !d_rough_raw || !d_metal_raw)) ||
+        (n_sky && (!d_angles || !d_radius || !radius_partials)))
+        return fail(GSR_E_ARG, "gsr_activations_backward: missing buffers");
+    const gsr::ActOut o{nullptr, scale, rot, op, alb, rough, metal};
+    const gsr::ActOut g{g_xyz, g_scale, g_rot, g_op, g_alb, g_rough, g_metal};
+    const gsr::ActGrad d{d_xyz_fg, d_angles, n_sky ? radius_partials : nullptr, d_scale_raw, d_rot_raw, d_op_raw,
+                         d_alb_raw, d_rough_raw, d_metal_raw};
+    gsr::launch_activations_bwd(a, o, g, d, n_sky ? d_radius : nullptr, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

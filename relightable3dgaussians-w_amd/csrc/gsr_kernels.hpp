@@ -387,6 +387,26 @@ void launch_densify_stats(int P, int V, const ViewPtrs<float>& g2d, const ViewPt
                           float* denom, float* maxr, hipStream_t s);
 void launch_sh_basis(int N, int deg, const float* dirs, float* out, hipStream_t s);
 int sky_blocks(int N);
+// the model's activations over P Gaussians (N_fg foreground rows, N_sky sky rows)
+struct ActArgs {
+    int P, Nfg, Nsky;
+    const int* src;  // [P]: the foreground row (>= 0) or -1 - the sky row; null: rows < Nfg are foreground
+    const float *xyz_fg, *angles, *radius, *center;
+    const float *scale_raw, *rot_raw, *op_raw, *alb_raw, *rough_raw, *metal_raw;
+};
+struct ActOut {  // activated tensors (or their upstream gradients)
+    const float *xyz, *scale, *rot, *op, *alb, *rough, *metal;
+};
+struct ActOutW {
+    float *xyz, *scale, *rot, *op, *alb, *rough, *metal;
+};
+struct ActGrad {  // the raw parameters' gradients
+    float *xyz_fg, *angles, *radius_part, *scale_raw, *rot_raw, *op_raw, *alb_raw, *rough_raw, *metal_raw;
+};
+int activation_blocks(const ActArgs& a);
+void launch_activations_fwd(const ActArgs& a, const ActOutW& o, hipStream_t s);
+void launch_activations_bwd(const ActArgs& a, const ActOut& o, const ActOut& g, const ActGrad& d, float* d_radius,
+                            hipStream_t s);
 void launch_sky_xyz_fwd(int N, const float* ang, const float* radius, const float* center, float* out, hipStream_t s);
 void launch_sky_xyz_bwd(int N, const float* ang, const float* radius, const float* g, float* d_ang, float* d_rad_part,
                         hipStream_t s);

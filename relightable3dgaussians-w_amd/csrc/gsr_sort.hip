@@ -20,12 +20,19 @@
 
 namespace gsr {
 
-constexpr int WAVE_ITEMS = SORT_TILE / 4;  // 1024 contiguous keys per wave
+constexpr int WAVE_ITEMS = SORT_TILE / 4;  // contiguous keys per wave
 
+// The depth sort's digit width (4 passes of 8 bits by default; GSR_DEPTH_BITS = 11 sorts the
+// 32-bit keys in 3 passes of 11 + 11 + 10 bits).
+#ifndef GSR_DEPTH_BITS
+#define GSR_DEPTH_BITS 8
+#endif
+
+template <int BITS>
 __device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
     uint64_t m = __ballot(valid);
 #pragma unroll
-    for (int b = 0; b < 8; b++) {
+    for (int b = 0; b < BITS; b++) {
         const bool bit = (d >> b) & 1u;
         const uint64_t bb = __ballot(bit);
         m &= bit ? bb : ~bb;
@@ -33,12 +40,14 @@ __device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
     return valid ? m : 0ull;
 }
 
+template <int BITS>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const uint32_t* keys, int shift,
                                                                uint32_t mask, uint32_t* hist, int nb) {
+    constexpr int NB = 1 << BITS;
     // per-wave LDS sub-histograms (ds_add_u32), keys read 16 B per lane
-    __shared__ uint32_t cnt[4][256];
+    __shared__ uint32_t cnt[4][NB];
     const int wave = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 4 * NB; i += SORT_THREADS) (&cnt[0][0])[i] = 0;
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring tiles' digit runs merge in one L2
     const long long tile_base = (long long)blk * SORT_TILE;
@@ -57,8 +66,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(long long n, const 
         for (long long i = tile_base + threadIdx.x; i < n; i += SORT_THREADS) atomicAdd(&wc[(keys[i] >> shift) & mask], 1u);
     }
     __syncthreads();
-    const int d = threadIdx.x;
-    hist[(long long)d * nb + blk] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
+    for (int d = threadIdx.x; d < NB; d += SORT_THREADS)
+        hist[(long long)d * nb + blk] = cnt[0][d] + cnt[1][d] + cnt[2][d] + cnt[3][d];
 }
 
 // hist[d][0..nb) -> exclusive prefix within digit d; digit_tot[d] = the digit's total
@@ -108,13 +117,29 @@ __global__ void __launch_bounds__(SORT_THREADS) k_digit_scan(uint32_t* hist, int
     digit_row_scan(hist + (long long)blockIdx.x * nb, nb, digit_tot + blockIdx.x, sh);
 }
 
+// Exclusive scan over the NB digits of a workgroup, DPT = NB / 256 consecutive digits per
+// thread: the values v[0..DPT) of digits threadIdx.x * DPT + j -> their exclusive prefixes.
+template <int DPT>
+__device__ __forceinline__ void digits_exclusive_scan(uint32_t (&v)[DPT], uint32_t* sh) {
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < DPT; j++) sum += v[j];
+    uint32_t run = block256_exclusive_scan(sum, sh, (uint32_t*)nullptr);
+#pragma unroll
+    for (int j = 0; j < DPT; j++) {
+        const uint32_t x = v[j];
+        v[j] = run;
+        run += x;
+    }
+}
+
 // AUX: an 8-byte side payload (the Gaussians' tile rects) moves with every pair, so that the
 // depth-sorted order never has to gather it at random afterwards
 // The offsets table has ocol columns (0: nb) and block blk's column is blk * ostride (the
 // preprocess-made first table of the depth sort has 8 columns per 2048-key block).
 // (Counting the NEXT pass's histogram here with global atomics per key, instead of the
 // separate k_radix_hist, measured 5-15x slower: ~1.5M L2 atomics per pass.)
-template <bool AUX>
+template <bool AUX, int BITS = 8>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
                                                                   const uint32_t* offsets, const uint32_t* digit_tot,
@@ -122,15 +147,17 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
                                                                   const uint2* aux_in, uint2* aux_out, int ocol = 0,
                                                                   int ostride = 1,
                                                                   unsigned long long* pv_out = nullptr) {
+    constexpr int NB = 1 << BITS, DPT = NB / SORT_THREADS;
+    static_assert(DPT >= 1, "at least one digit per thread");
     __shared__ uint32_t s_keys[SORT_TILE];
     __shared__ uint32_t s_vals[SORT_TILE];
     __shared__ uint2 s_aux[AUX ? SORT_TILE : 1];
-    __shared__ uint32_t wh[4][256];
-    __shared__ uint32_t dstart[256];
-    __shared__ uint32_t goff[256];
+    __shared__ uint32_t wh[4][NB];
+    __shared__ uint32_t dstart[NB];
+    __shared__ uint32_t goff[NB];
     __shared__ uint32_t scan_sh[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < 4 * 256; i += SORT_THREADS) (&wh[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < 4 * NB; i += SORT_THREADS) (&wh[0][0])[i] = 0;
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring tiles' digit runs merge in one L2
     const long long tile_base = (long long)blk * SORT_TILE;
@@ -139,7 +166,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     uint2 aux[AUX ? SORT_ITEMS : 1];
     volatile uint32_t* wc = wh[wave];
     const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
-    // all loads first (32 per lane in flight), then the ranking
+    // all loads first (SORT_ITEMS per lane in flight), then the ranking
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
         const long long i = base + k * 64 + lane;
@@ -152,7 +179,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         const long long i = base + k * 64 + lane;
         const bool valid = i < n;
         const uint32_t d = (key[k] >> shift) & mask;
-        const uint64_t m = peer_mask(d, valid);
+        const uint64_t m = peer_mask<BITS>(d, valid);
         const int leader = valid ? (int)(__ffsll((unsigned long long)m) - 1) : lane;
         uint32_t old = 0;
         if (valid && lane == leader) {
@@ -164,19 +191,32 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     }
     __syncthreads();
     {
-        const int d = threadIdx.x;
-        const uint32_t c0 = wh[0][d], c1 = wh[1][d], c2 = wh[2][d], c3 = wh[3][d];
-        const uint32_t start = block256_exclusive_scan(c0 + c1 + c2 + c3, scan_sh, (uint32_t*)nullptr);
-        wh[0][d] = start;
-        wh[1][d] = start + c0;
-        wh[2][d] = start + c0 + c1;
-        wh[3][d] = start + c0 + c1 + c2;
-        dstart[d] = start;
-        const uint32_t dbase = block256_exclusive_scan(digit_tot[d], scan_sh, (uint32_t*)nullptr);
-        // the depth sort's top-byte pass: culled keys (0xFFFFFFFF) are exactly digit 255, so
-        // its start is the visible count P_v
-        if (pv_out && blockIdx.x == 0 && d == 255) *pv_out = dbase;
-        goff[d] = dbase + offsets[(long long)d * (ocol ? ocol : nb) + (long long)blk * ostride];
+        // digits d = threadIdx.x * DPT + j: the tile's digit starts and each wave's run start,
+        // and the digits' global bases (exclusive scan of the digit totals)
+        uint32_t c[4][DPT], st[DPT], gb[DPT];
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            const int d = threadIdx.x * DPT + j;
+#pragma unroll
+            for (int w = 0; w < 4; w++) c[w][j] = wh[w][d];
+            st[j] = c[0][j] + c[1][j] + c[2][j] + c[3][j];
+            gb[j] = digit_tot[d];
+        }
+        digits_exclusive_scan<DPT>(st, scan_sh);
+        digits_exclusive_scan<DPT>(gb, scan_sh);
+#pragma unroll
+        for (int j = 0; j < DPT; j++) {
+            const int d = threadIdx.x * DPT + j;
+            wh[0][d] = st[j];
+            wh[1][d] = st[j] + c[0][j];
+            wh[2][d] = st[j] + c[0][j] + c[1][j];
+            wh[3][d] = st[j] + c[0][j] + c[1][j] + c[2][j];
+            dstart[d] = st[j];
+            // the depth sort's top pass: culled keys (0xFFFFFFFF) are exactly its largest digit
+            // (mask), so that digit's start is the visible count P_v
+            if (pv_out && blockIdx.x == 0 && (uint32_t)d == mask) *pv_out = gb[j];
+            goff[d] = gb[j] + offsets[(long long)d * (ocol ? ocol : nb) + (long long)blk * ostride];
+        }
     }
     __syncthreads();
 #pragma unroll
@@ -233,7 +273,7 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
     for (int shift = 0; shift < end_bit; shift += 8) {
         const int nbits = (end_bit - shift) < 8 ? (end_bit - shift) : 8;
         const uint32_t mask = (1u << nbits) - 1u;
-        hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
+        hipLaunchKernelGGL(k_radix_hist<8>, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, shift, mask, hist, nb);
         hipLaunchKernelGGL(k_digit_scan, dim3(256), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot);
         if (ain) {
             hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SORT_THREADS), 0, s, n, kin, vin, shift, mask,
@@ -251,17 +291,18 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
 }
 
 size_t depth_sort_temp_bytes(long long P) {
-    const size_t nb = (size_t)sort_blocks(P);
-    return 4 * (256 * nb + 256) + 256;
+    const size_t nb = (size_t)sort_blocks(P), NB = (size_t)1 << GSR_DEPTH_BITS;
+    return 4 * (NB * nb + NB) + 256;
 }
 
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
                unsigned long long* pv_out, hipStream_t s, void* zero, size_t zero_bytes) {
     if (P <= 0) return -1;
+    constexpr int BITS = GSR_DEPTH_BITS, NB = 1 << BITS, NPASS = (32 + BITS - 1) / BITS;
     const int nb = sort_blocks(P);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
-    uint32_t* digit_tot = hist + 256LL * nb;
+    uint32_t* digit_tot = hist + (long long)NB * nb;
     const uint32_t* kin = keys_in;
     const uint32_t* vin = nullptr;  // values 0..P-1
     uint32_t* out_k[2] = {keys, keys_alt};
@@ -269,19 +310,21 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
     const uint2* ain = aux_in;
     uint2* out_a[2] = {aux, aux_alt};
     int cur = 0;
-    for (int pass = 0; pass < 4; pass++) {
-        const int shift = 8 * pass;
-        hipLaunchKernelGGL(k_radix_hist, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, shift, 255u, hist, nb);
-        // a quarter of the zero-fill (16-B multiples) rides in each pass's digit scan
+    for (int pass = 0; pass < NPASS; pass++) {
+        const int shift = BITS * pass;
+        const int nbits = 32 - shift < BITS ? 32 - shift : BITS;
+        const uint32_t mask = (nbits >= 32) ? 0xFFFFFFFFu : ((1u << nbits) - 1u);
+        hipLaunchKernelGGL(k_radix_hist<BITS>, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, shift, mask, hist, nb);
+        // a share of the zero-fill (16-B multiples) rides in each pass's digit scan
         const long long n4 = (long long)(zero ? zero_bytes / 16 : 0);
-        const long long q0 = n4 * pass / 4, q1 = n4 * (pass + 1) / 4;
+        const long long q0 = n4 * pass / NPASS, q1 = n4 * (pass + 1) / NPASS;
         const long long per_blk = (long long)SORT_THREADS * ZERO_F4_PER_THREAD;
         const unsigned zb = (unsigned)((q1 - q0 + per_blk - 1) / per_blk);
-        hipLaunchKernelGGL(k_digit_scan, dim3(256 + zb), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot,
-                           zb ? reinterpret_cast<float4*>(zero) + q0 : (float4*)nullptr, q1 - q0, 256);
-        hipLaunchKernelGGL(k_radix_scatter<true>, dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift, 255u, hist,
-                           digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1,
-                           pass == 3 ? pv_out : (unsigned long long*)nullptr);
+        hipLaunchKernelGGL(k_digit_scan, dim3(NB + zb), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot,
+                           zb ? reinterpret_cast<float4*>(zero) + q0 : (float4*)nullptr, q1 - q0, NB);
+        hipLaunchKernelGGL((k_radix_scatter<true, BITS>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift, mask,
+                           hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1,
+                           pass == NPASS - 1 ? pv_out : (unsigned long long*)nullptr);
         ain = out_a[cur];
         kin = out_k[cur];
         vin = out_v[cur];

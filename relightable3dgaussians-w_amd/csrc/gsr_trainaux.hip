@@ -14,7 +14,11 @@
 //    view's visible Gaussians, in view order;
 //  * the real SH basis (utils/sh_utils.py:81-151, degrees 0-4) at normalised directions (the
 //    envlight regulariser's random directions);
-//  * the sky Gaussians' shell positions (gaussian_model.py:95-103,159-169) and their backward.
+//  * the sky Gaussians' shell positions (gaussian_model.py:95-103,159-169) and their backward;
+//  * the model's activations (gaussian_model.py:69-80,84-103: exp scaling, normalised
+//    rotation, sigmoid opacity and materials, get_xyz's scatter of the foreground rows and
+//    the shell) in one pass, and one backward pass writing the raw parameters' gradients
+//    straight into the optimizer's flat gradient (no autograd accumulation kernels).
 // All HBM-bound streaming kernels, FMA contraction off where a result is compared with
 // PyTorch's elementwise arithmetic.
 #include "gsr_kernels.hpp"
@@ -210,6 +214,137 @@ __global__ void __launch_bounds__(256) k_sky_xyz_bwd(int N, const float* __restr
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dr;
     __syncthreads();
     if (threadIdx.x == 0) d_rad_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// ---- activations (ActArgs, gsr_kernels.hpp) ----------------------------------------------
+__device__ __forceinline__ float act_sigmoid(float x) { return 1.f / (1.f + expf(-x)); }  // as torch's kernel
+constexpr float ACT_NORM_EPS = 1e-12f;  // F.normalize's eps
+
+__global__ void __launch_bounds__(256) k_activations_fwd(ActArgs a, ActOutW o) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t < a.P) {
+        // position: a foreground row or a point on the sky shell
+        const int r = a.src ? a.src[t] : (t < a.Nfg ? t : -1 - (t - a.Nfg));
+        float x, y, z;
+        if (r >= 0) {
+            x = a.xyz_fg[3 * r];
+            y = a.xyz_fg[3 * r + 1];
+            z = a.xyz_fg[3 * r + 2];
+        } else {
+            const int j = -1 - r;
+            const float th = fminf(fmaxf(a.angles[2 * j], 0.f), SKY_HALF_PI);
+            const float ph = fminf(fmaxf(a.angles[2 * j + 1], -SKY_HALF_PI), SKY_HALF_PI);
+            const float rad = a.radius[0];
+            const float st = sinf(th), ct = cosf(th), sp = sinf(ph), cp = cosf(ph);
+            x = rad * (st * sp) + a.center[0];
+            y = rad * (-ct) + a.center[1];
+            z = rad * (st * cp) + a.center[2];
+        }
+        o.xyz[3 * t] = x;
+        o.xyz[3 * t + 1] = y;
+        o.xyz[3 * t + 2] = z;
+#pragma unroll
+        for (int k = 0; k < 3; k++) o.scale[3 * t + k] = expf(a.scale_raw[3 * t + k]);
+        const float4 q = *reinterpret_cast<const float4*>(a.rot_raw + 4 * t);
+        const float n = sqrtf(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
+        const float d = fmaxf(n, ACT_NORM_EPS);
+        *reinterpret_cast<float4*>(o.rot + 4 * t) = make_float4(q.x / d, q.y / d, q.z / d, q.w / d);
+        o.op[t] = act_sigmoid(a.op_raw[t]);
+    }
+    if (t < a.Nfg) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) o.alb[3 * t + k] = act_sigmoid(a.alb_raw[3 * t + k]);
+        o.rough[t] = act_sigmoid(a.rough_raw[t]);
+        o.metal[t] = act_sigmoid(a.metal_raw[t]);
+    }
+}
+
+// upstream gradients g (any may be null: zero) of the activations o -> the raw parameters'
+// gradients d (written, not added), with torch's backward formulas: exp: g y; sigmoid:
+// g (1 - y) y; normalize (y = x / max(|x|, eps)): g / d - x (g . x) / d^2 / |x| (the second
+// term only when |x| > eps); shell: d angles zero where clamped, per-workgroup partials of
+// d radius (k_sum_into adds them)
+__global__ void __launch_bounds__(256) k_activations_bwd(ActArgs a, ActOut o, ActOut g, ActGrad d) {
+    __shared__ float red[4];
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    float drad = 0.f;
+    if (t < a.P) {
+        const int r = a.src ? a.src[t] : (t < a.Nfg ? t : -1 - (t - a.Nfg));
+        const float gx = g.xyz ? g.xyz[3 * t] : 0.f, gy = g.xyz ? g.xyz[3 * t + 1] : 0.f,
+                    gz = g.xyz ? g.xyz[3 * t + 2] : 0.f;
+        if (r >= 0) {
+            d.xyz_fg[3 * r] = gx;
+            d.xyz_fg[3 * r + 1] = gy;
+            d.xyz_fg[3 * r + 2] = gz;
+        } else {
+            const int j = -1 - r;
+            const float t0 = a.angles[2 * j], p0 = a.angles[2 * j + 1];
+            const float th = fminf(fmaxf(t0, 0.f), SKY_HALF_PI), ph = fminf(fmaxf(p0, -SKY_HALF_PI), SKY_HALF_PI);
+            const float rad = a.radius[0];
+            const float st = sinf(th), ct = cosf(th), sp = sinf(ph), cp = cosf(ph);
+            drad = (gx * (st * sp) + gy * (-ct)) + gz * (st * cp);
+            const float dt = rad * ((gx * (ct * sp) + gy * st) + gz * (ct * cp));
+            const float dp = rad * (gx * (st * cp) - gz * (st * sp));
+            d.angles[2 * j] = (t0 >= 0.f && t0 <= SKY_HALF_PI) ? dt : 0.f;
+            d.angles[2 * j + 1] = (p0 >= -SKY_HALF_PI && p0 <= SKY_HALF_PI) ? dp : 0.f;
+        }
+#pragma unroll
+        for (int k = 0; k < 3; k++) d.scale_raw[3 * t + k] = g.scale ? g.scale[3 * t + k] * o.scale[3 * t + k] : 0.f;
+        if (g.rot) {
+            const float4 x = *reinterpret_cast<const float4*>(a.rot_raw + 4 * t);
+            const float4 gr = *reinterpret_cast<const float4*>(g.rot + 4 * t);
+            const float n = sqrtf(((x.x * x.x + x.y * x.y) + x.z * x.z) + x.w * x.w);
+            const float dd = fmaxf(n, ACT_NORM_EPS);
+            const float c = n > ACT_NORM_EPS ? (((gr.x * x.x + gr.y * x.y) + gr.z * x.z) + gr.w * x.w) / (dd * dd) / n : 0.f;
+            *reinterpret_cast<float4*>(d.rot_raw + 4 * t) =
+                make_float4(gr.x / dd - x.x * c, gr.y / dd - x.y * c, gr.z / dd - x.z * c, gr.w / dd - x.w * c);
+        } else {
+            *reinterpret_cast<float4*>(d.rot_raw + 4 * t) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        d.op_raw[t] = g.op ? g.op[t] * (1.f - o.op[t]) * o.op[t] : 0.f;
+    }
+    if (t < a.Nfg) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) {
+            const float y = o.alb[3 * t + k];
+            d.alb_raw[3 * t + k] = g.alb ? g.alb[3 * t + k] * (1.f - y) * y : 0.f;
+        }
+        d.rough_raw[t] = g.rough ? g.rough[t] * (1.f - o.rough[t]) * o.rough[t] : 0.f;
+        d.metal_raw[t] = g.metal ? g.metal[t] * (1.f - o.metal[t]) * o.metal[t] : 0.f;
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) drad += __shfl_xor(drad, k, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = drad;
+    __syncthreads();
+    if (threadIdx.x == 0 && d.radius_part) d.radius_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// out[0] = the sum of n partials in a fixed order (one workgroup)
+__global__ void __launch_bounds__(256) k_sum_into(int n, const float* __restrict__ part, float* __restrict__ out) {
+    __shared__ float red[4];
+    float v = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) v += part[i];
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) v += __shfl_xor(v, k, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+int activation_blocks(const ActArgs& a) {
+    const int n = a.P > a.Nfg ? a.P : a.Nfg;
+    return (n + 255) / 256;
+}
+
+void launch_activations_fwd(const ActArgs& a, const ActOutW& o, hipStream_t s) {
+    hipLaunchKernelGGL(k_activations_fwd, dim3(activation_blocks(a)), dim3(256), 0, s, a, o);
+}
+
+void launch_activations_bwd(const ActArgs& a, const ActOut& o, const ActOut& g, const ActGrad& d, float* d_radius,
+                            hipStream_t s) {
+    const int nb = activation_blocks(a);
+    hipLaunchKernelGGL(k_activations_bwd, dim3(nb), dim3(256), 0, s, a, o, g, d);
+    if (d.radius_part && d_radius) hipLaunchKernelGGL(k_sum_into, dim3(1), dim3(256), 0, s, nb, d.radius_part, d_radius);
 }
 
 int view_regs_blocks(int P) {

@@ -78,6 +78,9 @@ def _declare(lib):
     lib.gsr_sky_xyz_partials.argtypes = [i]
     lib.gsr_sky_xyz_forward.argtypes = [i, vp, vp, vp, vp, vp]
     lib.gsr_sky_xyz_backward.argtypes = [i, vp, vp, vp, vp, vp, vp]
+    lib.gsr_activations_partials.argtypes = [i, i]
+    lib.gsr_activations_forward.argtypes = [i, i, i] + [vp] * 18 + [vp]
+    lib.gsr_activations_backward.argtypes = [i, i, i] + [vp] * 34 + [vp]
     lib.gsr_ssim_partials.argtypes = [i, i, i]
     lib.gsr_ssim_partials.restype = C.c_longlong
     lib.gsr_ssim_forward.argtypes = [i, i, i, vp, vp, vp, C.c_longlong, C.POINTER(C.c_float), vp, vp, vp]
@@ -103,7 +106,7 @@ def _declare(lib):
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward", "gsr_view_objective", "gsr_view_regularisers_forward",
                "gsr_view_regularisers_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
-               "gsr_sky_xyz_backward",
+               "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
                "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int

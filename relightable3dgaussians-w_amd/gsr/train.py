@@ -115,6 +115,8 @@ class FlatParams:
         """Autograd accumulated into the preset views (not into fresh tensors)."""
         for name, off in zip(self.names, self.offsets):
             g = self.params[name].grad
+            if self.params[name].numel() == 0:  # an empty group (no sky): nothing to accumulate
+                continue
             if g is None or g.data_ptr() != self.grad.data_ptr() + 4 * off:
                 raise RuntimeError(f"gradient of {name} left the flat buffer")
 
@@ -614,6 +616,55 @@ def sky_angles_clamped(a: torch.Tensor) -> torch.Tensor:
     return torch.cat((th.unsqueeze(1), ph.unsqueeze(1)), dim=1)
 
 
+class _Activations(torch.autograd.Function):
+    """RelitScene's activations (gaussian_model.py:69-103) in one HIP pass each way
+    (gsr_activations_forward / _backward).  The backward writes the raw parameters' gradients
+    into the scene's flat gradient (their preset .grad views) and returns none to autograd,
+    so no AccumulateGrad kernel runs for them; the parameters receive gradients from these
+    activations only."""
+
+    @staticmethod
+    def forward(ctx, scene, xyz_fg, angles, radius, scale_raw, rot_raw, op_raw, alb_raw, rough_raw, metal_raw):
+        lay = scene.layout
+        P, Nfg, Nsky = lay.P, lay.n_fg, lay.n_sky
+        dev = xyz_fg.device
+        f = dict(dtype=torch.float32, device=dev)
+        xyz, scale, rot = torch.empty(P, 3, **f), torch.empty(P, 3, **f), torch.empty(P, 4, **f)
+        op = torch.empty(P, 1, **f)
+        alb, rough, metal = torch.empty(Nfg, 3, **f), torch.empty(Nfg, 1, **f), torch.empty(Nfg, 1, **f)
+        center = scene.sky_center.float().contiguous()
+        ins = [xyz_fg, angles, radius, center, scale_raw, rot_raw, op_raw, alb_raw, rough_raw, metal_raw]
+        ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
+        src = None if lay.src is None else lay.src.data_ptr()
+        _lib.check(_lib.lib().gsr_activations_forward(P, Nfg, Nsky, src, *[ptr(t) for t in ins],
+                                                      *[ptr(t) for t in (xyz, scale, rot, op, alb, rough, metal)],
+                                                      _lib.stream_of(dev)), "gsr_activations_forward")
+        ctx.scene = scene
+        ctx.ins = ins
+        ctx.outs = (scale, rot, op, alb, rough, metal)
+        ctx.set_materialize_grads(False)
+        return xyz, scale, rot, op, alb, rough, metal
+
+    @staticmethod
+    def backward(ctx, *g):
+        scene = ctx.scene
+        lay, fp = scene.layout, scene.fp
+        P, Nfg, Nsky = lay.P, lay.n_fg, lay.n_sky
+        dev = ctx.ins[0].device
+        ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
+        gs = [None if t is None else t.float().contiguous() for t in g]
+        d = {n: fp.params[n].grad for n in ("xyz", "sky_angles", "sky_radius", "scaling", "rotation", "opacity",
+                                             "albedo", "roughness", "metalness")}
+        part = torch.empty(max(1, _lib.lib().gsr_activations_partials(P, Nfg)), dtype=torch.float32, device=dev)
+        src = None if lay.src is None else lay.src.data_ptr()
+        _lib.check(_lib.lib().gsr_activations_backward(
+            P, Nfg, Nsky, src, *[ptr(t) for t in ctx.ins], *[ptr(t) for t in ctx.outs], *[ptr(t) for t in gs],
+            ptr(d["xyz"]), ptr(d["sky_angles"]), ptr(d["sky_radius"]), part.data_ptr(), ptr(d["scaling"]),
+            ptr(d["rotation"]), ptr(d["opacity"]), ptr(d["albedo"]), ptr(d["roughness"]), ptr(d["metalness"]),
+            _lib.stream_of(dev)), "gsr_activations_backward")
+        return (None,) * 10
+
+
 class _FusedSkyXYZ(torch.autograd.Function):
     """sky_xyz as one HIP pass each way (gsr_sky_xyz_forward/backward); differentiable in
     the angles and the radius (the centre is a constant of the scene)."""
@@ -669,6 +720,14 @@ class SkyLayout:
         self.tail = bool(m[self.n_fg:].all()) and not bool(m[:self.n_fg].any())
         self.fg_idx = torch.nonzero(~m).reshape(-1)
         self.sky_idx = torch.nonzero(m).reshape(-1)
+        # the fused activations' row map (gsr_activations_*): the foreground row, or -1 - the
+        # sky row, per Gaussian; None for the tail layout
+        self.src = None
+        if self.n_sky and not self.tail:
+            src = torch.empty(self.P, dtype=torch.int32, device=m.device)
+            src[self.fg_idx] = torch.arange(self.n_fg, dtype=torch.int32, device=m.device)
+            src[self.sky_idx] = -1 - torch.arange(self.n_sky, dtype=torch.int32, device=m.device)
+            self.src = src
 
     def xyz(self, xyz_fg: torch.Tensor, xyz_sky: torch.Tensor) -> torch.Tensor:
         if self.n_sky == 0:
@@ -768,6 +827,18 @@ class RelitScene:
             sky = sky_xyz(p["sky_angles"], p["sky_radius"], self.sky_center)
         return self.layout.xyz(p["xyz"], sky)
 
+    def model_fused(self):
+        """model() on the fused activation kernels (gsr_activations_*): one launch forward,
+        and a backward that writes the raw parameters' gradients straight into the flat
+        gradient (no per-leaf autograd accumulation).  GPU scenes only."""
+        p = self.fp.params
+        outs = _Activations.apply(self, p["xyz"], p["sky_angles"], p["sky_radius"], p["scaling"], p["rotation"],
+                                  p["opacity"], p["albedo"], p["roughness"], p["metalness"])
+        xyz, scaling, rotation, opacity, albedo, rough, metal = outs
+        return types.SimpleNamespace(get_xyz=xyz, get_scaling=scaling, get_rotation=rotation, get_opacity=opacity,
+                                     get_albedo=albedo, get_roughness=rough, get_metalness=metal,
+                                     get_is_sky=self.is_sky)
+
     def model(self, params=None):
         p = self.fp.params if params is None else params
         # get_xyz is made on the current (main) stream: the views render on side streams, and
@@ -822,7 +893,7 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     streams = [main] if not streams else list(streams)
     # the activations are computed once per iteration and the views' losses share one
     # backward (autograd sums the views' gradients exactly as sequential backwards would)
-    pc = scene.model()
+    pc = scene.model_fused() if dev.type == "cuda" else scene.model()
     # the environment MLP runs once for the rank's views, on the main stream (its leaves live
     # there): embeddings -> MLPNet (training-mode dropout) -> env SH (+ noise) and sky SH
     V = len(views)

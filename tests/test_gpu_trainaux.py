@@ -124,3 +124,61 @@ def test_densify_stats_fused_matches_per_view():
     assert torch.equal(a.d["max_radii2D"], b.d["max_radii2D"])
     np.testing.assert_allclose(a.d["xyz_gradient_accum"].cpu().numpy(), b.d["xyz_gradient_accum"].cpu().numpy(),
                                rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("layout", ["tail", "interleaved", "no_sky"])
+def test_fused_activations_match_torch(layout):
+    """RelitScene.model_fused (gsr_activations_*) against model()'s PyTorch activations:
+    values, and the raw parameters' gradients it writes into the flat gradient against
+    autograd's, for the sky rows last, interleaved, and absent; angles past the clamp bounds
+    included."""
+    from gsr import train
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(17)
+    P = 5003
+    if layout == "tail":
+        is_sky = torch.zeros(P, dtype=torch.bool)
+        is_sky[P - 700:] = True
+    elif layout == "interleaved":
+        is_sky = torch.rand(P, generator=g) < 0.15
+    else:
+        is_sky = torch.zeros(P, dtype=torch.bool)
+    nf = int((~is_sky).sum())
+    xyz = torch.randn(P, 3, generator=g) * 2 + torch.tensor([0.0, 0.0, 5.0])
+    xyz[is_sky] = torch.nn.functional.normalize(torch.randn(int(is_sky.sum()), 3, generator=g), dim=-1) * 30
+    scene = train.RelitScene(xyz, torch.randn(P, 3, generator=g) - 3, torch.randn(P, 4, generator=g),
+                             torch.randn(P, 1, generator=g), torch.randn(nf, 3, generator=g), torch.randn(nf, 1, generator=g),
+                             torch.randn(nf, 1, generator=g), is_sky, 2, dev)
+    if int(is_sky.sum()):
+        with torch.no_grad():
+            a = scene.fp.params["sky_angles"]
+            a[:7, 0] = torch.tensor([-0.2, 0.0, torch.pi / 2, 1.7, 0.4, 0.4, 0.4])
+            a[:7, 1] = torch.tensor([0.1, 0.1, 0.1, 0.1, -1.8, torch.pi / 2, 1.9])
+    names = ["get_xyz", "get_scaling", "get_rotation", "get_opacity", "get_albedo", "get_roughness", "get_metalness"]
+    ref = scene.model()
+    got = scene.model_fused()
+    for n in names:
+        a, b = getattr(got, n), getattr(ref, n)
+        assert a.shape == b.shape, n
+        assert float((a - b).abs().max()) <= 2e-6 * max(1.0, float(b.abs().max())), n
+    ws = [torch.randn(getattr(ref, n).shape, generator=g).to(dev) for n in names]
+    scene.fp.zero_grad()
+    sum((getattr(got, n) * w).sum() for n, w in zip(names, ws)).backward()
+    fused = scene.fp.grad.clone()
+    scene.fp.check_grads_in_place()
+    scene.fp.zero_grad()
+    sum((getattr(ref, n) * w).sum() for n, w in zip(names, ws)).backward()
+    torch.cuda.synchronize()
+    for name in ("xyz", "sky_angles", "sky_radius", "scaling", "rotation", "opacity", "albedo", "roughness",
+                 "metalness"):
+        i = scene.fp.names.index(name)
+        a = fused[scene.fp.offsets[i]:scene.fp.ends[i]].cpu()
+        b = scene.fp.grad[scene.fp.offsets[i]:scene.fp.ends[i]].cpu()
+        if b.numel() == 0:  # an empty group (no sky rows)
+            assert a.numel() == 0, name
+            continue
+        if float(b.abs().max()) == 0:
+            assert float(a.abs().max()) == 0, name
+            continue
+        e = float((a - b).norm() / b.norm())
+        assert e < 1e-5, (name, e)
