@@ -139,7 +139,14 @@ int gsr_forward_channels(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_
 
 /* Backward of gsr_forward_channels: dL_dout [nch,H,W] -> dL_dfeatures [P][feature_stride]
  * (padding columns zero) and the geometric gradients of gsr_backward (their sum over the
- * channels' separate calls). */
+ * channels' separate calls).  dL_dcov3D may be null (no cov3D_precomp).  `accumulate`: bits
+ * GSR_ACC_MEAN3D / _SCALE / _ROT / _OPACITY add those gradients into the given buffers
+ * instead of overwriting them (several views' gradients summed by the kernel that makes
+ * them). */
+#define GSR_ACC_MEAN3D 1u
+#define GSR_ACC_SCALE 2u
+#define GSR_ACC_ROT 4u
+#define GSR_ACC_OPACITY 8u
 int gsr_backward_channels(int P, int nch, int feature_stride, const float* features, int R, const float* background,
                           int width, int height, const float* means3D, const float* scales, float scale_modifier,
                           const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
@@ -147,7 +154,7 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
                           const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
                           const float* dL_dout, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
                           float* dL_dfeatures, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
-                          void* stream);
+                          unsigned accumulate, void* stream);
 
 /* render()'s per-Gaussian channels in one pass (gaussian_renderer/__init__.py:120-200):
  * features [P][16] = [rgb, diffuse, specular, depth, 0.5 n + 0.5, 1, 0, 0], with
@@ -168,14 +175,19 @@ int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation,
                        float* features, void* workspace, void* stream);
 /* Backward: dL_dfeatures [P][16] -> d_xyz [P,3], d_rotation [P,4], d_albedo [N_fg,3],
  * d_roughness / d_metalness [N_fg] (may be NULL), d_base, d_sky_sh (may be NULL).  The
- * scaling gets no gradient (the axis is an argmin). */
+ * scaling gets no gradient (the axis is an argmin).  `accumulate`: bits GSR_ACC_MEAN3D
+ * (d_xyz), GSR_ACC_ROT (d_rotation), GSR_ACC_ALBEDO / _ROUGH / _METAL add into those
+ * buffers instead of overwriting them. */
+#define GSR_ACC_ALBEDO 16u
+#define GSR_ACC_ROUGH 32u
+#define GSR_ACC_METAL 64u
 int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
                                 const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
                                 const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
                                 int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
                                 const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
                                 float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
-                                void* workspace, void* stream);
+                                void* workspace, unsigned accumulate, void* stream);
 
 /* render()'s image-space tail over the composite's images ([H,W] planes, [3,H,W] for n01):
  *   normal     = ((n01 - 0.5) * 2 * (normal_view ? -1 : 1)) * sky + (1 - sky)
@@ -243,7 +255,8 @@ int gsr_view_loss_backward(int npix, const float* img, const float* gt, const fl
  * per view v: [0] #visible foreground, [1] #visible sky, [2] sum min-scale over visible
  * foreground, [3] sum depth over visible sky, [4] sum depth over visible foreground.
  * Backward: grad_sums [5V] (device) are the sums' upstream gradients; d_xyz / d_scaling
- * (either may be null) are overwritten.  gsr_densify_stats updates accum / denom /
+ * (either may be null) are overwritten, or added to with GSR_ACC_MEAN3D / GSR_ACC_SCALE in
+ * `accumulate`.  gsr_densify_stats updates accum / denom /
  * max_radii [P] in place over the views in order. */
 int gsr_view_regularisers_partials(int P);
 int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* scaling, const int* const* radii,
@@ -251,7 +264,7 @@ int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* s
                                   void* stream);
 int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int* const* radii,
                                    const unsigned char* is_sky, const float* depth_cols, const float* grad_sums,
-                                   float* d_xyz, float* d_scaling, void* stream);
+                                   float* d_xyz, float* d_scaling, unsigned accumulate, void* stream);
 int gsr_densify_stats(int P, int V, const float* const* grad_means2D, const int* const* radii, float* accum,
                       float* denom, float* max_radii, void* stream);
 /* Real SH basis [N][(deg+1)^2] at the normalised directions dirs [N,3], deg 0..4. */

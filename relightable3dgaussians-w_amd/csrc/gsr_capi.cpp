@@ -869,7 +869,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
                          float tan_fovy, const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
                          const float* dL_dpix, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
                          float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
-                         float* dL_drot, void* stream_, const McSpec* mc) {
+                         float* dL_drot, void* stream_, const McSpec* mc, unsigned acc_mask = 0) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     if (P < 0 || R < 0 || width <= 0 || height <= 0) return fail(GSR_E_ARG, "gsr_backward: bad sizes");
     if (P == 0) return GSR_OK;
@@ -992,6 +992,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
     pb.dL_dmean2D = dL_dmean2D; pb.dL_dconic = dL_dconic; pb.dL_dopacity = dL_dopacity; pb.dL_dcolor = dL_dcolor;
     pb.dL_dmean3D = dL_dmean3D; pb.dL_dcov3D = dL_dcov3D; pb.dL_dsh = M > 0 ? dL_dsh : nullptr;
     pb.dL_dscale = dL_dscale; pb.dL_drot = dL_drot;
+    pb.acc_mask = acc_mask;
     if ((dL_dscale == nullptr) != (dL_drot == nullptr)) return fail(GSR_E_ARG, "gsr_backward: dL_dscale/dL_drot must both be given");
     {
         GSR_STAGE(ST_PREPROCESS_BWD);
@@ -1022,7 +1023,7 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
                           const int* radii, void* geom_buffer, void* binning_buffer, void* img_buffer,
                           const float* dL_dout, float* dL_dmean2D, float* dL_dconic, float* dL_dopacity,
                           float* dL_dfeatures, float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
-                          void* stream_) {
+                          unsigned accumulate, void* stream_) {
     if (P == 0) return GSR_OK;
     const int e = check_mc("gsr_backward_channels", nch, feature_stride, features);
     if (e != GSR_OK) return e;
@@ -1031,7 +1032,8 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
     return backward_impl(P, 0, 0, R, background, width, height, means3D, nullptr, nullptr, scales, scale_modifier,
                          rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
                          geom_buffer, binning_buffer, img_buffer, nullptr, dL_dmean2D, dL_dconic, dL_dopacity, nullptr,
-                         dL_dmean3D, dL_dcov3D, nullptr, dL_dscale, dL_drot, stream_, &mc);
+                         dL_dmean3D, dL_dcov3D, nullptr, dL_dscale, dL_drot, stream_, &mc,
+                         accumulate & (gsr::ACC_MEAN3D | gsr::ACC_SCALE | gsr::ACC_ROT | gsr::ACC_OPACITY));
 }
 
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix, uint8_t* present,
@@ -1153,7 +1155,7 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
                                 int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
                                 const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
                                 float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
-                                void* workspace, void* stream_) {
+                                void* workspace, unsigned accumulate, void* stream_) {
     if (P < 0 || N_fg < 0 || N_fg > P || deg < 2 || deg > 5 || sky_deg < -1 || sky_deg > 3)
         return fail(GSR_E_ARG, "gsr_relit_features_backward: bad sizes");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
@@ -1178,12 +1180,13 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
             gsr::ShadeGrads g{dL_dfeatures, dL_dfeatures + 3, specular ? dL_dfeatures + 6 : nullptr,
                               at<float>(ws, wl.d_pos_fg), at<float>(ws, wl.d_normal_fg), d_albedo, nullptr,
                               specular ? d_roughness : nullptr, specular ? d_metalness : nullptr, d_base};
+            g.acc = accumulate & (gsr::ACC_ALBEDO | gsr::ACC_ROUGH | gsr::ACC_METAL);
             gsr::launch_shade_bwd(a, g, at<void>(ws, wl.shade_ws), s);
         } else if (d_base) {
             HIP_OK(hipMemsetAsync(d_base, 0, sizeof(float) * 3 * (deg + 1) * (deg + 1), s));
         }
         gsr::RelitGrads rg{dL_dfeatures, at<float>(ws, wl.d_normal_fg), at<float>(ws, wl.d_pos_fg), d_xyz, d_rotation,
-                           d_sky_sh, at<float>(ws, wl.relit_ws)};
+                           d_sky_sh, at<float>(ws, wl.relit_ws), accumulate & (gsr::ACC_MEAN3D | gsr::ACC_ROT)};
         gsr::launch_relit_prep_bwd(ra, rg, s);
     }
     GSR_LAUNCH_CHECK();
@@ -1380,7 +1383,7 @@ int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* s
 
 int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int* const* radii,
                                    const unsigned char* is_sky, const float* depth_cols, const float* grad_sums,
-                                   float* d_xyz, float* d_scaling, void* stream_) {
+                                   float* d_xyz, float* d_scaling, unsigned accumulate, void* stream_) {
     if (P <= 0 || V <= 0 || V > gsr::REG_MAXV)
         return fail(GSR_E_ARG, "gsr_view_regularisers_backward: bad P=%d V=%d (1..%d views)", P, V, gsr::REG_MAXV);
     if (!scaling || !radii || !is_sky || !depth_cols || !grad_sums)
@@ -1388,7 +1391,7 @@ int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int
     gsr::ViewPtrs<int> rp;
     if (!view_ptrs_int(V, radii, rp)) return fail(GSR_E_ARG, "gsr_view_regularisers_backward: missing radii");
     gsr::launch_view_regs_bwd(P, V, scaling, rp, is_sky, depth_cols, grad_sums, d_xyz, d_scaling,
-                              reinterpret_cast<hipStream_t>(stream_));
+                              accumulate & (gsr::ACC_MEAN3D | gsr::ACC_SCALE), reinterpret_cast<hipStream_t>(stream_));
     GSR_LAUNCH_CHECK();
     return GSR_OK;
 }

@@ -72,6 +72,11 @@ struct __align__(16) Rec {
 // to read in the preprocess backward.)
 constexpr int ACC_STRIDE = 12;
 
+// Gradient outputs added into (instead of overwritten): the backward kernels' accumulate
+// bits (include/gsr.h GSR_ACC_*), so several views' gradients are summed where they are made.
+constexpr unsigned ACC_MEAN3D = 1u, ACC_SCALE = 2u, ACC_ROT = 4u, ACC_OPACITY = 8u, ACC_ALBEDO = 16u, ACC_ROUGH = 32u,
+                   ACC_METAL = 64u;
+
 // float -> int exactly as v_cvt_i32_f32 / the reference's implicit conversions
 // (forward.cu:235, :251): truncation, saturation, NaN -> 0.
 __device__ __forceinline__ int f2i(float v) {

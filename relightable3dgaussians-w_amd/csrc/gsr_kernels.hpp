@@ -359,6 +359,9 @@ struct PreprocessBwdArgs {
     float* dL_dsh;
     float* dL_dscale;
     float* dL_drot;
+    // add into (instead of overwrite) dL_dmean3D (bit 0), dL_dscale (1), dL_drot (2),
+    // dL_dopacity (3): several views' gradients summed in the kernels that produce them
+    unsigned acc_mask;
 };
 void launch_preprocess_bwd(const PreprocessBwdArgs& a, hipStream_t s);
 
@@ -382,7 +385,8 @@ int view_regs_blocks(int P);
 void launch_view_regs_fwd(int P, int V, const float* xyz, const float* scaling, const ViewPtrs<int>& radii,
                           const unsigned char* is_sky, const float* dcol, float* partials, hipStream_t s);
 void launch_view_regs_bwd(int P, int V, const float* scaling, const ViewPtrs<int>& radii, const unsigned char* is_sky,
-                          const float* dcol, const float* g, float* d_xyz, float* d_scaling, hipStream_t s);
+                          const float* dcol, const float* g, float* d_xyz, float* d_scaling, unsigned acc,
+                          hipStream_t s);
 void launch_densify_stats(int P, int V, const ViewPtrs<float>& g2d, const ViewPtrs<int>& radii, float* accum,
                           float* denom, float* maxr, hipStream_t s);
 void launch_sh_basis(int N, int deg, const float* dirs, float* out, hipStream_t s);

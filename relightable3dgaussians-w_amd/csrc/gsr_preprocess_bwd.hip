@@ -120,7 +120,24 @@ __global__ void __launch_bounds__(256) k_preprocess_bwd(PreprocessBwdArgs a) {
 // One Gaussian: every per-Gaussian output, and (with dL_dsh) its LDS row for the dL/dsh
 // writer.  (A register SH row cost 182 VGPRs; the LDS-staged SH rows of round 1 held the
 // occupancy to 3 waves per SIMD.)
+// a gradient output: stored, or added to what earlier views left there (acc_mask)
+__device__ __forceinline__ void put(float* p, float v, bool add) { *p = add ? *p + v : v; }
+__device__ __forceinline__ void put3(float* p, float x, float y, float z, bool add) {
+    put(p, x, add);
+    put(p + 1, y, add);
+    put(p + 2, z, add);
+}
+__device__ __forceinline__ void put4(float* p, float4 v, bool add) {
+    if (add) {
+        const float4 o = *reinterpret_cast<const float4*>(p);
+        v = make_float4(o.x + v.x, o.y + v.y, o.z + v.z, o.w + v.w);
+    }
+    *reinterpret_cast<float4*>(p) = v;
+}
+
 __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, int idx, const BwdIn& in, float* brow) {
+    const bool am = (a.acc_mask & ACC_MEAN3D) != 0, as = (a.acc_mask & ACC_SCALE) != 0,
+               ar = (a.acc_mask & ACC_ROT) != 0, ao = (a.acc_mask & ACC_OPACITY) != 0;
     // ---- unpack the render-backward accumulator line ------------------------------
     const float4 l0 = in.l0, l1 = in.l1;
     const float l2 = in.l2;
@@ -131,30 +148,28 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     a.dL_dmean2D[3 * idx + 2] = 0.f;
     if (a.dL_dconic)  // the reference allocates it but returns it to no one (rasterize_points.cu:145,186)
         *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
-    a.dL_dopacity[idx] = dop;
+    put(a.dL_dopacity + idx, dop, ao);
     if (a.dL_dcolor) {  // absent for the multi-channel composite (its features have their own gradient)
         a.dL_dcolor[3 * idx + 0] = dcol0;
         a.dL_dcolor[3 * idx + 1] = dcol1;
         a.dL_dcolor[3 * idx + 2] = dcol2;
     }
 
-    float* dcov = a.dL_dcov3D + 6 * idx;
+    float dcov[6];  // dL/dcov3D, stored to dL_dcov3D when the caller wants it
     const bool want_dsh = a.dL_dsh != nullptr;
     if (!(in.radius > 0)) {
-        a.dL_dmean3D[3 * idx + 0] = 0.f;
-        a.dL_dmean3D[3 * idx + 1] = 0.f;
-        a.dL_dmean3D[3 * idx + 2] = 0.f;
+        if (!am) put3(a.dL_dmean3D + 3 * idx, 0.f, 0.f, 0.f, false);
+        if (a.dL_dcov3D) {
 #pragma unroll
-        for (int i = 0; i < 6; i++) dcov[i] = 0.f;
+            for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = 0.f;
+        }
         if (want_dsh) {
 #pragma unroll
             for (int i = 0; i < BROW; i++) brow[i] = 0.f;
         }
         if (a.dL_dscale) {
-            a.dL_dscale[3 * idx + 0] = 0.f;
-            a.dL_dscale[3 * idx + 1] = 0.f;
-            a.dL_dscale[3 * idx + 2] = 0.f;
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!as) put3(a.dL_dscale + 3 * idx, 0.f, 0.f, 0.f, false);
+            if (!ar) put4(a.dL_drot + 4 * idx, make_float4(0.f, 0.f, 0.f, 0.f), false);
         }
         return;
     }
@@ -309,16 +324,16 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
 #pragma unroll
         for (int i = 0; i < BROW; i++) brow[i] = 0.f;
     }
-    a.dL_dmean3D[3 * idx + 0] = dm.x;
-    a.dL_dmean3D[3 * idx + 1] = dm.y;
-    a.dL_dmean3D[3 * idx + 2] = dm.z;
+    put3(a.dL_dmean3D + 3 * idx, dm.x, dm.y, dm.z, am);
+    if (a.dL_dcov3D) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) a.dL_dcov3D[6 * idx + i] = dcov[i];
+    }
 
     if (a.dL_dscale) {
         if (!a.scales) {
-            a.dL_dscale[3 * idx + 0] = 0.f;
-            a.dL_dscale[3 * idx + 1] = 0.f;
-            a.dL_dscale[3 * idx + 2] = 0.f;
-            *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (!as) put3(a.dL_dscale + 3 * idx, 0.f, 0.f, 0.f, false);
+            if (!ar) put4(a.dL_drot + 4 * idx, make_float4(0.f, 0.f, 0.f, 0.f), false);
             return;
         }
         // ---- computeCov3D backward (backward.cu:278-341) ------------------------------
@@ -342,10 +357,9 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         const M3 dL_dM = mmul(M2, dL_dSigma);
         const M3 Rt = mtrans(R);
         M3 D = mtrans(dL_dM);
-        float* ds = a.dL_dscale + 3 * idx;
-        ds[0] = Rt.m[0][0] * D.m[0][0] + Rt.m[0][1] * D.m[0][1] + Rt.m[0][2] * D.m[0][2];
-        ds[1] = Rt.m[1][0] * D.m[1][0] + Rt.m[1][1] * D.m[1][1] + Rt.m[1][2] * D.m[1][2];
-        ds[2] = Rt.m[2][0] * D.m[2][0] + Rt.m[2][1] * D.m[2][1] + Rt.m[2][2] * D.m[2][2];
+        put3(a.dL_dscale + 3 * idx, Rt.m[0][0] * D.m[0][0] + Rt.m[0][1] * D.m[0][1] + Rt.m[0][2] * D.m[0][2],
+             Rt.m[1][0] * D.m[1][0] + Rt.m[1][1] * D.m[1][1] + Rt.m[1][2] * D.m[1][2],
+             Rt.m[2][0] * D.m[2][0] + Rt.m[2][1] * D.m[2][1] + Rt.m[2][2] * D.m[2][2], as);
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             D.m[0][j] *= s0;
@@ -362,7 +376,7 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
         dq.w = 2 * r * (DD(0, 1) - DD(1, 0)) + 2 * x * (DD(2, 0) + DD(0, 2)) + 2 * y * (DD(1, 2) + DD(2, 1)) -
                4 * z * (DD(1, 1) + DD(0, 0));
 #undef DD
-        *reinterpret_cast<float4*>(a.dL_drot + 4 * idx) = dq;
+        put4(a.dL_drot + 4 * idx, dq, ar);
     }
 }
 

@@ -516,10 +516,14 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     if (valid) {
         if (g.d_pos) st3(g.d_pos, i, g_p[0], g_p[1], g_p[2]);
         if (g.d_normal) st3(g.d_normal, i, g_n[0], g_n[1], g_n[2]);
-        if (g.d_albedo) st3(g.d_albedo, i, g_a[0], g_a[1], g_a[2]);
+        if (g.d_albedo) {
+            if (g.acc & ACC_ALBEDO) st3(g.d_albedo, i, g.d_albedo[3 * i] + g_a[0], g.d_albedo[3 * i + 1] + g_a[1],
+                                        g.d_albedo[3 * i + 2] + g_a[2]);
+            else st3(g.d_albedo, i, g_a[0], g_a[1], g_a[2]);
+        }
         if (g.d_view_pos) st3(g.d_view_pos, i, g_vp[0], g_vp[1], g_vp[2]);
-        if (g.d_kr) g.d_kr[i] = g_kr;
-        if (g.d_km) g.d_km[i] = g_km;
+        if (g.d_kr) g.d_kr[i] = (g.acc & ACC_ROUGH) ? g.d_kr[i] + g_kr : g_kr;
+        if (g.d_km) g.d_km[i] = (g.acc & ACC_METAL) ? g.d_km[i] + g_km : g_km;
     }
     if (!g.d_base) return;
     // d_base[k][c] = sum_i Y_k gw_l g_si[c] (+ diffuse coefficients for k < 9)
@@ -727,9 +731,18 @@ __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads 
     // q = r / |r|
     const float qg = qr * gqr + qx * gqx + qy * gqy + qz * gqz;
     if (valid) {
-        st3(gr.d_xyz, i, gx, gy, gz);
-        *reinterpret_cast<float4*>(gr.d_rotation + 4 * (size_t)i) =
-            make_float4((gqr - qr * qg) / g.qn, (gqx - qx * qg) / g.qn, (gqy - qy * qg) / g.qn, (gqz - qz * qg) / g.qn);
+        if (gr.acc & ACC_MEAN3D)
+            st3(gr.d_xyz, i, gr.d_xyz[3 * i] + gx, gr.d_xyz[3 * i + 1] + gy, gr.d_xyz[3 * i + 2] + gz);
+        else
+            st3(gr.d_xyz, i, gx, gy, gz);
+        float4 dr = make_float4((gqr - qr * qg) / g.qn, (gqx - qx * qg) / g.qn, (gqy - qy * qg) / g.qn,
+                                (gqz - qz * qg) / g.qn);
+        float4* rp = reinterpret_cast<float4*>(gr.d_rotation + 4 * (size_t)i);
+        if (gr.acc & ACC_ROT) {
+            const float4 o = *rp;
+            dr = make_float4(o.x + dr.x, o.y + dr.y, o.z + dr.z, o.w + dr.w);
+        }
+        *rp = dr;
     }
     if (SDEG < 0 || !gr.d_sky_sh) return;
     // dL/dsky_sh[k][c] = sum over sky Gaussians of Y_k(dir) gcol[c]: per-workgroup slab

@@ -36,6 +36,7 @@ struct ShadeGrads {
     float* d_kr;
     float* d_km;
     float* d_base;
+    unsigned acc;  // ACC_ALBEDO / ACC_ROUGH / ACC_METAL: add into d_albedo / d_kr / d_km
 };
 
 // Fused relit features (gsr_shade.hip k_relit_prep / k_relit_prep_bwd).
@@ -61,6 +62,7 @@ struct RelitGrads {
     float* d_rotation;          // [P,4]
     float* d_sky_sh;            // [(sky_deg+1)^2][3] or null
     float* workspace;           // relit_workspace_bytes
+    unsigned acc;               // ACC_MEAN3D / ACC_ROT: add into d_xyz / d_rotation
 };
 size_t relit_workspace_bytes(int P, int sky_deg);
 void launch_relit_prep(const RelitArgs& a, hipStream_t s);

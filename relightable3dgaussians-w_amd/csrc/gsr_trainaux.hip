@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(REG_THREADS) k_view_regs_bwd(int P, int V, con
                                                                const unsigned char* __restrict__ is_sky,
                                                                const float* __restrict__ dcol,
                                                                const float* __restrict__ g, float* __restrict__ d_xyz,
-                                                               float* __restrict__ d_scaling) {
+                                                               float* __restrict__ d_scaling, unsigned acc) {
     const int i = blockIdx.x * REG_THREADS + threadIdx.x;
     if (i >= P) return;
     const bool sky = is_sky[i] != 0;
@@ -98,16 +98,21 @@ __global__ void __launch_bounds__(REG_THREADS) k_view_regs_bwd(int P, int V, con
         gz += gd * dcol[4 * v + 2];
     }
     if (d_xyz) {
-        d_xyz[3 * i] = gx;
-        d_xyz[3 * i + 1] = gy;
-        d_xyz[3 * i + 2] = gz;
+        const bool add = (acc & ACC_MEAN3D) != 0;
+        d_xyz[3 * i] = add ? d_xyz[3 * i] + gx : gx;
+        d_xyz[3 * i + 1] = add ? d_xyz[3 * i + 1] + gy : gy;
+        d_xyz[3 * i + 2] = add ? d_xyz[3 * i + 2] + gz : gz;
     }
     if (d_scaling) {
         const float s0 = scaling[3 * i], s1 = scaling[3 * i + 1], s2 = scaling[3 * i + 2];
         const int am = (s1 < s0) ? ((s2 < s1) ? 2 : 1) : ((s2 < s0) ? 2 : 0);  // first index of the minimum
-        d_scaling[3 * i] = am == 0 ? gs : 0.f;
-        d_scaling[3 * i + 1] = am == 1 ? gs : 0.f;
-        d_scaling[3 * i + 2] = am == 2 ? gs : 0.f;
+        if (acc & ACC_SCALE) {
+            d_scaling[3 * i + am] += gs;
+        } else {
+            d_scaling[3 * i] = am == 0 ? gs : 0.f;
+            d_scaling[3 * i + 1] = am == 1 ? gs : 0.f;
+            d_scaling[3 * i + 2] = am == 2 ? gs : 0.f;
+        }
     }
 }
 
@@ -359,9 +364,10 @@ void launch_view_regs_fwd(int P, int V, const float* xyz, const float* scaling, 
 }
 
 void launch_view_regs_bwd(int P, int V, const float* scaling, const ViewPtrs<int>& radii, const unsigned char* is_sky,
-                          const float* dcol, const float* g, float* d_xyz, float* d_scaling, hipStream_t s) {
+                          const float* dcol, const float* g, float* d_xyz, float* d_scaling, unsigned acc,
+                          hipStream_t s) {
     hipLaunchKernelGGL(k_view_regs_bwd, dim3((P + REG_THREADS - 1) / REG_THREADS), dim3(REG_THREADS), 0, s, P, V,
-                       scaling, radii, is_sky, dcol, g, d_xyz, d_scaling);
+                       scaling, radii, is_sky, dcol, g, d_xyz, d_scaling, acc);
 }
 
 void launch_densify_stats(int P, int V, const ViewPtrs<float>& g2d, const ViewPtrs<int>& radii, float* accum,

@@ -208,20 +208,27 @@ def rasterize_gaussians_channels(background, means3D, features, opacity, scales,
 
 def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch, scales, rotations, scale_modifier,
                                           cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout, campos,
-                                          geomBuffer, R, binningBuffer, imageBuffer):
+                                          geomBuffer, R, binningBuffer, imageBuffer, dst=None, accumulate=0):
     """Backward of rasterize_gaussians_channels (gsr_backward_channels) -> (dL_dmeans2D,
-    dL_dfeatures [P, stride] (columns >= nch zero), dL_dopacity, dL_dmeans3D, dL_dcov3D,
-    dL_dscales, dL_drotations)."""
+    dL_dfeatures [P, stride] (columns >= nch zero), dL_dopacity, dL_dmeans3D, dL_dcov3D
+    (empty without cov3D_precomp), dL_dscales, dL_drotations).  dst: optional buffers for
+    "means3D", "scales", "rotations", "opacity" written in place, added into where their bit
+    (GSR_ACC_*) is set in `accumulate` (gsr.sink)."""
     _lib.require_gpu_tensor(means3D, "means3D")
     dev = means3D.device
     P = means3D.size(0)
     H, W = dL_dout.size(1), dL_dout.size(2)
     alloc = torch.zeros if P == 0 else torch.empty
     f = dict(dtype=torch.float32, device=dev)
-    dL_dmeans2D, dL_dopacity = alloc((P, 3), **f), alloc((P, 1), **f)
+    dst = dst or {}
+    dL_dmeans2D = alloc((P, 3), **f)
+    dL_dopacity = dst["opacity"] if "opacity" in dst else alloc((P, 1), **f)
     dL_dfeat = alloc((P, feat.size(1)), **f)
-    dL_dmeans3D, dL_dcov3D = alloc((P, 3), **f), alloc((P, 6), **f)
-    dL_dscales, dL_drotations = alloc((P, 3), **f), alloc((P, 4), **f)
+    dL_dmeans3D = dst["means3D"] if "means3D" in dst else alloc((P, 3), **f)
+    has_cov = cov3D_precomp is not None and cov3D_precomp.numel() > 0
+    dL_dcov3D = alloc((P, 6), **f) if has_cov else torch.empty(0, **f)
+    dL_dscales = dst["scales"] if "scales" in dst else alloc((P, 3), **f)
+    dL_drotations = dst["rotations"] if "rotations" in dst else alloc((P, 4), **f)
     if P != 0:
         keep = [_f32(x) for x in (background, means3D, scales, rotations, cov3D_precomp, viewmatrix, projmatrix,
                                   campos, dL_dout)]
@@ -232,8 +239,8 @@ def rasterize_gaussians_channels_backward(background, means3D, radii, feat, nch,
             float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
             float(tan_fovx), float(tan_fovy), radii.contiguous().data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
             ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), None, dL_dopacity.data_ptr(),
-            dL_dfeat.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), dL_dscales.data_ptr(),
-            dL_drotations.data_ptr(), _lib.stream_of(dev))
+            dL_dfeat.data_ptr(), dL_dmeans3D.data_ptr(), ptr(dL_dcov3D), dL_dscales.data_ptr(),
+            dL_drotations.data_ptr(), int(accumulate), _lib.stream_of(dev))
         _lib.check(ret, "rasterize_gaussians_channels_backward")
     return (dL_dmeans2D, dL_dfeat, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dscales, dL_drotations)
 

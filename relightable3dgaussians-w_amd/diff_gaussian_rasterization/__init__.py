@@ -175,18 +175,31 @@ class _RasterizeChannels(torch.autograd.Function):
         ctx.ncols = features.shape[1]
         ctx.save_for_backward(background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf,
                               img_buf)
+        # inputs whose gradient a training step's gsr.sink collects (the kernels add into it)
+        ctx.sink_in = (means3D, scales, rotations, opacities)
         return out, radii
 
     @staticmethod
     def backward(ctx, grad_out, _grad_radii):
+        from gsr import sink as gsink
         s = ctx.raster_settings
         background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf, img_buf = \
             ctx.saved_tensors
+        need = ctx.needs_input_grad
+        keys = ("means3D", "scales", "rotations", "opacity")
+        outs, ret, sk, claimed, acc = gsink.outputs(ctx.sink_in, (need[0], need[4], need[5], need[3]))
+        dst = {k: o for k, o in zip(keys, outs) if o is not None}
         (g_means2D, g_feat, g_opacities, g_means3D, g_cov3D, g_scales, g_rotations) = \
             _C.rasterize_gaussians_channels_backward(background, means3D, radii, feat, ctx.nch, scales, rotations,
                                                      s.scale_modifier, cov3Ds_precomp, s.viewmatrix, s.projmatrix,
                                                      s.tanfovx, s.tanfovy, grad_out, s.campos, geom_buf,
-                                                     ctx.num_rendered, bin_buf, img_buf)
+                                                     ctx.num_rendered, bin_buf, img_buf, dst=dst, accumulate=acc)
+        if sk is not None:
+            sk.done(claimed)
+            g_means3D, g_scales, g_rotations, g_opacities = (
+                g if r else None for g, r in zip((g_means3D, g_scales, g_rotations, g_opacities), ret))
+        if g_cov3D.numel() == 0:
+            g_cov3D = None
         if g_feat.shape[1] >= ctx.ncols:  # gradient for every input column (columns >= nch: 0)
             g_feat = g_feat[:, :ctx.ncols]
         else:

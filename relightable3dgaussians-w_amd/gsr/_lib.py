@@ -51,12 +51,12 @@ def _declare(lib):
     lib.gsr_forward_channels.argtypes = [RESIZE_FN, vp, RESIZE_FN, vp, RESIZE_FN, vp, i, i, i, vp, vp, i, i, vp, vp, vp,
                                          f, vp, vp, vp, vp, vp, f, f, i, vp, vp, vp, C.POINTER(C.c_int)]
     lib.gsr_backward_channels.argtypes = [i, i, i, vp, i, vp, i, i, vp, vp, f, vp, vp, vp, vp, vp, f, f, vp, vp, vp, vp,
-                                          vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+                                          vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_uint, vp]
     lib.gsr_relit_workspace_bytes.argtypes = [i, i, i, i]
     lib.gsr_relit_workspace_bytes.restype = sz
     lib.gsr_relit_features.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp]
     lib.gsr_relit_features_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp,
-                                                vp, vp, vp, vp, vp, vp, vp, vp, vp]
+                                                vp, vp, vp, vp, vp, vp, vp, vp, C.c_uint, vp]
     lib.gsr_relit_epilogue.argtypes = [i, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
     lib.gsr_relit_epilogue_backward.argtypes = [i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
     lib.gsr_texture2d_forward.argtypes = [i, i, i, i, i, i, vp, vp, i, i, vp, vp]
@@ -72,7 +72,7 @@ def _declare(lib):
     pa = C.POINTER(C.c_void_p)  # host array of device pointers, one per view
     lib.gsr_view_regularisers_partials.argtypes = [i]
     lib.gsr_view_regularisers_forward.argtypes = [i, i, vp, vp, pa, vp, vp, vp, vp]
-    lib.gsr_view_regularisers_backward.argtypes = [i, i, vp, pa, vp, vp, vp, vp, vp, vp]
+    lib.gsr_view_regularisers_backward.argtypes = [i, i, vp, pa, vp, vp, vp, vp, vp, C.c_uint, vp]
     lib.gsr_densify_stats.argtypes = [i, i, pa, pa, vp, vp, vp, vp]
     lib.gsr_sh_basis.argtypes = [i, i, vp, vp, vp]
     lib.gsr_sky_xyz_partials.argtypes = [i]

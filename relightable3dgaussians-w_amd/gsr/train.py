@@ -492,7 +492,7 @@ class _FusedViewRegs(torch.autograd.Function):
     foreground), differentiable in xyz and scaling."""
 
     @staticmethod
-    def forward(ctx, xyz, scaling, dcol, radii, is_sky):
+    def forward(ctx, xyz, scaling, dcol, radii, is_sky, sink_in=None):
         P, V = xyz.shape[0], len(radii)
         L = _lib.lib()
         parts = torch.empty(L.gsr_view_regularisers_partials(P), 5 * V, device=xyz.device)
@@ -502,22 +502,28 @@ class _FusedViewRegs(torch.autograd.Function):
                    "gsr_view_regularisers_forward")
         ctx.save_for_backward(scaling, dcol, is_sky, *radii)
         ctx.P, ctx.V = P, V
+        ctx.sink_in = sink_in or (None, None)  # the model's xyz and scaling (gsr.sink)
         return parts.sum(0).view(V, 5)
 
     @staticmethod
     def backward(ctx, g):
+        from . import sink as gsink
         scaling, dcol, is_sky, *radii = ctx.saved_tensors
-        dx = torch.empty(ctx.P, 3, device=scaling.device) if ctx.needs_input_grad[0] else None
-        ds = torch.empty_like(scaling) if ctx.needs_input_grad[1] else None
-        if dx is None and ds is None:
-            return None, None, None, None, None
+        need = ctx.needs_input_grad
+        if not (need[0] or need[1]):
+            return None, None, None, None, None, None
+        outs, ret, sk, claimed, acc = gsink.outputs(ctx.sink_in, (need[0], need[1]))
+        dx = outs[0] if outs[0] is not None else (torch.empty(ctx.P, 3, device=scaling.device) if need[0] else None)
+        ds = outs[1] if outs[1] is not None else (torch.empty_like(scaling) if need[1] else None)
         ptr = lambda t: None if t is None else t.data_ptr()
         _lib.check(_lib.lib().gsr_view_regularisers_backward(ctx.P, ctx.V, scaling.data_ptr(), _lib.ptr_array(radii),
                                                              is_sky.data_ptr(), dcol.data_ptr(),
-                                                             g.contiguous().data_ptr(), ptr(dx), ptr(ds),
+                                                             g.contiguous().data_ptr(), ptr(dx), ptr(ds), acc,
                                                              _lib.stream_of(scaling.device)),
                    "gsr_view_regularisers_backward")
-        return dx, ds, None, None, None
+        if sk is not None:
+            sk.done(claimed)
+        return (dx if ret[0] else None), (ds if ret[1] else None), None, None, None, None
 
 
 def sh_basis_fused(deg: int, dirs: torch.Tensor) -> torch.Tensor:
@@ -552,8 +558,8 @@ def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, d
     if fused:
         rl = [r.contiguous() for r in radii] if isinstance(radii, (list, tuple)) else list(radii.contiguous())
         sky_u8 = pc.get_is_sky.reshape(-1).contiguous()
-        sums = _FusedViewRegs.apply((x if depth_on else x.detach()).contiguous(), pc.get_scaling.contiguous(), c.float().contiguous(), rl,
-                                    sky_u8)
+        sums = _FusedViewRegs.apply((x if depth_on else x.detach()).contiguous(), pc.get_scaling.contiguous(),
+                                    c.float().contiguous(), rl, sky_u8, (x if depth_on else None, pc.get_scaling))
         nf, ns = sums[:, 0], sums[:, 1]
         ms = sums[:, 2] / nf
         avg_sky = sums[:, 3] / ns
@@ -623,8 +629,10 @@ class _Activations(torch.autograd.Function):
     so no AccumulateGrad kernel runs for them; the parameters receive gradients from these
     activations only."""
 
+    KEYS = ("xyz", "scaling", "rotation", "opacity", "albedo", "roughness", "metalness")
+
     @staticmethod
-    def forward(ctx, scene, xyz_fg, angles, radius, scale_raw, rot_raw, op_raw, alb_raw, rough_raw, metal_raw):
+    def forward(ctx, scene, box, xyz_fg, angles, radius, scale_raw, rot_raw, op_raw, alb_raw, rough_raw, metal_raw):
         lay = scene.layout
         P, Nfg, Nsky = lay.P, lay.n_fg, lay.n_sky
         dev = xyz_fg.device
@@ -640,6 +648,7 @@ class _Activations(torch.autograd.Function):
                                                       *[ptr(t) for t in (xyz, scale, rot, op, alb, rough, metal)],
                                                       _lib.stream_of(dev)), "gsr_activations_forward")
         ctx.scene = scene
+        ctx.box = box  # [GradSink]: set by model_fused once the outputs exist
         ctx.ins = ins
         ctx.outs = (scale, rot, op, alb, rough, metal)
         ctx.set_materialize_grads(False)
@@ -653,6 +662,12 @@ class _Activations(torch.autograd.Function):
         dev = ctx.ins[0].device
         ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
         gs = [None if t is None else t.float().contiguous() for t in g]
+        sk = ctx.box[0]
+        if sk is not None:  # the views' summed gradients (plus any autograd brought)
+            for i, k in enumerate(_Activations.KEYS):
+                b = sk.take(k)
+                if b is not None:
+                    gs[i] = b if gs[i] is None else gs[i] + b
         d = {n: fp.params[n].grad for n in ("xyz", "sky_angles", "sky_radius", "scaling", "rotation", "opacity",
                                              "albedo", "roughness", "metalness")}
         part = torch.empty(max(1, _lib.lib().gsr_activations_partials(P, Nfg)), dtype=torch.float32, device=dev)
@@ -662,7 +677,7 @@ class _Activations(torch.autograd.Function):
             ptr(d["xyz"]), ptr(d["sky_angles"]), ptr(d["sky_radius"]), part.data_ptr(), ptr(d["scaling"]),
             ptr(d["rotation"]), ptr(d["opacity"]), ptr(d["albedo"]), ptr(d["roughness"]), ptr(d["metalness"]),
             _lib.stream_of(dev)), "gsr_activations_backward")
-        return (None,) * 10
+        return (None,) * 11
 
 
 class _FusedSkyXYZ(torch.autograd.Function):
@@ -831,10 +846,15 @@ class RelitScene:
         """model() on the fused activation kernels (gsr_activations_*): one launch forward,
         and a backward that writes the raw parameters' gradients straight into the flat
         gradient (no per-leaf autograd accumulation).  GPU scenes only."""
+        from .sink import GradSink
         p = self.fp.params
-        outs = _Activations.apply(self, p["xyz"], p["sky_angles"], p["sky_radius"], p["scaling"], p["rotation"],
+        box = [None]
+        outs = _Activations.apply(self, box, p["xyz"], p["sky_angles"], p["sky_radius"], p["scaling"], p["rotation"],
                                   p["opacity"], p["albedo"], p["roughness"], p["metalness"])
         xyz, scaling, rotation, opacity, albedo, rough, metal = outs
+        # the views' backward kernels add their gradients of these into one buffer each
+        # (gsr.sink); _Activations.backward reads them
+        box[0] = GradSink(dict(zip(_Activations.KEYS, outs)))
         return types.SimpleNamespace(get_xyz=xyz, get_scaling=scaling, get_rotation=rotation, get_opacity=opacity,
                                      get_albedo=albedo, get_roughness=rough, get_metalness=metal,
                                      get_is_sky=self.is_sky)

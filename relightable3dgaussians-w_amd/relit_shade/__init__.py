@@ -125,7 +125,7 @@ class RelitFeaturesFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, xyz, rotation, scaling, albedo, roughness, metalness, base, sky_sh, fg_rank, fg_rows, campos,
-                viewmatrix, lut, deg, sky_deg, specular):
+                viewmatrix, lut, deg, sky_deg, specular, sink_in=None):
         P, N = xyz.shape[0], fg_rows.shape[0]
         dev = xyz.device
         feat = torch.empty((P, 16), dtype=torch.float32, device=dev)
@@ -143,6 +143,9 @@ class RelitFeaturesFunction(torch.autograd.Function):
         ctx.save_for_backward(xyz, rotation, scaling, albedo, roughness if roughness is not None else e,
                               metalness if metalness is not None else e, base, sky_sh if sky_sh is not None else e,
                               fg_rank, fg_rows, campos, viewmatrix, lut, ws)
+        # the model's tensors as render() passed them (xyz, rotation, albedo, roughness,
+        # metalness): a training step's gsr.sink collects their gradients
+        ctx.sink_in = sink_in
         return feat
 
     @staticmethod
@@ -151,14 +154,22 @@ class RelitFeaturesFunction(torch.autograd.Function):
          ws) = ctx.saved_tensors
         P, N = xyz.shape[0], fg_rows.shape[0]
         dev = xyz.device
+        from gsr import sink as gsink
         g_feat = g_feat.float().contiguous()
-        # every entry is written by the kernels (d_kr / d_km only with specular)
-        d_xyz = torch.empty_like(xyz)
-        d_rot = torch.empty_like(rotation)
-        d_alb = torch.empty_like(albedo)
+        need = ctx.needs_input_grad
+        # gradients a training step's sink collects are added into its buffers by the kernels
+        # (d_kr / d_km are written only with specular)
+        sin = ctx.sink_in or (None,) * 5
+        outs, ret, sk, claimed, acc = gsink.outputs(
+            sin, (need[0], need[1], need[3] and albedo.numel() > 0, need[4] and ctx.specular and ctx.has[0],
+                  need[5] and ctx.specular and ctx.has[1]))
+        flat = lambda b: None if b is None else b.view(-1)
+        d_xyz = outs[0] if outs[0] is not None else torch.empty_like(xyz)
+        d_rot = outs[1] if outs[1] is not None else torch.empty_like(rotation)
+        d_alb = outs[2] if outs[2] is not None else torch.empty_like(albedo)
         zk = torch.empty_like if ctx.specular else torch.zeros_like
-        d_kr = zk(roughness) if ctx.has[0] else None
-        d_km = zk(metalness) if ctx.has[1] else None
+        d_kr = flat(outs[3]) if outs[3] is not None else (zk(roughness) if ctx.has[0] else None)
+        d_km = flat(outs[4]) if outs[4] is not None else (zk(metalness) if ctx.has[1] else None)
         d_base = torch.empty_like(base)
         d_sky = torch.empty_like(sky_sh) if ctx.has[2] and ctx.sky_deg >= 0 else None
         ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
@@ -166,9 +177,15 @@ class RelitFeaturesFunction(torch.autograd.Function):
             P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),
             ptr(albedo), ptr(roughness), ptr(metalness), ctx.deg, base.data_ptr(), lut.data_ptr(), int(ctx.specular),
             ctx.sky_deg, ptr(sky_sh), campos.data_ptr(), viewmatrix.data_ptr(), g_feat.data_ptr(), d_xyz.data_ptr(),
-            d_rot.data_ptr(), ptr(d_alb), ptr(d_kr), ptr(d_km), d_base.data_ptr(), ptr(d_sky), ws.data_ptr(),
+            d_rot.data_ptr(), ptr(d_alb), ptr(d_kr), ptr(d_km), d_base.data_ptr(), ptr(d_sky), ws.data_ptr(), acc,
             _lib.stream_of(dev)), "gsr_relit_features_backward")
-        return (d_xyz, d_rot, None, d_alb, d_kr, d_km, d_base, d_sky, None, None, None, None, None, None, None, None)
+        if sk is not None:
+            sk.done(claimed)
+            keep = lambda g, i: None if outs[i] is not None else g
+            d_xyz, d_rot, d_alb, d_kr, d_km = (keep(d_xyz, 0), keep(d_rot, 1), keep(d_alb, 2), keep(d_kr, 3),
+                                               keep(d_km, 4))
+        return (d_xyz, d_rot, None, d_alb, d_kr, d_km, d_base, d_sky, None, None, None, None, None, None, None, None,
+                None)
 
 
 _FG_CACHE = {}
@@ -213,11 +230,17 @@ def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness,
     base = light.base.squeeze().reshape(-1, 3).float().contiguous()
     deg = int(round(base.shape[0] ** 0.5)) - 1
     sky_deg = -1 if (fix_sky or sky_sh is None) else int(sky_sh_degree)
-    sk = None if sky_deg < 0 else sky_sh.reshape(-1, 3)[:(sky_deg + 1) ** 2].float().contiguous()
+    sk = None
+    if sky_deg >= 0:
+        sk = sky_sh.reshape(-1, 3)
+        if sk.shape[0] != (sky_deg + 1) ** 2:  # (a full-size slice would cost a zero tensor + copy backward)
+            sk = sk[:(sky_deg + 1) ** 2]
+        sk = sk.float().contiguous()
     f = lambda t: None if t is None else t.float().contiguous()
     return RelitFeaturesFunction.apply(f(xyz), f(rotation), f(scaling), f(albedo), _flat1(roughness),
                                        _flat1(metalness), base, sk, fg_rank, fg_rows, f(campos), f(viewmatrix),
-                                       fg_lut(dev), deg, sky_deg, bool(specular))
+                                       fg_lut(dev), deg, sky_deg, bool(specular),
+                                       (xyz, rotation, albedo, roughness, metalness))
 
 
 class EnvironmentLight(torch.nn.Module):
