@@ -267,6 +267,19 @@ int gsr_view_regularisers_backward(int P, int V, const float* scaling, const int
                                    float* d_xyz, float* d_scaling, unsigned accumulate, void* stream);
 int gsr_densify_stats(int P, int V, const float* const* grad_means2D, const int* const* radii, float* accum,
                       float* denom, float* max_radii, void* stream);
+/* The regularisers' per-view tail (train.py:99-118) from gsr_view_regularisers_forward's
+ * summed sums [V][5], the SH basis [V*n_samples][25] at the envlight directions (gsr_sh_basis)
+ * and the environment SH [V][25][3]: total[v] = envl (when lambda_env > 0) + lambda_scale
+ * min-scale mean + (depth_on) lambda_depth exp(-gamma (sky depth mean - foreground depth
+ * mean)).  The backward writes d_sums [V][5] (the counts and the detached foreground mean
+ * get 0) and d_env_sh [V][25][3] from grad_total [V].  One workgroup; V <= 8, n_samples <= 32. */
+int gsr_view_regularisers_tail_forward(int V, int n_samples, const float* sums, const float* basis, const float* env_sh,
+                                       float lambda_env, float lambda_scale, float lambda_depth, float gamma,
+                                       int depth_on, float* total, void* stream);
+int gsr_view_regularisers_tail_backward(int V, int n_samples, const float* sums, const float* basis,
+                                        const float* env_sh, float lambda_env, float lambda_scale, float lambda_depth,
+                                        float gamma, int depth_on, const float* grad_total, float* d_sums,
+                                        float* d_env_sh, void* stream);
 /* Real SH basis [N][(deg+1)^2] at the normalised directions dirs [N,3], deg 0..4. */
 int gsr_sh_basis(int N, int deg, const float* dirs, float* out, void* stream);
 /* Sky shell: angles [N,2] (theta, phi; clamped to [0,pi/2] and [-pi/2,pi/2]), radius [1],

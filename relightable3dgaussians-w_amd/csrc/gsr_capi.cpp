@@ -1515,4 +1515,30 @@ int gsr_activations_backward(int P, int n_fg, int n_sky, const int* src, const f
     return GSR_OK;
 }
 
+int gsr_view_regularisers_tail_forward(int V, int n_samples, const float* sums, const float* basis, const float* env_sh,
+                                       float lambda_env, float lambda_scale, float lambda_depth, float gamma,
+                                       int depth_on, float* total, void* stream_) {
+    if (V <= 0 || V > 8 || n_samples <= 0 || n_samples > 32)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_tail_forward: bad V=%d samples=%d (1..8, 1..32)", V, n_samples);
+    if (!sums || !basis || !env_sh || !total) return fail(GSR_E_ARG, "gsr_view_regularisers_tail_forward: missing buffers");
+    const gsr::RegsTail t{V, n_samples, depth_on ? 1 : 0, lambda_env, lambda_scale, lambda_depth, gamma, sums, basis, env_sh};
+    gsr::launch_regs_tail_fwd(t, total, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
+int gsr_view_regularisers_tail_backward(int V, int n_samples, const float* sums, const float* basis,
+                                        const float* env_sh, float lambda_env, float lambda_scale, float lambda_depth,
+                                        float gamma, int depth_on, const float* grad_total, float* d_sums,
+                                        float* d_env_sh, void* stream_) {
+    if (V <= 0 || V > 8 || n_samples <= 0 || n_samples > 32)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_tail_backward: bad V=%d samples=%d (1..8, 1..32)", V, n_samples);
+    if (!sums || !basis || !env_sh || !grad_total || !d_sums || !d_env_sh)
+        return fail(GSR_E_ARG, "gsr_view_regularisers_tail_backward: missing buffers");
+    const gsr::RegsTail t{V, n_samples, depth_on ? 1 : 0, lambda_env, lambda_scale, lambda_depth, gamma, sums, basis, env_sh};
+    gsr::launch_regs_tail_bwd(t, grad_total, d_sums, d_env_sh, reinterpret_cast<hipStream_t>(stream_));
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 }  // extern "C"

@@ -408,6 +408,13 @@ struct ActGrad {  // the raw parameters' gradients
     float *xyz_fg, *angles, *radius_part, *scale_raw, *rot_raw, *op_raw, *alb_raw, *rough_raw, *metal_raw;
 };
 int activation_blocks(const ActArgs& a);
+struct RegsTail {  // the regularisers' scalar tail (gsr_trainaux.hip)
+    int V, NS, depth_on;
+    float lam_env, lam_scale, lam_depth, gamma;
+    const float *sums, *basis, *env;
+};
+void launch_regs_tail_fwd(const RegsTail& t, float* total, hipStream_t s);
+void launch_regs_tail_bwd(const RegsTail& t, const float* g, float* d_sums, float* d_env, hipStream_t s);
 void launch_activations_fwd(const ActArgs& a, const ActOutW& o, hipStream_t s);
 void launch_activations_bwd(const ActArgs& a, const ActOut& o, const ActOut& g, const ActGrad& d, float* d_radius,
                             hipStream_t s);

@@ -352,6 +352,98 @@ void launch_activations_bwd(const ActArgs& a, const ActOut& o, const ActOut& g, 
     if (d.radius_part && d_radius) hipLaunchKernelGGL(k_sum_into, dim3(1), dim3(256), 0, s, nb, d.radius_part, d_radius);
 }
 
+// ---- the regularisers' per-view scalar tail (gsr/train.py view_regularisers) ---------------
+// From the per-view sums [V][5] (k_view_regs_fwd), the SH basis at the envlight directions
+// [V*NS][25] and the environment SH [V][25][3]: total[v] = el + ls ms + (depth_on) ld dl, with
+// ms = S2 / S0, dl = exp(-gamma (S3 / S1 - S4 / S0)) (the foreground mean detached), and el
+// the mean squared negative part of vals = basis . env (0 when none is negative), as the
+// PyTorch composition it replaces; one workgroup, V <= 8, NS <= 32.
+constexpr int TAIL_K = 25;
+
+__device__ __forceinline__ void tail_vals(const RegsTail& t, float* vals, float* cnt, float* sq) {
+    // vals [V][NS][3] and per view the negative count and sum of squares (LDS), 256 threads
+    for (int i = threadIdx.x; i < t.V * t.NS * 3; i += 256) {
+        const int v = i / (t.NS * 3), r = i - v * t.NS * 3, n = r / 3, c = r - 3 * n;
+        const float* b = t.basis + ((size_t)v * t.NS + n) * TAIL_K;
+        const float* e = t.env + (size_t)v * TAIL_K * 3 + c;
+        float a = 0.f;
+        for (int k = 0; k < TAIL_K; k++) a = __builtin_fmaf(b[k], e[3 * k], a);
+        vals[i] = a;
+    }
+    __syncthreads();
+    if (threadIdx.x < t.V) {
+        const int v = threadIdx.x;
+        float nn = 0.f, q = 0.f;
+        for (int j = 0; j < t.NS * 3; j++) {
+            const float x = vals[v * t.NS * 3 + j];
+            if (x < 0.f) {
+                nn += 1.f;
+                q += x * x;
+            }
+        }
+        cnt[v] = nn;
+        sq[v] = q;
+    }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_regs_tail_fwd(RegsTail t, float* __restrict__ total) {
+    __shared__ float vals[8 * 32 * 3], cnt[8], sq[8];
+    tail_vals(t, vals, cnt, sq);
+    if (threadIdx.x < t.V) {
+        const int v = threadIdx.x;
+        const float* S = t.sums + 5 * v;
+        const float ms = S[2] / S[0];
+        const float dl = expf(-t.gamma * (S[3] / S[1] - S[4] / S[0]));
+        const float el = cnt[v] > 0.f ? sq[v] / fmaxf(cnt[v], 1.f) : 0.f;
+        float tot = 0.f;
+        if (t.lam_env > 0.f) tot = tot + el;
+        if (t.lam_scale > 0.f) tot = tot + t.lam_scale * ms;
+        if (t.depth_on && t.lam_depth > 0.f) tot = tot + t.lam_depth * dl;
+        total[v] = tot;
+    }
+}
+
+// g [V]: dL/dtotal.  d_sums [V][5] (the counts and the detached foreground depth get 0),
+// d_env [V][25][3]
+__global__ void __launch_bounds__(256) k_regs_tail_bwd(RegsTail t, const float* __restrict__ g,
+                                                       float* __restrict__ d_sums, float* __restrict__ d_env) {
+    __shared__ float vals[8 * 32 * 3], cnt[8], sq[8];
+    tail_vals(t, vals, cnt, sq);
+    if (threadIdx.x < t.V) {
+        const int v = threadIdx.x;
+        const float* S = t.sums + 5 * v;
+        const float gv = g[v];
+        const float dl = expf(-t.gamma * (S[3] / S[1] - S[4] / S[0]));
+        float* D = d_sums + 5 * v;
+        D[0] = 0.f;
+        D[1] = 0.f;
+        D[2] = t.lam_scale > 0.f ? t.lam_scale * gv / S[0] : 0.f;
+        D[3] = (t.depth_on && t.lam_depth > 0.f) ? (t.lam_depth * gv) * dl * -t.gamma / S[1] : 0.f;
+        D[4] = 0.f;
+    }
+    // d vals = g 2 x / n on the negative entries; d env[k][c] = sum_n basis[n][k] d vals[n][c]
+    for (int i = threadIdx.x; i < t.V * TAIL_K * 3; i += 256) {
+        const int v = i / (TAIL_K * 3), r = i - v * TAIL_K * 3, k = r / 3, c = r - 3 * k;
+        float a = 0.f;
+        if (t.lam_env > 0.f && cnt[v] > 0.f) {
+            const float s = g[v] / fmaxf(cnt[v], 1.f);
+            for (int n = 0; n < t.NS; n++) {
+                const float x = vals[(v * t.NS + n) * 3 + c];
+                a = __builtin_fmaf(t.basis[((size_t)v * t.NS + n) * TAIL_K + k], x < 0.f ? 2.f * x * s : 0.f, a);
+            }
+        }
+        d_env[i] = a;
+    }
+}
+
+void launch_regs_tail_fwd(const RegsTail& t, float* total, hipStream_t s) {
+    hipLaunchKernelGGL(k_regs_tail_fwd, dim3(1), dim3(256), 0, s, t, total);
+}
+void launch_regs_tail_bwd(const RegsTail& t, const float* g, float* d_sums, float* d_env, hipStream_t s) {
+    hipLaunchKernelGGL(k_regs_tail_bwd, dim3(1), dim3(256), 0, s, t, g, d_sums, d_env);
+}
+
 int view_regs_blocks(int P) {
     const int b = (P + REG_THREADS * 8 - 1) / (REG_THREADS * 8);
     return b < 1 ? 1 : (b > 2048 ? 2048 : b);

@@ -75,6 +75,8 @@ def _declare(lib):
     lib.gsr_view_regularisers_backward.argtypes = [i, i, vp, pa, vp, vp, vp, vp, vp, C.c_uint, vp]
     lib.gsr_densify_stats.argtypes = [i, i, pa, pa, vp, vp, vp, vp]
     lib.gsr_sh_basis.argtypes = [i, i, vp, vp, vp]
+    lib.gsr_view_regularisers_tail_forward.argtypes = [i, i, vp, vp, vp, f, f, f, f, i, vp, vp]
+    lib.gsr_view_regularisers_tail_backward.argtypes = [i, i, vp, vp, vp, f, f, f, f, i, vp, vp, vp, vp]
     lib.gsr_sky_xyz_partials.argtypes = [i]
     lib.gsr_sky_xyz_forward.argtypes = [i, vp, vp, vp, vp, vp]
     lib.gsr_sky_xyz_backward.argtypes = [i, vp, vp, vp, vp, vp, vp]
@@ -105,7 +107,8 @@ def _declare(lib):
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward", "gsr_view_objective", "gsr_view_regularisers_forward",
-               "gsr_view_regularisers_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
+               "gsr_view_regularisers_backward", "gsr_view_regularisers_tail_forward",
+               "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
                "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
                "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):

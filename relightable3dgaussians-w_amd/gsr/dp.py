@@ -136,6 +136,13 @@ class StepStats:
         self.d = {"xyz_gradient_accum": torch.zeros(P, 1, device=device), "denom": torch.zeros(P, 1, device=device),
                   "max_radii2D": torch.zeros(P, device=device)}
 
+    @classmethod
+    def view_of(cls, stats: Dict[str, torch.Tensor]) -> "StepStats":
+        """A StepStats over existing statistics tensors (add_views then updates them in place)."""
+        obj = cls.__new__(cls)
+        obj.d = stats
+        return obj
+
     def zero(self) -> None:
         for t in self.d.values():
             t.zero_()

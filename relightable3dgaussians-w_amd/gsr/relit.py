@@ -120,6 +120,39 @@ class _Epilogue(torch.autograd.Function):
 
 
 _GREY = {}
+_ZEROS = {}
+_BGCAT = {}
+
+
+def _zero_rows(like, dev=None, n=None):
+    """Zeros shaped like ``like`` [P, 3] (an expanded view of one cached zero: no fill kernel
+    per view), or a cached zero vector of n elements."""
+    dev = like.device if like is not None else dev
+    z = _ZEROS.get(str(dev))
+    if z is None:
+        z = _ZEROS[str(dev)] = torch.zeros(16, dtype=torch.float32, device=dev)
+        if z.is_cuda:  # complete before another stream reads it
+            torch.cuda.current_stream(z.device).synchronize()
+    if like is None:
+        return z[:n]
+    return z[:1].view(1, 1).expand(like.shape[0], like.shape[1])
+
+
+def _bg_cat(bg_color, widths, parts):
+    """torch.cat(parts): the composite's background vector, a function of the background
+    tensor (identity and version) and the channel widths; cached, since a training run
+    renders every view over the same background."""
+    key = (id(bg_color), bg_color._version, tuple(widths), str(bg_color.device))
+    hit = _BGCAT.get(key)
+    if hit is not None and hit[0] is bg_color:
+        return hit[1]
+    out = torch.cat(parts)
+    if out.is_cuda:  # complete before another view's stream reads it
+        torch.cuda.current_stream(out.device).synchronize()
+    if len(_BGCAT) > 16:
+        _BGCAT.clear()
+    _BGCAT[key] = (bg_color, out)
+    return out
 
 
 def _is_grey(bg_color):
@@ -232,7 +265,8 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
 
     # a leaf (the reference adds 0 to make it a non-leaf and retains its gradient: the same
     # .grad after backward, without a full-size add kernel per view)
-    screenspace_points = torch.zeros_like(pc.get_xyz, dtype=pc.get_xyz.dtype, requires_grad=True)
+    # (its values are never read, only its gradient: an expanded zero, no fill kernel)
+    screenspace_points = _zero_rows(pc.get_xyz).requires_grad_(True)
     tanfovx = math.tan(viewpoint_camera.FoVx * 0.5)
     tanfovy = math.tan(viewpoint_camera.FoVy * 0.5)
     settings = dgr.GaussianRasterizationSettings(
@@ -261,7 +295,7 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     # A value repeated over three channels (depth, alpha, roughness, metalness) is one
     # composite channel when the background is grey; otherwise three.
     grey = _is_grey(bg_color)
-    zero3 = torch.zeros(3, device=dev)
+    zero3 = _zero_rows(None, dev, 3)
     # (name, columns [P, k], background [k]); alpha is rendered with a black background
     chans = [("render", feat[:, 0:3], bg), ("diffuse_color", feat[:, 3:6], bg), ("specular_color", feat[:, 6:9], bg),
              ("depth", feat[:, 9:10], bg), ("normal", feat[:, 10:13], bg), ("alpha", feat[:, 13:14], zero3)]
@@ -288,7 +322,7 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     # without extras and with a grey background the relit rows are the features as they are
     features = feat if (not debug and grey) else torch.cat(cols, 1)
     image, radii = dgr.rasterize_channels(means3D, screenspace_points, features, opacity, scales, rotations,
-                                          cov3D_precomp, torch.cat(bgs), settings, nch=nch)
+                                          cov3D_precomp, _bg_cat(bg_color, widths, bgs), settings, nch=nch)
     H, W = settings.image_height, settings.image_width
     slab = GradSlab(image.shape, image.device)
     parts = _SplitChannels.apply(image, tuple(widths), slab)

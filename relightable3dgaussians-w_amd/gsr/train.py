@@ -537,8 +537,42 @@ def sh_basis_fused(deg: int, dirs: torch.Tensor) -> torch.Tensor:
     return out
 
 
+class _RegsTail(torch.autograd.Function):
+    """view_regularisers' per-view scalar tail (gsr_view_regularisers_tail_*): the sums
+    [V,5] of _FusedViewRegs, the environment SH [V,25,3] and the basis at the envlight
+    directions -> total [V], one workgroup each way (the ~40 [V]-sized PyTorch ops of the
+    composition, on the iteration's critical path between the views and the backward)."""
+
+    @staticmethod
+    def forward(ctx, sums, env_sh, basis, depth_on, gamma):
+        V = sums.shape[0]
+        ns = basis.shape[0] // V
+        s_, e_, b_ = sums.float().contiguous(), env_sh.reshape(V, 25, 3).float().contiguous(), basis.contiguous()
+        total = torch.empty(V, dtype=torch.float32, device=sums.device)
+        consts = (float(LAMBDA_ENVLIGHT), float(LAMBDA_SCALE), float(LAMBDA_SKY_GAUSS), float(gamma), int(depth_on))
+        _lib.check(_lib.lib().gsr_view_regularisers_tail_forward(V, ns, s_.data_ptr(), b_.data_ptr(), e_.data_ptr(),
+                                                                 *consts, total.data_ptr(),
+                                                                 _lib.stream_of(sums.device)),
+                   "gsr_view_regularisers_tail_forward")
+        ctx.save_for_backward(s_, e_, b_)
+        ctx.consts, ctx.ns, ctx.env_shape = consts, ns, env_sh.shape
+        return total
+
+    @staticmethod
+    def backward(ctx, g):
+        s_, e_, b_ = ctx.saved_tensors
+        V = s_.shape[0]
+        d_sums = torch.empty_like(s_)
+        d_env = torch.empty_like(e_)
+        _lib.check(_lib.lib().gsr_view_regularisers_tail_backward(
+            V, ctx.ns, s_.data_ptr(), b_.data_ptr(), e_.data_ptr(), *ctx.consts, g.float().contiguous().data_ptr(),
+            d_sums.data_ptr(), d_env.data_ptr(), _lib.stream_of(s_.device)), "gsr_view_regularisers_tail_backward")
+        return d_sums, d_env.view(ctx.env_shape), None, None, None
+
+
 def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, dirs: torch.Tensor,
-                      gamma: float = 0.02, depth_on: bool = True, fused: bool = None) -> torch.Tensor:
+                      gamma: float = 0.02, depth_on: bool = True, fused: bool = None,
+                      tail_fused: bool = True) -> torch.Tensor:
     """The three regularisers of train.py:99-118 for V views at once, as [V] losses:
     envl_sh_loss(env_sh[v]) (unweighted: lambda_envlight only switches it on, :99-102)
     + LAMBDA_SCALE min_scale_loss(radii[v]) + LAMBDA_SKY_GAUSS depth_loss_gaussians(view v)
@@ -547,9 +581,10 @@ def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, d
     (row-vector world-to-view), env_sh [V,25,3], dirs [V,10,3].
 
     ``fused`` (default: on GPU tensors): the per-Gaussian sums of all V views in one HIP pass
-    each way and the SH basis in one launch (csrc/gsr_trainaux.hip); otherwise the PyTorch
-    composition below (~15 [V,P] kernels each way plus V x 5 reductions), which is also the
-    fused path's test reference."""
+    each way, the SH basis in one launch and (``tail_fused``) the scalar tail in one
+    workgroup each way (csrc/gsr_trainaux.hip); otherwise the PyTorch composition below (~15
+    [V,P] kernels each way plus V x 5 reductions), which is also the fused path's test
+    reference."""
     V = len(radii)
     x = pc.get_xyz
     if fused is None:
@@ -560,6 +595,9 @@ def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, d
         sky_u8 = pc.get_is_sky.reshape(-1).contiguous()
         sums = _FusedViewRegs.apply((x if depth_on else x.detach()).contiguous(), pc.get_scaling.contiguous(),
                                     c.float().contiguous(), rl, sky_u8, (x if depth_on else None, pc.get_scaling))
+        if tail_fused:  # the scalar tail and the envlight term in one launch each way
+            basis = sh_basis_fused(4, dirs.reshape(-1, 3))
+            return _RegsTail.apply(sums, env_sh, basis, bool(depth_on), float(gamma))
         nf, ns = sums[:, 0], sums[:, 1]
         ms = sums[:, 2] / nf
         avg_sky = sums[:, 3] / ns
@@ -952,13 +990,16 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     total.backward()
     for s in streams:
         main.wait_stream(s)
-    # this step's densification deltas (zeroed per step; only they cross ranks)
-    if scene.step_stats is None or scene.step_stats.d["denom"].shape[0] != scene.P:
-        scene.step_stats = gdp.StepStats(scene.P, dev)
-    scene.step_stats.zero()
     for out in outs:
         out["viewspace_points"].grad.record_stream(main)
-    scene.step_stats.add_views([o["viewspace_points"].grad for o in outs], radii)
+    if world > 1:
+        # this step's densification deltas (zeroed per step; only they cross ranks)
+        if scene.step_stats is None or scene.step_stats.d["denom"].shape[0] != scene.P:
+            scene.step_stats = gdp.StepStats(scene.P, dev)
+        scene.step_stats.zero()
+        scene.step_stats.add_views([o["viewspace_points"].grad for o in outs], radii)
+    else:  # one rank: straight into the running statistics, view by view
+        gdp.StepStats.view_of(scene.stats).add_views([o["viewspace_points"].grad for o in outs], radii)
     del outs
     fp.check_grads_in_place()
     n_views = len(views)
@@ -966,7 +1007,8 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         import torch.distributed as dist
         dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=group)
         n_views *= world
-    scene.step_stats.commit(scene.stats, group=group, world=world)
+    if world > 1:
+        scene.step_stats.commit(scene.stats, group=group, world=world)
     if optimizer_step:
         fp.step(grad_scale=1.0 / n_views)
     return total.detach()

@@ -236,9 +236,10 @@ def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness,
         if sk.shape[0] != (sky_deg + 1) ** 2:  # (a full-size slice would cost a zero tensor + copy backward)
             sk = sk[:(sky_deg + 1) ** 2]
         sk = sk.float().contiguous()
+    from diff_gaussian_rasterization._C import _f32  # cached contiguous copies of camera matrices
     f = lambda t: None if t is None else t.float().contiguous()
     return RelitFeaturesFunction.apply(f(xyz), f(rotation), f(scaling), f(albedo), _flat1(roughness),
-                                       _flat1(metalness), base, sk, fg_rank, fg_rows, f(campos), f(viewmatrix),
+                                       _flat1(metalness), base, sk, fg_rank, fg_rows, _f32(campos), _f32(viewmatrix),
                                        fg_lut(dev), deg, sky_deg, bool(specular),
                                        (xyz, rotation, albedo, roughness, metalness))
 

@@ -29,11 +29,15 @@ def _pc(P, V, dev, seed=0, sky_frac=0.15):
     return pc, radii, vms, env, dirs
 
 
+@pytest.mark.parametrize("tail", [True, False])
 @pytest.mark.parametrize("P,V,depth_on", [(1000, 1, True), (70001, 4, True), (70001, 4, False), (4099, 8, True)])
-def test_view_regularisers_fused_matches_torch(P, V, depth_on):
+def test_view_regularisers_fused_matches_torch(P, V, depth_on, tail):
+    """The fused regularisers (per-Gaussian sums, and with ``tail`` the scalar tail and the
+    envlight term in one workgroup) against the PyTorch composition: values and the xyz,
+    scaling and environment-SH gradients."""
     from gsr import train
     pc, radii, vms, env, dirs = _pc(P, V, "cuda", seed=P + V)
-    got = train.view_regularisers(pc, radii, vms, env, dirs, depth_on=depth_on, fused=True)
+    got = train.view_regularisers(pc, radii, vms, env, dirs, depth_on=depth_on, fused=True, tail_fused=tail)
     w = torch.randn(V, device="cuda")
     gg = torch.autograd.grad((got * w).sum(), [pc.get_xyz, pc.get_scaling, env], allow_unused=True)
     ref = train.view_regularisers(pc, torch.stack(radii), vms, env, dirs, depth_on=depth_on, fused=False)
