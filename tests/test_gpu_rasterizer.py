@@ -132,6 +132,10 @@ CASES = [
     # lists above the heavy-tile thresholds (>= 8192 entries, n_contrib >= 2048): the
     # four-way quadrant split of the tile passes
     dict(name="heavy_tiles", P=70000, W=64, H=48, mode="colors", mutate="thin"),
+    # depths over 12 and 20 octaves (same screen footprints): the depth sort's range-reduced
+    # three-pass path with a large key base, and its four-pass fallback
+    dict(name="depth_12_octaves", P=4000, W=96, H=64, mode="colors", mutate="deep12"),
+    dict(name="depth_20_octaves", P=4000, W=96, H=64, mode="sh", sh_degree=1, mutate="deep20"),
 ]
 
 
@@ -151,6 +155,10 @@ def mutate(gs, how):
     elif how == "thin":  # low opacity, wide: long lists that never saturate
         gs["opacities"] = torch.empty_like(gs["opacities"]).uniform_(0.01, 0.03, generator=g)
         gs["scales"] *= 2.0
+    elif how in ("deep12", "deep20"):  # every Gaussian pushed along its ray by 2^U(0, n)
+        k = torch.pow(2.0, torch.rand(gs["means3D"].shape[0], 1, generator=g) * float(how[4:]))
+        gs["means3D"] *= k
+        gs["scales"] *= k
     elif how == "shift":  # half the cloud left of the frustum, some behind the near plane
         gs["means3D"][:, 0] -= 0.6 * gs["means3D"][:, 2]
         gs["means3D"][: gs["means3D"].shape[0] // 10, 2] = 0.1
