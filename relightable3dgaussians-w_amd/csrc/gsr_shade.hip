@@ -399,7 +399,40 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     float g_kr = 0.f, g_km = 0.f;
 #pragma unroll
     for (int c = 0; c < 3; c++) g_dh[c] = gdif[c] * gamma_d(dh[c]);
-    float Y[K], gw[DEG + 1];
+    float Y[K], gw[DEG + 1], gi[3];
+    // dL/d(diffuse irradiance) once g_dh is final
+    auto diffuse_gi = [&]() {
+#pragma unroll
+        for (int c = 0; c < 3; c++) gi[c] = irr_raw[c] >= 1e-4f ? g_dh[c] * alc[c] : 0.f;
+    };
+    // d_base[k][c] = sum_i Y_k gw_l g_si[c] (+ diffuse coefficients for k < 9): this
+    // workgroup's partial sums into sred, taken while Y is live and before the SH-gradient
+    // phase (so that Y and that phase's registers are never live together)
+    auto base_partials = [&]() {
+        if (!g.d_base) return;
+        const float dco[9] = {LC4, LC2x2 * y, LC2x2 * z, LC2x2 * x, LC1x2 * x * y, LC1x2 * y * z, LC3 * z * z - LC5,
+                              LC1x2 * x * z, LC1 * (x * x - y * y)};
+        // the 3K wave sums in chunks of 12 values, each one transposed butterfly
+        // (gsr_tile.hpp wave_multi_sum; chunks keep the live registers small)
+        const int vi = wave_multi_sum_index(lane);
+#pragma unroll
+        for (int e0 = 0; e0 < 3 * K; e0 += 12) {
+            float vb[12];
+#pragma unroll
+            for (int t = 0; t < 12; t++) {
+                const int e = e0 + t, k = e / 3, c = e - 3 * k;
+                float v = 0.f;
+                if (e < 3 * K) {
+                    const int l = k < 1 ? 0 : k < 4 ? 1 : k < 9 ? 2 : k < 16 ? 3 : k < 25 ? 4 : 5;
+                    v = Y[k] * gw[l] * g_si[c];
+                    if (k < 9) v += gi[c] * dco[k < 9 ? k : 0];
+                }
+                vb[t] = valid ? v : 0.f;
+            }
+            const float red = wave_multi_sum<12>(vb);
+            if ((lane & 15) < 3 && e0 + vi < 3 * K) sred[wave][e0 + vi] = red;
+        }
+    };
     if (!a.specular) {
 #pragma unroll
         for (int c = 0; c < 3; c++) g_dh[c] += grgb[c] * gamma_d(dh[c]);
@@ -407,6 +440,8 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         for (int k = 0; k < K; k++) Y[k] = 0.f;
 #pragma unroll
         for (int l = 0; l <= DEG; l++) gw[l] = 0.f;
+        diffuse_gi();
+        base_partials();
     } else {
         const float3 p = ld3s(a.pos, row, 3);
         const float3 vp = ld3s(a.view_pos, ii, a.vp_stride);
@@ -466,6 +501,8 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
                 g_a[c] += km * g_F0;
             }
         }
+        diffuse_gi();
+        base_partials();
         {
             float sk[K];
 #pragma unroll
@@ -504,11 +541,9 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         }
     }
     // diffuse irradiance backward
-    float gi[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         g_a[c] += g_dh[c] * irr[c];
-        gi[c] = irr_raw[c] >= 1e-4f ? g_dh[c] * alc[c] : 0.f;
         g_n[0] += gi[c] * (LC1 * sb[24 + c] * 2 * x + LC1x2 * sb[12 + c] * y + LC1x2 * sb[21 + c] * z + LC2x2 * sb[9 + c]);
         g_n[1] += gi[c] * (-LC1 * sb[24 + c] * 2 * y + LC1x2 * sb[12 + c] * x + LC1x2 * sb[15 + c] * z + LC2x2 * sb[3 + c]);
         g_n[2] += gi[c] * (LC3 * sb[18 + c] * 2 * z + LC1x2 * sb[21 + c] * x + LC1x2 * sb[15 + c] * y + LC2x2 * sb[6 + c]);
@@ -526,29 +561,6 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         if (g.d_km) g.d_km[i] = (g.acc & ACC_METAL) ? g.d_km[i] + g_km : g_km;
     }
     if (!g.d_base) return;
-    // d_base[k][c] = sum_i Y_k gw_l g_si[c] (+ diffuse coefficients for k < 9)
-    const float dco[9] = {LC4, LC2x2 * y, LC2x2 * z, LC2x2 * x, LC1x2 * x * y, LC1x2 * y * z, LC3 * z * z - LC5,
-                          LC1x2 * x * z, LC1 * (x * x - y * y)};
-    // the 3K wave sums in chunks of 12 values, each one transposed butterfly
-    // (gsr_tile.hpp wave_multi_sum; chunks keep the live registers small)
-    const int vi = wave_multi_sum_index(lane);
-#pragma unroll
-    for (int e0 = 0; e0 < 3 * K; e0 += 12) {
-        float vb[12];
-#pragma unroll
-        for (int t = 0; t < 12; t++) {
-            const int e = e0 + t, k = e / 3, c = e - 3 * k;
-            float v = 0.f;
-            if (e < 3 * K) {
-                const int l = k < 1 ? 0 : k < 4 ? 1 : k < 9 ? 2 : k < 16 ? 3 : k < 25 ? 4 : 5;
-                v = Y[k] * gw[l] * g_si[c];
-                if (k < 9) v += gi[c] * dco[k < 9 ? k : 0];
-            }
-            vb[t] = valid ? v : 0.f;
-        }
-        const float red = wave_multi_sum<12>(vb);
-        if ((lane & 15) < 3 && e0 + vi < 3 * K) sred[wave][e0 + vi] = red;
-    }
     __syncthreads();
     for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS)
         ws[(size_t)blockIdx.x * K * 3 + t] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
