@@ -66,11 +66,19 @@ struct __align__(16) Rec {
     float4 a, b, c;
 };
 
-// Per-Gaussian gradient accumulator line (48 B, 16-B aligned; one atomic request per
+// Per-Gaussian gradient accumulator line (64 B, 64-B aligned; one atomic instruction per
 // (tile, Gaussian)): [0] dL/dmean2D.x [1] .y [2] dL/dconic.x [3] .y [4] .w [5] dL/dopacity
-// [6..8] dL/dcolor [9..11] unused.  (64-B lines: 33 % more bytes to zero in the forward and
-// to read in the preprocess backward.)
-constexpr int ACC_STRIDE = 12;
+// [6..8] dL/dcolor [9..15] unused.  The float atomics execute at the memory side in 64-B
+// requests: with 48-B lines half of a Gaussian's 9-value atomics straddled two 64-B segments.
+// 64-B lines (measured at cfg2, rocprofv3 kernel trace): render_bwd 351 -> 334 us, the
+// preprocess backward 122 -> 131 us (33 % more accumulator bytes to read; a coalesced LDS
+// hand-out of the lines measured the same), the call pair -16 us.  GSR_ACC_STRIDE=12 builds
+// the 48-B layout.
+#ifndef GSR_ACC_STRIDE
+#define GSR_ACC_STRIDE 16
+#endif
+constexpr int ACC_STRIDE = GSR_ACC_STRIDE;
+static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9 floats, 16-B aligned");
 
 // Gradient outputs added into (instead of overwritten): the backward kernels' accumulate
 // bits (include/gsr.h GSR_ACC_*), so several views' gradients are summed where they are made.

@@ -3,7 +3,7 @@ import csv, glob, sys
 vs = sys.argv[1:]
 tabs = {}
 for v in vs:
-    f = glob.glob(f"gpurun_out/ktv_{v}/*/*_kernel_stats.csv")[0]
+    f = max(glob.glob(f"gpurun_out/ktv_{v}/*/*_kernel_stats.csv"), key=__import__("os").path.getmtime)
     tabs[v] = {r["Name"].split("(")[0][:60]: (float(r["AverageNs"]) / 1e3, int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3)
                for r in csv.DictReader(open(f))}
 names = sorted(set().union(*[set(t) for t in tabs.values()]), key=lambda n: -max(t.get(n, (0, 0, 0))[2] for t in tabs.values()))
