@@ -9,7 +9,8 @@
 // the reference), S = the sky mask; rays_d(x, y) = x M0 + y M1 + M2 and o are the camera's
 // (K^-1^T R^T rows and centre, computed on the host).
 // The backward gathers, per pixel, the contributions of the four neighbours whose
-// differences it enters (recomputing their cross products), so it needs no atomics.
+// differences it enters (their cross-product derivatives made once per tile in LDS), so it
+// needs no atomics.
 #include "gsr_kernels.hpp"
 
 namespace gsr {
@@ -74,42 +75,70 @@ __device__ __forceinline__ float3 epi_dcross(float3 cr, float3 g) {
     return make_float3((g.x - n.x * ng) / l, (g.y - n.y * ng) / l, (g.z - n.z * ng) / l);
 }
 
+// One 32x8 output tile per workgroup, in three LDS phases: the back-projected points of the
+// tile plus a two-pixel margin; for every interior pixel q of the tile plus a one-pixel margin
+// the derivative of its normal_ref term, dL/d(cross) -> dL/da = b x dc and dL/db = dc x a
+// (each computed once instead of once per neighbour that reads it); then per pixel the four
+// neighbours' contributions in the fixed order (x, y-1), (x, y+1), (x-1, y), (x+1, y).
+constexpr int EPI_TW = 32, EPI_TH = 8;
+constexpr int EPI_QW = EPI_TW + 2, EPI_QH = EPI_TH + 2;  // q: the tile and a 1-pixel margin
+constexpr int EPI_PW = EPI_TW + 4, EPI_PH = EPI_TH + 4;  // points: a 2-pixel margin
+
 __global__ void __launch_bounds__(256) k_epilogue_bwd(int W, int H, EpiCam cam, const float* depth,
                                                        const float* alpha, const float* sky, float nsign,
                                                        const float* g_normal, const float* g_normal_ref, float* d_n01,
                                                        float* d_depth) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
+    __shared__ float3 s_p[EPI_PH][EPI_PW];
+    __shared__ float3 s_ga[EPI_QH][EPI_QW], s_gb[EPI_QH][EPI_QW];
     const int HW = W * H;
-    if (i >= HW) return;
-    const int x = i % W, y = i / W;
-    const float s = sky[i];
-    if (d_n01) {
+    const int x0 = blockIdx.x * EPI_TW, y0 = blockIdx.y * EPI_TH;
+    const int tx = threadIdx.x % EPI_TW, ty = threadIdx.x / EPI_TW;
+    const int x = x0 + tx, y = y0 + ty;
+    const bool in = x < W && y < H;
+    const int i = y * W + x;
+    const float s = in ? sky[i] : 0.f;
+    if (d_n01 && in) {
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) d_n01[ch * HW + i] = g_normal ? g_normal[ch * HW + i] * 2.f * nsign * s : 0.f;
     }
     if (!d_depth) return;
-    float3 gp = make_float3(0.f, 0.f, 0.f);
-    if (g_normal_ref) {
-        // neighbour (nx, ny) interior: its dc; this pixel enters its a (rows) or b (columns)
-        const int nbx[4] = {x, x, x - 1, x + 1}, nby[4] = {y - 1, y + 1, y, y};
-        const float sg[4] = {1.f, -1.f, 1.f, -1.f};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int qx = nbx[k], qy = nby[k];
-            if (qx < 1 || qx > W - 2 || qy < 1 || qy > H - 2) continue;
+    if (!g_normal_ref) {
+        if (in) d_depth[i] = s * 0.f;
+        return;
+    }
+    for (int e = threadIdx.x; e < EPI_PH * EPI_PW; e += 256) {
+        const int px = x0 - 2 + e % EPI_PW, py = y0 - 2 + e / EPI_PW;
+        s_p[e / EPI_PW][e % EPI_PW] = (px >= 0 && px < W && py >= 0 && py < H) ? epi_point(cam, depth, sky, W, px, py)
+                                                                                : make_float3(0.f, 0.f, 0.f);
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < EPI_QH * EPI_QW; e += 256) {
+        const int lx = e % EPI_QW, ly = e / EPI_QW;  // q = (x0 - 1 + lx, y0 - 1 + ly); its points at (lx + 1, ly + 1)
+        const int qx = x0 - 1 + lx, qy = y0 - 1 + ly;
+        float3 ga = make_float3(0.f, 0.f, 0.f), gb = ga;
+        if (qx >= 1 && qx <= W - 2 && qy >= 1 && qy <= H - 2) {
             const int j = qy * W + qx;
             const float al = alpha[j];
             const float3 g = make_float3(g_normal_ref[j] * al, g_normal_ref[HW + j] * al, g_normal_ref[2 * HW + j] * al);
-            float3 a, b;
-            epi_diffs(cam, depth, sky, W, qx, qy, a, b);
+            const float3 a = f3sub(s_p[ly + 2][lx + 1], s_p[ly][lx + 1]);
+            const float3 b = f3sub(s_p[ly + 1][lx + 2], s_p[ly + 1][lx]);
             const float3 dc = epi_dcross(f3cross(a, b), g);
             // c = a x b: dL/da = b x dc, dL/db = dc x a
-            const float3 ga = k < 2 ? f3cross(b, dc) : f3cross(dc, a);
-            gp.x += sg[k] * ga.x;
-            gp.y += sg[k] * ga.y;
-            gp.z += sg[k] * ga.z;
+            ga = f3cross(b, dc);
+            gb = f3cross(dc, a);
         }
+        s_ga[ly][lx] = ga;
+        s_gb[ly][lx] = gb;
     }
+    __syncthreads();
+    if (!in) return;
+    // this pixel enters a of (x, y-1) (+) and (x, y+1) (-), b of (x-1, y) (+) and (x+1, y) (-)
+    const float3 c0 = s_ga[ty][tx + 1], c1 = s_ga[ty + 2][tx + 1], c2 = s_gb[ty + 1][tx], c3 = s_gb[ty + 1][tx + 2];
+    float3 gp = make_float3(0.f, 0.f, 0.f);
+    gp.x += c0.x; gp.y += c0.y; gp.z += c0.z;
+    gp.x += -c1.x; gp.y += -c1.y; gp.z += -c1.z;
+    gp.x += c2.x; gp.y += c2.y; gp.z += c2.z;
+    gp.x += -c3.x; gp.y += -c3.y; gp.z += -c3.z;
     const float fx = (float)x, fy = (float)y;
     const float rx = fx * cam.m[0] + fy * cam.m[3] + cam.m[6];
     const float ry = fx * cam.m[1] + fy * cam.m[4] + cam.m[7];
@@ -136,8 +165,8 @@ void launch_epilogue_bwd(int W, int H, const float* m12, const float* depth, con
     for (int k = 0; k < 3; k++) c.o[k] = m12[9 + k];
     const int n = W * H;
     if (n == 0) return;
-    hipLaunchKernelGGL(k_epilogue_bwd, dim3((n + 255) / 256), dim3(256), 0, s, W, H, c, depth, alpha, sky,
-                       normal_view ? -1.f : 1.f, g_normal, g_normal_ref, d_n01, d_depth);
+    hipLaunchKernelGGL(k_epilogue_bwd, dim3((W + EPI_TW - 1) / EPI_TW, (H + EPI_TH - 1) / EPI_TH), dim3(256), 0, s, W, H,
+                       c, depth, alpha, sky, normal_view ? -1.f : 1.f, g_normal, g_normal_ref, d_n01, d_depth);
 }
 
 }  // namespace gsr
