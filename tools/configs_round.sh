@@ -10,6 +10,6 @@ run() {  # name, args...
   local rc=$?; echo "$n rc=$rc"; grep -o '"value": [0-9.]*, "unit": "[^"]*"' gpurun_out/${TAG}_$n.log | head -1
   return $rc
 }
-run cfg3 --config cfg3 --steps 20 --warmup 5 && run cfg4 --config cfg4 --steps 10 --warmup 3 &&
+run cfg3 --config cfg3 --steps 20 --warmup 5 && run cfg4 --config cfg4 --steps 30 --warmup 5 &&
   run cfg5 --config cfg5 --steps 5 --warmup 2 --no-cpu-baseline --no-refalgo &&
   run cfg5r --config cfg5-relit --steps 5 --warmup 2
