@@ -226,6 +226,14 @@ int gsr_ssim_forward(int C, int height, int width, const float* img1, const floa
                      long long mask_cstride, const float* window, float* block_sums, float* dmaps, void* stream);
 int gsr_ssim_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
                       const float* gscale, const float* window, float* dimg1, int accumulate, void* stream);
+/* gsr_ssim_backward that also makes the loss's L1 term's image gradient (train.py:78 through
+ * gsr_view_loss_backward's d_img: l1_coef[0] * sign(img1 * occ - img2 * occ) * occ, occ the
+ * [H,W] occluder mask) and writes the sum (the same two roundings as gsr_view_loss_backward's
+ * d_img followed by gsr_ssim_backward with accumulate): one pass over dimg1 instead of a write
+ * and a read-modify-write.  l1_coef: device pointer. */
+int gsr_ssim_l1_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
+                         const float* gscale, const float* window, const float* occ, const float* l1_coef,
+                         float* dimg1, void* stream);
 
 /* The pointwise terms of the training loss (train.py:77-99) over one view: images img, gt,
  * diff, spec, nrm, nref are [3,H,W] (npix = H*W), the sky and occluder masks [H,W].

@@ -1316,6 +1316,19 @@ int gsr_ssim_backward(int C, int height, int width, const float* img1, const flo
     return GSR_OK;
 }
 
+int gsr_ssim_l1_backward(int C, int height, int width, const float* img1, const float* img2, const float* dmaps,
+                         const float* gscale, const float* window, const float* occ, const float* l1_coef,
+                         float* dimg1, void* stream_) {
+    if (C <= 0 || C > 65535 || height <= 0 || width <= 0) return fail(GSR_E_ARG, "gsr_ssim_l1_backward: bad sizes");
+    gsr::SsimWindow w;
+    if (!img1 || !img2 || !dmaps || !gscale || !occ || !l1_coef || !dimg1 || !ssim_window(window, w))
+        return fail(GSR_E_ARG, "gsr_ssim_l1_backward: missing buffers");
+    gsr::launch_ssim_bwd(C, height, width, img1, img2, dmaps, gscale, w, dimg1, 0, reinterpret_cast<hipStream_t>(stream_),
+                         occ, l1_coef);
+    GSR_LAUNCH_CHECK();
+    return GSR_OK;
+}
+
 int gsr_view_objective(int n_loss_partials, const float* loss_partials, long long n_ssim_partials,
                        const float* ssim_partials, int npix, double lambda_dssim, double lambda_sky,
                        double lambda_normal, float* loss, float* coef, void* stream_) {

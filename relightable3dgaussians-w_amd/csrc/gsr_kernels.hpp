@@ -314,7 +314,8 @@ void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, 
                      long long mask_cstride, const SsimWindow& win, float C1, float C2, float* block_sums,
                      float* dmaps, hipStream_t s);
 void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
-                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s);
+                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s,
+                     const float* occ = nullptr, const float* l1k = nullptr);
 
 // ---- fused pointwise training-loss terms (gsr_loss.hip) ---------------------------------
 int view_loss_blocks(int npix);

@@ -222,7 +222,8 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
 __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __restrict__ img1,
                                                   const float* __restrict__ img2, const float* __restrict__ dmaps,
                                                   const float* __restrict__ gscale, SsimWindow win,
-                                                  float* __restrict__ dimg1, int accumulate) {
+                                                  float* __restrict__ dimg1, int accumulate,
+                                                  const float* __restrict__ occ, const float* __restrict__ l1k) {
     __shared__ float sr[3][SS_LH][SS_LW];
     __shared__ float hm[3][SS_LH][SS_TW + 1];
     const int c = blockIdx.z;
@@ -231,6 +232,7 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
     const float* const src[3] = {dmaps + c * plane, dmaps + cs + c * plane, dmaps + 2 * cs + c * plane};
     const int x0 = blockIdx.x * SS_TW - SS_R;
     const float sc = *gscale;
+    const float k0 = l1k ? *l1k : 0.f;
     const int ty_first = blockIdx.y * SS_CH * SS_TH;
     float pf[3][SS_PF];
     {
@@ -295,8 +297,16 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
                     q2 += g * col[2][o + k];
                 }
                 const size_t oo = c * plane + (size_t)y * W + x;
-                const float d = sc * (q0 + 2.f * img1[oo] * q1 + img2[oo] * q2);
-                dimg1[oo] = accumulate ? dimg1[oo] + d : d;  // accumulate: onto the pointwise terms' gradient
+                const float x1 = img1[oo], x2 = img2[oo];
+                const float d = sc * (q0 + 2.f * x1 * q1 + x2 * q2);
+                if (l1k) {  // the L1 term's gradient made here (gsr_view_loss_backward's, same order)
+                    const float o = occ[(size_t)y * W + x];
+                    const float a = x1 * o - x2 * o;
+                    const float l1 = __fmul_rn(k0 * (a > 0.f ? 1.f : (a < 0.f ? -1.f : 0.f)), o);
+                    dimg1[oo] = __fadd_rn(l1, d);  // no contraction: the unfused path's two roundings
+                } else {
+                    dimg1[oo] = accumulate ? dimg1[oo] + d : d;  // accumulate: onto the pointwise terms' gradient
+                }
             }
         }
         __syncthreads();
@@ -321,9 +331,10 @@ void launch_ssim_fwd(int C, int H, int W, const float* img1, const float* img2, 
 }
 
 void launch_ssim_bwd(int C, int H, int W, const float* img1, const float* img2, const float* dmaps,
-                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s) {
+                     const float* gscale, const SsimWindow& win, float* dimg1, int accumulate, hipStream_t s, const float* occ,
+                     const float* l1k) {
     hipLaunchKernelGGL(k_ssim_bwd, ssim_grid(C, H, W), dim3(256), 0, s, H, W, img1, img2, dmaps, gscale, win, dimg1,
-                       accumulate);
+                       accumulate, occ, l1k);
 }
 
 }  // namespace gsr

@@ -87,6 +87,7 @@ def _declare(lib):
     lib.gsr_ssim_partials.restype = C.c_longlong
     lib.gsr_ssim_forward.argtypes = [i, i, i, vp, vp, vp, C.c_longlong, C.POINTER(C.c_float), vp, vp, vp]
     lib.gsr_ssim_backward.argtypes = [i, i, i, vp, vp, vp, vp, C.POINTER(C.c_float), vp, i, vp]
+    lib.gsr_ssim_l1_backward.argtypes = [i, i, i, vp, vp, vp, vp, C.POINTER(C.c_float), vp, vp, vp, vp]
     lib.gsr_view_objective.argtypes = [i, vp, C.c_longlong, vp, i, C.c_double, C.c_double, C.c_double, vp, vp, vp]
     lib.gsr_shade_workspace_bytes.argtypes = [i, i]
     lib.gsr_shade_workspace_bytes.restype = sz
@@ -106,6 +107,7 @@ def _declare(lib):
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
+               "gsr_ssim_l1_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward", "gsr_view_objective", "gsr_view_regularisers_forward",
                "gsr_view_regularisers_backward", "gsr_view_regularisers_tail_forward",
                "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",

@@ -345,12 +345,13 @@ class _FusedViewObjective(torch.autograd.Function):
             outs.append(d)
         ptr = lambda t: None if t is None else t.data_ptr()
         st = _lib.stream_of(ts[0].device)
-        _lib.check(_lib.lib().gsr_view_loss_backward(H * W, *[t.data_ptr() for t in ts], cg.data_ptr(),
-                                                     *[ptr(t) for t in outs], st), "gsr_view_loss_backward")
-        if outs[0] is not None:  # the SSIM term's image gradient, added in place
-            _lib.check(_lib.lib().gsr_ssim_backward(3, H, W, ts[0].data_ptr(), ts[1].data_ptr(), ctx.dmaps.data_ptr(),
-                                                    cg.data_ptr() + 12, _WIN11, outs[0].data_ptr(), 1, st),
-                       "gsr_ssim_backward")
+        # the image gradient (L1 + SSIM terms) in the SSIM backward's one pass; the other four here
+        _lib.check(_lib.lib().gsr_view_loss_backward(H * W, *[t.data_ptr() for t in ts], cg.data_ptr(), None,
+                                                     *[ptr(t) for t in outs[1:]], st), "gsr_view_loss_backward")
+        if outs[0] is not None:
+            _lib.check(_lib.lib().gsr_ssim_l1_backward(3, H, W, ts[0].data_ptr(), ts[1].data_ptr(), ctx.dmaps.data_ptr(),
+                                                       cg.data_ptr() + 12, _WIN11, ts[7].data_ptr(), cg.data_ptr(),
+                                                       outs[0].data_ptr(), st), "gsr_ssim_l1_backward")
         return (*outs, None, None, None, None)
 
 
