@@ -111,3 +111,45 @@ def test_fused_objective_matches_scalar_tail(H, W, case):
             assert float(ga.abs().max()) == 0, k
             continue
         assert rel_l2(ga.cpu().numpy(), gb.cpu().numpy()) < 1e-6, k
+
+
+@pytest.mark.parametrize("H,W,occ_kind", [(97, 131, "rand"), (1080, 1920, "rand"), (64, 80, "empty")])
+def test_ssim_l1_backward_matches_two_pass(H, W, occ_kind):
+    """gsr_ssim_l1_backward (the image gradient's L1 term made inside the SSIM backward) against
+    the two-pass path it replaces: gsr_view_loss_backward's d_img, then gsr_ssim_backward with
+    accumulate.  Same two roundings per value (no contraction across them): equal up to the
+    SSIM term's own fused multiply-add, checked at 1e-6 relative per value."""
+    import ctypes as C
+    from gsr import _lib, train
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(7)
+    img = torch.rand(3, H, W, device=dev, generator=g)
+    gt = (img + 0.05 * torch.randn(3, H, W, device=dev, generator=g)).clamp(0, 1)
+    gt[:, : H // 4] = img[:, : H // 4]  # exact ties: sign 0 in the L1 term
+    planes = [torch.rand(3, H, W, device=dev, generator=g) for _ in range(4)]  # diff, spec, nrm, nref
+    sky = (torch.rand(H, W, device=dev, generator=g) > 0.3).float()
+    occ = torch.zeros(H, W, device=dev) if occ_kind == "empty" else (torch.rand(H, W, device=dev, generator=g) > 0.2).float()
+    L = _lib.lib()
+    st = _lib.stream_of(dev)
+    win = (C.c_float * 11)(*train.gaussian_1d(11).tolist())
+    nss = int(L.gsr_ssim_partials(3, H, W))
+    parts = torch.empty(2 * nss, device=dev)
+    dmaps = torch.empty(3, 3, H, W, device=dev)
+    _lib.check(L.gsr_ssim_forward(3, H, W, img.data_ptr(), gt.data_ptr(), occ.data_ptr(), 0, win, parts.data_ptr(),
+                                  dmaps.data_ptr(), st), "gsr_ssim_forward")
+    coef = torch.tensor([0.37, 0.11, -0.02, -0.61], device=dev)  # (k_img, k_brdf, k_normal, k_ssim)
+    ts = [img, gt, *planes, sky, occ]
+    two = torch.empty_like(img)
+    _lib.check(L.gsr_view_loss_backward(H * W, *[t.data_ptr() for t in ts], coef.data_ptr(), two.data_ptr(), None, None,
+                                        None, None, st), "gsr_view_loss_backward")
+    _lib.check(L.gsr_ssim_backward(3, H, W, img.data_ptr(), gt.data_ptr(), dmaps.data_ptr(), coef.data_ptr() + 12, win,
+                                   two.data_ptr(), 1, st), "gsr_ssim_backward")
+    one = torch.full_like(img, float("nan"))
+    _lib.check(L.gsr_ssim_l1_backward(3, H, W, img.data_ptr(), gt.data_ptr(), dmaps.data_ptr(), coef.data_ptr() + 12,
+                                      win, occ.data_ptr(), coef.data_ptr(), one.data_ptr(), st), "gsr_ssim_l1_backward")
+    torch.cuda.synchronize()
+    assert torch.isfinite(one).all()
+    d = (one - two).abs()
+    assert float(d.max()) <= 1e-6 * float(two.abs().max()) + 1e-12, float(d.max())
+    if occ_kind == "empty":  # no mask: no L1 term and a zero SSIM gradient
+        assert float(one.abs().max()) == 0.0
