@@ -563,14 +563,16 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     if (!g.d_base) return;
     __syncthreads();
     for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS)
-        ws[(size_t)blockIdx.x * K * 3 + t] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+        ws[(size_t)t * gridDim.x + blockIdx.x] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
 }
 
-// fixed-order reduction of the per-workgroup d_base slabs: one workgroup per output value
+// fixed-order reduction of the per-workgroup d_base slabs: one workgroup per output value; the
+// slabs are stored value-major (ws[value][workgroup]), so each reads one contiguous row
 __global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const float* ws, float* d_base) {
     __shared__ float sh[4];
     float v = 0.f;
-    for (int b = threadIdx.x; b < nb; b += 256) v += ws[(size_t)b * KC + blockIdx.x];
+    const float* row = ws + (size_t)blockIdx.x * nb;
+    for (int b = threadIdx.x; b < nb; b += 256) v += row[b];
     v = wave_reduce_sum(v);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
@@ -772,7 +774,7 @@ __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads 
     }
     __syncthreads();
     for (int t = threadIdx.x; t < 3 * KS; t += 256)
-        gr.workspace[(size_t)blockIdx.x * 3 * KS + t] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+        gr.workspace[(size_t)t * gridDim.x + blockIdx.x] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
 }
 
 size_t relit_workspace_bytes(int P, int sky_deg) {
