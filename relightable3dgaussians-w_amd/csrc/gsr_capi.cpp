@@ -1128,6 +1128,8 @@ int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation,
         (N_fg > 0 && (!fg_rows || !albedo || !base || !fg_lut || (specular && !roughness))) ||
         (sky_deg >= 0 && !sky_sh))
         return fail(GSR_E_ARG, "gsr_relit_features: missing inputs");
+    if ((reinterpret_cast<uintptr_t>(features) & 15u) != 0)
+        return fail(GSR_E_ARG, "gsr_relit_features: features must be 16-B aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
     char* ws = align_base(workspace);
@@ -1142,6 +1144,7 @@ int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation,
             a.rows = fg_rows;
             a.io_stride = gsr::RELIT_STRIDE;
             a.vp_stride = 0;
+            a.viewmatrix = viewmatrix;  // whole rows (k_relit_prep skips the shaded ones)
             gsr::launch_shade_fwd(a, features, features + 3, features + 6, s);
         }
     }

@@ -310,12 +310,30 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         dl[c] = gamma_f(dh[c]);
     }
     const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
-    st3s(dif, row, a.io_stride, dl[0], dl[1], dl[2]);
+    // the relit features' whole row: rgb, diffuse, specular, depth, 0.5 n + 0.5, 1, 0, 0 as four
+    // 16-B stores (k_relit_prep leaves the shaded rows to this kernel)
+    auto store_row = [&](const float (&r)[3], const float (&d)[3], const float (&sp)[3]) {
+        const float3 q = ld3s(a.pos, row, 3);
+        const float* V = a.viewmatrix;
+        const float depth = q.x * V[2] + q.y * V[6] + q.z * V[10] + V[14];
+        float4* o = reinterpret_cast<float4*>(rgb + row * (size_t)a.io_stride);
+        o[0] = make_float4(r[0], r[1], r[2], d[0]);
+        o[1] = make_float4(d[1], d[2], sp[0], sp[1]);
+        o[2] = make_float4(sp[2], depth, 0.5f * x + 0.5f, 0.5f * y + 0.5f);
+        o[3] = make_float4(0.5f * z + 0.5f, 1.f, 0.f, 0.f);
+    };
     if (!a.specular) {
+        if (a.viewmatrix) {
+            const float zero[3] = {0.f, 0.f, 0.f};
+            store_row(dl, dl, zero);
+            return;
+        }
+        st3s(dif, row, a.io_stride, dl[0], dl[1], dl[2]);
         st3s(rgb, row, a.io_stride, dl[0], dl[1], dl[2]);
         st3s(spe, row, a.io_stride, 0.f, 0.f, 0.f);
         return;
     }
+    if (!a.viewmatrix) st3s(dif, row, a.io_stride, dl[0], dl[1], dl[2]);
     const float3 p = ld3s(a.pos, row, 3);
     const float3 vp = ld3s(a.view_pos, i, a.vp_stride);
     const float kr = a.kr[i];
@@ -351,6 +369,10 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         const float shaded = a.km ? (1 - km) * dh[c] + sh_hdr : dh[c] + sh_hdr;
         out_rgb[c] = gamma_f(shaded);
         out_spe[c] = gamma_f(sh_hdr);
+    }
+    if (a.viewmatrix) {
+        store_row(out_rgb, dl, out_spe);
+        return;
     }
     st3s(rgb, row, a.io_stride, out_rgb[0], out_rgb[1], out_rgb[2]);
     st3s(spe, row, a.io_stride, out_spe[0], out_spe[1], out_spe[2]);
@@ -643,28 +665,24 @@ __global__ void __launch_bounds__(256) k_relit_prep(RelitArgs a) {
     if (i >= a.P) return;
     const float3 xyz = ld3(a.xyz, i);
     const RelitGeom g = relit_geom(a, i, xyz);
-    float* f = a.features + (size_t)i * RELIT_STRIDE;
+    const int rank = a.fg_rank[i];
+    if (rank >= 0) {  // the shade writes this Gaussian's whole row (ShadeArgs.viewmatrix)
+        st3(a.normal_fg, rank, g.n.x, g.n.y, g.n.z);
+        return;
+    }
     // depth: row 2 of W2V = column 2 of world_view_transform (gaussian_model.py:125-130)
     const float* V = a.viewmatrix;
-    f[9] = xyz.x * V[2] + xyz.y * V[6] + xyz.z * V[10] + V[14];
-    f[10] = 0.5f * g.n.x + 0.5f;
-    f[11] = 0.5f * g.n.y + 0.5f;
-    f[12] = 0.5f * g.n.z + 0.5f;
-    f[13] = 1.f;
-    f[14] = 0.f;
-    f[15] = 0.f;
-    const int rank = a.fg_rank[i];
-    if (rank >= 0) {
-        st3(a.normal_fg, rank, g.n.x, g.n.y, g.n.z);
-    } else {
-        float3 c = make_float3(1.f, 1.f, 1.f);
-        if (SDEG >= 0) {
-            c = sky_colour<(SDEG < 0 ? 0 : SDEG)>(g.dir, a.sky_sh);
-            c = make_float3(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f));
-        }
-        f[0] = c.x; f[1] = c.y; f[2] = c.z;
-        f[3] = f[4] = f[5] = f[6] = f[7] = f[8] = 0.f;
+    const float depth = xyz.x * V[2] + xyz.y * V[6] + xyz.z * V[10] + V[14];
+    float3 c = make_float3(1.f, 1.f, 1.f);
+    if (SDEG >= 0) {
+        c = sky_colour<(SDEG < 0 ? 0 : SDEG)>(g.dir, a.sky_sh);
+        c = make_float3(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f));
     }
+    float4* o = reinterpret_cast<float4*>(a.features + (size_t)i * RELIT_STRIDE);
+    o[0] = make_float4(c.x, c.y, c.z, 0.f);
+    o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    o[2] = make_float4(0.f, depth, 0.5f * g.n.x + 0.5f, 0.5f * g.n.y + 0.5f);
+    o[3] = make_float4(0.5f * g.n.z + 0.5f, 1.f, 0.f, 0.f);
 }
 
 // Backward of the preparation: dL/dxyz (depth, sky direction, + the shade's dL/dpos of the

@@ -23,6 +23,10 @@ struct ShadeArgs {
     const int* rows = nullptr;
     int io_stride = 3;
     int vp_stride = 3;
+    // Whole-row mode (gsr_relit_features, io_stride == RELIT_STRIDE, rgb/diffuse/specular at
+    // row offsets 0/3/6): also the row's depth (viewmatrix column 2, device), 0.5 n + 0.5, alpha
+    // 1 and the padding, so every 64-B feature row is written by one kernel in full.
+    const float* viewmatrix = nullptr;
 };
 
 struct ShadeGrads {
