@@ -121,6 +121,20 @@ __device__ __forceinline__ void preprocess_one(const PreprocessArgs& a, const in
         stc = ((rmax.x + GSR_ST_W - 1) / GSR_ST_W - rmin.x / GSR_ST_W) *
               (((rmax.y + (1u << sth) - 1) >> sth) - (rmin.y >> sth));
     } while (false);
+    if (irad == 0) {
+        // culled: defaults into the record, rect and Jacobian rows nobody reads, so that every
+        // cache line of them is written whole (a partly written line costs the memory a
+        // read-modify-write when culled and visible Gaussians interleave)
+        Rec r;
+        r.a = r.b = r.c = make_float4(0.f, 0.f, 0.f, 0.f);
+        a.rec[idx] = r;
+        a.rect[idx] = make_uint2(0u, 0u);
+        if (!a.colors_precomp && a.shs && a.shjac) {
+            const size_t P = (size_t)a.P;
+#pragma unroll
+            for (int k = 0; k < SHJAC_ROWS; k++) a.shjac[(size_t)k * P + idx] = 0.f;
+        }
+    }
     a.depth_key[idx] = key;
     key_out = key;
     a.radii[idx] = irad;
