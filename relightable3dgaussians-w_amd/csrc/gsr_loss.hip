@@ -98,10 +98,14 @@ __global__ void __launch_bounds__(256) k_view_objective(int nvl, const float* __
 #pragma clang fp contract(off)
     __shared__ double red[7][4];
     double a[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    // each thread's partials in the plain strided order, their loads issued 8 iterations at a
+    // time (one workgroup: the latency of one dependent load per iteration was the kernel)
+#pragma unroll 8
     for (int i = threadIdx.x; i < nvl; i += 256) {
 #pragma unroll
         for (int k = 0; k < 5; k++) a[k] += (double)vl[(size_t)i * 5 + k];
     }
+#pragma unroll 8
     for (int i = threadIdx.x; i < nss; i += 256) {
         a[5] += (double)ss[(size_t)i * 2];
         a[6] += (double)ss[(size_t)i * 2 + 1];
