@@ -108,8 +108,13 @@ class FlatParams:
         with torch.no_grad():
             self.params[name].copy_(value.reshape(self.params[name].shape))
 
-    def zero_grad(self) -> None:
-        self.grad.zero_()
+    def zero_grad(self, keep: Sequence[str] = ()) -> None:
+        """Zero the gradient.  keep: segments this step's producers overwrite whole (the fused
+        activations' backward): the zeroing starts at the first segment not kept (one fill of
+        the buffer's tail instead of all of it; kept segments past that point are zeroed too,
+        harmlessly)."""
+        lo = min((o for n, o in zip(self.names, self.offsets) if n not in keep), default=self.n)
+        self.grad[lo:].zero_()
 
     def check_grads_in_place(self) -> None:
         """Autograd accumulated into the preset views (not into fresh tensors)."""
@@ -661,6 +666,9 @@ def sky_angles_clamped(a: torch.Tensor) -> torch.Tensor:
     return torch.cat((th.unsqueeze(1), ph.unsqueeze(1)), dim=1)
 
 
+_ACT_OVERWRITES = ("xyz", "albedo", "opacity", "scaling", "rotation", "roughness", "metalness", "sky_angles")
+
+
 class _Activations(torch.autograd.Function):
     """RelitScene's activations (gaussian_model.py:69-103) in one HIP pass each way
     (gsr_activations_forward / _backward).  The backward writes the raw parameters' gradients
@@ -939,8 +947,9 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     from . import relit
     from . import dp as gdp
     fp = scene.fp
-    fp.zero_grad()
     dev = fp.device
+    # the fused activations' backward overwrites its segments (sky_radius: it adds)
+    fp.zero_grad(keep=_ACT_OVERWRITES if dev.type == "cuda" else ())
     scene.iteration = it = scene.iteration + 1 if iteration is None else int(iteration)
     lam_normal = LAMBDA_NORMAL if (it > REG_NORMAL_FROM_ITER and LAMBDA_NORMAL > 0) else 0.0
     if bg is None:  # one tensor per device: render()'s grey-background check is cached on it
