@@ -232,9 +232,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
-// whole tile.
+// whole tile.  Five waves per SIMD (96 VGPRs, 8 B of scratch per lane outside the survivor
+// walk): 336.6-337.1 -> 330.4-332.5 us at cfg2 against four since the 64-B accumulator lines
+// (tools/r3_check44.sh; neutral before them).
 #ifndef GSR_BWD_WAVES
-#define GSR_BWD_WAVES 4
+#define GSR_BWD_WAVES 5
 #endif
 template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
