@@ -178,8 +178,16 @@ __device__ __forceinline__ int block_visible(int pv_host, const unsigned long lo
     return (int)__builtin_amdgcn_readfirstlane((int)*pv);
 }
 
-template <int ST_W>
-__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const uint2* rect_sorted, unsigned gsx, unsigned sth,
+// The depth-sorted rects: 8 B each, or packed to 4 (pack_rect) on a grid of at most 255 x 255
+// tiles (the depth sort moves 4 bytes less per key and pass, the binning reads 4 less).
+template <bool PACKED>
+__device__ __forceinline__ uint2 sorted_rect(const void* r, int p) {
+    if constexpr (PACKED) return unpack_rect(reinterpret_cast<const uint32_t*>(r)[p]);
+    else return reinterpret_cast<const uint2*>(r)[p];
+}
+
+template <int ST_W, bool PACKED>
+__global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const void* rect_sorted, unsigned gsx, unsigned sth,
                                                   int NS, int nb, uint32_t* table, uint32_t* wcounts) {
     extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
@@ -191,7 +199,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
     uint32_t* wh = hist + wave * NS;
     for (int p = p0 + lane; p < p1; p += 64) {
-        const uint2 sr = st_rect_of(rect_sorted[p], sth);
+        const uint2 sr = st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth);
         for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
             for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
     }
@@ -240,7 +248,8 @@ __device__ __forceinline__ void lds_order() { asm volatile("s_waitcnt lgkmcnt(0)
 // exactly the entries of that super-tile in depth order); the lowest lane then advances
 // the run and clears the mask.  Order-independent atomics only, so the output is
 // deterministic, and each super-tile's entries come out in depth order.
-__device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const uint2* rect_sorted,
+template <bool PACKED>
+__device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_ids, const void* rect_sorted,
                                         unsigned gsx, unsigned sth, uint32_t* wcnt, unsigned long long* wmask, uint2* ent,
                                         uint32_t cap) {
     const int lane = threadIdx.x & 63;
@@ -249,7 +258,7 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
     uint2 r_nx = make_uint2(0u, 0u);
     uint32_t gid_nx = 0;
     if (p0 + lane < p1) {
-        r_nx = rect_sorted[p0 + lane];
+        r_nx = sorted_rect<PACKED>(rect_sorted, p0 + lane);
         gid_nx = sorted_ids[p0 + lane];
     }
     for (int c0 = p0; c0 < p1; c0 += 64) {
@@ -257,7 +266,7 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
         const uint32_t gid = gid_nx;
         const uint2 sr = (c0 + lane < p1) ? st_rect_of(r, sth) : make_uint2(0u, 0u);
         if (c0 + 64 + lane < p1) {
-            r_nx = rect_sorted[c0 + 64 + lane];
+            r_nx = sorted_rect<PACKED>(rect_sorted, c0 + 64 + lane);
             gid_nx = sorted_ids[c0 + 64 + lane];
         }
         const uint32_t sx0 = sr.x & 0xffffu, sx1 = sr.x >> 16, sy0 = sr.y & 0xffffu, sy1 = sr.y >> 16;
@@ -289,9 +298,9 @@ if (pos < cap)  // S beyond the speculative capacity: the forward redoes the bin
 // forward's dispatch order, one workgroup per XCD band (costs from the super-tile totals, so
 // neither needs a launch of its own).  Each scatter block scans the super-tile totals into
 // the super-tile bases itself (block 0 also writes the ranges and header[0] = S).
-template <int ST_W>
+template <int ST_W, bool PACKED>
 __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
-                                                     const uint2* rect_sorted, unsigned gsx, unsigned sth, int NS, int nb,
+                                                     const void* rect_sorted, unsigned gsx, unsigned sth, int NS, int nb,
                                                      const uint32_t* table, const uint32_t* wcounts,
                                                      const uint32_t* tot, uint2* st_ranges, unsigned long long* header,
                                                      uint2* ent, uint32_t cap, FrameTotals ft, TileOrderArgs ord) {
@@ -334,7 +343,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) header[0] = min(carry, cap);
     __syncthreads();
-    st_pass(p0, p1, sorted_ids, rect_sorted, gsx, sth, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
+    st_pass<PACKED>(p0, p1, sorted_ids, rect_sorted, gsx, sth, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
 }
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
@@ -347,9 +356,10 @@ size_t st_bin_temp_bytes(long long Pv, int NS) {
 // per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
 bool st_bin_supported(int NS) { return 12 * 4 * NS <= 65536; }
 
-void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
-                   uint32_t cap, hipStream_t s, const FrameTotals* ftp, const TileOrderArgs* ordp) {
+void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids, const void* rect_sorted,
+                   bool packed, unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges,
+                   unsigned long long* header, uint32_t cap, hipStream_t s, const FrameTotals* ftp,
+                   const TileOrderArgs* ordp) {
     FrameTotals ft{};
     if (ftp) ft = *ftp;
     TileOrderArgs ord{};
@@ -376,21 +386,21 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
-    if (W == 8)
-        hipLaunchKernelGGL(k_st_hist<8>, dim3(nb), dim3(512), 4 * 8 * NS, s, Pv, totals, rect_sorted, gsx, sth, NS, nb,
-                           table, wcounts);
-    else
-        hipLaunchKernelGGL(k_st_hist<4>, dim3(nb), dim3(256), 4 * 4 * NS, s, Pv, totals, rect_sorted, gsx, sth, NS, nb,
-                           table, wcounts);
+    auto hist = [&](auto kern, int threads) {
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(threads), 4 * (threads / 64) * NS, s, Pv, totals, rect_sorted, gsx, sth,
+                           NS, nb, table, wcounts);
+    };
+    if (W == 8) packed ? hist(k_st_hist<8, true>, 512) : hist(k_st_hist<8, false>, 512);
+    else packed ? hist(k_st_hist<4, true>, 256) : hist(k_st_hist<4, false>, 256);
     launch_digit_scan(NS, table, nb, tot, s);
     if (ordp) ord.st_tot = tot;
     const dim3 grid(nb + (ftp ? 1 : 0) + (ordp && ord.ntile ? 8 : 0));
-    if (W == 8)
-        hipLaunchKernelGGL(k_st_scatter<8>, grid, dim3(512), 12 * 8 * NS, s, Pv, totals, sorted_ids, rect_sorted,
+    auto scatter = [&](auto kern, int threads) {
+        hipLaunchKernelGGL(kern, grid, dim3(threads), 12 * (threads / 64) * NS, s, Pv, totals, sorted_ids, rect_sorted,
                            gsx, sth, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
-    else
-        hipLaunchKernelGGL(k_st_scatter<4>, grid, dim3(256), 12 * 4 * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, sth, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
+    };
+    if (W == 8) packed ? scatter(k_st_scatter<8, true>, 512) : scatter(k_st_scatter<8, false>, 512);
+    else packed ? scatter(k_st_scatter<4, true>, 256) : scatter(k_st_scatter<4, false>, 256);
 }
 
 // super-tile segment bounds in the sorted entry list; empty super-tiles stay (0, 0)

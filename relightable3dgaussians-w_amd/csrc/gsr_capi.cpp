@@ -611,6 +611,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     // Depth sort of all P Gaussians: culled ones carry key 0xFFFFFFFF and sort last, so the
     // first P_v sorted entries are the visible Gaussians in the reference's (depth, index)
     // order -- no separate visibility compaction.  Its last pass stores P_v to tot_dev.
+    const bool rect_packed = gsr::rect_packable(gx, gy);  // 4-B rects through the sort and the binning
     uint32_t* vis_key = at<uint32_t>(geom, gl.vis_key);
     uint32_t* vis_val = at<uint32_t>(geom, gl.vis_val);
     int flip;
@@ -619,7 +620,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         flip = gsr::depth_sort(P, pa.depth_key, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
                                at<uint32_t>(geom, gl.vis_val_alt), pa.rect, at<uint2>(geom, gl.rect_s),
                                at<uint2>(geom, gl.rect_s_alt), at<void>(geom, gl.sort_tmp), tot_dev, s,
-                               at<void>(geom, gl.acc), sizeof(float) * gsr::ACC_STRIDE * (size_t)P);
+                               at<void>(geom, gl.acc), sizeof(float) * gsr::ACC_STRIDE * (size_t)P, rect_packed);
     }
     zeroed_set(geom, true);  // the backward's accumulators are zero from here on
     GSR_LAUNCH_CHECK();
@@ -638,7 +639,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         return GSR_OK;
     };
     const uint32_t* sorted_ids = flip ? at<uint32_t>(geom, gl.vis_val_alt) : vis_val;
-    const uint2* rect_sorted = flip ? at<uint2>(geom, gl.rect_s_alt) : at<uint2>(geom, gl.rect_s);
+    const void* rect_sorted = flip ? at<void>(geom, gl.rect_s_alt) : at<void>(geom, gl.rect_s);
     char* bin = nullptr;
     BinLayout bl{};
     // binning into a buffer of entry capacity capS; dev: read P_v on the device (and run the
@@ -660,7 +661,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
-            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, gsx, st_h(width, height), NS,
+            gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, rect_packed, gsx, st_h(width, height), NS,
                                at<void>(bin, bl.st_bin_tmp), ent, st_ranges, header, (uint32_t)capS, s,
                                dev ? &ft : nullptr, &ord);
             GSR_LAUNCH_CHECK();

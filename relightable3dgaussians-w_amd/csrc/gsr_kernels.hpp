@@ -94,7 +94,17 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 size_t depth_sort_temp_bytes(long long P);
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
-               unsigned long long* pv_out, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0);
+               unsigned long long* pv_out, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0,
+               bool pack = false);
+// A grid of at most 255 x 255 tiles sorts and bins its rects packed to 4 bytes (pack_rect).
+inline bool rect_packable(unsigned gx, unsigned gy) { return gx <= 255u && gy <= 255u; }
+// (x0 | x1 << 16, y0 | y1 << 16) <-> x0 | x1 << 8 | y0 << 16 | y1 << 24 (every bound <= 255)
+__host__ __device__ inline uint32_t pack_rect(uint2 r) {
+    return (r.x & 0xffu) | ((r.x >> 8) & 0xff00u) | ((r.y & 0xffu) << 16) | ((r.y << 8) & 0xff000000u);
+}
+__host__ __device__ inline uint2 unpack_rect(uint32_t p) {
+    return make_uint2((p & 0xffu) | ((p & 0xff00u) << 8), ((p >> 16) & 0xffu) | ((p >> 8) & 0xff0000u));
+}
 
 // One pass's dispatch order (k_tile_order, or extra workgroups of the binning scatter).
 struct TileOrderArgs {
@@ -146,8 +156,9 @@ bool st_bin_supported(int NS);
 // reading the visible count *dev_totals (depth_sort's pv_out) on the device.  Entries at
 // positions >= cap are not written (the speculative forward detects the overflow and redoes
 // the binning).  ft (optional): the frame totals run as one extra workgroup of the scatter.
-void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const uint2* rect_sorted,
-                   unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges, unsigned long long* header,
+void launch_st_bin(int Pv, const unsigned long long* dev_totals, const uint32_t* sorted_ids, const void* rect_sorted,
+                   bool packed, unsigned gsx, unsigned sth, int NS, void* temp, uint2* ent, uint2* st_ranges,
+                   unsigned long long* header,
                    uint32_t cap, hipStream_t s, const FrameTotals* ft = nullptr, const TileOrderArgs* order = nullptr);
 // Large images (NS > 1365): in depth order, every visible Gaussian emits one (super-tile,
 // gaussian) pair per super-tile its rect touches, at offsets[s] (exclusive scan of st_count

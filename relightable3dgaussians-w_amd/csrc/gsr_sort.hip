@@ -133,25 +133,37 @@ __device__ __forceinline__ void digits_exclusive_scan(uint32_t (&v)[DPT], uint32
     }
 }
 
-// AUX: an 8-byte side payload (the Gaussians' tile rects) moves with every pair, so that the
-// depth-sorted order never has to gather it at random afterwards
+// AUX: a side payload (the Gaussians' tile rects) moves with every pair, so that the
+// depth-sorted order never has to gather it at random afterwards.  PACK: 0 = an 8-byte rect
+// (four 16-bit tile bounds) in and out; 1 = 8 bytes in, packed to 4 (four 8-bit bounds,
+// pack_rect) as it is loaded; 2 = 4 bytes in and out.  A grid of at most 255 x 255 tiles (4080
+// x 4080 pixels) sorts its rects packed: 12 instead of 16 bytes move per key and pass.
 // The offsets table has ocol columns (0: nb) and block blk's column is blk * ostride (the
 // preprocess-made first table of the depth sort has 8 columns per 2048-key block).
 // (Counting the NEXT pass's histogram here with global atomics per key, instead of the
 // separate k_radix_hist, measured 5-15x slower: ~1.5M L2 atomics per pass.)
-template <bool AUX, int BITS = 8>
+template <int PACK> struct AuxT { using in = uint2; using out = uint2; };
+template <> struct AuxT<1> { using in = uint2; using out = uint32_t; };
+template <> struct AuxT<2> { using in = uint32_t; using out = uint32_t; };
+__device__ __forceinline__ uint2 aux_cvt(uint2 r, uint2*) { return r; }
+__device__ __forceinline__ uint32_t aux_cvt(uint2 r, uint32_t*) { return pack_rect(r); }
+__device__ __forceinline__ uint32_t aux_cvt(uint32_t r, uint32_t*) { return r; }
+
+template <bool AUX, int BITS = 8, int PACK = 0>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
                                                                   const uint32_t* offsets, const uint32_t* digit_tot,
                                                                   int nb, uint32_t* keys_out, uint32_t* vals_out,
-                                                                  const uint2* aux_in, uint2* aux_out, int ocol = 0,
+                                                                  const typename AuxT<PACK>::in* aux_in,
+                                                                  typename AuxT<PACK>::out* aux_out, int ocol = 0,
                                                                   int ostride = 1,
                                                                   unsigned long long* pv_out = nullptr) {
     constexpr int NB = 1 << BITS, DPT = NB / SORT_THREADS;
     static_assert(DPT >= 1, "at least one digit per thread");
+    using AO = typename AuxT<PACK>::out;
     __shared__ uint32_t s_keys[SORT_TILE];
     __shared__ uint32_t s_vals[SORT_TILE];
-    __shared__ uint2 s_aux[AUX ? SORT_TILE : 1];
+    __shared__ AO s_aux[AUX ? SORT_TILE : 1];
     __shared__ uint32_t wh[4][NB];
     __shared__ uint32_t dstart[NB];
     __shared__ uint32_t goff[NB];
@@ -163,7 +175,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     const long long tile_base = (long long)blk * SORT_TILE;
     const long long base = tile_base + wave * WAVE_ITEMS;
     uint32_t key[SORT_ITEMS], val[SORT_ITEMS], rank[SORT_ITEMS];
-    uint2 aux[AUX ? SORT_ITEMS : 1];
+    // the rects stay as loaded in registers (PACK 1 packs them on their way into LDS: packing at
+    // the load would wait for each load before the ranking starts)
+    using AI = typename AuxT<PACK>::in;
+    AI aux[AUX ? SORT_ITEMS : 1];
     volatile uint32_t* wc = wh[wave];
     const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     // all loads first (SORT_ITEMS per lane in flight), then the ranking
@@ -172,7 +187,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
         const long long i = base + k * 64 + lane;
         key[k] = i < n ? keys_in[i] : 0u;
         val[k] = i < n ? (vals_in ? vals_in[i] : (uint32_t)i) : 0u;
-        if constexpr (AUX) aux[k] = i < n ? aux_in[i] : make_uint2(0u, 0u);
+        if constexpr (AUX) aux[k] = i < n ? aux_in[i] : AI{};
     }
 #pragma unroll
     for (int k = 0; k < SORT_ITEMS; k++) {
@@ -227,7 +242,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
             const uint32_t p = wh[wave][d] + rank[k];
             s_keys[p] = key[k];
             s_vals[p] = val[k];
-            if constexpr (AUX) s_aux[p] = aux[k];
+            if constexpr (AUX) s_aux[p] = aux_cvt(aux[k], (AO*)nullptr);
         }
     }
     __syncthreads();
@@ -297,7 +312,7 @@ size_t depth_sort_temp_bytes(long long P) {
 
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
-               unsigned long long* pv_out, hipStream_t s, void* zero, size_t zero_bytes) {
+               unsigned long long* pv_out, hipStream_t s, void* zero, size_t zero_bytes, bool pack) {
     if (P <= 0) return -1;
     constexpr int BITS = GSR_DEPTH_BITS, NB = 1 << BITS, NPASS = (32 + BITS - 1) / BITS;
     const int nb = sort_blocks(P);
@@ -322,9 +337,18 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
         const unsigned zb = (unsigned)((q1 - q0 + per_blk - 1) / per_blk);
         hipLaunchKernelGGL(k_digit_scan, dim3(NB + zb), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot,
                            zb ? reinterpret_cast<float4*>(zero) + q0 : (float4*)nullptr, q1 - q0, NB);
-        hipLaunchKernelGGL((k_radix_scatter<true, BITS>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift, mask,
-                           hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1,
-                           pass == NPASS - 1 ? pv_out : (unsigned long long*)nullptr);
+        unsigned long long* pv = pass == NPASS - 1 ? pv_out : (unsigned long long*)nullptr;
+        if (!pack)
+            hipLaunchKernelGGL((k_radix_scatter<true, BITS, 0>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
+                               mask, hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1, pv);
+        else if (pass == 0)  // the packed rects (4 B) in the first half of each 8-B buffer
+            hipLaunchKernelGGL((k_radix_scatter<true, BITS, 1>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
+                               mask, hist, digit_tot, nb, out_k[cur], out_v[cur], ain,
+                               reinterpret_cast<uint32_t*>(out_a[cur]), 0, 1, pv);
+        else
+            hipLaunchKernelGGL((k_radix_scatter<true, BITS, 2>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
+                               mask, hist, digit_tot, nb, out_k[cur], out_v[cur], reinterpret_cast<const uint32_t*>(ain),
+                               reinterpret_cast<uint32_t*>(out_a[cur]), 0, 1, pv);
         ain = out_a[cur];
         kin = out_k[cur];
         vin = out_v[cur];
