@@ -65,10 +65,12 @@ VALU_CYCLES_PER_INST = 2
 
 def _pmc_record(stage, workload):
     """The newest committed rocprofv3 record (profiles/r*_hbm_traffic.json, tools/profile_summary.py)
-    of the stage's kernel whose profiled bench line ran the same workload; ({}, None) if none."""
+    of the stage's kernel whose profiled bench line ran the same workload; ({}, None) if none.
+    Newest = the latest `created` stamp; records written before the stamp existed rank below
+    every stamped one, among themselves by tag."""
     import glob
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json")), reverse=True):
-        d = json.load(open(f))
+    recs = [(json.load(open(f)), f) for f in glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json"))]
+    for d, f in sorted(recs, key=lambda r: (r[0].get("created", ""), os.path.basename(r[1])), reverse=True):
         b = d.get("bench_under_profiler") or {}
         if (b.get("config") or {}).get("workload", "").split(",")[0] != workload.split(",")[0]:
             continue

@@ -20,6 +20,7 @@ import json
 import os
 import statistics
 import sys
+import time
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -71,7 +72,8 @@ def main(tag="r01"):
         for line in open(log):
             if line.startswith("{\"metric\""):
                 bench = json.loads(line)
-    json.dump(dict(tag=tag, correction="traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch (gfx950)",
+    json.dump(dict(tag=tag, created=time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+                   correction="traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch (gfx950)",
                    command="rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
                            "--no-cpu-baseline --no-refalgo --no-train [--no-minibatch] <workload args>; separate "
                            "--pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES passes",
