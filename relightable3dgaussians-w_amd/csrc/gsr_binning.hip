@@ -166,6 +166,11 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 #define GSR_ST_G 1024
 #endif
 constexpr int ST_G = GSR_ST_G;  // Gaussians per block
+// 1: k_st_hist stores its per-wave counts and k_st_scatter reads them (the round-3 layout, kept
+// for A/B); 0: k_st_scatter counts its waves' entries itself
+#ifndef GSR_ST_WCOUNTS
+#define GSR_ST_WCOUNTS 0
+#endif
 // waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
 // per-wave LDS state of 8 waves would not fit (st_waves)
 
@@ -204,8 +209,10 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
             for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
     }
     __syncthreads();
+#if GSR_ST_WCOUNTS
     uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) wc[i] = hist[i];
+#endif
     for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
         uint32_t t = 0;
 #pragma unroll
@@ -320,8 +327,26 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     const int g0 = blk * ST_G;
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
     // super-tile s's base (exclusive scan of the totals); each wave's run of s starts there +
-    // the block's offset + the counts of the block's earlier waves (k_st_hist's per-wave counts)
+    // the block's offset + the counts of the block's earlier waves.  The waves count their
+    // entries per super-tile again here, into the run counters, from the rects k_st_hist read
+    // (4 KiB per block, L2-resident): storing k_st_hist's per-wave counts and reading them back
+    // moved 4 x ST_W x NS bytes per block through HBM (80 MB each way at cfg5).
+#if GSR_ST_WCOUNTS
     const uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
+#else
+    for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) wcnt_all[i] = 0u;
+    __syncthreads();
+    {
+        const int lane = threadIdx.x & 63;
+        uint32_t* wh = wcnt_all + wave * NS;
+        for (int p = p0 + lane; p < p1; p += 64) {
+            const uint2 sr = st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth);
+            for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
+                for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
+        }
+    }
+    __syncthreads();
+#endif
     uint32_t carry = 0;
     for (int c = 0; c < NS; c += 64 * ST_W) {
         const int i = c + (int)threadIdx.x;
@@ -334,9 +359,14 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
             if (blockIdx.x == 0) st_ranges[i] = v ? make_uint2(min(ex, cap), min(ex + v, cap)) : make_uint2(0u, 0u);
             uint32_t run = ex + table[(size_t)i * nb + blk];
             for (int w = 0; w < ST_W; w++) {
+#if GSR_ST_WCOUNTS
+                const uint32_t c = wc[w * NS + i];
+#else
+                const uint32_t c = wcnt_all[w * NS + i];  // this thread's super-tile only
+#endif
                 wmask_all[w * NS + i] = 0ull;
                 wcnt_all[w * NS + i] = run;
-                run += wc[w * NS + i];
+                run += c;
             }
         }
         carry += t;
@@ -350,7 +380,7 @@ static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
 
 size_t st_bin_temp_bytes(long long Pv, int NS) {
     const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
-    return (4 + 4 * (size_t)st_waves(NS)) * (size_t)NS * nb + 8 * (size_t)NS + 4 * 256 + 1024;
+    return (4 + (GSR_ST_WCOUNTS ? 4 * (size_t)st_waves(NS) : 0)) * (size_t)NS * nb + 8 * (size_t)NS + 4 * 256 + 1024;
 }
 
 // per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
@@ -385,7 +415,7 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     };
     uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
-    uint32_t* wcounts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb));
+    uint32_t* wcounts = GSR_ST_WCOUNTS ? reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb)) : nullptr;
     auto hist = [&](auto kern, int threads) {
         hipLaunchKernelGGL(kern, dim3(nb), dim3(threads), 4 * (threads / 64) * NS, s, Pv, totals, rect_sorted, gsx, sth,
                            NS, nb, table, wcounts);
