@@ -136,7 +136,7 @@ __device__ __forceinline__ void digits_exclusive_scan(uint32_t (&v)[DPT], uint32
 // AUX: a side payload (the Gaussians' tile rects) moves with every pair, so that the
 // depth-sorted order never has to gather it at random afterwards.  PACK: 0 = an 8-byte rect
 // (four 16-bit tile bounds) in and out; 1 = 8 bytes in, packed to 4 (four 8-bit bounds,
-// pack_rect) as it is loaded; 2 = 4 bytes in and out.  A grid of at most 255 x 255 tiles (4080
+// pack_rect) on its way into LDS; 2 = 4 bytes in and out.  A grid of at most 255 x 255 tiles (4080
 // x 4080 pixels) sorts its rects packed: 12 instead of 16 bytes move per key and pass.
 // The offsets table has ocol columns (0: nb) and block blk's column is blk * ostride (the
 // preprocess-made first table of the depth sort has 8 columns per 2048-key block).
