@@ -191,18 +191,26 @@ __device__ __forceinline__ uint2 sorted_rect(const void* r, int p) {
     else return reinterpret_cast<const uint2*>(r)[p];
 }
 
+// k_st_hist's LDS histograms: one per wave when the per-wave counts are stored, else one per
+// block unless GSR_ST_HIST_SHARED=0 (one per wave, summed)
+#ifndef GSR_ST_HIST_SHARED
+#define GSR_ST_HIST_SHARED 1
+#endif
+constexpr int st_hist_count(int st_w) { return (GSR_ST_WCOUNTS || !GSR_ST_HIST_SHARED) ? st_w : 1; }
+
 template <int ST_W, bool PACKED>
 __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const void* rect_sorted, unsigned gsx, unsigned sth,
                                                   int NS, int nb, uint32_t* table, uint32_t* wcounts) {
-    extern __shared__ uint32_t hist[];  // [ST_W][NS]: per wave, the waves of k_st_scatter
-    for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) hist[i] = 0;
+    constexpr int NH = st_hist_count(ST_W);
+    extern __shared__ uint32_t hist[];  // [NH][NS]
+    for (int i = threadIdx.x; i < NH * NS; i += (64 * ST_W)) hist[i] = 0;
     Pv = block_visible(Pv, totals);
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int g0 = blk * ST_G;
     const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
-    uint32_t* wh = hist + wave * NS;
+    uint32_t* wh = hist + (NH > 1 ? wave : 0) * NS;
     for (int p = p0 + lane; p < p1; p += 64) {
         const uint2 sr = st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth);
         for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
@@ -216,7 +224,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned lo
     for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
         uint32_t t = 0;
 #pragma unroll
-        for (int w = 0; w < ST_W; w++) t += hist[w * NS + i];
+        for (int w = 0; w < NH; w++) t += hist[w * NS + i];
         table[(size_t)i * nb + blk] = t;
     }
 }
@@ -417,7 +425,7 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
     uint32_t* wcounts = GSR_ST_WCOUNTS ? reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb)) : nullptr;
     auto hist = [&](auto kern, int threads) {
-        hipLaunchKernelGGL(kern, dim3(nb), dim3(threads), 4 * (threads / 64) * NS, s, Pv, totals, rect_sorted, gsx, sth,
+        hipLaunchKernelGGL(kern, dim3(nb), dim3(threads), 4 * st_hist_count(threads / 64) * NS, s, Pv, totals, rect_sorted, gsx, sth,
                            NS, nb, table, wcounts);
     };
     if (W == 8) packed ? hist(k_st_hist<8, true>, 512) : hist(k_st_hist<8, false>, 512);
