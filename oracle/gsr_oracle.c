@@ -60,6 +60,49 @@ typedef float REAL;
 #define POW powf
 #endif
 
+/* ---- the Gaussian's exponent at a pixel: forward.cu:335,343 and backward.cu:494-498 --------
+ * power = -0.5 (a dx^2 + c dy^2) - b dx dy,  G = exp(power).
+ * Error-budget variants (oracle/Makefile; tools/error_budget.py) -- the canonical
+ * build defines none of them:
+ *   ORC_GPU_EXPONENT  the HIP tile passes' arithmetic (gsr_tile.hpp gauss_power / tile_exp2):
+ *                     conic pre-scaled by log2(e), two fused multiply-adds, exp2.  It proves
+ *                     (or refutes) that the GPU's per-pair decisions differ from this oracle's
+ *                     only through this arithmetic.
+ *   ORC_EXP_ULP=k     expf's result moved by a deterministic pseudo-random whole number of
+ *                     ulps in [-k, k] (CUDA's expf is specified to 2 ulp, glibc's to < 1):
+ *                     how far the reference's own libm choice moves its outputs.
+ * (A third variant, liboracle_fma.so, is this source built with FMA contraction on, as nvcc
+ * builds the reference by default: -fmad=true.) */
+#if defined(ORC_GPU_EXPONENT) && !defined(ORC_F64)
+static inline REAL orc_gauss(const REAL* co, REAL dx, REAL dy, REAL* power) {
+    const float h = -0.5f * 1.44269504088896340736f, n = -1.44269504088896340736f;
+    const float na = h * co[0], nb = n * co[1], nc = h * co[2];
+    *power = fmaf(na * dx, dx, fmaf(nc * dy, dy, (nb * dx) * dy));  /* log2 units: same sign */
+    return exp2f(*power);
+}
+#else
+static inline REAL orc_gauss(const REAL* co, REAL dx, REAL dy, REAL* power) {
+    *power = F(-0.5) * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+    REAL G = EXP(*power);
+#if defined(ORC_EXP_ULP) && !defined(ORC_F64)
+    {
+        uint32_t u, k;
+        memcpy(&u, power, 4);
+        k = u * 2654435761u;
+        k ^= k >> 15;
+        k *= 2246822519u;
+        k ^= k >> 13;
+        int off = (int)(k % (2u * ORC_EXP_ULP + 1u)) - ORC_EXP_ULP;
+        uint32_t g;
+        memcpy(&g, &G, 4);
+        if (G >= 1.17549435e-38f) g = (uint32_t)((int32_t)g + off); /* normal numbers only */
+        memcpy(&G, &g, 4);
+    }
+#endif
+    return G;
+}
+#endif
+
 #define BLOCK_X 16
 #define BLOCK_Y 16
 
@@ -396,9 +439,10 @@ void orc_render_fwd(int W, int H, const uint32_t* ranges, const uint32_t* point_
                     uint32_t g = point_list[j];
                     REAL d[2] = {points_xy[2 * g] - pixf[0], points_xy[2 * g + 1] - pixf[1]};
                     const REAL* co = conic_opacity + 4 * g;
-                    REAL power = F(-0.5) * (co[0] * d[0] * d[0] + co[2] * d[1] * d[1]) - co[1] * d[0] * d[1];
+                    REAL power;
+                    const REAL G = orc_gauss(co, d[0], d[1], &power);
                     if (power > F(0.0)) continue;
-                    REAL alpha = FMIN(F(0.99), co[3] * EXP(power));
+                    REAL alpha = FMIN(F(0.99), co[3] * G);
                     if (alpha < F(1.0) / F(255.0)) continue;
                     REAL test_T = T * (1 - alpha);
                     if (test_T < F(0.0001)) break;
@@ -449,9 +493,9 @@ void orc_render_bwd(int P, int W, int H, const uint32_t* ranges, const uint32_t*
                     uint32_t g = point_list[ry - k - 1];
                     REAL d[2] = {points_xy[2 * g] - pixf[0], points_xy[2 * g + 1] - pixf[1]};
                     const REAL* co = conic_opacity + 4 * g;
-                    REAL power = F(-0.5) * (co[0] * d[0] * d[0] + co[2] * d[1] * d[1]) - co[1] * d[0] * d[1];
+                    REAL power;
+                    REAL G = orc_gauss(co, d[0], d[1], &power);
                     if (power > F(0.0)) continue;
-                    REAL G = EXP(power);
                     REAL alpha = FMIN(F(0.99), co[3] * G);
                     if (alpha < F(1.0) / F(255.0)) continue;
                     T = T / (F(1.0) - alpha);

@@ -28,10 +28,27 @@ def build():
     subprocess.check_call(["make", "-s", "-C", _HERE])
 
 
+# float build used by every f32 call: "" = the canonical oracle; "gpuexp", "ulp1", "ulp2", "fma"
+# = the error-budget variants of oracle/Makefile (tools/error_budget.py, tests/test_error_budget.py)
+VARIANTS = ("", "gpuexp", "ulp1", "ulp2", "fma")
+_variant = os.environ.get("GSR_ORACLE_VARIANT", "")
+_variant = "" if _variant == "f64" else _variant  # "f64": oracle_torch runs the float64 build
+
+
+def use_variant(name=""):
+    """Route every later float oracle call to build `name` (see VARIANTS); returns the previous."""
+    global _variant
+    if name not in VARIANTS:
+        raise ValueError(f"unknown oracle variant {name!r}")
+    prev, _variant = _variant, name
+    return prev
+
+
 def _lib(f64=False):
-    key = "f64" if f64 else "f32"
+    key = "f64" if f64 else "f32" + _variant
     if key not in _libs:
-        path = os.path.join(_BUILD, "liboracle64.so" if f64 else "liboracle.so")
+        path = os.path.join(_BUILD, "liboracle64.so" if f64 else
+                            ("liboracle_%s.so" % _variant if _variant else "liboracle.so"))
         if not os.path.exists(path):
             build()
         _libs[key] = C.CDLL(path)

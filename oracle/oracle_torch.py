@@ -33,10 +33,17 @@ class GaussianRasterizationSettings(NamedTuple):
     prefiltered: bool
 
 
+import os
+
+# GSR_ORACLE_VARIANT=f64: the rasterizer calls run the float64 build (exact-arithmetic proxy for
+# tools/error_budget.py); their outputs are rounded to float32 as render() expects
+F64 = os.environ.get("GSR_ORACLE_VARIANT", "") == "f64"
+
+
 def _np(t):
     if t is None or (isinstance(t, torch.Tensor) and t.numel() == 0):
         return None
-    return t.detach().cpu().contiguous().numpy().astype(np.float32)
+    return t.detach().cpu().contiguous().numpy().astype(np.float64 if F64 else np.float32)
 
 
 class _OracleRasterize(torch.autograd.Function):
@@ -50,18 +57,21 @@ class _OracleRasterize(torch.autograd.Function):
                     viewmatrix=_np(st.viewmatrix), projmatrix=_np(st.projmatrix), tanfovx=float(st.tanfovx),
                     tanfovy=float(st.tanfovy), sh=_np(sh), sh_degree=int(st.sh_degree), campos=_np(st.campos))
         fwd = orc.forward(opacities=_np(opacities), H=int(st.image_height), W=int(st.image_width),
-                          prefiltered=bool(st.prefiltered), **args)
+                          prefiltered=bool(st.prefiltered), f64=F64, **args)
         ctx.fwd, ctx.args = fwd, args
         ctx.shapes = [None if t is None else t.shape for t in (means3D, sh, colors_precomp, opacities, scales,
                                                                 rotations, cov3Ds_precomp)]
-        color = torch.from_numpy(fwd["color"].copy())
+        color = torch.from_numpy(fwd["color"].astype(np.float32))
         radii = torch.from_numpy(fwd["radii"].copy())
         ctx.mark_non_differentiable(radii)
         return color, radii
 
     @staticmethod
     def backward(ctx, grad_color, _grad_radii):
-        g = orc.backward(ctx.fwd, dL_dout=grad_color.detach().contiguous().numpy().astype(np.float32), **ctx.args)
+        g = orc.backward(ctx.fwd, dL_dout=grad_color.detach().contiguous().numpy().astype(
+            np.float64 if F64 else np.float32), f64=F64, **ctx.args)
+        g = {k: (v.astype(np.float32) if isinstance(v, np.ndarray) and v.dtype == np.float64 else v)
+             for k, v in g.items()}
         s_m3, s_sh, s_col, s_op, s_sc, s_rot, s_cov = ctx.shapes
         t = lambda a, shp: torch.from_numpy(np.ascontiguousarray(a)).reshape(shp) if shp is not None and \
             int(np.prod(shp)) > 0 else None

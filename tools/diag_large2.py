@@ -38,3 +38,13 @@ if d.any():
     ys, xs = np.nonzero(d)
     print("first mismatches (y, x, gpu, oracle):", list(zip(ys[:10].tolist(), xs[:10].tolist(), nc_g[d][:10].tolist(),
                                                             nc_r[d][:10].tolist())))
+# alpha-threshold decision flips (per (pixel, Gaussian) `alpha < 1/255` decisions that differ):
+# n_contrib only sees the last contributor, but a flipped Gaussian with alpha ~ 1/255 moves the
+# pixel's final transmittance by a factor (1 - alpha) ~ 0.996, while rounding moves it ~1e-6
+tg, tr = st["final_T"].reshape(H, W), ref["final_T"].reshape(H, W)
+rel = np.abs(tg - tr) / tr
+fl = rel > 1e-3
+print("final_T max rel", float(rel.max()), "flip pixels", int(fl.sum()), "ratios", (tg[fl] / tr[fl])[:20].tolist())
+ys, xs = np.nonzero(fl)
+print("flip pixels (y, x):", list(zip(ys[:20].tolist(), xs[:20].tolist())))
+print("colour max abs outside flip pixels", float(np.abs(c - ref["color"]).reshape(3, H, W)[:, ~fl].max()))

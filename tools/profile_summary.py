@@ -38,7 +38,7 @@ def counters(pattern):
     return acc
 
 
-def main(tag="r01"):
+def main(tag="r01", workload=None):
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     g = os.path.join(ROOT, "gpurun_out")
@@ -74,14 +74,18 @@ def main(tag="r01"):
                 bench = json.loads(line)
     json.dump(dict(tag=tag, created=time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
                    correction="traffic = (2*FETCH_SIZE + WRITE_SIZE) * 1024 B per launch (gfx950)",
-                   command="rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
+                   command=("tools/profile_train.sh: rocprofv3 --kernel-trace --stats, then separate --pmc FETCH_SIZE, "
+                            "--pmc WRITE_SIZE, --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES passes over "
+                            "tools/train_kernels.py") if workload else
+                           ("rocprofv3 --kernel-trace --stats -- python3 bench.py --steps 10 --warmup 3 "
                            "--no-cpu-baseline --no-refalgo --no-train [--no-minibatch] <workload args>; separate "
-                           "--pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES passes",
-                   kernels=res, bench_under_profiler=bench),
+                           "--pmc FETCH_SIZE, --pmc WRITE_SIZE and --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES passes"),
+                   workload=workload, kernels=res, bench_under_profiler=bench),
               open(os.path.join(out_dir, f"{tag}_hbm_traffic.json"), "w"), indent=1)
     with open(os.path.join(out_dir, f"{tag}_summary.md"), "w") as f:
-        wl = ((bench or {}).get("config") or {}).get("workload", "bench.py's default workload")
-        f.write(f"# rocprofv3 summary {tag}\n\nbench.py under rocprofv3, workload: {wl}; "
+        wl = workload or ((bench or {}).get("config") or {}).get("workload", "bench.py's default workload")
+        f.write(f"# rocprofv3 summary {tag}\n\n{'tools/profile_train.sh' if workload else 'bench.py'} under "
+                f"rocprofv3, workload: {wl}; "
                 "traffic = (2*FETCH_SIZE + WRITE_SIZE)*1024 B per launch.\n\n")
         f.write("| kernel | calls | avg ms | % | FETCH KiB | WRITE KiB | HBM MB/launch | GB/s | VALU Minst/launch "
                 "| SALU Minst/launch |\n|---|---|---|---|---|---|---|---|---|---|\n")
