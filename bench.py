@@ -2,13 +2,14 @@
 """bench.py -- MPix/s fwd+bwd of the MI355X rasterizer on BASELINE.json's headline config.
 
 Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): 1.5M synthetic Gaussians, SH degree 3,
-1920x1080.  A step is one view per GPU at N = 1: one rasterizer forward + backward through the
-drop-in diff_gaussian_rasterization._C (libgsr.so, hand-written gfx950 HIP) -- the reference's
-call pair, inputs resident in HBM.  With --gpus N > 1 (one process per GPU, launched by
-torch.distributed.run) every rank holds the same replicated scene and renders 4 distinct
-views per step (cfg4's per-GPU mini-batch), and the per-Gaussian gradients of the step are
-summed over ranks with one RCCL all-reduce (weak scaling: view-parallel data parallelism,
-SURVEY §8e).
+1920x1080.  A step is 4 views per GPU at every N (cfg4's per-GPU mini-batch), each one
+rasterizer forward + backward through the drop-in diff_gaussian_rasterization._C (libgsr.so,
+hand-written gfx950 HIP) -- the reference's call pair, inputs resident in HBM -- one after
+another on one stream.  With --gpus N > 1 (one process per GPU, launched by
+torch.distributed.run) every rank holds the same replicated scene and renders its own 4
+distinct views per step, and the per-Gaussian gradients of the step are summed over ranks with
+one RCCL all-reduce (weak scaling: view-parallel data parallelism).  The per-rank
+work is the same at every N, so the driver's value(N) / (N value(1)) compares like with like.
 
 Prints ONE JSON line (rank 0).  value = whole-job MPix/s = N * V * W * H / step time (max over
 ranks).  Beside it: `single_call` = SURVEY §8d's definition (median of 50 call pairs, HIP
@@ -269,6 +270,100 @@ def bench_relight(args, dev):
 
 TRAIN_VIEWS_PER_RANK = 4
 TRAIN_ITERATION = 15001  # past reg_normal_from_iter (15000): the normal-consistency term is on
+TRAIN_NCH = 14  # channels of the fused render()'s composite (gsr.relit.RELIT_CHANNELS)
+TRAIN_DOM_KERNEL = "k_render_bwd_mc"
+
+
+def train_algorithmic_bytes(P, P_fg, Pv, R, T, Npix, V, n_params, nch=TRAIN_NCH):
+    """Compulsory HBM bytes of one cfg4 iteration (each array touched once), by kernel family.
+    The rasterizer terms are SURVEY §8d's B_fwd / B_bwd with the composite's nch float channels
+    in place of the 3 colours (a record read per instance: id 4 + xy 8 + conic/opacity 16 +
+    4 nch feature bytes; nch planes out, nch gradient planes in); the shade is §8d's B_shade;
+    the rest counts the arrays the iteration's other kernels must read and write once."""
+    F = 4 * nch
+    per_view = {
+        "relit_features": P * (12 + 16 + 12 + F) + P_fg * 20,  # xyz, rotation, scale, materials -> features
+        "shade": P_fg * (80 + 136),  # §8d B_shade forward + backward
+        "preprocess": P * 12 + Pv * 44 + P * 8 + Pv * 67,
+        "binning": P * 8 + P * 4 + Pv * 16 + R * 12 + R * 24 + R * 8 + T * 16,  # scan, duplicate, sort, ranges
+        "render_fwd_mc": T * 8 + R * (28 + F) + Npix * (F + 8),
+        "render_bwd_mc": T * 8 + R * (28 + F) + Npix * (8 + F) + Pv * (44 + F),
+        "preprocess_bwd": P * 108 + P * 4 + Pv * 88 + P * 4 + Pv * 143,
+        "relit_features_bwd": P * (F + 12 + 16 + 12) + P * 40 + P_fg * 20,  # dL/dfeatures + inputs -> grads
+        # losses, SSIM and the normal epilogue: the nch planes, target, masks and the SSIM maps
+        # forward (28 planes); the maps, planes and their gradients backward (42 planes)
+        "image_space": Npix * 4 * (28 + 42),
+    }
+    per_iter = {"activations": n_params * 16,  # raw params -> activated, activated grads -> raw grads
+                "adam": n_params * 28,  # param, grad, two moments read; param, two moments written
+                "densify_stats": V * P * 16}
+    return V * sum(per_view.values()) + sum(per_iter.values()), per_view, per_iter
+
+
+def _pmc_train_record():
+    """The newest committed rocprofv3 record of the cfg4 iteration (tools/profile_train.sh ->
+    profiles/<tag>_hbm_traffic.json with workload "cfg4 training iteration ...")."""
+    import glob
+    recs = [(json.load(open(f)), f) for f in glob.glob(os.path.join(ROOT, "profiles", "r*_hbm_traffic.json"))]
+    for d, f in sorted(recs, key=lambda r: (r[0].get("created", ""), os.path.basename(r[1])), reverse=True):
+        if (d.get("workload") or "").startswith("cfg4 training iteration"):
+            return d, os.path.relpath(f, ROOT)
+    return None, None
+
+
+def train_roofline(live, stats, ms_iter, iters_timed_by_events):
+    """The training leg's roofline (north_star: train iters/s "as fraction of HBM roofline").
+    The iteration's dominant kernel is the composite's backward tile pass (k_render_bwd_mc<4,14>,
+    a third of the iteration's kernel time): VALU-issue bound like the 3-channel pass, so
+    `bound` = "valu" (committed PMC VALU count / live launch time against the spec issue rate),
+    with its HBM view and the whole iteration's algorithmic bytes / ms_per_iter beside it."""
+    rec, src = _pmc_train_record()
+    ks = (rec or {}).get("kernels", {})
+    kname = next((k for k in ks if k.startswith(TRAIN_DOM_KERNEL + "<")), None)
+    kinfo = ks.get(kname, {}) if kname else {}
+    ms_b, n_b = live.get("render_bwd_mc", (0.0, 0))
+    ms_f, n_f = live.get("render_fwd_mc", (0.0, 0))
+    t_b = ms_b / max(n_b, 1)
+    B_iter, per_view, per_iter = train_algorithmic_bytes(**stats)
+    peak = 1024 * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST
+    b_launch = per_view["render_bwd_mc"]
+    hbm = {"achieved": round(b_launch / (t_b * 1e-3) / 1e9, 1) if t_b > 0 else None, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "bytes_per_launch": int(b_launch),
+           "traffic": kinfo.get("traffic_bytes"), "traffic_source": src,
+           "bytes": "SURVEY §8d render-backward bytes with the composite's 14 float channels (bench.py "
+                    "train_algorithmic_bytes), measured R and P_v"}
+    if hbm["achieved"] is not None:
+        hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
+    pmc_iter = None
+    if ks:
+        n_iter = max(v.get("calls", 0) for k, v in ks.items() if k.startswith("k_adam")) or None
+        if n_iter:
+            pmc_iter = sum((v.get("traffic_bytes") or 0) * v["calls"] for v in ks.values()) / n_iter
+    it = {"bytes": int(B_iter), "achieved": round(B_iter / (ms_iter * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
+          "unit": "GB/s", "frac": round(B_iter / (ms_iter * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+          "per_view_bytes": {k: int(v) for k, v in per_view.items()},
+          "per_iteration_bytes": {k: int(v) for k, v in per_iter.items()},
+          "pmc_traffic_per_iter": None if pmc_iter is None else int(pmc_iter), "traffic_source": src,
+          "what": "the iteration's algorithmic bytes (bench.py train_algorithmic_bytes) / ms_per_iter"}
+    r = {"kernel": kname or TRAIN_DOM_KERNEL, "avg_launch_ms": round(t_b, 4), "launches": int(n_b),
+         "render_fwd_mc_avg_launch_ms": round(ms_f / max(n_f, 1), 4),
+         "launch_timing": f"HIP events on the launch stream around each composite tile pass, "
+                          f"{iters_timed_by_events} iterations on one stream after the timed region (as "
+                          "tools/train_kernels.py runs under rocprofv3)",
+         "hbm": hbm, "iteration_hbm": it}
+    if kinfo.get("valu_insts") and t_b > 0:
+        ach = kinfo["valu_insts"] / (t_b * 1e-3) / 1e9
+        r.update(bound="valu", achieved=round(ach, 1), peak=round(peak, 1), unit="Gwave-inst/s",
+                 frac=round(ach / peak, 4), traffic=kinfo.get("traffic_bytes"),
+                 valu_insts_per_launch=int(kinfo["valu_insts"]), valu_source=src,
+                 peak_source="1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md)")
+        if kinfo.get("salu_insts"):
+            r["salu_insts_per_launch"] = int(kinfo["salu_insts"])
+    else:
+        r.update(bound="valu", achieved=None, peak=round(peak, 1), unit="Gwave-inst/s", frac=None,
+                 traffic=kinfo.get("traffic_bytes"),
+                 frac_null_reason="no committed rocprofv3 SQ_INSTS_VALU pass of the cfg4 iteration (profiles/)")
+    return r
 
 
 def train_leg(args, dev, dist, rank, world, backend, steps, warmup):
@@ -322,7 +417,26 @@ def train_leg(args, dev, dist, rank, world, backend, steps, warmup):
             dist.all_reduce(scene.fp.grad)
         torch.cuda.synchronize()
         ar_ms = (time.perf_counter() - t1) * 1e3 / 10
+    # live launch times of the composite's tile passes for the roofline: a few iterations on
+    # ONE stream after the timed region, the two passes bracketed by HIP events on their stream
+    import diff_gaussian_rasterization as dgr
+    from gsr import _lib
+    ev_iters = max(1, args.event_steps)
+    _lib.profile_read(reset=True)
+    _lib.profile_stages(["render_fwd_mc", "render_bwd_mc"])
+    _lib.profile_enable(True)
+    for _ in range(ev_iters):
+        train.train_step(scene, my_views, mine, my_gts, world=world, streams=None)
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    live = _lib.profile_read(reset=True)
+    _lib.profile_stages(None)
+    radii = dgr.last_channels_call["radii"]
+    stats = dict(P=scene.P, P_fg=P_fg, Pv=int((radii > 0).sum().item()), R=int(dgr.last_channels_call["num_rendered"]),
+                 T=((W + 15) // 16) * ((H + 15) // 16), Npix=W * H, V=vpr, n_params=scene.fp.n)
+    roof = train_roofline(live, stats, ms, ev_iters)
     return {"value": round(1e3 / ms, 3), "unit": "iters/s", "ms_per_iter": round(ms, 4), "steps": steps,
+            "roofline": roof, "measured": {k: stats[k] for k in ("R", "Pv")},
             "warmup": warmup, "views_per_s": round(vpr * world * 1e3 / ms, 3),
             "workload": f"cfg4: {scene.P} Gaussians ({P_fg} fg + {scene.P - P_fg} sky), {W}x{H}, {vpr} views per "
                         f"GPU per iteration, env SH deg 4, sky SH deg 1, iteration {TRAIN_ITERATION} (every loss "
@@ -346,6 +460,7 @@ def bench_train(args, dev, dist, rank, world, backend, joined):
                        "views_per_iter": r["views_per_iter"],
                        "parallelism": f"views x{world}" + (f" ({backend})" if backend else ""),
                        "flat_params": r["flat_params"], "streams": r["streams"]},
+            "roofline": r["roofline"], "measured": r["measured"],
             "views_per_s": r["views_per_s"], "grad_all_reduce_ms": r["grad_all_reduce_ms"],
             "all_reduce_backend": backend, "grad_bucket_mb": r["grad_bucket_mb"],
             "final_loss_rank0": r["final_loss_rank0"]}), flush=True)
@@ -471,16 +586,16 @@ def main():
     ap.add_argument("--view", type=int, default=0)
     ap.add_argument("--fused-only", action="store_true", help="cfg3: time only the fused render()")
     ap.add_argument("--views-per-step", "--views-per-sync", dest="views_per_step", type=int, default=None,
-                    help="views per step per GPU (default 1 at N = 1, 4 at N > 1: the per-GPU mini-batch whose "
-                         "gradients cross the ranks in one all-reduce)")
+                    help="views per step per GPU (default 4 at every N: the per-GPU mini-batch whose gradients "
+                         "cross the ranks in one all-reduce at N > 1)")
     ap.add_argument("--streams", type=int, default=None,
                     help="HIP streams the views of a step (cfg2, default 1) or a training iteration (cfg4, "
                          "default 2) alternate over")
     ap.add_argument("--no-minibatch", action="store_true", help="skip the 4-view multi-stream extra leg")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
     ap.add_argument("--event-steps", type=int, default=5,
-                    help="record the dominant stage's HIP events on the last N timed steps (default 5; two "
-                         "event records cost ~10 us per view, so on every step they would be ~1 %% of it)")
+                    help="steps (each V views, one stream) run after the timed region with the dominant stage's "
+                         "HIP events, for roofline.avg_launch_ms (default 5); the timed region carries no events")
     ap.add_argument("--no-train", action="store_true", help="skip the cfg4 training-iteration leg (train iters/s)")
     ap.add_argument("--train-steps", type=int, default=None, help="timed iterations of the training leg "
                                                                   "(default min(--steps, 20))")
@@ -534,11 +649,13 @@ def main():
     gen = torch.Generator().manual_seed(1)
     dout_cpu = torch.randn(3, H, W, generator=gen)
     dout = dout_cpu.to(dev)
-    # V views per step per rank (default 1 at N = 1: the reference's one call pair; 4 at N > 1:
-    # cfg4's per-GPU mini-batch, whose gradients accumulate into one bucket and cross the ranks
-    # in ONE RCCL all-reduce).  Rank r renders global views r*V .. r*V+V-1 of the scene.
-    V = max(1, args.views_per_step if args.views_per_step is not None else (1 if world == 1 else 4))
-    NS = max(1, min(1 if args.streams is None else args.streams, V))
+    # V views per step per rank, 4 by default at every N (cfg4's per-GPU mini-batch, whose
+    # gradients accumulate into one bucket and cross the ranks in ONE RCCL all-reduce at N > 1;
+    # the same per-rank work at every N).  Rank r renders global views r*V .. r*V+V-1 of the scene.
+    V = max(1, args.views_per_step if args.views_per_step is not None else 4)
+    # the step's views alternate over NS HIP streams (default 3): one view's latency-bound
+    # geometry passes overlap another's tile passes
+    NS = max(1, min(3 if args.streams is None else args.streams, V))
     cams = [scenes.view_camera(cam, rank * V + k).to(dev) for k in range(V)]
     mats = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in cams]
     main_s = torch.cuda.current_stream(dev)
@@ -616,9 +733,8 @@ def main():
         dist.barrier()
     # Stage breakdown (before the W warmup steps, so the timed region follows them directly
     # and starts on a busy GPU's clocks): three profiled views, one at a time on one stream
-    # (every stage bracketed by HIP events).  Inside it only the dominant stage
-    # keeps its events, on the last --event-steps steps, so the step time carries two events
-    # per view on those steps instead of sixteen on every one.
+    # (every stage bracketed by HIP events).  The timed region carries no events; the dominant
+    # stage's launch time comes from --event-steps steps on one stream after it.
     _lib.profile_read(reset=True)
     _lib.profile_stages(None)
     _lib.profile_enable(True)
@@ -638,17 +754,12 @@ def main():
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
-    _lib.profile_stages([dom_name])
-    ev_from = max(0, args.steps - max(1, args.event_steps))
-    _lib.profile_enable(ev_from <= 0)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k_step in range(args.steps):
-        if k_step == ev_from and ev_from > 0:
-            _lib.profile_enable(True)
+    for _ in range(args.steps):
         step()
     drain()  # ... and ends with every step's exchange finished
     torch.cuda.synchronize()
@@ -656,6 +767,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    # the dominant stage's live launch time: --event-steps steps' views one after another on ONE
+    # stream, that stage bracketed by HIP events on the stream it launches on (in the timed
+    # region the views overlap on NS streams, which would fold the other streams' kernels into
+    # a launch's duration); tools/profile_round.sh profiles the same one-stream layout
+    _lib.profile_stages([dom_name])
+    _lib.profile_enable(True)
+    ev_steps = max(1, args.event_steps)
+    for _ in range(ev_steps):
+        for i in range(V):
+            view(i)
+    torch.cuda.synchronize()
     _lib.profile_enable(False)
     live = _lib.profile_read(reset=True).get(dom_name, (0.0, 0))
     _lib.profile_stages(None)
@@ -698,7 +820,7 @@ def main():
         single = {"median_ms": round(med, 4), "p10_ms": round(t_ms[5], 4), "p90_ms": round(t_ms[45], 4),
                   "calls": len(t_ms), "value": round(W * H / (med * 1e-3) / 1e6, 3), "unit": "MPix/s",
                   "what": "one rasterizer forward + backward call pair, median of 50 (HIP events, 10 warm-up)"}
-        if not args.no_minibatch:
+        if not args.no_minibatch and not (V == 4 and NS == 3):  # (the timed step already is this layout)
             # a 4-view mini-batch of DISTINCT cameras on 3 HIP streams: one view's latency-bound
             # geometry passes overlap another's tile passes (throughput, not the reference's pattern)
             mcams = [scenes.view_camera(cam, k).to(dev) for k in range(4)]
@@ -799,8 +921,8 @@ def main():
         "roofline": roofline,
         "stage_ms": per_stage,
         "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
-                           "stage); roofline.avg_launch_ms is the dominant stage's events on the last "
-                           f"{min(args.steps, max(1, args.event_steps))} steps of the timed region",
+                           "stage); roofline.avg_launch_ms is the dominant stage's events over "
+                           f"{ev_steps} steps' views run one at a time on one stream right after the timed region",
     }
     if single is not None:
         out["single_call"] = single

@@ -266,7 +266,9 @@ int gsr_view_loss_backward(int npix, const float* img, const float* gt, const fl
  * Backward: grad_sums [5V] (device) are the sums' upstream gradients; d_xyz / d_scaling
  * (either may be null) are overwritten, or added to with GSR_ACC_MEAN3D / GSR_ACC_SCALE in
  * `accumulate`.  gsr_densify_stats updates accum / denom /
- * max_radii [P] in place over the views in order. */
+ * max_radii [P] in place over the views in order; with accum = denom = NULL (grad_means2D
+ * may then be NULL too) it updates max_radii alone (train.py:130 runs every iteration, the
+ * sums only below densify_until_iter, train.py:143-144). */
 int gsr_view_regularisers_partials(int P);
 int gsr_view_regularisers_forward(int P, int V, const float* xyz, const float* scaling, const int* const* radii,
                                   const unsigned char* is_sky, const float* depth_cols, float* partials,

@@ -280,11 +280,15 @@ int wait_totals(const unsigned long long* p, unsigned long long seq, hipStream_t
 // ---- stage profiling: hipEvents recorded on the call's stream around each stage ----------
 enum Stage {
     ST_PREPROCESS, ST_COMPACT, ST_DEPTH_SORT, ST_OFFSETS, ST_DUPLICATE, ST_TILE_SORT, ST_RANGES, ST_RENDER_FWD,
-    ST_BWD_ZERO, ST_RENDER_BWD, ST_PREPROCESS_BWD, ST_SHADE_FWD, ST_SHADE_BWD, ST_COUNT
+    ST_BWD_ZERO, ST_RENDER_BWD, ST_PREPROCESS_BWD, ST_SHADE_FWD, ST_SHADE_BWD, ST_RENDER_FWD_MC, ST_RENDER_BWD_MC,
+    ST_COUNT
 };
+// render_fwd_mc / render_bwd_mc: the multi-channel composite's tile-pass launches alone (inside
+// render_fwd / render_bwd, which also hold the backward's tile order), for the training leg's
+// live launch times (bench.py)
 const char* kStageNames[ST_COUNT] = {"preprocess",  "compact",      "depth_sort",     "offsets_scan", "st_emit",
                                      "st_sort",     "tile_order",       "render_fwd",     "bwd_zero",     "render_bwd",
-                                     "preprocess_bwd", "shade_fwd", "shade_bwd"};
+                                     "preprocess_bwd", "shade_fwd", "shade_bwd", "render_fwd_mc", "render_bwd_mc"};
 // Forward calls run on the Python thread and backward calls on autograd's device thread,
 // so the pending list and the event pool are guarded by one mutex.
 struct Prof {
@@ -715,6 +719,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         if (!mc) {
             gsr::launch_render_fwd(ra, s);
         } else {
+            GSR_STAGE(ST_RENDER_FWD_MC);
             for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
                 gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, gsx, ra.st_ranges, ra.ent, pa.rec, ra.order,
                                                ra.nheavy, ra.tile_nmax, ra.tile_emax, *mc, c0);
@@ -934,12 +939,16 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         ra.partial = partial;
         {
-            GSR_STAGE(ST_RENDER_BWD);
+            GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
+        }
+        {
+            GSR_STAGE(ST_RENDER_BWD);  // the tile pass alone (roofline.avg_launch_ms in bench.py)
             if (!mc) {
                 gsr::launch_render_bwd(ra, s);
             } else {
+                GSR_STAGE(ST_RENDER_BWD_MC);
                 for (int c0 = 0; c0 < mc->nch; c0 += MC_GROUP) {
                     gsr::RenderMcArgs ma = mc_args(width, height, gx, gy, ra.gsx, ra.st_ranges, ra.ent, ra.rec, ra.order,
                                                    ra.nheavy, at<uint32_t>(img, il.tile_nmax),
@@ -1418,13 +1427,14 @@ int gsr_densify_stats(int P, int V, const float* const* grad_means2D, const int*
     if (P < 0 || V <= 0 || V > gsr::REG_MAXV)
         return fail(GSR_E_ARG, "gsr_densify_stats: bad P=%d V=%d (1..%d views)", P, V, gsr::REG_MAXV);
     if (P == 0) return GSR_OK;
-    if (!grad_means2D || !radii || !accum || !denom || !max_radii)
+    const bool sums = accum || denom;
+    if (!radii || !max_radii || (sums && (!accum || !denom || !grad_means2D)))
         return fail(GSR_E_ARG, "gsr_densify_stats: missing buffers");
     gsr::ViewPtrs<int> rp;
     gsr::ViewPtrs<float> gp;
     if (!view_ptrs_int(V, radii, rp)) return fail(GSR_E_ARG, "gsr_densify_stats: missing radii");
     for (int v = 0; v < gsr::REG_MAXV; v++) gp.p[v] = nullptr;
-    for (int v = 0; v < V; v++) {
+    for (int v = 0; sums && v < V; v++) {
         if (!grad_means2D[v]) return fail(GSR_E_ARG, "gsr_densify_stats: missing means2D gradient");
         gp.p[v] = grad_means2D[v];
     }

@@ -121,17 +121,24 @@ __global__ void __launch_bounds__(256) k_densify_stats(int P, int V, const ViewP
                                                        float* __restrict__ denom, float* __restrict__ maxr) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= P) return;
-    float a = accum[i], d = denom[i], m = maxr[i];
+    // accum == nullptr: the max radii alone (train.py:130 runs every iteration, the sums of
+    // add_densification_stats only below densify_until_iter, train.py:143-144)
+    const bool sums = accum != nullptr;
+    float a = sums ? accum[i] : 0.f, d = sums ? denom[i] : 0.f, m = maxr[i];
     for (int v = 0; v < V; v++) {
         const int r = radii.p[v][i];
         if (r <= 0) continue;
-        const float gx = g2d.p[v][3 * i], gy = g2d.p[v][3 * i + 1];
-        a += sqrtf(gx * gx + gy * gy);
-        d += 1.f;
+        if (sums) {
+            const float gx = g2d.p[v][3 * i], gy = g2d.p[v][3 * i + 1];
+            a += sqrtf(gx * gx + gy * gy);
+            d += 1.f;
+        }
         m = fmaxf(m, (float)r);
     }
-    accum[i] = a;
-    denom[i] = d;
+    if (sums) {
+        accum[i] = a;
+        denom[i] = d;
+    }
     maxr[i] = m;
 }
 

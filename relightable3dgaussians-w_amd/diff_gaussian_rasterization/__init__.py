@@ -146,6 +146,11 @@ class _RasterizeGaussians(torch.autograd.Function):
         return g_means3D, g_means2D, g_sh, g_colors, g_opacities, g_scales, g_rotations, g_cov3D, None
 
 
+# num_rendered (the reference's R, the sum of tiles touched) of the latest multi-channel call:
+# bench.py's training leg reads it for its algorithmic bytes
+last_channels_call = {"num_rendered": None, "radii": None}
+
+
 def rasterize_channels(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
                        raster_settings, nch=None):
     """Composite of the first nch (default all) per-Gaussian channels of `features` [P, C]
@@ -171,6 +176,8 @@ class _RasterizeChannels(torch.autograd.Function):
             nch)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
+        last_channels_call["num_rendered"] = num_rendered
+        last_channels_call["radii"] = radii
         ctx.nch = features.shape[1] if nch is None else int(nch)
         ctx.ncols = features.shape[1]
         ctx.save_for_backward(background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf,

@@ -102,9 +102,16 @@ def _reset_stats(scene, P, dev):
 
 
 def densify_and_prune(scene, max_grad: float, min_opacity: float, extent: float, max_screen_size: Optional[float],
-                      percent_dense: float = 0.01, N: int = 2, generator: Optional[torch.Generator] = None) -> None:
+                      percent_dense: float = 0.01, N: int = 2, generator: Optional[torch.Generator] = None,
+                      group=None) -> None:
     """gaussian_model.py:610-625 on a RelitScene, in place (the scene's FlatParams is
-    rebuilt with the new row counts; the Adam step count is kept)."""
+    rebuilt with the new row counts; the Adam step count is kept).  Under data parallelism
+    the ranks' rank-local max_radii2D (gsr.dp.finish_step) are MAX-reduced first: every rank
+    must call this at the same iteration, as train.py's densification interval does."""
+    if getattr(scene, "max_radii_local", False):
+        from . import dp
+        dp.sync_max_radii(scene.stats, group)
+        scene.max_radii_local = False
     fp = scene.fp
     dev = fp.device
     rows = _Rows(scene)
@@ -164,7 +171,7 @@ def densify_and_prune(scene, max_grad: float, min_opacity: float, extent: float,
 def _rebuild(scene, rows: _Rows) -> None:
     old = scene.fp
     spec = [(name, tuple(rows.t[name][0].shape), lr) for name, lr in zip(old.names, old.lrs)]
-    fp = FlatParams(spec, old.device, betas=old.betas, eps=old.eps)
+    fp = FlatParams(spec, old.device, betas=old.betas, eps=old.eps, tail=2 * rows.is_sky.shape[0])
     fp.t = old.t
     with torch.no_grad():
         for name, off in zip(fp.names, fp.offsets):

@@ -177,6 +177,83 @@ class StepStats:
         torch.maximum(running["max_radii2D"], d["max_radii2D"], out=running["max_radii2D"])
 
 
+# ---- the training iteration's exchange (gsr.train.train_step) ------------------------------
+
+DENSIFY_UNTIL_ITER = 15000  # configs/optimizer/optimization_params.yaml:16 densify_until_iter
+
+
+def add_views(accum: Optional[torch.Tensor], denom: Optional[torch.Tensor], max_radii: torch.Tensor,
+              mean2D_grads, radii) -> None:
+    """The views' densification updates in view order (train.py:130, gaussian_model.py:627-629):
+    max_radii = max(max_radii, radii) on the visible Gaussians and, unless accum / denom are
+    None, accum += ||dL/dmean2D[:, :2]||, denom += 1.  On GPU tensors one HIP pass per 8 views
+    (gsr_densify_stats)."""
+    if not radii[0].is_cuda:
+        for g, r in zip(mean2D_grads, radii):
+            vis = r > 0
+            torch.where(vis, torch.maximum(max_radii, r.to(max_radii.dtype)), max_radii, out=max_radii)
+            if accum is not None:
+                v1 = vis[:, None]
+                accum.add_(torch.where(v1, torch.norm(g[:, :2], dim=-1, keepdim=True), 0.0))
+                denom.add_(v1.to(denom.dtype))
+        return
+    from . import _lib
+    P = max_radii.shape[0]
+    ptr = lambda t: None if t is None else t.data_ptr()
+    for i in range(0, len(radii), 8):
+        rs = [r.contiguous() for r in radii[i:i + 8]]
+        gs = [g.contiguous() for g in mean2D_grads[i:i + 8]] if accum is not None else None
+        _lib.check(_lib.lib().gsr_densify_stats(P, len(rs), None if gs is None else _lib.ptr_array(gs),
+                                                _lib.ptr_array(rs), ptr(accum), ptr(denom), max_radii.data_ptr(),
+                                                _lib.stream_of(rs[0].device)), "gsr_densify_stats")
+
+
+def step_sums(fp, P: int):
+    """This step's densification sums (xyz_gradient_accum and denom deltas, [P,1] each) as views
+    of the flat gradient's tail, zeroed with it by FlatParams.zero_grad."""
+    if fp.tail < 2 * P:
+        raise RuntimeError(f"the flat gradient's tail holds {fp.tail} floats, the step's sums need {2 * P}")
+    t = fp.grad_tail
+    return t[:P].view(P, 1), t[P:2 * P].view(P, 1)
+
+
+def sync_max_radii(stats: Dict[str, torch.Tensor], group=None) -> None:
+    """max_radii2D stays rank-local between densifications: MAX is associative and only
+    densify_and_prune reads it (gaussian_model.py:620), so the ranks' running maxima are
+    MAX-reduced once, right before it does (gsr.densify.densify_and_prune)."""
+    dist.all_reduce(stats["max_radii2D"], op=dist.ReduceOp.MAX, group=group)
+
+
+def finish_step(scene, mean2D_grads, radii, iteration: int, world: int = 1, group=None) -> int:
+    """The tail of gsr.train.train_step after the views' backward: the densification
+    statistics and the iteration's exchange.  Returns the number of collectives it issued.
+
+    * train.py:130 updates max_radii2D every iteration; train.py:143-144 adds the gradient-norm
+      sums only while iteration < densify_until_iter.
+    * One rank: straight into the running statistics.
+    * N ranks: ONE SUM all-reduce per iteration.  The step's sums ride in the flat gradient's
+      tail (step_sums) while they are on, so the bucket is [gradient | accum deltas | denom
+      deltas], and they are folded into the running statistics after; past densify_until_iter
+      the bucket is the gradient alone.  max_radii2D is updated rank-locally (sync_max_radii
+      reduces it when densification needs it); ``scene.max_radii_local`` marks it."""
+    st = scene.stats
+    stats_on = iteration < DENSIFY_UNTIL_ITER
+    fp = scene.fp
+    if world > 1:
+        acc, den = step_sums(fp, scene.P) if stats_on else (None, None)
+        scene.max_radii_local = True
+    else:
+        acc, den = (st["xyz_gradient_accum"], st["denom"]) if stats_on else (None, None)
+    add_views(acc, den, st["max_radii2D"], mean2D_grads, radii)
+    if world <= 1:
+        return 0
+    dist.all_reduce(fp.bucket(stats_on), op=dist.ReduceOp.SUM, group=group)
+    if stats_on:
+        st["xyz_gradient_accum"].add_(acc)
+        st["denom"].add_(den)
+    return 1
+
+
 def shared_seed(group=None, device="cpu") -> int:
     """A fresh 63-bit seed drawn on rank 0 and broadcast to every rank."""
     seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64)

@@ -68,6 +68,42 @@ ENV_NOISE_STD = 0.025   # train.py:70
 LAMBDA_DSSIM, LAMBDA_SKY_BRDF, LAMBDA_NORMAL = 0.2, 0.5, 0.05
 LAMBDA_ENVLIGHT, LAMBDA_SCALE, LAMBDA_SKY_GAUSS = 100.0, 100.0, 0.05
 REG_NORMAL_FROM_ITER, REG_SKY_GAUSS_DEPTH_FROM_ITER = 15000, 0
+# the position learning-rate schedule (configs/optimizer/optimization_params.yaml:4-7)
+POSITION_LR_INIT, POSITION_LR_FINAL, POSITION_LR_DELAY_MULT, POSITION_LR_MAX_STEPS = 0.00016, 0.0000016, 0.01, 30000
+MLP_LR_DROP_ITER, MLP_LR_AFTER_DROP = 20000, 0.0002  # relit3DGW_model.py:153-158
+
+
+def expon_lr(step, lr_init, lr_final, lr_delay_steps=0, lr_delay_mult=1.0, max_steps=1000000) -> float:
+    """utils/general_utils.py:46-80 get_expon_lr_func's helper: log-linear from lr_init (step 0)
+    to lr_final (max_steps), with the optional reverse-cosine delay, in double precision."""
+    if step < 0 or (lr_init == 0.0 and lr_final == 0.0):
+        return 0.0
+    if lr_delay_steps > 0:
+        delay = lr_delay_mult + (1 - lr_delay_mult) * math.sin(0.5 * math.pi * min(max(step / lr_delay_steps, 0.0),
+                                                                                   1.0))
+    else:
+        delay = 1.0
+    t = min(max(step / max_steps, 0.0), 1.0)
+    return delay * math.exp(math.log(lr_init) * (1 - t) + math.log(lr_final) * t)
+
+
+def apply_lr_schedule(scene, iteration: int) -> None:
+    """The learning rates the reference's Adam step of ``iteration`` uses (train.py:156-159 steps,
+    then calls update_learning_rate(iteration) for the next one): xyz and sky_angles follow
+    get_expon_lr_func at iteration - 1 (gaussian_model.py:277-293; its value at 0 is
+    training_setup's initial rate), and the MLP / embedding groups are set to 0.0002 once
+    iteration 20000 has stepped (relit3DGW_model.py:153-158).  Stateless: any iteration may be
+    the first one run."""
+    s = scene.spatial_lr_scale
+    lr = expon_lr(iteration - 1, POSITION_LR_INIT * s, POSITION_LR_FINAL * s, lr_delay_mult=POSITION_LR_DELAY_MULT,
+                  max_steps=POSITION_LR_MAX_STEPS)
+    fp = scene.fp
+    fp.set_lr("xyz", lr)
+    fp.set_lr("sky_angles", lr)
+    if iteration - 1 >= MLP_LR_DROP_ITER:
+        for n in fp.names:
+            if n == "embeddings" or n.startswith("mlp."):
+                fp.set_lr(n, MLP_LR_AFTER_DROP)
 
 
 class FlatParams:
@@ -75,9 +111,12 @@ class FlatParams:
 
     ``params[name]`` is a leaf view of ``flat`` with ``.grad`` preset to the matching view
     of ``grad``; ``step()`` is one fused Adam launch (torch.optim.Adam semantics, eps as the
-    reference's 1e-15)."""
+    reference's 1e-15).  ``tail`` extra floats follow ``grad`` in the same storage
+    (``grad_tail``): the data-parallel step carries its densification sums there, so one
+    all-reduce of ``bucket(True)`` moves both (gsr.dp.exchange)."""
 
-    def __init__(self, spec: Sequence[Tuple[str, Tuple[int, ...], float]], device, betas=(0.9, 0.999), eps=1e-15):
+    def __init__(self, spec: Sequence[Tuple[str, Tuple[int, ...], float]], device, betas=(0.9, 0.999), eps=1e-15,
+                 tail: int = 0):
         self.names, self.shapes, self.lrs, self.offsets, ends = [], [], [], [], []
         o = 0
         for name, shape, lr in spec:
@@ -92,7 +131,10 @@ class FlatParams:
         self.ends = ends
         self.device = torch.device(device)
         self.flat = torch.zeros(self.n, device=self.device)
-        self.grad = torch.zeros(self.n, device=self.device)
+        self.tail = int(tail)
+        self._gstore = torch.zeros(self.n + self.tail, device=self.device)
+        self.grad = self._gstore[:self.n]
+        self.grad_tail = self._gstore[self.n:]
         self.exp_avg = torch.zeros(self.n, device=self.device)
         self.exp_avg_sq = torch.zeros(self.n, device=self.device)
         self.betas, self.eps, self.t = betas, eps, 0
@@ -114,7 +156,15 @@ class FlatParams:
         the buffer's tail instead of all of it; kept segments past that point are zeroed too,
         harmlessly)."""
         lo = min((o for n, o in zip(self.names, self.offsets) if n not in keep), default=self.n)
-        self.grad[lo:].zero_()
+        # the kept segments must be a prefix (GAUSSIAN_GROUPS' order): one behind a zeroed
+        # segment would be zeroed too, and a reordering would silently change what is kept
+        assert all(o < lo for n, o in zip(self.names, self.offsets) if n in keep), \
+            "zero_grad: a kept segment lies behind the first zeroed one"
+        self._gstore[lo:].zero_()  # the tail too: this step's densification sums start at 0
+
+    def bucket(self, with_tail: bool = False) -> torch.Tensor:
+        """The flat gradient as one contiguous tensor, with the tail (``with_tail``) or not."""
+        return self._gstore if with_tail else self.grad
 
     def check_grads_in_place(self) -> None:
         """Autograd accumulated into the preset views (not into fresh tensors)."""
@@ -491,6 +541,9 @@ def depth_loss_gaussians(gaussians, camera, visibility_filter: torch.Tensor, gam
     return torch.exp(-gamma * (avg_sky - avg_fg))
 
 
+REG_MAXV = 8  # views per launch of the fused regulariser passes (gsr::REG_MAXV, csrc/gsr_trainaux.hip)
+
+
 class _FusedViewRegs(torch.autograd.Function):
     """The per-Gaussian half of view_regularisers as one HIP pass each way
     (csrc/gsr_trainaux.hip): sums [V,5] per view = (#visible foreground, #visible sky,
@@ -595,6 +648,11 @@ def view_regularisers(pc, radii, viewmats: torch.Tensor, env_sh: torch.Tensor, d
     x = pc.get_xyz
     if fused is None:
         fused = x.is_cuda
+    if fused and V > REG_MAXV:
+        # the HIP passes take up to REG_MAXV views per launch; each view's terms are independent
+        return torch.cat([view_regularisers(pc, radii[i:i + REG_MAXV], viewmats[i:i + REG_MAXV],
+                                            env_sh[i:i + REG_MAXV], dirs[i:i + REG_MAXV], gamma, depth_on, fused,
+                                            tail_fused) for i in range(0, V, REG_MAXV)])
     c = viewmats[:, :, 2]                                      # [V,4]: the depth column
     if fused:
         rl = [r.contiguous() for r in radii] if isinstance(radii, (list, tuple)) else list(radii.contiguous())
@@ -666,7 +724,9 @@ def sky_angles_clamped(a: torch.Tensor) -> torch.Tensor:
     return torch.cat((th.unsqueeze(1), ph.unsqueeze(1)), dim=1)
 
 
-_ACT_OVERWRITES = ("xyz", "albedo", "opacity", "scaling", "rotation", "roughness", "metalness", "sky_angles")
+# the leading segments of GAUSSIAN_GROUPS that _Activations.backward overwrites whole every step
+# (sky_angles is overwritten too but sits behind sky_radius, so zero_grad zeroes it)
+_ACT_OVERWRITES = ("xyz", "albedo", "opacity", "scaling", "rotation", "roughness", "metalness")
 
 
 class _Activations(torch.autograd.Function):
@@ -724,6 +784,7 @@ class _Activations(torch.autograd.Function):
             ptr(d["xyz"]), ptr(d["sky_angles"]), ptr(d["sky_radius"]), part.data_ptr(), ptr(d["scaling"]),
             ptr(d["rotation"]), ptr(d["opacity"]), ptr(d["albedo"]), ptr(d["roughness"]), ptr(d["metalness"]),
             _lib.stream_of(dev)), "gsr_activations_backward")
+        scene.act_grads_written = True  # train_step: the kept (unzeroed) segments hold this step's values
         return (None,) * 11
 
 
@@ -845,7 +906,8 @@ class RelitScene:
         spec.append(("embeddings", (n_views, EMBEDDING_DIM), EMBEDDINGS_LR))
         for name, fout, fin in MLP_LAYERS:
             spec += [(f"mlp.{name}.weight", (fout, fin), MLP_LR), (f"mlp.{name}.bias", (fout,), MLP_LR)]
-        self.fp = FlatParams(spec, device)
+        self.fp = FlatParams(spec, device, tail=2 * P)  # tail: a step's densification sums (gsr.dp)
+        self.spatial_lr_scale = float(spatial_lr_scale)
         for name, v in (("xyz", xyz[~m]), ("scaling", scaling_raw), ("rotation", rotation_raw),
                         ("opacity", opacity_raw), ("albedo", albedo_raw), ("roughness", rough_raw),
                         ("metalness", metal_raw), ("sky_radius", torch.tensor([float(sky_radius)])),
@@ -948,8 +1010,12 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
     from . import dp as gdp
     fp = scene.fp
     dev = fp.device
-    # the fused activations' backward overwrites its segments (sky_radius: it adds)
-    fp.zero_grad(keep=_ACT_OVERWRITES if dev.type == "cuda" else ())
+    # the fused activations' backward overwrites the _ACT_OVERWRITES segments (a prefix of the
+    # buffer), so only the rest is zeroed here (sky_radius included: the backward writes it
+    # only when sky Gaussians exist); act_grads_written confirms the overwrite before Adam
+    keep = _ACT_OVERWRITES if dev.type == "cuda" else ()
+    fp.zero_grad(keep=keep)
+    scene.act_grads_written = False
     scene.iteration = it = scene.iteration + 1 if iteration is None else int(iteration)
     lam_normal = LAMBDA_NORMAL if (it > REG_NORMAL_FROM_ITER and LAMBDA_NORMAL > 0) else 0.0
     if bg is None:  # one tensor per device: render()'s grey-background check is cached on it
@@ -1003,25 +1069,16 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         main.wait_stream(s)
     for out in outs:
         out["viewspace_points"].grad.record_stream(main)
-    if world > 1:
-        # this step's densification deltas (zeroed per step; only they cross ranks)
-        if scene.step_stats is None or scene.step_stats.d["denom"].shape[0] != scene.P:
-            scene.step_stats = gdp.StepStats(scene.P, dev)
-        scene.step_stats.zero()
-        scene.step_stats.add_views([o["viewspace_points"].grad for o in outs], radii)
-    else:  # one rank: straight into the running statistics, view by view
-        gdp.StepStats.view_of(scene.stats).add_views([o["viewspace_points"].grad for o in outs], radii)
-    del outs
+    if keep and not scene.act_grads_written:  # the activations' backward did not run: no stale values
+        for n in keep:
+            fp.params[n].grad.zero_()
     fp.check_grads_in_place()
-    n_views = len(views)
-    if world > 1:
-        import torch.distributed as dist
-        dist.all_reduce(fp.grad, op=dist.ReduceOp.SUM, group=group)
-        n_views *= world
-    if world > 1:
-        scene.step_stats.commit(scene.stats, group=group, world=world)
+    # densification statistics (train.py:130, 143-144) and the iteration's ONE collective
+    gdp.finish_step(scene, [o["viewspace_points"].grad for o in outs], radii, it, world=world, group=group)
+    del outs
     if optimizer_step:
-        fp.step(grad_scale=1.0 / n_views)
+        apply_lr_schedule(scene, it)
+        fp.step(grad_scale=1.0 / (len(views) * max(world, 1)))
     return total.detach()
 
 

@@ -187,3 +187,65 @@ def run_identical_probe(rank, world, port, out_path):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+# ---- the training iteration's exchange: gsr.dp.finish_step, one collective per iteration ----
+
+EX_ITERS = (14998, 14999, 15000, 15001)  # across densify_until_iter (15000)
+COLLECTIVES = ("all_reduce", "all_gather", "broadcast", "reduce_scatter", "reduce", "all_to_all",
+               "all_reduce_coalesced", "all_gather_into_tensor", "reduce_scatter_tensor")
+
+
+def exchange_grad(it, r, n):
+    return torch.randn(n, generator=torch.Generator().manual_seed(7919 * it + r))
+
+
+def exchange_run(rank, world):
+    """train_step's tail over EX_ITERS: each rank's flat gradient and 2 views' statistics, then
+    gsr.dp.finish_step (world 1: both ranks' views in one process, the gradients summed in rank
+    order).  Returns (scene, collectives issued per iteration as counted by wrapping every
+    torch.distributed collective)."""
+    from gsr import dp
+    counts, calls = [], []
+    if world > 1:
+        for name in COLLECTIVES:
+            orig = getattr(dist, name, None)
+            if orig is not None:
+                def wrap(*a, _orig=orig, _n=name, **k):
+                    calls.append(_n)
+                    return _orig(*a, **k)
+                setattr(dist, name, wrap)
+    scene = small_scene()
+    P, fp = scene.P, scene.fp
+    for it in EX_ITERS:
+        fp.zero_grad()
+        ranks = [rank] if world > 1 else list(range(2))
+        for r in ranks:
+            fp.grad.add_(exchange_grad(it, r, fp.n))
+        g2d, rad = [], []
+        for r in ranks:
+            for j in range(VIEWS_PER_RANK):
+                g, radii = view_stats(it, r * VIEWS_PER_RANK + j, P)
+                g2d.append(g * 0.02)
+                rad.append(radii)
+        n0 = len(calls)
+        ret = dp.finish_step(scene, g2d, rad, it, world=world)
+        counts.append((ret, len(calls) - n0))
+    if world > 1:
+        dp.sync_max_radii(scene.stats)
+    return scene, counts
+
+
+def run_exchange(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        scene, counts = exchange_run(rank, world)
+        if rank == 0:
+            out = {k: v.numpy() for k, v in scene.stats.items()}
+            out.update(grad=scene.fp.grad.numpy(), counts=np.array(counts), tail=np.array(scene.fp.tail))
+            np.savez(out_path, **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

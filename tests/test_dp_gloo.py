@@ -97,3 +97,32 @@ def test_replicas_identical_sees_one_bit(tmp_path):
     out = str(tmp_path / "flags.npy")
     mp.spawn(dp_worker.run_identical_probe, args=(2, free_port(), out), nprocs=2, join=True)
     assert np.load(out).tolist() == [False, True, False]
+
+
+def test_iteration_exchange_is_one_collective(tmp_path):
+    """gsr.dp.finish_step (train_step's tail) issues exactly ONE collective
+    per iteration at world size 2 -- the flat gradient's SUM all-reduce, carrying the step's
+    densification sums in its tail below densify_until_iter and the gradient alone past it --
+    and the result equals the sequential accumulation over both ranks' views: gradient
+    bit-exact (two-rank sums commute), denom and max_radii2D exact (the rank-local maxima
+    MAX-reduced once, as densification does), the norm accumulator to float order; the sums
+    stop at iteration 15000 (train.py:143) while max_radii2D keeps updating (train.py:130)."""
+    out = str(tmp_path / "exchange.npz")
+    mp.spawn(dp_worker.run_exchange, args=(2, free_port(), out), nprocs=2, join=True)
+    got = np.load(out, allow_pickle=False)
+    ref, ref_counts = dp_worker.exchange_run(0, 1)
+    assert got["counts"].tolist() == [[1, 1]] * len(dp_worker.EX_ITERS), got["counts"]
+    assert [c[0] for c in ref_counts] == [0] * len(dp_worker.EX_ITERS)
+    assert int(got["tail"]) == 2 * ref.P
+    assert np.array_equal(got["grad"], ref.fp.grad.numpy())
+    assert np.array_equal(got["denom"], ref.stats["denom"].numpy())
+    assert np.array_equal(got["max_radii2D"], ref.stats["max_radii2D"].numpy())
+    np.testing.assert_allclose(got["xyz_gradient_accum"], ref.stats["xyz_gradient_accum"].numpy(), rtol=1e-6,
+                               atol=1e-7)
+    # two iterations below densify_until_iter (14998, 14999) count; 15000 and 15001 do not
+    on = sum(1 for it in dp_worker.EX_ITERS if it < 15000)
+    assert float(ref.stats["denom"].max()) <= on * 2 * dp_worker.VIEWS_PER_RANK
+    assert float(ref.stats["denom"].max()) >= on
+    # max_radii2D did take the last iterations' views
+    _, r_last = dp_worker.view_stats(dp_worker.EX_ITERS[-1], 0, ref.P)
+    assert (ref.stats["max_radii2D"] >= r_last.float()).all()

@@ -103,6 +103,14 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
             loss.backward(retain_graph=vid == 0)
         for p in leaves.values():
             p.grad /= len(views)
+        # the reference's position schedule (gaussian_model.py:285-290; gsr.train.apply_lr_schedule,
+        # pinned by tests/test_train_golden.py::test_lr_schedule_matches_reference)
+        lr_x = train.expon_lr(it - 1, train.POSITION_LR_INIT * scene.spatial_lr_scale,
+                              train.POSITION_LR_FINAL * scene.spatial_lr_scale,
+                              lr_delay_mult=train.POSITION_LR_DELAY_MULT, max_steps=train.POSITION_LR_MAX_STEPS)
+        for grp, n in zip(opt.param_groups, fp.names):
+            if n in ("xyz", "sky_angles"):
+                grp["lr"] = lr_x
         opt.step()
         loss_flat = train.train_step(scene, views, [0, 1], gts, streams=streams, rand=rand)
         assert scene.iteration == it
@@ -114,8 +122,14 @@ def test_train_step_matches_plain_autograd_and_adam(nstreams):
     for n in ("embeddings", "mlp.base.0.weight", "mlp.sh_envl_outlayer.bias", "mlp.sh_sky_outlayer.weight",
               "sky_angles", "sky_radius"):
         assert float(fp.grad[fp.offsets[fp.names.index(n)]:fp.ends[fp.names.index(n)]].abs().sum()) > 0, n
-    assert float(scene.stats["denom"].max()) == 4.0  # 2 views x 2 iterations
-    assert float(scene.stats["xyz_gradient_accum"].sum()) > 0
+    # iterations 15000 and 15001 are not below densify_until_iter (15000): no gradient-norm
+    # sums (train.py:143-144), but max_radii2D is updated every iteration (train.py:130)
+    assert float(scene.stats["denom"].max()) == 0.0
+    assert float(scene.stats["xyz_gradient_accum"].abs().sum()) == 0.0
+    assert float(scene.stats["max_radii2D"].max()) > 0
+    train.train_step(scene, views, [0, 1], gts, streams=streams, iteration=14000)  # below: the sums count
+    torch.cuda.synchronize()
+    assert float(scene.stats["denom"].max()) == 2.0 and float(scene.stats["xyz_gradient_accum"].sum()) > 0
 
 
 def test_full_size_step_properties():

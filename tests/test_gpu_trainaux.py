@@ -30,7 +30,8 @@ def _pc(P, V, dev, seed=0, sky_frac=0.15):
 
 
 @pytest.mark.parametrize("tail", [True, False])
-@pytest.mark.parametrize("P,V,depth_on", [(1000, 1, True), (70001, 4, True), (70001, 4, False), (4099, 8, True)])
+@pytest.mark.parametrize("P,V,depth_on", [(1000, 1, True), (70001, 4, True), (70001, 4, False), (4099, 8, True),
+                                          (4099, 11, True)])  # 11: two launches of up to 8 views
 def test_view_regularisers_fused_matches_torch(P, V, depth_on, tail):
     """The fused regularisers (per-Gaussian sums, and with ``tail`` the scalar tail and the
     envlight term in one workgroup) against the PyTorch composition: values and the xyz,
@@ -186,3 +187,28 @@ def test_fused_activations_match_torch(layout):
             continue
         e = float((a - b).norm() / b.norm())
         assert e < 1e-5, (name, e)
+
+
+@pytest.mark.parametrize("sums", [True, False])
+def test_dp_add_views_fused_matches_torch(sums):
+    """gsr.dp.add_views (train_step's statistics, gsr_densify_stats in launches of up to 8
+    views) against its PyTorch path over 11 views; sums=False: max radii alone (past
+    densify_until_iter, train.py:130 vs :143-144) -- accum and denom untouched."""
+    from gsr import dp
+    P, V = 20011, 11
+    g = torch.Generator().manual_seed(4)
+    grads = [torch.randn(P, 3, generator=g) for _ in range(V)]
+    radii = [((torch.rand(P, generator=g) < 0.5) * torch.randint(1, 40, (P,), generator=g)).int() for _ in range(V)]
+    base = {"a": torch.rand(P, 1, generator=g), "d": torch.randint(0, 5, (P, 1), generator=g).float(),
+            "m": torch.full((P,), 7.0)}
+    cpu = {k: v.clone() for k, v in base.items()}
+    gpu = {k: v.cuda() for k, v in base.items()}
+    dp.add_views(cpu["a"] if sums else None, cpu["d"] if sums else None, cpu["m"], grads, radii)
+    dp.add_views(gpu["a"] if sums else None, gpu["d"] if sums else None, gpu["m"], [t.cuda() for t in grads],
+                 [r.cuda() for r in radii])
+    torch.cuda.synchronize()
+    assert torch.equal(gpu["m"].cpu(), cpu["m"])
+    assert torch.equal(gpu["d"].cpu(), cpu["d"])
+    np.testing.assert_allclose(gpu["a"].cpu().numpy(), cpu["a"].numpy(), rtol=1e-6, atol=0)
+    if not sums:
+        assert torch.equal(gpu["a"].cpu(), base["a"]) and torch.equal(gpu["d"].cpu(), base["d"])

@@ -132,3 +132,36 @@ def test_view_regularisers_batched_equal_single_view(depth_on):
     gb = torch.autograd.grad(want.sum(), ins)
     for a, b in zip(ga, gb):
         assert rel_l2(a.numpy(), b.numpy()) < 1e-5
+
+
+def test_lr_schedule_matches_reference():
+    """gsr.train.apply_lr_schedule against the rates the reference's optimizer holds at each
+    iteration's step (tests/golden/train_lr.npz from tools/gen_golden_train.py lr: training_setup's
+    groups, get_expon_lr_func, GaussianModel / Relightable3DGW.update_learning_rate driven as
+    train.py:156-159 drives them), spatial_lr_scale 2.5, with the default MLP rate and with one
+    that makes the iteration-20000 reset visible."""
+    import numpy as np
+    from gsr import train
+    d = np.load(os.path.join(os.path.dirname(GOLD), "train_lr.npz"), allow_pickle=False)
+    g = torch.Generator().manual_seed(0)
+    P_fg, P_sky = 30, 5
+    P = P_fg + P_sky
+    is_sky = torch.zeros(P, dtype=torch.bool)
+    is_sky[P_fg:] = True
+    xyz = torch.randn(P, 3, generator=g)
+    scale = float(d["lr/spatial_lr_scale"])
+    for tag, mlp_lr in (("default", 0.0002), ("mlp1e-3", 0.001)):
+        scene = train.RelitScene(xyz, torch.randn(P, 3, generator=g), torch.randn(P, 4, generator=g),
+                                 torch.randn(P, 1, generator=g), torch.randn(P_fg, 3, generator=g),
+                                 torch.randn(P_fg, 1, generator=g), torch.randn(P_fg, 1, generator=g), is_sky, 2, "cpu",
+                                 spatial_lr_scale=scale)
+        fp = scene.fp
+        for n in fp.names:
+            if n == "embeddings" or n.startswith("mlp."):
+                fp.set_lr(n, mlp_lr)
+        for k, it in enumerate(d["lr/iters"].tolist()):
+            train.apply_lr_schedule(scene, it)
+            for n, lr in zip(fp.names, fp.lrs):
+                ref_name = "mlp" if n.startswith("mlp.") else n
+                want = float(d[f"lr/{tag}/{ref_name}"][k])
+                assert lr == pytest.approx(want, rel=1e-12), (tag, it, n, lr, want)

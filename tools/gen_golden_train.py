@@ -3,7 +3,8 @@ by importing the REFERENCE's own Python (read-only at /root/reference) on the CP
 stubs of tools/gen_golden.py.  Output: tests/golden/train_step.npz (inputs + expected
 outputs and gradients only; no reference source is stored).
 
-    python tools/gen_golden_train.py
+    python tools/gen_golden_train.py        (everything)
+    python tools/gen_golden_train.py lr     (tests/golden/train_lr.npz only)
 
 Pinned by these fixtures:
   MLPNet.forward          scene/net_models.py:16-52 (eval mode: dropout is the identity;
@@ -219,5 +220,64 @@ def sky_and_densify(GaussianModel):
     print("wrote", os.path.join(OUT, "train_sky.npz"), {k: v.shape for k, v in fx.items() if k.startswith("dens/a")})
 
 
+LR_ITERS = (1, 2, 3, 100, 500, 14999, 15000, 15001, 15002, 19999, 20000, 20001, 20002, 29999, 30000, 30001, 30002,
+            39999, 40000)
+
+
+def lr_schedule():
+    """tests/golden/train_lr.npz: the learning rate every param group's Adam step uses at the
+    iterations LR_ITERS, from the reference's own training_setup groups, get_expon_lr_func
+    (utils/general_utils.py:46-80) and update_learning_rate (gaussian_model.py:285-290 through
+    relit3DGW_model.py:153-158), driven as train.py:156-159 drives them: step, then
+    update_learning_rate(iteration).  Twice: the default config (mlp_lr = embeddings_lr =
+    0.0002, so the iteration-20000 reset is a no-op) and mlp_lr = embeddings_lr = 0.001 (the
+    reset visible), both with spatial_lr_scale 2.5."""
+    gen_golden.setup_reference_import()
+    gen_golden._stub("data")
+    gen_golden._stub("data.dataloader_net", load_train_test=None)
+    sys.modules["data"].dataloader_net = sys.modules["data.dataloader_net"]
+    from scene.gaussian_model import GaussianModel
+    from utils.general_utils import get_expon_lr_func
+    # relit3DGW_model's module-level imports: hydra's decorator as the identity, the config and
+    # dataset types as placeholders (only the unbound update_learning_rate is called)
+    gen_golden._stub("omegaconf", OmegaConf=object, DictConfig=object)
+    gen_golden._stub("hydra", main=lambda **kw: (lambda f: f))
+    gen_golden._stub("torchvision")
+    for m in ("diff_gaussian_rasterization",):
+        if m not in sys.modules:
+            gen_golden._stub(m, GaussianRasterizationSettings=object, GaussianRasterizer=object)
+    sys.modules["scene"].GaussianModel = GaussianModel
+    sys.modules["scene"].Scene = object
+    from scene.relit3DGW_model import Relightable3DGW
+    scale = 2.5
+    fx = {"lr/iters": np.array(LR_ITERS), "lr/spatial_lr_scale": np.array(scale)}
+    for tag, mlp_lr in (("default", 0.0002), ("mlp1e-3", 0.001)):
+        lrs0 = {"xyz": 0.00016 * scale, "albedo": 0.0025, "opacity": 0.05, "scaling": 0.001 * scale,
+                "rotation": 0.001, "roughness": 0.0002, "metalness": 0.0002, "sky_radius": 0.0001,
+                "sky_angles": 0.00016 * scale, "mlp": mlp_lr, "embeddings": mlp_lr}
+        groups = [{"params": [torch.zeros(1, requires_grad=True)], "lr": lr, "name": n} for n, lr in lrs0.items()]
+        opt = torch.optim.Adam(groups, lr=0.01, eps=1e-15)
+        gm = types.SimpleNamespace(optimizer=opt, xyz_scheduler_args=get_expon_lr_func(
+            lr_init=0.00016 * scale, lr_final=0.0000016 * scale, lr_delay_mult=0.01, max_steps=30_000))
+        gm.update_learning_rate = types.MethodType(GaussianModel.update_learning_rate, gm)
+        model = types.SimpleNamespace(gaussians=gm, optimizer=opt)
+        names = [g["name"] for g in opt.param_groups]
+        rec = {n: [] for n in names}
+        want = set(LR_ITERS)
+        for it in range(1, max(LR_ITERS) + 1):
+            if it in want:  # the rates this iteration's step uses
+                for g in opt.param_groups:
+                    rec[g["name"]].append(g["lr"])
+            Relightable3DGW.update_learning_rate(model, it)
+        for n in names:
+            fx[f"lr/{tag}/{n}"] = np.array(rec[n], np.float64)
+    np.savez_compressed(os.path.join(OUT, "train_lr.npz"), **fx)
+    print("wrote", os.path.join(OUT, "train_lr.npz"))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["lr"]:
+        lr_schedule()
+    else:
+        main()
+        lr_schedule()
