@@ -624,9 +624,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         flip = gsr::depth_sort(P, pa.depth_key, vis_key, vis_val, at<uint32_t>(geom, gl.vis_key_alt),
                                at<uint32_t>(geom, gl.vis_val_alt), pa.rect, at<uint2>(geom, gl.rect_s),
                                at<uint2>(geom, gl.rect_s_alt), at<void>(geom, gl.sort_tmp), tot_dev, s,
-                               at<void>(geom, gl.acc), sizeof(float) * gsr::ACC_STRIDE * (size_t)P, rect_packed);
+                               nullptr, 0, rect_packed);
     }
-    zeroed_set(geom, true);  // the backward's accumulators are zero from here on
     GSR_LAUNCH_CHECK();
 
     unsigned long long Pv = 0, R64 = 0, S64 = 0;
@@ -702,7 +701,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         GSR_LAUNCH_CHECK();
         return GSR_OK;
     };
-    gsr::RenderFwdArgs ra;
+    gsr::RenderFwdArgs ra{};
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
     ra.gsx = gsx; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
@@ -711,7 +710,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
-    // the forward tile pass over the binning in `bin`
+    // the forward tile pass over the binning in `bin`; its workgroups also zero the backward's
+    // accumulator lines (zero_slice; the depth sort's digit scans did it up to round 3)
+    ra.zero = reinterpret_cast<float4*>(at<float>(geom, gl.acc));
+    ra.zero_n4 = (long long)gsr::ACC_STRIDE * P / 4;
     auto render_pass = [&]() -> int {
         ra.st_ranges = at<uint2>(bin, bl.st_ranges);
         ra.ent = at<uint2>(bin, bl.ent);
@@ -728,6 +730,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                 if (c0 == 0) {  // the other groups would write the same values
                     ma.final_T = ra.final_T;
                     ma.n_contrib = ra.n_contrib;
+                    ma.zero = ra.zero;
+                    ma.zero_n4 = ra.zero_n4;
                 } else {
                     ma.tile_nmax = nullptr;
                 }
@@ -735,6 +739,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
             }
         }
         GSR_LAUNCH_CHECK();
+        zeroed_set(geom, true);  // the backward's accumulators are zero from here on
         return GSR_OK;
     };
     int rc;
@@ -847,7 +852,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     HIP_OK(hipMemcpyAsync(geom + gl.rect, src + gl.rect, 8 * (size_t)P, hipMemcpyDeviceToDevice, s));
     GSR_LAUNCH_CHECK();
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
-    gsr::RenderFwdArgs ra;  // with R == 0 every super-tile list is empty: background everywhere
+    gsr::RenderFwdArgs ra{};  // with R == 0 every super-tile list is empty: background everywhere
     ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
     ra.gsx = st_x(width);
     ra.st_ranges = bin ? at<uint2>(bin, bl.st_ranges) : nullptr;
@@ -991,13 +996,16 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
             if (miss) return fail(GSR_E_DEVICE_CHECK, "gsr_backward (deterministic): %u instances not found in their tile lists", miss);
         }
     }
-    gsr::PreprocessBwdArgs pb;
+    gsr::PreprocessBwdArgs pb{};
     pb.P = P; pb.D = D; pb.M = M;
     pb.means3D = means3D; pb.radii = radii; pb.shs = shs; pb.scales = scales; pb.rotations = rotations;
     pb.scale_modifier = scale_modifier; pb.cov3D_precomp = cov3D_precomp;
     pb.viewmatrix = viewmatrix; pb.projmatrix = projmatrix; pb.campos = campos;
     pb.tan_fovx = tan_fovx; pb.tan_fovy = tan_fovy; pb.focal_x = focal_x; pb.focal_y = focal_y;
     pb.acc = acc;
+    pb.acc_raw = 1;  // the tile passes' raw sums (gsr_render_bwd.hip)
+    pb.W = width;
+    pb.H = height;
     pb.shjac = at<float>(geom, gl.shjac);
     pb.dL_dmean2D = dL_dmean2D; pb.dL_dconic = dL_dconic; pb.dL_dopacity = dL_dopacity; pb.dL_dcolor = dL_dcolor;
     pb.dL_dmean3D = dL_dmean3D; pb.dL_dcov3D = dL_dcov3D; pb.dL_dsh = M > 0 ? dL_dsh : nullptr;

@@ -206,6 +206,11 @@ struct RenderFwdArgs {
     uint32_t* tile_nmax;  // out: per tile, the largest n_contrib (the backward's cost; atomicMax, zeroed)
     uint32_t* tile_emax;  // out: per tile, 1 + the entry index of that last contributor (where the backward starts)
     uint32_t* tile_cost;  // out (when non-null): per tile, the sum of its quadrants' largest n_contrib (atomicAdd, zeroed)
+    // when non-null: zero_n4 float4s the backward needs zeroed (the gradient accumulator lines),
+    // cleared by the pass's workgroups a slice each (zero_slice): VALU-bound waves have the HBM
+    // write bandwidth to spare
+    float4* zero;
+    long long zero_n4;
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -262,6 +267,8 @@ struct RenderMcArgs {
     // (added over the groups)][every channel]; pc0 = this group's first channel
     float* partial;
     int pstride, pc0;
+    float4* zero;  // forward: as RenderFwdArgs::zero
+    long long zero_n4;
 };
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);
@@ -360,6 +367,11 @@ struct PreprocessBwdArgs {
     const float* campos;
     float tan_fovx, tan_fovy, focal_x, focal_y;
     const float* acc;  // [P][ACC_STRIDE] from the render backward
+    // acc_raw: the line holds the tile passes' raw sums (gsr_render_bwd.hip): op * (sum G dL/dalpha
+    // dx, ... dy, ... dx dx, ... dx dy, ... dy dy), sum G dL/dalpha, the colour sums; the conic and
+    // the screen scale are applied here, once per Gaussian.  0: the line holds the reference's
+    // values (dL/dmean2D, dL/dconic, dL/dopacity, dL/dcolor; baseline/refalgo.hip)
+    int acc_raw, W, H;
     const float* shjac;  // [SHJAC_ROWS][P] from the forward preprocess (required with shs)
     // outputs (fully written, no pre-zeroing needed)
     float* dL_dmean2D;

@@ -141,11 +141,17 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     // ---- unpack the render-backward accumulator line ------------------------------
     const float4 l0 = in.l0, l1 = in.l1;
     const float l2 = in.l2;
-    const float dm2x = l0.x, dm2y = l0.y, dcx = l0.z, dcy = l0.w, dcw = l1.x, dop = l1.y;
+    // raw lines (acc_raw): dL/dconic = -1/2 op sum G dL/dalpha (dx dx, dx dy, dy dy)
+    // (backward.cu:548-550; the tile passes applied op), dL/dmean2D once the conic is known below
+    const float cs = a.acc_raw ? -0.5f : 1.f;
+    float dm2x = l0.x, dm2y = l0.y;
+    const float dcx = cs * l0.z, dcy = cs * l0.w, dcw = cs * l1.x, dop = l1.y;
     const float dcol0 = l1.z, dcol1 = l1.w, dcol2 = l2;
-    a.dL_dmean2D[3 * idx + 0] = dm2x;
-    a.dL_dmean2D[3 * idx + 1] = dm2y;
-    a.dL_dmean2D[3 * idx + 2] = 0.f;
+    if (!a.acc_raw || !(in.radius > 0)) {  // (a culled Gaussian's line is zero)
+        a.dL_dmean2D[3 * idx + 0] = a.acc_raw ? 0.f : dm2x;
+        a.dL_dmean2D[3 * idx + 1] = a.acc_raw ? 0.f : dm2y;
+        a.dL_dmean2D[3 * idx + 2] = 0.f;
+    }
     if (a.dL_dconic)  // the reference allocates it but returns it to no one (rasterize_points.cu:145,186)
         *reinterpret_cast<float4*>(a.dL_dconic + 4 * idx) = make_float4(dcx, dcy, 0.f, dcw);
     put(a.dL_dopacity + idx, dop, ao);
@@ -208,6 +214,18 @@ __device__ __forceinline__ void preprocess_bwd_one(const PreprocessBwdArgs& a, i
     const float cb = cov2D.m[0][1];
     const float cc = cov2D.m[1][1] += 0.3f;
     const float denom = ca * cc - cb * cb;
+    if (a.acc_raw) {
+        // the conic exactly as the forward computed it (forward.cu:219-222: det, 1/det, products;
+        // contraction off in both TUs, so the record's bits), then dL/dmean2D in NDC units
+        // (backward.cu:540-545): -(W/2) (a M1 + b M2), -(H/2) (b M1 + c M2) with M = op sum G dL/dalpha d
+        const float det_inv = 1.f / denom;
+        const float ka = cc * det_inv, kb = -cb * det_inv, kc = ca * det_inv;
+        dm2x = -0.5f * (float)a.W * (ka * l0.x + kb * l0.y);
+        dm2y = -0.5f * (float)a.H * (kb * l0.x + kc * l0.y);
+        a.dL_dmean2D[3 * idx + 0] = dm2x;
+        a.dL_dmean2D[3 * idx + 1] = dm2y;
+        a.dL_dmean2D[3 * idx + 2] = 0.f;
+    }
     float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
     const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
 #define TT(i, j) T.m[i][j]

@@ -75,8 +75,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
     const int vidx = col == 0 ? vrow : col == 8 ? 4 + vrow : col == 4 ? 8 : -1;
     const lmask mb3 = __ballot((col & 8) != 0), mb2 = __ballot((col & 4) != 0);
-    // per-value scale: dL/dmean2D gets op * (W/2, H/2), dL/dconic -op/2, the rest 1
-    const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : vidx <= 4 ? -0.5f : 1.f;
+    // values 0-4 (the conic-weighted sums) carry the opacity; the conic, -1/2 and the screen
+    // scale are applied once per Gaussian by the preprocess backward (acc_raw)
     const bool vop = vidx >= 0 && vidx <= 4;
     // deterministic mode: the slot of this lane's value in the instance's partial row
     // (values 0..7, then value 8's four row partials)
@@ -174,19 +174,19 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             }
             if (any) {
             BWD_STAT(5, 1);
-            // conic part of dL/dmean2D (backward.cu:540-545): -(a M1 + b M2), -(b M1 + c M2)
-            const float S0 = __builtin_fmaf(ka, M1 + M1, kb * M2);
-            const float S1 = __builtin_fmaf(kc, M2 + M2, kb * M1);
-            // wave reduction: permlane32 swaps pair (S0,S1),(S2,S3),(S4,S5),(S6,S7)
+            // raw sums (the line's layout, acc_raw): M1, M2 -- dL/dmean2D is -(a M1 + b M2),
+            // -(b M1 + c M2) in pixels (backward.cu:540-545), formed per Gaussian by the
+            // preprocess backward, as is the conic's -1/2 and the NDC scale
+            // wave reduction: permlane32 swaps pair (M1,M2),(S2,S3),(S4,S5),(S6,S7)
             // into half-wave sums, permlane16 swaps pair those into row sums of four values
             // per register, then the three registers' 16-lane rows sum transposed (row_sum3)
-            float P0 = swap32_sum(S0, S1), P1 = swap32_sum(S2, S3), P2 = swap32_sum(S4, S5);
+            float P0 = swap32_sum(M1, M2), P1 = swap32_sum(S2, S3), P2 = swap32_sum(S4, S5);
             float P3 = swap32_sum(S6, S7);
             // S8 skips both swap stages: its four row sums go to the atomic as partial sums
             // (lanes 4, 20, 36, 52)
             const float Q0 = swap16_sum(P0, P1), Q1 = swap16_sum(P2, P3), Q2 = S8;
             float v = row_sum3(Q0, Q1, Q2, mb3, mb2);
-            v *= vop ? op * vscale : vscale;
+            v = vop ? v * op : v;
             if (DET) {  // one row per instance, summed per Gaussian in tile order (k_det_gather)
                 if (vidx >= 0 && v != 0.f) a.partial[(size_t)(rbase + pos) * DET_ROW3 + pslot] = v;
             } else if (vidx >= 0 && v != 0.f) {

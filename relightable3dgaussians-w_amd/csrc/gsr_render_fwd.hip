@@ -211,6 +211,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD
 k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
+    zero_slice(a.zero, a.zero_n4);
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
     render_fwd_tile(a, tile, qallow);
 }

@@ -198,7 +198,8 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     const int vreg = row_sums_t_reg<NQ>(col);  // the register whose row sums this lane ends with
     const int vidx = (vreg >= 0 && 4 * vreg + vrow < V) ? 4 * vreg + vrow : -1;
     const lmask mb3 = __ballot((col & 8) != 0), mb2 = __ballot((col & 4) != 0);
-    const float vscale = vidx == 0 ? 0.5f * a.W * TILE_LN2 : vidx == 1 ? 0.5f * a.H * TILE_LN2 : (vidx >= 2 && vidx <= 4) ? -0.5f : 1.f;
+    // values 0-4 carry the opacity; the conic, -1/2 and the screen scale are applied per
+    // Gaussian by the preprocess backward (acc_raw), as in gsr_render_bwd.hip
     const bool vop = vidx >= 0 && vidx <= 4;
     const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
 
@@ -294,8 +295,8 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             }
             if (any) {
                 float S[2 * NP];
-                S[0] = __builtin_fmaf(ka, M1 + M1, kb * M2);
-                S[1] = __builtin_fmaf(kc, M2 + M2, kb * M1);
+                S[0] = M1;  // raw: the preprocess backward applies the conic (acc_raw)
+                S[1] = M2;
                 S[2] = S2;
                 S[3] = S3;
                 S[4] = S4;
@@ -313,7 +314,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
 #pragma unroll
                 for (int t = 0; t < NQ; t++) Qr[t] = swap16_sum(Pp[2 * t], Pp[2 * t + 1]);
                 float v = row_sums_t<NQ>(Qr, mb3, mb2, col);
-                v *= vop ? op * vscale : vscale;
+                v = vop ? v * op : v;
                 if (DET) {  // the groups run one after another: plain read-modify-write
                     float* prow = a.partial + (size_t)(rbase + pos) * a.pstride;
                     if (vidx >= 0 && vidx < 6) prow[vidx] += v;
@@ -332,6 +333,7 @@ template <int NC4, int NCH = 4 * NC4>
 __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
+    zero_slice(a.zero, a.zero_n4);
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }

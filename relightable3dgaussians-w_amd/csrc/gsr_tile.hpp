@@ -303,6 +303,20 @@ __device__ __forceinline__ float wave_sum(float v) {
     return __uint_as_float(t[0]) + __uint_as_float(t[1]);  // halves
 }
 
+// The forward tile passes clear the backward's gradient accumulator lines: workgroup b of the
+// grid stores zeros over float4s [b per, (b + 1) per), per = ceil(n4 / grid), before it takes
+// its unit (so the blocks past the last unit clear their slice too).  Non-temporal: the lines
+// are next touched by the backward, and the pass's records stay in the caches.
+__device__ __forceinline__ void zero_slice(float4* z, long long n4) {
+    if (!z) return;
+    const long long per = (n4 + gridDim.x - 1) / gridDim.x;
+    const long long b0 = (long long)blockIdx.x * per;
+    const long long b1 = b0 + per < n4 ? b0 + per : n4;
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    for (long long i = b0 + (threadIdx.x & 63); i < b1; i += 64)
+        __builtin_nontemporal_store((f4v){0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f4v*>(z + i));
+}
+
 // ---- one wave per 16x16 tile --------------------------------------------------------
 // Lane l owns pixel (l % 8, l / 8) of each of the tile's four 8x8 quadrants q (offset
 // (8 (q & 1), 8 (q >> 1))), so a wave holds the whole tile and every per-Gaussian quadrant

@@ -10,6 +10,7 @@ import sys
 
 
 def runs(v):
+    v = os.environ.get("KTP", "") + v
     out = []
     for f in sorted(glob.glob(f"gpurun_out/ktv_{v}_*/*/*_kernel_stats.csv")) + \
             sorted(glob.glob(f"gpurun_out/ktv_{v}/*/*_kernel_stats.csv")):
