@@ -170,19 +170,25 @@ class _RelitModel:
 
 
 def bench_relight(args, dev):
+    """--config cfg3 / cfg5-relit: relight_leg as the JSON line."""
+    print(json.dumps(relight_leg(args, dev, args.config == "cfg5-relit", args.steps, args.warmup,
+                                 with_calls=not args.fused_only)), flush=True)
+
+
+def relight_leg(args, dev, stress, steps, warmup, with_calls=True, P_fg=None):
     """cfg3: the relightable render() step (gaussian_renderer/__init__.py:69-280,
     debug=False) and a training-style loss backward through all of its images (render,
     diffuse, specular, depth, normal, alpha, normal_ref).  value = views/s of the fused path
     (gsr.relit.render: relit features + one multi-channel composite); render()'s own call
     sequence on the drop-in ops (gsr.relit.render_calls: PyTorch per-Gaussian steps + six
-    rasterizer calls), with and without the geometry cache, is reported beside it."""
+    rasterizer calls), with and without the geometry cache, is reported beside it
+    (with_calls, cfg3 only).  stress: cfg5 -- 5M Gaussians at 3840x2160."""
     import types
 
     import diff_gaussian_rasterization as dgr
     import relit_shade
     from gsr import relit, scenes, shrot
-    stress = args.config == "cfg5-relit"  # cfg5: 5M Gaussians at 3840x2160, relit render with backward
-    P_fg = args.P or (4_545_455 if stress else 1_000_000)
+    P_fg = P_fg or args.P or (4_545_455 if stress else 1_000_000)
     P = P_fg + P_fg // 10  # + 10 % sky Gaussians
     cam, gs, c = scenes.build_config("cfg5" if stress else "cfg2", device="cpu", seed=0, P=P)
     W, H = cam.image_width, cam.image_height
@@ -236,25 +242,25 @@ def bench_relight(args, dev):
             loss.backward()
 
     def timed(fn):
-        for _ in range(args.warmup):
+        for _ in range(warmup):
             step(fn)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(steps):
             step(fn)
         torch.cuda.synchronize()
-        return (time.perf_counter() - t0) * 1e3 / args.steps
+        return (time.perf_counter() - t0) * 1e3 / steps
 
     ms = timed(relit.render)
     res = {True: float("nan"), False: float("nan")}
-    if not args.fused_only and not stress:
+    if with_calls and not stress:
         for cached in (True, False):
             dgr.geometry_cache(cached)
             res[cached] = timed(relit.render_calls)
         dgr.geometry_cache(True)
-    print(json.dumps({
+    return {
         "metric": "relit render() views/s (render()'s images + training loss backward)", "value": round(1e3 / ms, 3),
-        "unit": "views/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+        "unit": "views/s", "n_gpus": 1, "steps": steps, "warmup": warmup, "ms_per_step": round(ms, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": f"{'cfg5 (relit stress)' if stress else 'cfg3'}: {P_fg} foreground + {P - P_fg} sky "
                                f"Gaussians, {W}x{H}, env SH deg 4 rotated about y over the reference's 30 relight "
@@ -265,7 +271,7 @@ def bench_relight(args, dev):
                           "HIP streams",
         "render_calls": None if res[True] != res[True] else {
             "cached_ms": round(res[True], 4), "uncached_ms": round(res[False], 4),
-            "fused_speedup_vs_cached": round(res[True] / ms, 3)}}), flush=True)
+            "fused_speedup_vs_cached": round(res[True] / ms, 3)}}
 
 
 TRAIN_VIEWS_PER_RANK = 4
@@ -593,6 +599,7 @@ def main():
                          "default 2) alternate over")
     ap.add_argument("--no-minibatch", action="store_true", help="skip the 4-view multi-stream extra leg")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
+    ap.add_argument("--no-relit", action="store_true", help="skip the cfg3 / cfg5-relit relight legs of the default line")
     ap.add_argument("--event-steps", type=int, default=5,
                     help="steps (each V views, one stream) run after the timed region with the dominant stage's "
                          "HIP events, for roofline.avg_launch_ms (default 5); the timed region carries no events")
@@ -938,6 +945,16 @@ def main():
         state.pop("buckets", None)
         out["train"] = train_leg(args, dev, dist, rank, world, backend,
                                  args.train_steps or min(args.steps, 20), max(3, min(args.warmup, 10)))
+    if rank == 0 and world == 1 and not args.no_relit and not args.ply:
+        # BASELINE configs[2] and configs[4] at their sizes, timed by the same run: the relight
+        # render with backward (cfg3: 1M + 0.1M sky Gaussians at 1080p; cfg5: 4.55M + 0.45M at 4K)
+        rl = {}
+        for key, stress in (("cfg3", False), ("cfg5_relit", True)):
+            r = relight_leg(args, dev, stress, 10, 3, with_calls=False, P_fg=4_545_455 if stress else 1_000_000)
+            rl[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "mpix_per_s", "config",
+                                          "implementation")}
+            torch.cuda.empty_cache()
+        out["relit"] = rl
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:
         ms_view = single["median_ms"] if single is not None else ms / V
         vm, pm, cp = mats[0]
