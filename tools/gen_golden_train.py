@@ -5,6 +5,7 @@ outputs and gradients only; no reference source is stored).
 
     python tools/gen_golden_train.py        (everything)
     python tools/gen_golden_train.py lr     (tests/golden/train_lr.npz only)
+    python tools/gen_golden_train.py iteration   (tests/golden/train_iter.npz only)
 
 Pinned by these fixtures:
   MLPNet.forward          scene/net_models.py:16-52 (eval mode: dropout is the identity;
@@ -275,9 +276,206 @@ def lr_schedule():
     print("wrote", os.path.join(OUT, "train_lr.npz"))
 
 
+def iteration():
+    """tests/golden/train_iter.npz: ONE training iteration of the reference, composed as
+    train.py:62-159 composes it from the reference's own pieces -- the embedding row through
+    MLPNet (training-mode dropout, with the mask drawn here and stored), the environment SH
+    plus N(0, 0.025) noise (stored) into EnvironmentLight.set_base, render() (debug=False,
+    specular, fix_sky off; the C oracle stands in for diff_gaussian_rasterization, as in
+    tools/gen_golden_render.py), the reconstruction (L1 + D-SSIM under the occluder mask),
+    sky-BRDF, normal-consistency (iteration 15001 > reg_normal_from_iter), envlight (its random
+    directions re-drawn from the same seed and stored), min-scale and sky-depth losses with the
+    configured weights, loss.backward(), the Adam step over Relightable3DGW.training_set_up's
+    groups (lr 0.01, eps 1e-15; every group with an Adam state from one earlier step with fixed
+    gradients, so the step is not sign-dominated) and update_learning_rate(iteration).  The
+    scene is a GaussianModel with interleaved sky Gaussians on their (theta, phi) shell.
+    Stored: every raw parameter and Adam moment before, the step's raw gradients, the
+    parameters after, the loss, and the inputs (camera, target, masks, draws)."""
+    import yaml
+    from torch import nn
+
+    gen_golden.setup_reference_import()
+    gen_golden._stub("data")
+    gen_golden._stub("data.dataloader_net", load_train_test=None)
+    sys.modules["data"].dataloader_net = sys.modules["data.dataloader_net"]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import oracle_torch
+    stub = types.ModuleType("diff_gaussian_rasterization")
+    stub.GaussianRasterizationSettings = oracle_torch.GaussianRasterizationSettings
+    stub.GaussianRasterizer = oracle_torch.GaussianRasterizer
+    stub.rasterize_gaussians = oracle_torch.rasterize_gaussians
+    sys.modules["diff_gaussian_rasterization"] = stub
+    gen_golden._stub("omegaconf", OmegaConf=object, DictConfig=object)
+    gen_golden._stub("hydra", main=lambda **kw: (lambda f: f))
+    gen_golden._stub("torchvision")
+    from scene.gaussian_model import GaussianModel
+    sys.modules["scene"].GaussianModel = GaussianModel
+    sys.modules["scene"].Scene = object
+    from gaussian_renderer import render
+    from scene.cameras import Camera
+    from scene.NVDIFFREC.light import EnvironmentLight
+    from scene.net_models import MLPNet
+    from scene.relit3DGW_model import Relightable3DGW
+    from utils import general_utils as gu
+    from utils.loss_utils import depth_loss_gaussians, envl_sh_loss, l1_loss, min_scale_loss, ssim
+
+    cfg = yaml.load(open(os.path.join(gen_golden.REF, "configs", "optimizer", "optimization_params.yaml")),
+                    Loader=yaml.SafeLoader)
+    top = yaml.load(open(os.path.join(gen_golden.REF, "configs", "relightable3DG-W.yaml")), Loader=yaml.SafeLoader)
+    opt = types.SimpleNamespace(**cfg)
+    rng = np.random.default_rng(31)
+    torch.manual_seed(31)
+    t = lambda a: torch.tensor(np.asarray(a), dtype=torch.float32)
+    W, H, P, n_sky, n_views, vid, iteration = 64, 48, 700, 70, 2, 1, 15001
+    is_sky = np.zeros((P, 1), bool)
+    is_sky[rng.choice(P, n_sky, replace=False)] = True
+    n_fg = P - n_sky
+    gm = GaussianModel()
+    gm.spatial_lr_scale = 1.0
+    center = t([[0.0, 0.0, 0.0]])
+    radius = 30.0
+    sky_dirs = rng.normal(0, 1, (n_sky, 3)) * [0.35, 0.25, 1.0]
+    sky_dirs[:, 1] = -np.abs(sky_dirs[:, 1])
+    sky_dirs[:, 2] = np.abs(sky_dirs[:, 2])
+    sky_pts = center + radius * t(sky_dirs / np.linalg.norm(sky_dirs, axis=1, keepdims=True))
+    gm._xyz = nn.Parameter(t(rng.normal(0, 1.0, (n_fg, 3)) * [1.2, 0.9, 1.0] + [0.0, 0.0, 5.0]))
+    gm._sky_gauss_center = center
+    gm._sky_radius = nn.Parameter(torch.tensor(radius))
+    gm._sky_angles = nn.Parameter(gu.cartesian_to_polar_coord(sky_pts, center.squeeze(), gm._sky_radius).detach())
+    sc = rng.normal(np.log(0.07), 0.4, (P, 3))
+    sc[is_sky[:, 0]] += np.log(10.0)
+    gm._scaling = nn.Parameter(t(sc))
+    gm._rotation = nn.Parameter(t(rng.normal(0, 1, (P, 4))))
+    gm._opacity = nn.Parameter(t(rng.normal(-0.5, 1.0, (P, 1))))
+    gm._albedo = nn.Parameter(t(rng.normal(0, 1, (n_fg, 3))))
+    gm._roughness = nn.Parameter(t(rng.normal(0, 1, (n_fg, 1))))
+    gm._metalness = nn.Parameter(t(rng.normal(0, 1, (n_fg, 1))))
+    gm._is_sky = torch.tensor(is_sky)
+    gm.max_radii2D = torch.zeros(P)
+    groups = gm.training_setup(opt)
+    mlp = MLPNet(sh_degree_envl=top["envlight_sh_degree"], sh_degree_sky=top["sky_sh_degree"],
+                 embedding_dim=top["embeddings_dim"])
+    mlp.train()
+    emb = nn.Embedding(n_views, top["embeddings_dim"])
+    emb.weight = nn.Parameter(torch.nn.functional.normalize(t(rng.normal(0, 1, (n_views, top["embeddings_dim"]))),
+                                                            p=2, dim=-1))
+    params = [{"params": mlp.parameters(), "lr": opt.mlp_lr, "name": "mlp"},
+              {"params": emb.parameters(), "lr": opt.embeddings_lr, "name": "embeddings"}] + groups
+    optimizer = torch.optim.Adam(params, lr=0.01, eps=1e-15)  # relit3DGW_model.py:147-149
+    gm.optimizer = optimizer
+    named = {n: getattr(gm, "_" + n) for n in GROUPS}
+    named.update({f"mlp.{n}": p for n, p in mlp.named_parameters()})
+    named["embeddings"] = emb.weight
+    # an earlier step with fixed gradients: every parameter has an Adam state
+    for n, p in named.items():
+        p.grad = t(rng.normal(0, 1e-2, tuple(p.shape)))
+    optimizer.step()
+    optimizer.zero_grad(set_to_none=True)
+    fx = {"it/W": np.array(W), "it/H": np.array(H), "it/iteration": np.array(iteration), "it/vid": np.array(vid),
+          "it/n_views": np.array(n_views), "it/is_sky": is_sky, "it/center": center.numpy().reshape(3),
+          "it/names": np.array(list(named))}
+    for n, p in named.items():
+        st = optimizer.state[p]
+        fx[f"before/{n}"] = p.detach().numpy().copy()
+        fx[f"before/m/{n}"] = st["exp_avg"].numpy().copy()
+        fx[f"before/v/{n}"] = st["exp_avg_sq"].numpy().copy()
+        fx[f"before/step/{n}"] = np.array(float(st["step"]))
+
+    # the camera (scene/cameras.py), its target, sky and occluder masks
+    a = np.array([0.05, -0.08, 0.03])
+    th = np.linalg.norm(a)
+    k = a / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    Rm = np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+    Tv = np.array([0.1, -0.05, 0.2])
+    fovx = np.radians(60.0)
+    fovy = 2 * np.arctan(np.tan(fovx / 2) * H / W)
+    sky_mask = (rng.uniform(0, 1, (1, H, W)) > 0.25).astype(np.float32)
+    occ_mask = (rng.uniform(0, 1, (1, H, W)) > 0.1).astype(np.float32)
+    gt = rng.uniform(0, 1, (3, H, W)).astype(np.float32)
+    cam = Camera(colmap_id=0, R=Rm, T=Tv, FoVx=fovx, FoVy=fovy, image=torch.from_numpy(gt), gt_alpha_mask=None,
+                 image_name="iter", uid=vid, data_device="cpu", sky_mask=torch.from_numpy(sky_mask))
+    cam.occluders_mask = torch.from_numpy(occ_mask)
+    # the draws: MLPNet's dropout multiplier (0 or 1/(1-p), as nn.Dropout in training mode), the
+    # environment SH noise, the envlight directions (envl_sh_loss's own draw, same seed)
+    drop = (torch.rand(1, 256) >= 0.2).float() / 0.8
+
+    class FixedDropout(nn.Module):
+        def forward(self, x):
+            return x * drop
+    assert isinstance(mlp.base[1], nn.Dropout)
+    mlp.base[1] = FixedDropout()
+    noise = torch.randn(1, 25, 3) * 0.025
+
+    # ---- train.py:62-118 ----
+    viewpoint_cam_id = torch.tensor([vid])
+    gt_image = cam.original_image
+    sky_m = cam.sky_mask.expand_as(gt_image)
+    occluders_mask = cam.occluders_mask.expand_as(gt_image)
+    embedding_gt_image = emb(viewpoint_cam_id)
+    envlight_sh, sky_sh = mlp(embedding_gt_image)
+    envlight = EnvironmentLight(base=torch.zeros(25, 3), sh_degree=top["envlight_sh_degree"])
+    envlight.set_base(envlight_sh + noise)
+    pipe = types.SimpleNamespace(compute_cov3D_python=False)
+    background = torch.zeros(3)
+    render_pkg = render(cam, gm, envlight, sky_sh, top["sky_sh_degree"], pipe, background, debug=False,
+                        fix_sky=top["fix_sky"], specular=top["specular"])
+    image, radii = render_pkg["render"], render_pkg["radii"]
+    visibility_filter = render_pkg["visibility_filter"]
+    diff_col, spec_col = render_pkg["diffuse_color"], render_pkg["specular_color"]
+    Ll1 = l1_loss(image, gt_image, mask=occluders_mask)
+    Ssim = (1.0 - ssim(image, gt_image, mask=occluders_mask))
+    loss = Ll1 * (1 - opt.lambda_dssim) + opt.lambda_dssim * Ssim
+    loss_sky_brdf = l1_loss(diff_col, torch.zeros_like(diff_col), mask=1 - sky_m) + \
+        l1_loss(spec_col, torch.zeros_like(spec_col), mask=1 - sky_m)
+    loss = loss + opt.lambda_sky_brdf * loss_sky_brdf
+    assert iteration > opt.reg_normal_from_iter and opt.lambda_normal > 0
+    rendered_normal = render_pkg["normal"] * occluders_mask * sky_m
+    rendered_surf_normal = render_pkg["normal_ref"] * occluders_mask * sky_m
+    ncl = (1 - (rendered_normal * rendered_surf_normal).sum(dim=0))[None]
+    loss = loss + opt.lambda_normal * ncl.mean()
+    torch.manual_seed(4711)
+    loss = loss + envl_sh_loss(envlight_sh, top["envlight_sh_degree"])
+    torch.manual_seed(4711)
+    dirs = torch.empty(10, 3).uniform_(-1, 1)  # the draw envl_sh_loss made (utils/loss_utils.py:188)
+    loss = loss + opt.lambda_scale * min_scale_loss(radii, gm)
+    assert iteration > opt.reg_sky_gauss_depth_from_iter and opt.lambda_sky_gauss > 0
+    loss = loss + opt.lambda_sky_gauss * depth_loss_gaussians(gm, cam, visibility_filter)
+    loss.backward()
+    for n, p in named.items():
+        fx[f"grad/{n}"] = p.grad.numpy().copy()
+    # the rates this step uses: the loop called update_learning_rate(iteration - 1) at the end of
+    # the previous iteration (train.py:159; training_setup made gm.xyz_scheduler_args)
+    model = types.SimpleNamespace(gaussians=gm, optimizer=optimizer)
+    Relightable3DGW.update_learning_rate(model, iteration - 1)
+    fx["it/lrs"] = np.array([g["lr"] for g in optimizer.param_groups], np.float64)
+    optimizer.step()  # train.py:156-159
+    for n, p in named.items():
+        fx[f"after/{n}"] = p.detach().numpy().copy()
+    fx["after/lr_groups"] = np.array([g["name"] for g in optimizer.param_groups])
+    fx["it/loss"] = np.array(float(loss.detach()), np.float64)
+    fx["it/dropout"] = drop.numpy()
+    fx["it/noise"] = noise.numpy()
+    fx["it/dirs"] = dirs.numpy()
+    fx["it/gt"] = gt
+    fx["it/sky_mask"] = sky_mask
+    fx["it/occ_mask"] = occ_mask
+    fx["it/FoVx"] = np.array(fovx)
+    fx["it/FoVy"] = np.array(fovy)
+    fx["it/world_view_transform"] = cam.world_view_transform.numpy()
+    fx["it/full_proj_transform"] = cam.full_proj_transform.numpy()
+    fx["it/camera_center"] = cam.camera_center.numpy()
+    fx["it/radii"] = radii.numpy()
+    np.savez_compressed(os.path.join(OUT, "train_iter.npz"), **fx)
+    print("wrote", os.path.join(OUT, "train_iter.npz"), "loss", float(loss), "visible", int((radii > 0).sum()))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["lr"]:
         lr_schedule()
+    elif sys.argv[1:] == ["iteration"]:
+        iteration()
     else:
         main()
         lr_schedule()
+        iteration()
