@@ -342,7 +342,7 @@ def train_roofline(live, stats, ms_iter, iters_timed_by_events):
         hbm["frac"] = round(hbm["achieved"] / HBM_PEAK_GBS, 5)
     pmc_iter = None
     if ks:
-        n_iter = max(v.get("calls", 0) for k, v in ks.items() if k.startswith("k_adam")) or None
+        n_iter = max((v.get("calls", 0) for k, v in ks.items() if k.startswith("k_adam")), default=0) or None
         if n_iter:
             pmc_iter = sum((v.get("traffic_bytes") or 0) * v["calls"] for v in ks.values()) / n_iter
     it = {"bytes": int(B_iter), "achieved": round(B_iter / (ms_iter * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS,
