@@ -321,7 +321,7 @@ int gsr_ref_forward(GsrRefCtx* ctx, void* stream, int P, int D, int M, const flo
     uint32_t* depth_key = (uint32_t*)(aux + 3 * al(4 * (size_t)P));
     uint2* rect = (uint2*)(aux + 4 * al(4 * (size_t)P));
 
-    gsr::PreprocessArgs pa;
+    gsr::PreprocessArgs pa{};
     memset(&pa, 0, sizeof(pa));
     pa.P = P; pa.D = D; pa.M = M;
     pa.means3D = means3D; pa.scales = scales; pa.scale_modifier = scale_modifier; pa.rotations = rotations;

@@ -565,7 +565,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
 
     unsigned long long* tot_dev = at<unsigned long long>(geom, gl.tot_dev);
 
-    gsr::PreprocessArgs pa;
+    gsr::PreprocessArgs pa{};
     pa.P = P; pa.D = D; pa.M = M;
     pa.means3D = means3D; pa.scales = scales; pa.scale_modifier = scale_modifier; pa.rotations = rotations;
     pa.opacities = opacities; pa.shs = shs; pa.cov3D_precomp = cov3D_precomp; pa.colors_precomp = colors_precomp;

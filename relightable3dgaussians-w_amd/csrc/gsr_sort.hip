@@ -179,7 +179,11 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
     // the load would wait for each load before the ranking starts)
     using AI = typename AuxT<PACK>::in;
     AI aux[AUX ? SORT_ITEMS : 1];
-    volatile uint32_t* wc = wh[wave];
+    // the leader lanes' read-modify-writes of the per-wave counters: volatile, so a lane never
+    // reuses a value another lane has since bumped; typed as LDS, so they are ds_ instructions
+    // and not flat ones (a volatile generic pointer compiles to flat_load/flat_store)
+    volatile __attribute__((address_space(3))) uint32_t* wc =
+        (volatile __attribute__((address_space(3))) uint32_t*)(wh[wave]);
     const uint64_t lt = (lane == 0) ? 0ull : ((~0ull) >> (64 - lane));
     // all loads first (SORT_ITEMS per lane in flight), then the ranking
 #pragma unroll

@@ -132,10 +132,12 @@ CASES = [
     # lists above the heavy-tile thresholds (>= 8192 entries, n_contrib >= 2048): the
     # four-way quadrant split of the tile passes
     dict(name="heavy_tiles", P=70000, W=64, H=48, mode="colors", mutate="thin"),
-    # depths over 12 and 20 octaves (same screen footprints): the depth sort's range-reduced
-    # three-pass path with a large key base, and its four-pass fallback
+    # depths over 12 and 20 octaves (same screen footprints): every byte of the depth keys varies
     dict(name="depth_12_octaves", P=4000, W=96, H=64, mode="colors", mutate="deep12"),
     dict(name="depth_20_octaves", P=4000, W=96, H=64, mode="sh", sh_degree=1, mutate="deep20"),
+    # runs of equal depth keys across many 2048-key sort tiles and chains: the sort's stability
+    # (the reference's (depth, index) order) is all that orders them
+    dict(name="depth_ties", P=40000, W=96, H=64, mode="colors", mutate="ties"),
 ]
 
 
@@ -159,6 +161,8 @@ def mutate(gs, how):
         k = torch.pow(2.0, torch.rand(gs["means3D"].shape[0], 1, generator=g) * float(how[4:]))
         gs["means3D"] *= k
         gs["scales"] *= k
+    elif how == "ties":  # every depth on a 1/4 grid: thousands of Gaussians per depth key
+        gs["means3D"][:, 2] = torch.round(gs["means3D"][:, 2] * 4.0) / 4.0
     elif how == "shift":  # half the cloud left of the frustum, some behind the near plane
         gs["means3D"][:, 0] -= 0.6 * gs["means3D"][:, 2]
         gs["means3D"][: gs["means3D"].shape[0] // 10, 2] = 0.1
