@@ -89,8 +89,9 @@ void launch_digit_scan(int ndigits, uint32_t* table, int nb, uint32_t* digit_tot
 
 // The forward's depth sort of all P keys (stable LSD, 4 passes of 8 bits, values = indices,
 // an 8-B side payload moving along).  The last pass also stores the visible count P_v (the
-// start of the culled keys' top byte 0xFF) to *pv_out.  Returns 1 if the result is in the
-// alt buffers.
+// start of the culled keys' top byte 0xFF) to *pv_out, and does not store the sorted keys
+// (nothing reads them: the values and the payload are the result).  Returns 1 if the result
+// is in the alt buffers.
 size_t depth_sort_temp_bytes(long long P);
 int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* vals, uint32_t* keys_alt,
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,

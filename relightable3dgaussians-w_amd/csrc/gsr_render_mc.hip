@@ -329,8 +329,20 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     }
 }
 
+// occupancy experiments (waves per SIMD the compiler must fit; unset: its own choice)
+#ifdef GSR_MC_FWD_WAVES
+#define GSR_MC_FWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MC_FWD_WAVES, GSR_MC_FWD_WAVES)))
+#else
+#define GSR_MC_FWD_ATTR
+#endif
+#ifdef GSR_MC_BWD_WAVES
+#define GSR_MC_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MC_BWD_WAVES, GSR_MC_BWD_WAVES)))
+#else
+#define GSR_MC_BWD_ATTR
+#endif
+
 template <int NC4, int NCH = 4 * NC4>
-__global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
+__global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
@@ -339,7 +351,7 @@ __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
 }
 
 template <int NC4, int NCH = 4 * NC4, bool DET = false>
-__global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
+__global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row

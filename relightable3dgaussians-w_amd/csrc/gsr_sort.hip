@@ -149,7 +149,8 @@ __device__ __forceinline__ uint2 aux_cvt(uint2 r, uint2*) { return r; }
 __device__ __forceinline__ uint32_t aux_cvt(uint2 r, uint32_t*) { return pack_rect(r); }
 __device__ __forceinline__ uint32_t aux_cvt(uint32_t r, uint32_t*) { return r; }
 
-template <bool AUX, int BITS = 8, int PACK = 0>
+// KOUT false: the sorted keys are not stored (the depth sort's last pass: nothing reads them)
+template <bool AUX, int BITS = 8, int PACK = 0, bool KOUT = true>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, const uint32_t* keys_in,
                                                                   const uint32_t* vals_in, int shift, uint32_t mask,
                                                                   const uint32_t* offsets, const uint32_t* digit_tot,
@@ -258,7 +259,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(long long n, con
             const uint32_t kk = s_keys[p];
             const uint32_t d = (kk >> shift) & mask;
             const uint32_t g = goff[d] + (uint32_t)(p - dstart[d]);
-            keys_out[g] = kk;
+            if constexpr (KOUT) keys_out[g] = kk;
             vals_out[g] = s_vals[p];
             if constexpr (AUX) aux_out[g] = s_aux[p];
         }
@@ -341,14 +342,22 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
         const unsigned zb = (unsigned)((q1 - q0 + per_blk - 1) / per_blk);
         hipLaunchKernelGGL(k_digit_scan, dim3(NB + zb), dim3(SORT_THREADS), 0, s, hist, nb, digit_tot,
                            zb ? reinterpret_cast<float4*>(zero) + q0 : (float4*)nullptr, q1 - q0, NB);
-        unsigned long long* pv = pass == NPASS - 1 ? pv_out : (unsigned long long*)nullptr;
-        if (!pack)
+        const bool lastp = pass == NPASS - 1;
+        unsigned long long* pv = lastp ? pv_out : (unsigned long long*)nullptr;
+        if (!pack && lastp)
+            hipLaunchKernelGGL((k_radix_scatter<true, BITS, 0, false>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin,
+                               shift, mask, hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1, pv);
+        else if (!pack)
             hipLaunchKernelGGL((k_radix_scatter<true, BITS, 0>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
                                mask, hist, digit_tot, nb, out_k[cur], out_v[cur], ain, out_a[cur], 0, 1, pv);
         else if (pass == 0)  // the packed rects (4 B) in the first half of each 8-B buffer
             hipLaunchKernelGGL((k_radix_scatter<true, BITS, 1>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
                                mask, hist, digit_tot, nb, out_k[cur], out_v[cur], ain,
                                reinterpret_cast<uint32_t*>(out_a[cur]), 0, 1, pv);
+        else if (lastp)
+            hipLaunchKernelGGL((k_radix_scatter<true, BITS, 2, false>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin,
+                               shift, mask, hist, digit_tot, nb, out_k[cur], out_v[cur],
+                               reinterpret_cast<const uint32_t*>(ain), reinterpret_cast<uint32_t*>(out_a[cur]), 0, 1, pv);
         else
             hipLaunchKernelGGL((k_radix_scatter<true, BITS, 2>), dim3(nb), dim3(SORT_THREADS), 0, s, P, kin, vin, shift,
                                mask, hist, digit_tot, nb, out_k[cur], out_v[cur], reinterpret_cast<const uint32_t*>(ain),

@@ -1,6 +1,6 @@
 // sort_probe.cpp -- the depth sort (gsr::depth_sort, libgsr.so) on its own against std::stable_sort:
 // random float depth keys with a share of culled keys (0xFFFFFFFF), the rect payload moving along
-// (8-B and packed 4-B), P_v, every output word compared.  Diagnostic tool, not the product.
+// (8-B and packed 4-B), P_v, every sorted id and payload word compared.  Diagnostic tool, not the product.
 //
 //   hipcc --offload-arch=gfx950 -O2 -std=c++17 tools/sort_probe.cpp -I relightable3dgaussians-w_amd/csrc \
 //       -L relightable3dgaussians-w_amd/lib -lgsr -Wl,-rpath,'$ORIGIN/../relightable3dgaussians-w_amd/lib' \
@@ -79,7 +79,7 @@ static int run(long long P, unsigned seed, bool pack, int reps) {
         long long nbad = 0, first = -1;
         for (long long i = 0; i < P; i++) {
             const uint32_t id = order[i];
-            bool ok = gv[i] == id && gk[i] == keys[id];
+            bool ok = gv[i] == id;  // (the last pass does not store the sorted keys)
             if (pack) ok = ok && reinterpret_cast<uint32_t*>(ga.data())[i] == gsr::pack_rect(rect[id]);
             else ok = ok && ga[i].x == rect[id].x && ga[i].y == rect[id].y;
             if (!ok) {
@@ -92,8 +92,8 @@ static int run(long long P, unsigned seed, bool pack, int reps) {
         if (nbad || (long long)gpv != pv_ref) {
             bad = 1;
             if (first >= 0)
-                printf("  at %lld: got (key %08x, id %u), want (key %08x, id %u)\n", first, gk[first], gv[first],
-                       keys[order[first]], order[first]);
+                printf("  at %lld: got id %u, want id %u (key %08x)\n", first, gv[first], order[first],
+                       keys[order[first]]);
         }
     }
     hipFree(dk); hipFree(k0); hipFree(v0); hipFree(k1); hipFree(v1); hipFree(dr); hipFree(a0); hipFree(a1);
