@@ -160,7 +160,11 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
 
 template <int NC4, int NCH = 4 * NC4, bool DET = false>
 __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
+#ifdef GSR_MC_DIAG_NOFEAT  // timing diagnostic only (wrong dL/dfeatures): no feature sums
+    constexpr int V = 6;
+#else
     constexpr int V = 6 + NCH;       // 6 geometric sums + the feature sums
+#endif
     constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
     constexpr int NQ = (NP + 1) / 2;  // after the permlane16 stage: registers reduced by DPP rows
     WaveTile wt;
@@ -289,8 +293,12 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 S2 = __builtin_fmaf(wdx, dx, S2);
                 S3 = __builtin_fmaf(wdx, dy, S3);
                 S4 = __builtin_fmaf(wdy, dy, S4);
+#ifndef GSR_MC_DIAG_NOFEAT
 #pragma unroll
                 for (int c = 0; c < NCH; c++) SF[c] = __builtin_fmaf(dch, dp[q][c], SF[c]);
+#else
+                SF[0] += dch;
+#endif
                 T[q] = Tn;
             }
             if (any) {
@@ -302,7 +310,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 S[4] = S4;
                 S[5] = S5;
 #pragma unroll
-                for (int c = 0; c < NCH; c++) S[6 + c] = SF[c];
+                for (int c = 0; c < V - 6; c++) S[6 + c] = SF[c];
 #pragma unroll
                 for (int c = V; c < 2 * NP; c++) S[c] = 0.f;
                 float Pp[2 * NQ];
