@@ -18,6 +18,8 @@
 // same permlane32 / permlane16 / DPP tree as the 3-channel pass; geometric sums go to the
 // Gaussian's accumulator line, feature sums to dL/dfeatures (one atomic per value per
 // (tile, Gaussian)).
+#include <type_traits>
+
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
@@ -158,45 +160,37 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     }
 }
 
-template <int NC4, int NCH = 4 * NC4, bool DET = false>
-__device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
+// The composite backward's LDS (declared once per kernel: the walks below share it).
+template <int NC4>
+struct McBwdLds {
+    float4 a[64], b[64];
+    float4 f[NC4][64];
+    uint2 q[64];  // (quadrant mask, Gaussian id)
+    TileListLds list;
+};
+
+// The back-to-front walk of one tile over NL channels.  COMPACT: the channels are the tile's
+// live ones (lch[i], i < L; -1 past them), the others have dL/dout == 0 at every pixel of the
+// tile, so every term they would add -- to cdp, to their feature sums -- is exactly zero and
+// is skipped; dpl[q][i] holds dL/dout of channel lch[i].  Otherwise channel i is i (NL = NCH).
+template <int NC4, int NCH, int NL, bool COMPACT, bool DET>
+__device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigned tile, const WaveTile& wt,
+                                            McBwdLds<NC4>& sm, float (&T)[4], const float (&Tb)[4],
+                                            const float (&dpl)[4][NL], const uint32_t (&last)[4],
+                                            const uint32_t (&qlim)[4], const uint32_t nmax, const int (&lch)[NL]) {
 #ifdef GSR_MC_DIAG_NOFEAT  // timing diagnostic only (wrong dL/dfeatures): no feature sums
     constexpr int V = 6;
 #else
-    constexpr int V = 6 + NCH;       // 6 geometric sums + the feature sums
+    constexpr int V = 6 + NL;         // 6 geometric sums + the feature sums
 #endif
     constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
     constexpr int NQ = (NP + 1) / 2;  // after the permlane16 stage: registers reduced by DPP rows
-    WaveTile wt;
-    wt.init(tile, a.grid_x, a.W, a.H);
+    constexpr int NL4 = (NL + 3) / 4;
     const int lane = threadIdx.x;
-    const int HW = a.H * a.W;
-
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
-    __shared__ float4 s_a[64], s_b[64];
-    __shared__ float4 s_f[NC4][64];
-    __shared__ uint2 s_q[64];  // (quadrant mask, Gaussian id)
-    float T[4], Tb[4], dp[4][NCH], Sr[4];  // Sr: the recurrence as in gsr_render_bwd.hip
-    uint32_t last[4], qlim[4];
-    uint32_t nmax = 0;
+    float Sr[4];  // the recurrence as in gsr_render_bwd.hip
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const bool in = wt.inside(q, a.W, a.H);
-        const int pix = in ? wt.pixel(q, a.W) : 0;
-        const float Tf = in ? a.final_T[pix] : 0.f;
-        last[q] = in ? a.n_contrib[pix] : 0u;
-        float bd = 0.f;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            dp[q][c] = (in && c < a.nch) ? a.dL_dout[c * HW + pix] : 0.f;
-            bd = c < a.nch ? __builtin_fmaf(a.bg[c], dp[q][c], bd) : bd;
-        }
-        T[q] = Tf;
-        Tb[q] = -Tf * bd;
-        Sr[q] = 0.f;
-        qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
-        nmax = qlim[q] > nmax ? qlim[q] : nmax;
-    }
+    for (int q = 0; q < 4; q++) Sr[q] = 0.f;
     const int row = lane >> 4, col = lane & 15;
     const int vrow = row == 0 ? 0 : row == 1 ? 2 : row == 2 ? 1 : 3;
     const int vreg = row_sums_t_reg<NQ>(col);  // the register whose row sums this lane ends with
@@ -205,19 +199,26 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
     // values 0-4 carry the opacity; the conic, -1/2 and the screen scale are applied per
     // Gaussian by the preprocess backward (acc_raw), as in gsr_render_bwd.hip
     const bool vop = vidx >= 0 && vidx <= 4;
-    const bool vfeat = vidx >= 6 && vidx - 6 < a.nch;
+    // the channel of this lane's feature sum
+    int fch = vidx - 6;
+    if constexpr (COMPACT) {
+        int c = -1;
+#pragma unroll
+        for (int i = 0; i < NL; i++) c = (vidx - 6 == i) ? lch[i] : c;
+        fch = vidx >= 6 ? c : -1;
+    }
+    const bool vfeat = vidx >= 6 && fch >= 0 && fch < a.nch;
 
     // back to front from the tile's last contributor (as gsr_render_bwd.hip)
     const unsigned sth = st_sth(a.grid_x, a.grid_y);
     const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
-    __shared__ TileListLds s_list;
     TileList<false> tl;
     tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
     for (;;) {
-        tl.fill(s_list);
+        tl.fill(sm.list);
         uint32_t id = 0, ei = 0, p0 = 0;
-        const uint32_t nb = tl.take(s_list, id, ei, p0);
+        const uint32_t nb = tl.take(sm.list, id, ei, p0);
         if (nb == 0) break;
         const uint32_t p = p0 - (uint32_t)lane;
         uint32_t qm = 0;
@@ -234,22 +235,33 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
         wave_lds_sync();
-        s_a[lane] = ra;
-        s_b[lane] = rb;
-        s_q[lane] = make_uint2(qm, id);
+        sm.a[lane] = ra;
+        sm.b[lane] = rb;
+        sm.q[lane] = make_uint2(qm, id);
 #pragma unroll
-        for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
+        for (int g = 0; g < NC4; g++) sm.f[g][lane] = f[g];
+        if constexpr (COMPACT) {
+            // the record's live channels, in order, back into its first NL4 rows (each lane
+            // rewrites only its own column, after reading it: no other lane's data involved)
+            wave_lds_sync();
+            float v[4 * NL4];
+#pragma unroll
+            for (int i = 0; i < 4 * NL4; i++)
+                v[i] = (i < NL && lch[i] >= 0) ? reinterpret_cast<const float*>(&sm.f[lch[i] >> 2][lane])[lch[i] & 3] : 0.f;
+#pragma unroll
+            for (int g = 0; g < NL4; g++) sm.f[g][lane] = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
+        }
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         while (todo) {
             const int k = sgpr_ff1(todo);
             todo = sgpr_clear_bit(todo, k);
-            const float4 A = s_a[k], B = s_b[k];
-            const uint2 Q2 = s_q[k];
-            float F[4 * NC4];
+            const float4 A = sm.a[k], B = sm.b[k];
+            const uint2 Q2 = sm.q[k];
+            float F[4 * NL4];
 #pragma unroll
-            for (int g = 0; g < NC4; g++) {
-                const float4 v = s_f[g][k];
+            for (int g = 0; g < NL4; g++) {
+                const float4 v = sm.f[g][k];
                 F[4 * g] = v.x;
                 F[4 * g + 1] = v.y;
                 F[4 * g + 2] = v.z;
@@ -259,9 +271,9 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
             const uint32_t pos = p0 - (uint32_t)k;
             float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f;
-            float SF[NCH];
+            float SF[NL];
 #pragma unroll
-            for (int c = 0; c < NCH; c++) SF[c] = 0.f;
+            for (int c = 0; c < NL; c++) SF[c] = 0.f;
             bool any = false;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
@@ -279,9 +291,9 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 const float inv = __builtin_amdgcn_rcpf(1.f - ae);
                 const float Tn = T[q] * inv;
                 const float dch = ae * Tn;
-                float cdp = F[0] * dp[q][0];
+                float cdp = F[0] * dpl[q][0];
 #pragma unroll
-                for (int c = 1; c < NCH; c++) cdp = __builtin_fmaf(F[c], dp[q][c], cdp);
+                for (int c = 1; c < NL; c++) cdp = __builtin_fmaf(F[c], dpl[q][c], cdp);
                 const float dcs = cdp - Sr[q];
                 const float dLda = __builtin_fmaf(Tn, dcs, inv * Tb[q]);
                 Sr[q] = __builtin_fmaf(ae, dcs, Sr[q]);
@@ -295,7 +307,7 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 S4 = __builtin_fmaf(wdy, dy, S4);
 #ifndef GSR_MC_DIAG_NOFEAT
 #pragma unroll
-                for (int c = 0; c < NCH; c++) SF[c] = __builtin_fmaf(dch, dp[q][c], SF[c]);
+                for (int c = 0; c < NL; c++) SF[c] = __builtin_fmaf(dch, dpl[q][c], SF[c]);
 #else
                 SF[0] += dch;
 #endif
@@ -326,14 +338,97 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
                 if (DET) {  // the groups run one after another: plain read-modify-write
                     float* prow = a.partial + (size_t)(rbase + pos) * a.pstride;
                     if (vidx >= 0 && vidx < 6) prow[vidx] += v;
-                    else if (vfeat) prow[a.pc0 + vidx] = v;
+                    else if (vfeat) prow[a.pc0 + 6 + fch] = v;
                 } else if (v != 0.f) {
                     const uint32_t gid = Q2.y;
                     if (vidx >= 0 && vidx < 6) atomicAdd(a.acc + (size_t)gid * ACC_STRIDE + vidx, v);
-                    else if (vfeat) atomicAdd(a.dL_dfeat + (size_t)gid * a.fstride + (vidx - 6), v);
+                    else if (vfeat) atomicAdd(a.dL_dfeat + (size_t)gid * a.fstride + fch, v);
                 }
             }
         }
+    }
+}
+
+// GSR_MC_LIVE: 1 -- the backward runs as two launches over the same dispatch order: one walks
+// the tiles whose dL/dout is nonzero in at most MC_NL_SMALL channels, over those channels only
+// (training: the sky-BRDF loss reaches diffuse / specular only on sky pixels, the
+// normal-consistency term the normal and depth channels only off them, and alpha never: 7
+// live channels of 14 off the sky, 9 on it); the other walks the remaining tiles over every
+// channel.  0 (default): one launch, every channel of every tile.
+#ifndef GSR_MC_LIVE
+#define GSR_MC_LIVE 0
+#endif
+#ifndef GSR_MC_NL_SMALL
+#define GSR_MC_NL_SMALL 10
+#endif
+constexpr int MC_NL_SMALL = GSR_MC_NL_SMALL;
+
+// The tile's state (T, the background term, dL/dout, the last contributors), then the walk.
+// CLS < 0: every tile, every channel; CLS == 0: the tiles with more than MC_NL_SMALL live
+// channels, every channel; CLS == MC_NL_SMALL: the other tiles, their live channels only.
+// (Two launches, not one kernel with two walks: the two walks inlined together took 166-213
+// VGPRs against 151, non-inlined 197 + scratch.)
+template <int NC4, int NCH, bool DET, int CLS>
+__device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
+    WaveTile wt;
+    wt.init(tile, a.grid_x, a.W, a.H);
+    const int HW = a.H * a.W;
+    __shared__ McBwdLds<NC4> sm;
+    float T[4], Tb[4], dp[4][NCH];
+    uint32_t last[4], qlim[4];
+    uint32_t nmax = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const bool in = wt.inside(q, a.W, a.H);
+        const int pix = in ? wt.pixel(q, a.W) : 0;
+        const float Tf = in ? a.final_T[pix] : 0.f;
+        last[q] = in ? a.n_contrib[pix] : 0u;
+        float bd = 0.f;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            dp[q][c] = (in && c < a.nch) ? a.dL_dout[c * HW + pix] : 0.f;
+            bd = c < a.nch ? __builtin_fmaf(a.bg[c], dp[q][c], bd) : bd;
+        }
+        T[q] = Tf;
+        Tb[q] = -Tf * bd;
+        qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
+        nmax = qlim[q] > nmax ? qlim[q] : nmax;
+    }
+    if constexpr (CLS >= 0) {
+        // the tile's live channels (wave-uniform)
+        uint32_t live = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; c++)
+            if (__ballot(dp[0][c] != 0.f || dp[1][c] != 0.f || dp[2][c] != 0.f || dp[3][c] != 0.f)) live |= 1u << c;
+        const bool small = __popc(live) <= MC_NL_SMALL;
+        if (small != (CLS == MC_NL_SMALL)) return;  // the other launch's tile
+        if constexpr (CLS == MC_NL_SMALL) {
+            constexpr int NL = MC_NL_SMALL;
+            int lch[NL];
+            uint32_t rest = live;
+#pragma unroll
+            for (int i = 0; i < NL; i++) {
+                lch[i] = rest ? __builtin_ctz(rest) : -1;
+                rest &= rest - 1u;
+            }
+            // dL/dout of the live channels loaded again (L2-hot) rather than selected from dp
+            float dpl[4][NL];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const bool in = wt.inside(q, a.W, a.H);
+                const int pix = in ? wt.pixel(q, a.W) : 0;
+#pragma unroll
+                for (int i = 0; i < NL; i++) dpl[q][i] = (in && lch[i] >= 0) ? a.dL_dout[(size_t)lch[i] * HW + pix] : 0.f;
+            }
+            mc_bwd_walk<NC4, NCH, NL, true, DET>(a, tile, wt, sm, T, Tb, dpl, last, qlim, nmax, lch);
+            return;
+        }
+    }
+    if constexpr (CLS != MC_NL_SMALL) {
+        int lch[NCH];
+#pragma unroll
+        for (int i = 0; i < NCH; i++) lch[i] = i;
+        mc_bwd_walk<NC4, NCH, NCH, false, DET>(a, tile, wt, sm, T, Tb, dp, last, qlim, nmax, lch);
     }
 }
 
@@ -358,12 +453,37 @@ __global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcAr
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
-template <int NC4, int NCH = 4 * NC4, bool DET = false>
+#ifdef GSR_RENDER_STATS
+// timing build (make times): per unit of each composite-backward launch, (start, end)
+// s_memrealtime, (tile | qallow << 20 | launch << 28), the unit's largest n_contrib
+// (tools/mc_bwd_times.py); launch 0 = the only or the few-channel launch, 1 = the other
+constexpr int MCB_UNITS = 1 << 17;
+__device__ unsigned long long g_mcb_times[2][4 * MCB_UNITS];
+extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mcb_times), sizeof(unsigned long long) * 2 * 4 * (size_t)n) == hipSuccess
+               ? 0
+               : -1;
+}
+#endif
+
+template <int NC4, int NCH = 4 * NC4, bool DET = false, int CLS = -1>
 __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row
-    render_bwd_mc_tile<NC4, NCH, DET>(a, tile, qallow);
+#ifdef GSR_RENDER_STATS
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+#endif
+    render_bwd_mc_tile<NC4, NCH, DET, CLS>(a, tile, qallow);
+#ifdef GSR_RENDER_STATS
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)MCB_UNITS) {
+        unsigned long long* r = g_mcb_times[CLS == 0 ? 1 : 0] + 4 * (size_t)blockIdx.x;
+        r[0] = t0;
+        r[1] = __builtin_amdgcn_s_memrealtime();
+        r[2] = tile | ((unsigned long long)qallow << 20) | ((unsigned long long)(CLS == 0 ? 1 : 0) << 28);
+        r[3] = a.tile_nmax[tile];
+    }
+#endif
 }
 
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
@@ -388,8 +508,14 @@ static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s)
         case 2: hipLaunchKernelGGL((k_render_bwd_mc<2, 8, DET>), grid, dim3(64), 0, s, a); break;
         case 3: hipLaunchKernelGGL((k_render_bwd_mc<3, 12, DET>), grid, dim3(64), 0, s, a); break;
         default:
-            if (a.nch == 14) hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET>), grid, dim3(64), 0, s, a);
-            else hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET>), grid, dim3(64), 0, s, a);
+            if (a.nch == 14 && GSR_MC_LIVE && !DET) {  // the few-channel tiles, then the rest
+                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, false, MC_NL_SMALL>), grid, dim3(64), 0, s, a);
+                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, false, 0>), grid, dim3(64), 0, s, a);
+            } else if (a.nch == 14) {
+                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET>), grid, dim3(64), 0, s, a);
+            } else {
+                hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET>), grid, dim3(64), 0, s, a);
+            }
             break;
     }
 }
