@@ -113,7 +113,7 @@ ImgLayout img_layout(int W, int H) {
     L.tile_cost = c.take(4 * T);  // the backward's cost estimate: sum of the quadrants' largest n_contrib
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    L.nheavy = c.take(4 * 16);  // forward [0..8), backward [8..16)
+    L.nheavy = c.take(4 * 32);  // forward [0..8), backward [8..16), the backward's band bounds [16..25)
     L.total = c.o + 256;
     return L;
 }

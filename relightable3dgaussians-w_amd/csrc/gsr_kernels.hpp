@@ -118,6 +118,7 @@ struct TileOrderArgs {
     uint32_t* nheavy;
     int heavy_bits;
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
+    int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
 };
 
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup

@@ -43,12 +43,71 @@ __device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return (heavy
 // One band's order (any block size): order[lo .. lo+len) = the band's tiles, cost buckets
 // descending; nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4
 // ways).  Also zeroes the optional per-tile targets of the forward (tile maxima, summed cost).
+// Cost-balanced band b: the contiguous tile range over which the prefix of cost' = cost + mean / 2
+// crosses b / 8 and (b + 1) / 8 of its total (the half-mean floor bounds a band at 3 ntile / 8
+// tiles: tile_pass_blocks_bal).  Every workgroup of the order launch computes the same bounds
+// (one chunk of tiles per thread, a serial scan of the 512 chunk sums); equal bands when the
+// frame's total cost is 0.
+__device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs& a, unsigned& lo, unsigned& len) {
+    __shared__ unsigned long long s_part[512];
+    __shared__ unsigned long long s_total;
+    __shared__ unsigned s_bound[2];
+    const unsigned n = a.ntile, nt = blockDim.x;
+    const unsigned chunk = (n + nt - 1) / nt;
+    const unsigned b0 = min(n, threadIdx.x * chunk), b1 = min(n, b0 + chunk);
+    unsigned long long sum = 0;
+    for (unsigned t = b0; t < b1; t++) sum += tile_cost(t, a);
+    s_part[threadIdx.x] = sum;
+    if (threadIdx.x < 2) s_bound[threadIdx.x] = threadIdx.x == 0 ? 0u : n;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long run = 0;
+        for (unsigned i = 0; i < nt; i++) {
+            const unsigned long long v = s_part[i];
+            s_part[i] = run;
+            run += v;
+        }
+        s_total = run;
+    }
+    __syncthreads();
+    const unsigned long long total = s_total;
+    if (total == 0) {
+        band_of(band, n, lo, len);
+        return;
+    }
+    const unsigned long long add = total / (2ull * n) > 0 ? total / (2ull * n) : 1ull;
+    const unsigned long long tp = total + add * n;
+    const unsigned long long tlo = band * tp / 8, thi = (band + 1) * tp / 8;
+    // the tile whose cost' interval (p, p + cost'] holds a target ends the band before the boundary
+    unsigned long long p = s_part[threadIdx.x] + (unsigned long long)b0 * add;
+    for (unsigned t = b0; t < b1; t++) {
+        const unsigned long long q = p + tile_cost(t, a) + add;
+        if (band > 0 && p < tlo && tlo <= q) s_bound[0] = t + 1;
+        if (band < 7 && p < thi && thi <= q) s_bound[1] = t + 1;
+        p = q;
+    }
+    __syncthreads();
+    lo = s_bound[0];
+    len = s_bound[1] - s_bound[0];
+}
+
+// BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning
+// scatter's order workgroups carry none of its LDS)
+template <bool BAL = false>
 __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderArgs& a) {
     __shared__ uint32_t hist[NBUCKET];
     __shared__ uint32_t cur[NBUCKET];
     __shared__ uint32_t scan[512];
     unsigned lo, len;
-    band_of(band, a.ntile, lo, len);
+    if constexpr (BAL) {
+        balanced_band(band, a, lo, len);
+        if (threadIdx.x == 0) {
+            a.nheavy[8 + band] = lo;
+            if (band == 7) a.nheavy[16] = lo + len;
+        }
+    } else {
+        band_of(band, a.ntile, lo, len);
+    }
     for (int i = threadIdx.x; i < NBUCKET; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {

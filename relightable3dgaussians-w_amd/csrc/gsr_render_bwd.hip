@@ -243,7 +243,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
 k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
+        return;  // det: one writer per row
     render_bwd_tile<DET>(a, tile, qallow);
 }
 
@@ -265,7 +266,7 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    const dim3 grid(tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }

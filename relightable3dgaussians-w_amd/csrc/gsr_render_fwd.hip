@@ -67,6 +67,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
+    uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
         tl.fill(s_list);
         uint32_t id = 0, ei = 0, p0 = 0;
@@ -102,6 +103,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         uint64_t todo = todo0;
         auto blend_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
+            nev += (uint32_t)__popc(m);
             // the list position + 1 in a VGPR once per survivor (the selects below cannot read
             // it from an SGPR beside their SGPR mask: one constant-bus read per VOP3 on gfx950)
             uint32_t pos1;
@@ -200,7 +202,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     if (lane == 0 && nm) {
         atomicMax(&a.tile_nmax[tile], nm);
         atomicMax(&a.tile_emax[tile], elast + 1u);
-        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nsum);
+        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
     }
 }
 

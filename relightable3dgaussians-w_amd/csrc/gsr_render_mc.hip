@@ -56,6 +56,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         if (((qallow >> q) & 1u) && __ballot(in)) live |= 1u << q;
     }
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere
+    uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
         tl.fill(s_list);
         uint32_t id = 0, ei = 0, p0 = 0;
@@ -93,6 +94,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
 #pragma unroll
             for (int g = 0; g < NC4; g++) F[g] = s_f[g][k];
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[k]) & live;
+            nev += (uint32_t)__popc(m);
             const uint32_t pos1 = p0 + (uint32_t)k + 1u;
             lmask blended = 0;
 #pragma unroll
@@ -155,7 +157,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         if (lane == 0 && nm) {
             atomicMax(&a.tile_nmax[tile], nm);
             atomicMax(&a.tile_emax[tile], elast + 1u);
-            if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nsum);
+            if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
         }
     }
 }
@@ -470,7 +472,8 @@ template <int NC4, int NCH = 4 * NC4, bool DET = false, int CLS = -1>
 __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT)) return;  // det: one writer per row
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
+        return;  // det: one writer per row
 #ifdef GSR_RENDER_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -523,7 +526,7 @@ static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s)
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) launch_bwd_mc<true>(a, grid, s);
     else launch_bwd_mc<false>(a, grid, s);
 }

@@ -15,11 +15,13 @@
 
 namespace gsr {
 
-__global__ void __launch_bounds__(512) k_tile_order(TileOrderArgs a) { tile_order_band(blockIdx.x, a); }
+template <bool BAL>
+__global__ void __launch_bounds__(512) k_tile_order(TileOrderArgs a) { tile_order_band<BAL>(blockIdx.x, a); }
 
 void launch_tile_order_args(const TileOrderArgs& a, hipStream_t s) {
     if (a.ntile == 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(512), 0, s, a);
+    if (a.balance) hipLaunchKernelGGL(k_tile_order<true>, dim3(8), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(k_tile_order<false>, dim3(8), dim3(512), 0, s, a);
 }
 
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
@@ -27,7 +29,9 @@ void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost
     if (ntile == 0) return;
     TileOrderArgs a{};
     a.ntile = ntile; a.ranges = ranges; a.cost = cost; a.order = order; a.nheavy = nheavy; a.heavy_bits = heavy_bits;
-    hipLaunchKernelGGL(k_tile_order, dim3(8), dim3(512), 0, s, a);
+    a.balance = GSR_BAL_BANDS;  // the backward passes' bands (tile_unit ... bal)
+    if (a.balance) hipLaunchKernelGGL(k_tile_order<true>, dim3(8), dim3(512), 0, s, a);
+    else hipLaunchKernelGGL(k_tile_order<false>, dim3(8), dim3(512), 0, s, a);
 }
 
 }  // namespace gsr

@@ -34,13 +34,26 @@ constexpr unsigned HEAVY_CAP = 64;  // split heavy tiles per band
 #ifndef GSR_BWD_TAIL
 #define GSR_BWD_TAIL 0
 #endif
+// The backward's per-tile cost estimate (its dispatch order, heaviest first), written by the
+// forward: 1 -- the forward's (survivor, quadrant) evaluations, 0 -- the sum of the quadrants'
+// largest n_contrib
+#ifndef GSR_EVAL_COST
+#define GSR_EVAL_COST 0
+#endif
 constexpr unsigned FWD_TAIL_SPLIT = GSR_FWD_TAIL;  // split tail tiles per band, forward passes
 constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
+// bal: the bands are the cost-balanced ranges k_tile_order stored after the band counts
+// (nheavy[8 + b] = band b's first tile, nheavy[16] = ntile; GSR_BAL_BANDS); else equal bands.
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
-                                          unsigned& tile, uint32_t& qallow, unsigned ntail) {
+                                          unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false) {
     const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
     unsigned lo, len;
-    band_of(band, ntile, lo, len);
+    if (bal) {
+        lo = nheavy[8 + band];
+        len = nheavy[9 + band] - lo;
+    } else {
+        band_of(band, ntile, lo, len);
+    }
     const unsigned h = min(min(nheavy[band], HEAVY_CAP), len);
     const unsigned t = min(ntail, len - h);
     const unsigned whole = len - h - t;
@@ -64,6 +77,15 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
 __host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned ntail) {
     return 8u * ((ntile + 7u) / 8u + 3u * HEAVY_CAP + 3u * ntail);
 }
+// the same with cost-balanced bands: a band holds at most 3 ntile / 8 tiles (tile_order_band)
+__host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsigned ntail) {
+    return 8u * (3u * ((ntile + 7u) / 8u) + 3u * HEAVY_CAP + 3u * ntail);
+}
+// The backward passes' bands: 1 -- cost-balanced (each band a contiguous tile range holding an
+// eighth of the tiles' estimated cost), 0 -- equal tile counts
+#ifndef GSR_BAL_BANDS
+#define GSR_BAL_BANDS 0
+#endif
 // LDS ordering within one wave (the tile passes' waves share no LDS)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -35,6 +35,9 @@ def main():
         torch.cuda.synchronize()
         buf = np.zeros((2, UNITS, 4), np.uint64)
         assert L.gsr_debug_mcb_times(buf.ctypes.data, UNITS) == 0
+        dump = os.environ.get("GSR_STATS_DUMP")
+        if dump:  # raw records for offline analysis (row = the launch's blockIdx)
+            np.save(f"{dump}_{it}.npy", buf)
         for launch in range(2):
             t = buf[launch].astype(np.int64)
             ok = t[:, 1] > 0
