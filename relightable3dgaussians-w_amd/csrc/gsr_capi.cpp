@@ -63,7 +63,7 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, order_fwd, order_bwd, nheavy, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -111,6 +111,7 @@ ImgLayout img_layout(int W, int H) {
     L.tile_nmax = c.take(4 * T);
     L.tile_emax = c.take(4 * T);
     L.tile_cost = c.take(4 * T);  // the backward's cost estimate: sum of the quadrants' largest n_contrib
+    L.row_cost = c.take(4 * (size_t)tiles_y(H));  // the same per tile row (the backward's balanced bands)
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
     L.nheavy = c.take(4 * 32);  // forward [0..8), backward [8..16), the backward's band bounds [16..25)
@@ -662,6 +663,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.nheavy = at<uint32_t>(img, il.nheavy); ord.heavy_bits = gsr::FWD_HEAVY_BITS;
         ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
+        ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, rect_packed, gsx, st_h(width, height), NS,
@@ -710,6 +712,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
+    ra.row_cost = at<uint32_t>(img, il.row_cost);
     // the forward tile pass over the binning in `bin`; its workgroups also zero the backward's
     // accumulator lines (zero_slice; the depth sort's digit scans did it up to round 3)
     ra.zero = reinterpret_cast<float4*>(at<float>(geom, gl.acc));
@@ -726,6 +729,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                 gsr::RenderMcArgs ma = mc_args(ra.W, ra.H, gx, gy, gsx, ra.st_ranges, ra.ent, pa.rec, ra.order,
                                                ra.nheavy, ra.tile_nmax, ra.tile_emax, *mc, c0);
                 ma.tile_cost = ra.tile_cost;
+                ma.row_cost = ra.row_cost;
                 ma.out = mc->out + (size_t)c0 * width * height;
                 if (c0 == 0) {  // the other groups would write the same values
                     ma.final_T = ra.final_T;
@@ -946,7 +950,8 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         {
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
-                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s);  // det: one writer per row
+                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s,  // det: one writer per row
+                                   at<uint32_t>(img, il.row_cost), gy);
         }
         {
             GSR_STAGE(ST_RENDER_BWD);  // the tile pass alone (roofline.avg_launch_ms in bench.py)

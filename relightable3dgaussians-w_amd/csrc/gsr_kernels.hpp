@@ -119,6 +119,11 @@ struct TileOrderArgs {
     int heavy_bits;
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
+    // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
+    // forward's order for its tile pass to raise (zero_rows); nrows = tile rows
+    const uint32_t* row_cost;
+    uint32_t* zero_rows;
+    unsigned nrows;
 };
 
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
@@ -183,8 +188,9 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
 // order: per XCD band of tiles (xcd_remap bands), heaviest first by log2 of `cost` (or of
 // the tile's list length when cost is null); nheavy[8]: per band, the leading tiles with
 // cost >= 2^heavy_bits.
+// row_cost [nrows] (optional): the forward's summed cost per tile row (the balanced bands)
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s);
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0);
 
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
@@ -208,6 +214,7 @@ struct RenderFwdArgs {
     uint32_t* tile_nmax;  // out: per tile, the largest n_contrib (the backward's cost; atomicMax, zeroed)
     uint32_t* tile_emax;  // out: per tile, 1 + the entry index of that last contributor (where the backward starts)
     uint32_t* tile_cost;  // out (when non-null): per tile, the sum of its quadrants' largest n_contrib (atomicAdd, zeroed)
+    uint32_t* row_cost;   // out (when non-null): the same summed per tile row (the backward's balanced bands)
     // when non-null: zero_n4 float4s the backward needs zeroed (the gradient accumulator lines),
     // cleared by the pass's workgroups a slice each (zero_slice): VALU-bound waves have the HBM
     // write bandwidth to spare
@@ -260,6 +267,7 @@ struct RenderMcArgs {
     uint32_t* n_contrib;
     uint32_t* tile_nmax;  // forward: atomicMax when non-null
     uint32_t* tile_cost;  // forward: atomicAdd of the quadrants' largest n_contrib when non-null
+    uint32_t* row_cost;   // forward: the same per tile row when non-null
     const uint32_t* order;
     const uint32_t* nheavy;
     const float* dL_dout;  // backward: [nch][H][W]

@@ -1,6 +1,7 @@
 // gsr_order.hpp -- a tile pass's dispatch order for one XCD band (k_tile_order in
 // gsr_schedule.hip, or extra workgroups of the binning scatter in gsr_binning.hip).
 #pragma once
+#include "gsr_block.hpp"
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
@@ -43,52 +44,43 @@ __device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return (heavy
 // One band's order (any block size): order[lo .. lo+len) = the band's tiles, cost buckets
 // descending; nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4
 // ways).  Also zeroes the optional per-tile targets of the forward (tile maxima, summed cost).
-// Cost-balanced band b: the contiguous tile range over which the prefix of cost' = cost + mean / 2
-// crosses b / 8 and (b + 1) / 8 of its total (the half-mean floor bounds a band at 3 ntile / 8
-// tiles: tile_pass_blocks_bal).  Every workgroup of the order launch computes the same bounds
-// (one chunk of tiles per thread, a serial scan of the 512 chunk sums); equal bands when the
-// frame's total cost is 0.
+// Cost-balanced band b: whole tile rows, the contiguous range over which the prefix of the row
+// costs' (row cost + mean / 2) crosses b / 8 and (b + 1) / 8 of their total (the half-mean
+// floor bounds a band at 3/8 of the rows: tile_pass_blocks_bal).  The forward's tile pass sums
+// the rows' costs (row_cost), so every workgroup of the order launch computes the same bounds
+// from a few hundred words: one row per thread, a workgroup scan.  Equal bands when the
+// frame's total cost is 0 or no row costs exist.  (Balancing tile by tile from every tile's
+// cost made the order launch 10-37 us longer: it read all the tiles' costs in every
+// workgroup.)
 __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs& a, unsigned& lo, unsigned& len) {
-    __shared__ unsigned long long s_part[512];
-    __shared__ unsigned long long s_total;
+    __shared__ unsigned long long s_scan[16];
     __shared__ unsigned s_bound[2];
-    const unsigned n = a.ntile, nt = blockDim.x;
-    const unsigned chunk = (n + nt - 1) / nt;
-    const unsigned b0 = min(n, threadIdx.x * chunk), b1 = min(n, b0 + chunk);
-    unsigned long long sum = 0;
-    for (unsigned t = b0; t < b1; t++) sum += tile_cost(t, a);
-    s_part[threadIdx.x] = sum;
-    if (threadIdx.x < 2) s_bound[threadIdx.x] = threadIdx.x == 0 ? 0u : n;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long run = 0;
-        for (unsigned i = 0; i < nt; i++) {
-            const unsigned long long v = s_part[i];
-            s_part[i] = run;
-            run += v;
-        }
-        s_total = run;
+    const unsigned n = a.nrows, gx = n ? a.ntile / n : 0u;
+    if (!a.row_cost || n == 0 || n > blockDim.x || gx * n != a.ntile) {
+        band_of(band, a.ntile, lo, len);
+        return;
     }
-    __syncthreads();
-    const unsigned long long total = s_total;
+    const unsigned r = threadIdx.x;
+    const unsigned long long c = r < n ? a.row_cost[r] : 0ull;
+    if (threadIdx.x < 2) s_bound[threadIdx.x] = threadIdx.x == 0 ? 0u : n;
+    unsigned long long total;
+    const unsigned long long before = block_exclusive_scan<8>(c, s_scan, &total);  // 512 threads = 8 waves
     if (total == 0) {
-        band_of(band, n, lo, len);
+        band_of(band, a.ntile, lo, len);
         return;
     }
     const unsigned long long add = total / (2ull * n) > 0 ? total / (2ull * n) : 1ull;
     const unsigned long long tp = total + add * n;
     const unsigned long long tlo = band * tp / 8, thi = (band + 1) * tp / 8;
-    // the tile whose cost' interval (p, p + cost'] holds a target ends the band before the boundary
-    unsigned long long p = s_part[threadIdx.x] + (unsigned long long)b0 * add;
-    for (unsigned t = b0; t < b1; t++) {
-        const unsigned long long q = p + tile_cost(t, a) + add;
-        if (band > 0 && p < tlo && tlo <= q) s_bound[0] = t + 1;
-        if (band < 7 && p < thi && thi <= q) s_bound[1] = t + 1;
-        p = q;
+    // the row whose cost' interval (p, p + cost'] holds a target ends the band before the boundary
+    if (r < n) {
+        const unsigned long long p = before + (unsigned long long)r * add, q = p + c + add;
+        if (band > 0 && p < tlo && tlo <= q) s_bound[0] = r + 1;
+        if (band < 7 && p < thi && thi <= q) s_bound[1] = r + 1;
     }
     __syncthreads();
-    lo = s_bound[0];
-    len = s_bound[1] - s_bound[0];
+    lo = s_bound[0] * gx;
+    len = (s_bound[1] - s_bound[0]) * gx;
 }
 
 // BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning
@@ -109,6 +101,8 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
         band_of(band, a.ntile, lo, len);
     }
     for (int i = threadIdx.x; i < NBUCKET; i += blockDim.x) hist[i] = 0;
+    if (a.zero_rows && band == 0)
+        for (unsigned i = threadIdx.x; i < a.nrows; i += blockDim.x) a.zero_rows[i] = 0u;
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
         const unsigned t = lo + i;

@@ -203,6 +203,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         atomicMax(&a.tile_nmax[tile], nm);
         atomicMax(&a.tile_emax[tile], elast + 1u);
         if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
+        if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], GSR_EVAL_COST ? nev : nsum);
     }
 }
 

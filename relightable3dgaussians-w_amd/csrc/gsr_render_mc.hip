@@ -158,6 +158,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
             atomicMax(&a.tile_nmax[tile], nm);
             atomicMax(&a.tile_emax[tile], elast + 1u);
             if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
+            if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], GSR_EVAL_COST ? nev : nsum);
         }
     }
 }
@@ -461,10 +462,14 @@ __global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcAr
 // (tools/mc_bwd_times.py); launch 0 = the only or the few-channel launch, 1 = the other
 constexpr int MCB_UNITS = 1 << 17;
 __device__ unsigned long long g_mcb_times[2][4 * MCB_UNITS];
-extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mcb_times), sizeof(unsigned long long) * 2 * 4 * (size_t)n) == hipSuccess
-               ? 0
-               : -1;
+extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_mcb_times), sizeof(unsigned long long) * 2 * 4 * (size_t)n) != hipSuccess)
+        return -1;
+    if (reset) {  // the next launches' units then leave no stale records (their block -> unit map varies)
+        static unsigned long long zeros[2 * 4 * MCB_UNITS];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_mcb_times), zeros, sizeof(zeros)) != hipSuccess) return -1;
+    }
+    return 0;
 }
 #endif
 

@@ -81,8 +81,8 @@ __host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned
 __host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsigned ntail) {
     return 8u * (3u * ((ntile + 7u) / 8u) + 3u * HEAVY_CAP + 3u * ntail);
 }
-// The backward passes' bands: 1 -- cost-balanced (each band a contiguous tile range holding an
-// eighth of the tiles' estimated cost), 0 -- equal tile counts
+// The backward passes' bands: 1 -- cost-balanced (each band a contiguous range of tile rows
+// holding an eighth of the rows' estimated cost), 0 (default) -- equal tile counts
 #ifndef GSR_BAL_BANDS
 #define GSR_BAL_BANDS 0
 #endif

@@ -28,13 +28,15 @@ def main():
     scene, views, gts = train.synthetic_relit_scene(1_363_637, 4, 1920, 1080, 1400.0, dev, seed=0)
     scene.iteration = train.REG_NORMAL_FROM_ITER
     L = _lib.lib()
-    L.gsr_debug_mcb_times.argtypes = [C.c_void_p, C.c_int]
+    L.gsr_debug_mcb_times.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    scratch = np.zeros((2, UNITS, 4), np.uint64)  # (kept alive across the call)
+    L.gsr_debug_mcb_times(scratch.ctypes.data, UNITS, 1)  # start clean
     for it in range(iters):
         # one view per step, so the records hold that view's launches only
         train.train_step(scene, views, [it % 4], gts)
         torch.cuda.synchronize()
         buf = np.zeros((2, UNITS, 4), np.uint64)
-        assert L.gsr_debug_mcb_times(buf.ctypes.data, UNITS) == 0
+        assert L.gsr_debug_mcb_times(buf.ctypes.data, UNITS, 1) == 0
         dump = os.environ.get("GSR_STATS_DUMP")
         if dump:  # raw records for offline analysis (row = the launch's blockIdx)
             np.save(f"{dump}_{it}.npy", buf)
