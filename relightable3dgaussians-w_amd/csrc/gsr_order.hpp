@@ -44,43 +44,73 @@ __device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return (heavy
 // One band's order (any block size): order[lo .. lo+len) = the band's tiles, cost buckets
 // descending; nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4
 // ways).  Also zeroes the optional per-tile targets of the forward (tile maxima, summed cost).
-// Cost-balanced band b: whole tile rows, the contiguous range over which the prefix of the row
-// costs' (row cost + mean / 2) crosses b / 8 and (b + 1) / 8 of their total (the half-mean
-// floor bounds a band at 3/8 of the rows: tile_pass_blocks_bal).  The forward's tile pass sums
-// the rows' costs (row_cost), so every workgroup of the order launch computes the same bounds
-// from a few hundred words: one row per thread, a workgroup scan.  Equal bands when the
-// frame's total cost is 0 or no row costs exist.  (Balancing tile by tile from every tile's
-// cost made the order launch 10-37 us longer: it read all the tiles' costs in every
-// workgroup.)
+// Cost-balanced band b: the contiguous tile range over which the prefix of cost' = cost + a
+// floor (half the mean tile cost, rounded up) crosses b / 8 and (b + 1) / 8 of its total (the floor bounds
+// a band at 3 ntile / 8 + 2 tiles: tile_pass_blocks_bal).  The forward's tile pass also sums the
+// costs per tile row (row_cost), so every workgroup of the order launch finds its two
+// boundaries cheaply: a workgroup scan over the rows finds the row holding each boundary, a
+// second over that row's tiles the tile.  Equal bands when the frame's total cost is 0 or no
+// row costs exist.  (Reading every tile's cost in every workgroup made the launch 10-37 us
+// longer; whole-row bounds balanced too coarsely.)
 __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs& a, unsigned& lo, unsigned& len) {
     __shared__ unsigned long long s_scan[16];
-    __shared__ unsigned s_bound[2];
+    __shared__ unsigned long long s_rowp[2];  // cost' before the boundary rows
+    __shared__ unsigned s_row[2], s_bound[2];
     const unsigned n = a.nrows, gx = n ? a.ntile / n : 0u;
-    if (!a.row_cost || n == 0 || n > blockDim.x || gx * n != a.ntile) {
+    if (!a.row_cost || n == 0 || n > blockDim.x || gx > blockDim.x || gx * n != a.ntile) {
         band_of(band, a.ntile, lo, len);
         return;
     }
     const unsigned r = threadIdx.x;
     const unsigned long long c = r < n ? a.row_cost[r] : 0ull;
-    if (threadIdx.x < 2) s_bound[threadIdx.x] = threadIdx.x == 0 ? 0u : n;
+    if (threadIdx.x < 2) {
+        s_row[threadIdx.x] = 0xffffffffu;
+        s_bound[threadIdx.x] = threadIdx.x == 0 ? (band > 0 ? 0xffffffffu : 0u) : (band < 7 ? 0xffffffffu : a.ntile);
+    }
     unsigned long long total;
     const unsigned long long before = block_exclusive_scan<8>(c, s_scan, &total);  // 512 threads = 8 waves
     if (total == 0) {
         band_of(band, a.ntile, lo, len);
         return;
     }
-    const unsigned long long add = total / (2ull * n) > 0 ? total / (2ull * n) : 1ull;
-    const unsigned long long tp = total + add * n;
-    const unsigned long long tlo = band * tp / 8, thi = (band + 1) * tp / 8;
-    // the row whose cost' interval (p, p + cost'] holds a target ends the band before the boundary
+    // the per-tile floor, rounded up so that total <= 2 ntile add: a band's tiles then number at
+    // most 3 ntile / 8 + 2 (tile_pass_blocks_bal)
+    const unsigned long long add = (total + 2ull * a.ntile - 1) / (2ull * a.ntile);
+    const unsigned long long tp = total + add * a.ntile;
+    const unsigned long long tgt[2] = {band * tp / 8, (band + 1) * tp / 8};
+    const bool need[2] = {band > 0, band < 7};
+    // the row whose cost' interval (p, p + cost'] holds each target
     if (r < n) {
-        const unsigned long long p = before + (unsigned long long)r * add, q = p + c + add;
-        if (band > 0 && p < tlo && tlo <= q) s_bound[0] = r + 1;
-        if (band < 7 && p < thi && thi <= q) s_bound[1] = r + 1;
+        const unsigned long long p = before + (unsigned long long)r * gx * add, q = p + c + gx * add;
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            if (need[k] && p < tgt[k] && tgt[k] <= q) {
+                s_row[k] = r;
+                s_rowp[k] = p;
+            }
     }
     __syncthreads();
-    lo = s_bound[0] * gx;
-    len = (s_bound[1] - s_bound[0]) * gx;
+    // the tile of that row whose cost' interval holds it: the band boundary follows it
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        if (!need[k]) continue;  // workgroup-uniform
+        const unsigned row = s_row[k];
+        const unsigned long long ct =
+            (row < n && threadIdx.x < gx) ? a.cost[(size_t)row * gx + threadIdx.x] + add : 0ull;
+        unsigned long long rt;
+        const unsigned long long bt = block_exclusive_scan<8>(ct, s_scan, &rt);
+        if (row < n && threadIdx.x < gx) {
+            const unsigned long long p = s_rowp[k] + bt, q = p + ct;
+            if (p < tgt[k] && tgt[k] <= q) s_bound[k] = row * gx + threadIdx.x + 1;
+        }
+    }
+    __syncthreads();
+    if (s_bound[0] == 0xffffffffu || s_bound[1] == 0xffffffffu) {  // a boundary not found: costs inconsistent
+        band_of(band, a.ntile, lo, len);
+        return;
+    }
+    lo = s_bound[0];
+    len = s_bound[1] - s_bound[0];
 }
 
 // BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning

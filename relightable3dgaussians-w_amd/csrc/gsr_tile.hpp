@@ -77,14 +77,14 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
 __host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned ntail) {
     return 8u * ((ntile + 7u) / 8u + 3u * HEAVY_CAP + 3u * ntail);
 }
-// the same with cost-balanced bands: a band holds at most 3 ntile / 8 tiles (tile_order_band)
+// the same with cost-balanced bands: a band holds at most 3 ntile / 8 + 2 tiles (balanced_band)
 __host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsigned ntail) {
-    return 8u * (3u * ((ntile + 7u) / 8u) + 3u * HEAVY_CAP + 3u * ntail);
+    return 8u * (3u * ((ntile + 7u) / 8u) + 2u + 3u * HEAVY_CAP + 3u * ntail);
 }
-// The backward passes' bands: 1 -- cost-balanced (each band a contiguous range of tile rows
-// holding an eighth of the rows' estimated cost), 0 (default) -- equal tile counts
+// The backward passes' bands: 1 (default) -- cost-balanced (each band a contiguous tile range
+// holding an eighth of the estimated cost: balanced_band), 0 -- equal tile counts
 #ifndef GSR_BAL_BANDS
-#define GSR_BAL_BANDS 0
+#define GSR_BAL_BANDS 1
 #endif
 // LDS ordering within one wave (the tile passes' waves share no LDS)
 __device__ __forceinline__ void wave_lds_sync() {
