@@ -75,7 +75,7 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     }
     // the per-tile floor, rounded up so that total <= 2 ntile add: a band's tiles then number at
     // most 3 ntile / 8 + 2 (tile_pass_blocks_bal)
-    const unsigned long long add = (total + 2ull * a.ntile - 1) / (2ull * a.ntile);
+    const unsigned long long add = (total + GSR_BAL_FLOOR_DIV * a.ntile - 1) / (GSR_BAL_FLOOR_DIV * a.ntile);
     const unsigned long long tp = total + add * a.ntile;
     const unsigned long long tgt[2] = {band * tp / 8, (band + 1) * tp / 8};
     const bool need[2] = {band > 0, band < 7};

@@ -86,6 +86,11 @@ __host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsi
 #ifndef GSR_BAL_BANDS
 #define GSR_BAL_BANDS 1
 #endif
+// the balanced bands' per-tile floor: the mean tile cost / GSR_BAL_FLOOR_DIV (1 or 2; the grid
+// bound of tile_pass_blocks_bal holds for both)
+#ifndef GSR_BAL_FLOOR_DIV
+#define GSR_BAL_FLOOR_DIV 2ull
+#endif
 // LDS ordering within one wave (the tile passes' waves share no LDS)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
