@@ -375,6 +375,10 @@ typedef struct gsr_layout {
     size_t geom_radii, geom_tiles, geom_depth_key, geom_rect, geom_rec, geom_acc;
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_nmax, img_tile_emax;
     size_t bin_st_ranges, bin_entries;
+    /* the backward's dispatch order (appended in round 4): the forward's per-tile cost estimate
+     * [T] and its per-tile-row sums [tiles_y], the order [T], and the band table (u32 [32]:
+     * forward band heavy counts [0..8), backward [8..16), backward band bounds [16..25)) */
+    size_t img_tile_cost, img_row_cost, img_order_bwd, img_nheavy;
 } gsr_layout;
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
 

@@ -524,6 +524,10 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     out->img_tile_emax = im.tile_emax;
     out->bin_st_ranges = b.st_ranges;
     out->bin_entries = b.ent;
+    out->img_tile_cost = im.tile_cost;
+    out->img_row_cost = im.row_cost;
+    out->img_order_bwd = im.order_bwd;
+    out->img_nheavy = im.nheavy;
     return GSR_OK;
 }
 

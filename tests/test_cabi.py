@@ -38,6 +38,12 @@ def test_layout_query_is_consistent():
     assert L.geom_bytes > 1000 * (48 + 64) and L.bin_bytes >= 8 * 255 and L.img_bytes >= 1920 * 1080 * 8
     for off in (L.geom_rec, L.geom_acc, L.img_ranges, L.bin_st_ranges, L.bin_entries):
         assert off % 256 == 0
+    # the backward's order buffers (appended fields): disjoint, in order, inside the image buffer
+    T, gy = 120 * 68, 68
+    spans = [(L.img_tile_cost, 4 * T), (L.img_row_cost, 4 * gy), (L.img_order_bwd, 4 * T), (L.img_nheavy, 4 * 32)]
+    for (a, n), (b, _) in zip(spans, spans[1:]):
+        assert a + n <= b
+    assert spans[-1][0] + spans[-1][1] <= L.img_bytes
 
 
 def test_cpu_tensors_are_rejected():

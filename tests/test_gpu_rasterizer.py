@@ -138,6 +138,11 @@ CASES = [
     # runs of equal depth keys across many 2048-key sort tiles and chains: the sort's stability
     # (the reference's (depth, index) order) is all that orders them
     dict(name="depth_ties", P=40000, W=96, H=64, mode="colors", mutate="ties"),
+    # more than 512 tiles per row / tile rows: the backward's cost-balanced bands fall back to
+    # equal bands (balanced_band scans one row or one row's tiles per thread of a 512-thread
+    # workgroup)
+    dict(name="wide_strip_520_tiles", P=3000, W=8320, H=40, mode="colors"),
+    dict(name="tall_strip_520_rows", P=3000, W=40, H=8320, mode="sh", sh_degree=1),
 ]
 
 
