@@ -138,3 +138,24 @@ def test_channels_bad_arguments():
     with pytest.raises(Exception):
         dgr.GaussianRasterizer(s).render_channels(means3D=g["means3D"], means2D=g["means3D"],
                                                   opacities=g["opacities"], colors=[g["means3D"]])
+
+
+@pytest.mark.parametrize("W,H", [(640, 360), (8320, 40), (40, 8320)], ids=["640x360", "wide_520_tiles", "tall_520_rows"])
+def test_channels_frame_shapes(W, H):
+    """render()'s 14-channel layout on a frame with cost-balanced backward bands (640x360) and on
+    strips of more than 512 tiles per row / tile rows, where the bands fall back to equal tile
+    counts (gsr_order.hpp balanced_band)."""
+    dgr, g, s = _setup(P=6000, W=W, H=H, seed=7, camera="identity")
+    P = g["means3D"].shape[0]
+    ks = (3, 3, 3, 1, 3, 1)
+    cols = _colour_sets(P, ks, seed=6)
+    gen = torch.Generator(device="cuda").manual_seed(8)
+    bgs = [torch.rand(k, device="cuda", generator=gen) for k in ks]
+    weights = [torch.randn(k, H, W, device="cuda", generator=gen) for k in ks]
+    imgs_s, radii_s, grads_s, cg_s = _separate(dgr, g, s, cols, bgs, weights)
+    imgs_m, radii_m, grads_m, cg_m = _multi(dgr, g, s, cols, bgs, weights)
+    assert torch.equal(radii_m, radii_s)
+    for a, b in zip(imgs_m, imgs_s):
+        assert torch.equal(a, b)
+    for a, b in zip(cg_m + grads_m, cg_s + grads_s):
+        assert _rel(a, b) < 1e-5
