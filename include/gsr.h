@@ -113,8 +113,11 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
 /* Backward rasterization.  geom/binning/img buffers are the ones the forward filled.
  * dL_dpix is [3,H,W].  All nine gradient outputs are fully written (no zero-fill needed):
  * dL_dmean2D [P,3] (z = 0), dL_dconic [P,2,2] (may be NULL: the reference's _C returns it to
- * no one), dL_dopacity [P], dL_dcolor [P,3], dL_dmean3D [P,3], dL_dcov3D [P,6],
- * dL_dsh [P,M,3] (may be NULL if M == 0), dL_dscale [P,3], dL_drot [P,4]. */
+ * no one), dL_dopacity [P], dL_dcolor [P,3] (may be NULL: not stored),
+ * dL_dmean3D [P,3], dL_dcov3D [P,6] (may be NULL: not stored), dL_dsh [P,M,3] (may be NULL
+ * if M == 0), dL_dscale [P,3], dL_drot [P,4].  The reference's RasterizeGaussiansBackwardCUDA
+ * (rasterize_points.cu:115-192) fills all of them; an autograd caller skips the gradients of
+ * inputs that need none (an empty colors_precomp or cov3D_precomp). */
 int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height, const float* means3D,
                  const float* shs, const float* colors_precomp, const float* scales, float scale_modifier,
                  const float* rotations, const float* cov3D_precomp, const float* viewmatrix,

@@ -1036,7 +1036,8 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
                  void* geom_buffer, void* binning_buffer, void* img_buffer, const float* dL_dpix, float* dL_dmean2D,
                  float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dmean3D, float* dL_dcov3D,
                  float* dL_dsh, float* dL_dscale, float* dL_drot, void* stream_) {
-    if (!dL_dcolor && P > 0) return fail(GSR_E_ARG, "gsr_backward: dL_dcolor required");
+    // dL_dcolor / dL_dcov3D may be NULL: not stored (the SH and scale/rotation gradients keep
+    // them in registers; an autograd caller passes NULL for inputs that need no gradient)
     return backward_impl(P, D, M, R, background, width, height, means3D, shs, colors_precomp, scales, scale_modifier,
                          rotations, cov3D_precomp, viewmatrix, projmatrix, campos, tan_fovx, tan_fovy, radii,
                          geom_buffer, binning_buffer, img_buffer, dL_dpix, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor,

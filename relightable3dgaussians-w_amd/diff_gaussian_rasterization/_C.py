@@ -113,9 +113,14 @@ def _rasterize_reuse(background, colors, image_height, image_width, src_geom, sr
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color, sh, degree,
-                                 campos, geomBuffer, R, binningBuffer, imageBuffer):
+                                 campos, geomBuffer, R, binningBuffer, imageBuffer, *, colors_grad=True,
+                                 cov3D_grad=True):
     """rasterize_points.cu:115-192 RasterizeGaussiansBackwardCUDA -> (dL_dmeans2D, dL_dcolors,
-    dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
+
+    colors_grad / cov3D_grad (keyword-only, default True as in the reference): False skips
+    storing dL_dcolors / dL_dcov3D (returned as None) -- the autograd node passes them for
+    inputs that need no gradient (render()'s empty colors_precomp and cov3D_precomp)."""
     _lib.require_gpu_tensor(means3D, "means3D")
     dev = means3D.device
     P = means3D.size(0)
@@ -124,15 +129,16 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
     # one allocation for the eight outputs (views of one flat buffer: each is written in full,
     # and the allocator calls were the host-side cost of this call); the reference's
     # dL_dconic is never returned, so it is not computed (NULL)
-    widths = (3, NUM_CHANNELS, 1, 3, 6, 3 * M, 3, 4)
+    colors_grad, cov3D_grad = bool(colors_grad), bool(cov3D_grad)
+    widths = (3, NUM_CHANNELS if colors_grad else 0, 1, 3, 6 if cov3D_grad else 0, 3 * M, 3, 4)
     flat = (torch.zeros if P == 0 else torch.empty)(P * sum(widths), dtype=torch.float32, device=dev)
     outs, o = [], 0
     for w in widths:
         outs.append(flat[o:o + P * w])
         o += P * w
     dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations = (
-        outs[0].view(P, 3), outs[1].view(P, NUM_CHANNELS), outs[2].view(P, 1), outs[3].view(P, 3),
-        outs[4].view(P, 6), outs[5].view(P, M, 3), outs[6].view(P, 3), outs[7].view(P, 4))
+        outs[0].view(P, 3), outs[1].view(P, widths[1]), outs[2].view(P, 1), outs[3].view(P, 3),
+        outs[4].view(P, widths[4]), outs[5].view(P, M, 3), outs[6].view(P, 3), outs[7].view(P, 4))
     if P != 0:
         keep = [_f32(x) for x in (background, means3D, sh, colors, scales, rotations, cov3D_precomp, viewmatrix,
                                   projmatrix, campos, dL_dout_color)]
@@ -144,10 +150,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, scales, rot
             _lib.fptr(sc_), float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_),
             _lib.fptr(cp_), float(tan_fovx), float(tan_fovy), radii_.data_ptr(), ptr(geomBuffer), ptr(binningBuffer),
             ptr(imageBuffer), _lib.fptr(dout_), dL_dmeans2D.data_ptr(), None,
-            dL_dopacity.data_ptr(), dL_dcolors.data_ptr(), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(),
+            dL_dopacity.data_ptr(), dL_dcolors.data_ptr() if colors_grad else None, dL_dmeans3D.data_ptr(),
+            dL_dcov3D.data_ptr() if cov3D_grad else None,
             dL_dsh.data_ptr() if M else None, dL_dscales.data_ptr(), dL_drotations.data_ptr(), _lib.stream_of(dev))
         _lib.check(ret, "rasterize_gaussians_backward")
-    return dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations
+    return (dL_dmeans2D, dL_dcolors if colors_grad else None, dL_dopacity, dL_dmeans3D,
+            dL_dcov3D if cov3D_grad else None, dL_dsh, dL_dscales, dL_drotations)
 
 
 def pack_features(features, nch=None):

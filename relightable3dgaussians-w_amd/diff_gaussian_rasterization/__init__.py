@@ -141,8 +141,10 @@ class _RasterizeGaussians(torch.autograd.Function):
             _C.rasterize_gaussians_backward(s.bg, means3D, radii, colors_precomp, scales, rotations,
                                             s.scale_modifier, cov3Ds_precomp, s.viewmatrix, s.projmatrix, s.tanfovx,
                                             s.tanfovy, grad_out_color, sh, s.sh_degree, s.campos, geom_buf,
-                                            ctx.num_rendered, bin_buf, img_buf)
-        # gradients in the order of forward()'s inputs; None for raster_settings
+                                            ctx.num_rendered, bin_buf, img_buf,
+                                            colors_grad=ctx.needs_input_grad[3], cov3D_grad=ctx.needs_input_grad[7])
+        # gradients in the order of forward()'s inputs; None for raster_settings (and for an empty
+        # colors_precomp / cov3D_precomp, which need none: their 36 B per Gaussian are not stored)
         return g_means3D, g_means2D, g_sh, g_colors, g_opacities, g_scales, g_rotations, g_cov3D, None
 
 

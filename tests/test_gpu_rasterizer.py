@@ -421,3 +421,44 @@ def test_second_backward_over_one_forward():
     for a, b in zip(g1, g2):
         if a.numel():
             assert rel_l2(b.cpu().numpy(), a.cpu().numpy()) < 1e-6
+
+
+@pytest.mark.parametrize("mode", ["sh", "colors"])
+def test_backward_skips_unneeded_outputs(mode):
+    """colors_grad / cov3D_grad = False (what the autograd node passes for an empty
+    colors_precomp / cov3D_precomp): dL_dcolors and dL_dcov3D come back as None, the other six
+    outputs bit-equal to the reference's full output set (deterministic mode: fixed-order sums);
+    through GaussianRasterizer the SH path's gradients are unchanged."""
+    dgr, _C, _lib = _dgr()
+    cam, gs = make_case(P=3000, W=96, H=80, sh_degree=2 if mode == "sh" else 0, camera="orbit")
+    kw = dict(mode=mode, sh_degree=2 if mode == "sh" else 0)
+    W, H = cam.image_width, cam.image_height
+    dout = torch.randn(3, H, W, generator=torch.Generator().manual_seed(4)).cuda()
+    _lib.set_deterministic(True)
+    try:
+        st = run_gpu(cam, gs, **kw)
+        args = (st["bg"], st["means"], st["radii"], st["colors"], st["scales"], st["rots"], 1.0, st["cov3"], st["vm"],
+                st["pm"], cam.tanfovx, cam.tanfovy, dout, st["sh"], kw["sh_degree"], st["cp"], st["geom"], st["R"],
+                st["binb"], st["img"])
+        full = _C.rasterize_gaussians_backward(*args)
+        part = _C.rasterize_gaussians_backward(*args, colors_grad=False, cov3D_grad=False)
+    finally:
+        _lib.set_deterministic(False)
+    assert part[1] is None and part[4] is None
+    assert full[1] is not None and full[4] is not None and full[4].abs().max() > 0
+    for i in (0, 2, 3, 5, 6, 7):
+        assert torch.equal(part[i], full[i]), i
+    if mode == "sh":  # the autograd node passes the flags: gradients unchanged against the full call
+        dev = torch.device("cuda")
+        leaves = {k: gs[k].to(dev).requires_grad_(True) for k in ("means3D", "shs", "opacities", "scales", "rotations")}
+        means2D = torch.zeros_like(leaves["means3D"], requires_grad=True)
+        s = dgr.GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, bg=st["bg"], scale_modifier=1.0,
+            viewmatrix=st["vm"], projmatrix=st["pm"], sh_degree=kw["sh_degree"], campos=st["cp"], prefiltered=False)
+        img, _ = dgr.GaussianRasterizer(s)(means3D=leaves["means3D"], means2D=means2D, shs=leaves["shs"],
+                                           opacities=leaves["opacities"], scales=leaves["scales"],
+                                           rotations=leaves["rotations"])
+        (img * dout).sum().backward()
+        for got, ref in ((means2D.grad, full[0]), (leaves["means3D"].grad, full[3]), (leaves["shs"].grad, full[5]),
+                         (leaves["scales"].grad, full[6]), (leaves["rotations"].grad, full[7])):
+            assert rel_l2(got.cpu().numpy(), ref.cpu().numpy()) < 1e-5
