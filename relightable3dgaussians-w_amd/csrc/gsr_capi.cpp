@@ -933,7 +933,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         if (rc != GSR_OK) return rc;
     }
     if (R > 0) {
-        gsr::RenderBwdArgs ra;
+        gsr::RenderBwdArgs ra{};
         ra.W = width; ra.H = height; ra.grid_x = gx; ra.grid_y = gy;
         ra.st_ranges = at<uint2>(bin, bl.st_ranges);
         ra.ent = at<uint2>(bin, bl.ent);
