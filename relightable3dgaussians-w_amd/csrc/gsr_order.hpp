@@ -119,7 +119,7 @@ template <bool BAL = false>
 __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderArgs& a) {
     __shared__ uint32_t hist[NBUCKET];
     __shared__ uint32_t cur[NBUCKET];
-    __shared__ uint32_t scan[512];
+    __shared__ uint32_t scan[8];  // per-wave bucket sums
     unsigned lo, len;
     if constexpr (BAL) {
         balanced_band(band, a, lo, len);
@@ -145,20 +145,17 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
     }
     __syncthreads();
     // cur[b] = tiles in buckets above b (heaviest bucket first): a block scan over the
-    // buckets in descending order, thread j holding bucket NBUCKET - 1 - j (one thread serially
-    // when the block is smaller than the bucket count)
+    // buckets in descending order, thread j holding bucket NBUCKET - 1 - j -- wave scans and one
+    // barrier (one thread serially when the block is smaller than the bucket count)
     if (blockDim.x >= NBUCKET && blockDim.x <= 512) {
-        const int j = threadIdx.x, bj = NBUCKET - 1 - j;
+        const int j = threadIdx.x, bj = NBUCKET - 1 - j, wave = j >> 6;
         const uint32_t hj = bj >= 0 ? hist[bj] : 0u;
-        scan[j] = hj;
+        const uint32_t inc = wave_inclusive_scan(hj);
+        if ((j & 63) == 63) scan[wave] = inc;
         __syncthreads();
-        for (int o = 1; o < NBUCKET; o <<= 1) {
-            const uint32_t v = j >= o ? scan[j - o] : 0u;
-            __syncthreads();
-            scan[j] += v;
-            __syncthreads();
-        }
-        if (bj >= 0) cur[bj] = scan[j] - hj;
+        uint32_t off = 0;
+        for (int w = 0; w < wave; w++) off += scan[w];
+        if (bj >= 0) cur[bj] = off + inc - hj;
     } else if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (int b = NBUCKET - 1; b >= 0; b--) {
