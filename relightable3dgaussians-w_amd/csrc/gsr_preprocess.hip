@@ -12,6 +12,13 @@
 
 namespace gsr {
 
+// LDS ordering within one wave (wave-private LDS rows)
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One Gaussian's inputs, loaded up front (all of them unconditionally, so that a wave has
 // every global load in flight at once instead of one dependent round trip per stage).
 struct GaussIn {
@@ -238,6 +245,57 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
     preprocess_block_out(a, tiles, stc, err);
 }
 
+// SH path with 3M a multiple of 4 (M in {4, 16}): each wave loads its 64 Gaussians' SH rows
+// (contiguous, 64 * 3M floats) with coalesced 16-B loads -- every lane's 3M/4 loads in flight
+// at once, each instruction one contiguous 1 KiB -- into wave-private LDS rows padded to 3M + 4
+// floats (16-B aligned; the row reads below then hit distinct banks), and each lane reads its
+// own row back.  The register-row kernel's per-lane 16-B loads touch 64 scattered lines per
+// instruction.  No barrier: the rows are wave-private.
+#ifndef GSR_PRE_WAVE_SH
+#define GSR_PRE_WAVE_SH 1
+#endif
+template <int M>
+__global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
+    static_assert((3 * M) % 4 == 0, "16-B rows");
+    constexpr int F4 = 3 * M / 4, RS4 = F4 + 1;  // float4s per row, per padded LDS row
+    __shared__ float4 s_rows[4][64 * RS4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const long long g0 = (long long)blockIdx.x * blockDim.x + wave * 64;  // the wave's first Gaussian
+    const int nf = (int)(a.P - g0 < 64 ? (a.P - g0 > 0 ? a.P - g0 : 0) : 64) * F4;
+    GaussIn gin;
+    if (idx < a.P) load_gauss(a, idx, gin);
+    {
+        const float4* src = reinterpret_cast<const float4*>(a.shs) + g0 * F4;
+        float4 v[F4];
+#pragma unroll
+        for (int j = 0; j < F4; j++) {
+            const int f = j * 64 + lane;
+            v[j] = f < nf ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        float4* rows = s_rows[wave];
+#pragma unroll
+        for (int j = 0; j < F4; j++) {
+            const int f = j * 64 + lane, r = f / F4;
+            rows[r * RS4 + (f - r * F4)] = v[j];
+        }
+    }
+    wave_lds_fence();
+    float shr[3 * M];
+#pragma unroll
+    for (int k = 0; k < F4; k++) {
+        const float4 t = s_rows[wave][lane * RS4 + k];
+        shr[4 * k] = t.x;
+        shr[4 * k + 1] = t.y;
+        shr[4 * k + 2] = t.z;
+        shr[4 * k + 3] = t.w;
+    }
+    uint32_t tiles = 0, stc = 0, key = 0;
+    bool err = false;
+    if (idx < a.P)
+        preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr, key, err);
+    preprocess_block_out(a, tiles, stc, err);
+}
 
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,
                                                        bool* present) {
@@ -280,7 +338,10 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
             case 1: hipLaunchKernelGGL(k_preprocess_regsh<1>, grid, blk, 0, s, a); return;
             case 4: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<4>, grid, blk, 0, s, a); return; } break;
             case 9: hipLaunchKernelGGL(k_preprocess_regsh<9>, grid, blk, 0, s, a); return;
-            case 16: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<16>, grid, blk, 0, s, a); return; } break;
+            case 16:
+                if (al16 && GSR_PRE_WAVE_SH) { hipLaunchKernelGGL(k_preprocess_wavesh<16>, grid, blk, 0, s, a); return; }
+                if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<16>, grid, blk, 0, s, a); return; }
+                break;
             default: break;
         }
     }
