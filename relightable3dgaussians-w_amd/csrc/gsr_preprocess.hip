@@ -254,6 +254,9 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
 #ifndef GSR_PRE_WAVE_SH
 #define GSR_PRE_WAVE_SH 1
 #endif
+#ifndef GSR_PRE_SH_NT
+#define GSR_PRE_SH_NT 1
+#endif
 template <int M>
 __global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
     static_assert((3 * M) % 4 == 0, "16-B rows");
@@ -271,7 +274,17 @@ __global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
 #pragma unroll
         for (int j = 0; j < F4; j++) {
             const int f = j * 64 + lane;
+#if GSR_PRE_SH_NT  // non-temporal: the rows are read once per call (the backward reads the Jacobian)
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            if (f < nf) {
+                const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + f));
+                v[j] = make_float4(t.x, t.y, t.z, t.w);
+            } else {
+                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#else
             v[j] = f < nf ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
         }
         float4* rows = s_rows[wave];
 #pragma unroll
