@@ -30,11 +30,30 @@ struct BwdIn {
     uint32_t clampf;
 };
 
+// The accumulator lines and the Jacobian rows are read for the last time here: non-temporal
+// loads (GSR_PREBWD_NT) keep them from evicting what the next stages read.
+#ifndef GSR_PREBWD_NT
+#define GSR_PREBWD_NT 1
+#endif
+template <typename T>
+__device__ __forceinline__ T last_load(const T* p) {
+#if GSR_PREBWD_NT
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ float4 last_load4(const float* p) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v t = last_load(reinterpret_cast<const f4v*>(p));
+    return make_float4(t.x, t.y, t.z, t.w);
+}
+
 __device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx, BwdIn& in) {
-    const float4* line = reinterpret_cast<const float4*>(a.acc + (size_t)idx * ACC_STRIDE);
-    in.l0 = line[0];
-    in.l1 = line[1];
-    in.l2 = a.acc[(size_t)idx * ACC_STRIDE + 8];
+    const float* line = a.acc + (size_t)idx * ACC_STRIDE;
+    in.l0 = last_load4(line);
+    in.l1 = last_load4(line + 4);
+    in.l2 = last_load(line + 8);
     in.radius = a.radii[idx];
     in.mean = make_float3(a.means3D[3 * idx], a.means3D[3 * idx + 1], a.means3D[3 * idx + 2]);
     if (a.cov3D_precomp) {
@@ -47,8 +66,8 @@ __device__ __forceinline__ void load_bwd_in(const PreprocessBwdArgs& a, int idx,
     if (a.shs) {
         const size_t P = (size_t)a.P;  // coalesced SoA rows
 #pragma unroll
-        for (int k = 0; k < 9; k++) in.jac[k] = a.shjac[(size_t)k * P + idx];
-        in.clampf = __float_as_uint(a.shjac[9 * P + idx]);
+        for (int k = 0; k < 9; k++) in.jac[k] = last_load(a.shjac + (size_t)k * P + idx);
+        in.clampf = __float_as_uint(last_load(a.shjac + 9 * P + idx));
     }
 }
 
