@@ -212,6 +212,16 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     preprocess_block_out(a, tiles, stc, err);
 }
 
+// GSR_PRE_WAVE_SH: the wave-staged SH rows (k_preprocess_wavesh) for M = 16, with GSR_PRE_SH_NT
+// its loads non-temporal.  Off by default: its single call is faster (preprocess 0.107 ->
+// 0.094 ms at cfg2), but its 53 KB of LDS per workgroup starves the overlapping views' kernels
+// and the default 3-stream bench drops 3 % (profiles/r4zj_ab_preprocess_default_bench.txt)
+#ifndef GSR_PRE_WAVE_SH
+#define GSR_PRE_WAVE_SH 0
+#endif
+#ifndef GSR_PRE_SH_NT
+#define GSR_PRE_SH_NT 1
+#endif
 // SH path with M in {1, 4, 9, 16}: each thread loads its own SH row into registers with
 // the other inputs (16-B loads when 3M is a multiple of 4) -- no LDS, so occupancy is
 // bounded by registers only (16 coefficients: 102 vs 130 us at cfg2 against the
@@ -227,7 +237,7 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
             const float4* s4 = reinterpret_cast<const float4*>(a.shs + (size_t)idx * 3 * M);
 #pragma unroll
             for (int k = 0; k < 3 * M / 4; k++) {
-                const float4 v = s4[k];
+                const float4 v = s4[k];  // (non-temporal here: the preprocess 0.107 -> 0.20 ms, r4zj)
                 shr[4 * k] = v.x;
                 shr[4 * k + 1] = v.y;
                 shr[4 * k + 2] = v.z;
@@ -251,12 +261,6 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
 // floats (16-B aligned; the row reads below then hit distinct banks), and each lane reads its
 // own row back.  The register-row kernel's per-lane 16-B loads touch 64 scattered lines per
 // instruction.  No barrier: the rows are wave-private.
-#ifndef GSR_PRE_WAVE_SH
-#define GSR_PRE_WAVE_SH 1
-#endif
-#ifndef GSR_PRE_SH_NT
-#define GSR_PRE_SH_NT 1
-#endif
 template <int M>
 __global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
     static_assert((3 * M) % 4 == 0, "16-B rows");

@@ -31,9 +31,10 @@ struct BwdIn {
 };
 
 // The accumulator lines and the Jacobian rows are read for the last time here: non-temporal
-// loads (GSR_PREBWD_NT) keep them from evicting what the next stages read.
+// loads (GSR_PREBWD_NT=1) were measured neutral at cfg2 and slower at cfg5 (+20 us a call,
+// profiles/r4zi_ab_prebwd_nt.txt): off.
 #ifndef GSR_PREBWD_NT
-#define GSR_PREBWD_NT 1
+#define GSR_PREBWD_NT 0
 #endif
 template <typename T>
 __device__ __forceinline__ T last_load(const T* p) {
