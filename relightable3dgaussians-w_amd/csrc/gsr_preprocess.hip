@@ -314,6 +314,66 @@ __global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
     preprocess_block_out(a, tiles, stc, err);
 }
 
+// The same staged in two half-wave rounds of 32 rows (half the LDS: 26.6 KB per workgroup),
+// GSR_PRE_WAVE_SH == 2: each round's 32 rows are 6 KiB contiguous (6 coalesced 16-B loads per
+// lane), and the lanes of that half read their rows.
+template <int M>
+__global__ void __launch_bounds__(256) k_preprocess_halfsh(PreprocessArgs a) {
+    static_assert((3 * M) % 4 == 0 && (3 * M / 4 * 32) % 64 == 0, "16-B rows, whole loads per round");
+    constexpr int F4 = 3 * M / 4, RS4 = F4 + 1, NJ = F4 * 32 / 64;
+    __shared__ float4 s_rows[4][32 * RS4];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    GaussIn gin;
+    if (idx < a.P) load_gauss(a, idx, gin);
+    float shr[3 * M];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const long long g0 = (long long)blockIdx.x * blockDim.x + wave * 64 + 32 * h;
+        const int nf = (int)(a.P - g0 < 32 ? (a.P - g0 > 0 ? a.P - g0 : 0) : 32) * F4;
+        const float4* src = reinterpret_cast<const float4*>(a.shs) + g0 * F4;
+        float4 v[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const int f = j * 64 + lane;
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            if (f < nf) {
+#if GSR_PRE_SH_NT
+                const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + f));
+#else
+                const f4v t = *reinterpret_cast<const f4v*>(src + f);
+#endif
+                v[j] = make_float4(t.x, t.y, t.z, t.w);
+            } else {
+                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+        wave_lds_fence();  // the previous round's row reads are done
+        float4* rows = s_rows[wave];
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            const int f = j * 64 + lane, r = f / F4;
+            rows[r * RS4 + (f - r * F4)] = v[j];
+        }
+        wave_lds_fence();
+        if ((lane >> 5) == h) {
+#pragma unroll
+            for (int k = 0; k < F4; k++) {
+                const float4 t = rows[(lane & 31) * RS4 + k];
+                shr[4 * k] = t.x;
+                shr[4 * k + 1] = t.y;
+                shr[4 * k + 2] = t.z;
+                shr[4 * k + 3] = t.w;
+            }
+        }
+    }
+    uint32_t tiles = 0, stc = 0, key = 0;
+    bool err = false;
+    if (idx < a.P)
+        preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr, key, err);
+    preprocess_block_out(a, tiles, stc, err);
+}
+
 __global__ void __launch_bounds__(256) k_mark_visible(int P, const float* means3D, const float* viewmatrix,
                                                        bool* present) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -356,6 +416,7 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
             case 4: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<4>, grid, blk, 0, s, a); return; } break;
             case 9: hipLaunchKernelGGL(k_preprocess_regsh<9>, grid, blk, 0, s, a); return;
             case 16:
+                if (al16 && GSR_PRE_WAVE_SH == 2) { hipLaunchKernelGGL(k_preprocess_halfsh<16>, grid, blk, 0, s, a); return; }
                 if (al16 && GSR_PRE_WAVE_SH) { hipLaunchKernelGGL(k_preprocess_wavesh<16>, grid, blk, 0, s, a); return; }
                 if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<16>, grid, blk, 0, s, a); return; }
                 break;
