@@ -232,11 +232,13 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
-// whole tile.  Five waves per SIMD (96 VGPRs, 8 B of scratch per lane outside the survivor
-// walk): 336.6-337.1 -> 330.4-332.5 us at cfg2 against four since the 64-B accumulator lines
-// (tools/r3_check44.sh; neutral before them).
+// whole tile.  Four waves per SIMD: the kernel alone is faster at five (336.6-337.1 ->
+// 330.4-332.5 us at cfg2, tools/r3_check44.sh), but in the bench's throughput mode -- views on
+// 3 HIP streams, this pass overlapping other views' forward and geometry kernels -- four leave
+// them room: the headline +0.9 % at cfg2 and +1.3 % at cfg5, the isolated call pair +7 / +22 us
+// (profiles/r4zo_ab_bwd_waves_default_bench.txt).
 #ifndef GSR_BWD_WAVES
-#define GSR_BWD_WAVES 5
+#define GSR_BWD_WAVES 4
 #endif
 template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
