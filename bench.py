@@ -4,8 +4,9 @@
 Workload (BASELINE.json configs[1], SURVEY §8d cfg 2): 1.5M synthetic Gaussians, SH degree 3,
 1920x1080.  A step is 4 views per GPU at every N (cfg4's per-GPU mini-batch), each one
 rasterizer forward + backward through the drop-in diff_gaussian_rasterization._C (libgsr.so,
-hand-written gfx950 HIP) -- the reference's call pair, inputs resident in HBM -- one after
-another on one stream.  With --gpus N > 1 (one process per GPU, launched by
+hand-written gfx950 HIP) -- the reference's call pair, inputs resident in HBM -- the views
+alternating over 3 HIP streams by default (--streams 1: one after another on one stream; the
+layout is in config.views_per_step / config.streams).  With --gpus N > 1 (one process per GPU, launched by
 torch.distributed.run) every rank holds the same replicated scene and renders its own 4
 distinct views per step, and the per-Gaussian gradients of the step are summed over ranks with
 one RCCL all-reduce (weak scaling: view-parallel data parallelism).  The per-rank
@@ -103,6 +104,96 @@ def unique_bytes(stage, P, Pv, R, T, Npix, M):
     instead; the records are re-read from L2 across the tiles a Gaussian touches."""
     return {"render_fwd": T * 8 + Pv * (48 + 12) + Npix * 20,
             "render_bwd": T * 8 + Pv * (48 + 12) + Npix * 20 + Pv * 44}.get(stage)
+
+
+STAGE_VIEWS = 24  # views (one at a time, one stream) behind stage_ms
+
+
+def stage_breakdown(view, n):
+    """Per-stage HIP-event times over ``n`` views run one at a time on one stream:
+    {stage: (total ms, launches)}."""
+    from gsr import _lib
+    _lib.profile_read(reset=True)
+    _lib.profile_stages(None)
+    _lib.profile_enable(True)
+    for _ in range(n):
+        view()
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    return _lib.profile_read(reset=True)
+
+
+def single_call_median(view, W, H, n=50, warm=10):
+    """SURVEY §8d's definition: W*H / (t_fwd + t_bwd) of ONE call, the median of ``n`` calls
+    after ``warm`` warm-up, HIP events on the stream the calls run on."""
+    for _ in range(warm):
+        view()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in evs:
+        a.record()
+        view()
+        b.record()
+    torch.cuda.synchronize()
+    t_ms = sorted(a.elapsed_time(b) for a, b in evs)
+    med = t_ms[len(t_ms) // 2]
+    return {"median_ms": round(med, 4), "p10_ms": round(t_ms[n // 10], 4), "p90_ms": round(t_ms[(9 * n) // 10], 4),
+            "calls": len(t_ms), "value": round(W * H / (med * 1e-3) / 1e6, 3), "unit": "MPix/s",
+            "what": f"one rasterizer forward + backward call pair, median of {n} (HIP events, {warm} warm-up)"}
+
+
+def tile_roofline(dom, P, Pv, R, T, W, H, M, workload, dev):
+    """The roofline object of the dominant stage ``dom`` = (stage, avg launch ms)."""
+    dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
+    achieved_gbs = dom_bytes / (dom[1] * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(dom[0], workload)
+    hbm = {"achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes": "algorithmic (SURVEY §8d per-stage figure x "
+                                                                   "this launch's measured P, P_v, R)",
+           "algorithmic_bytes_per_launch": int(dom_bytes),
+           "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src}
+    ub = unique_bytes(dom[0], P, Pv, R, T, W * H, M)
+    if ub is not None:
+        hbm["unique_bytes_per_launch"] = int(ub)
+        hbm["unique_frac"] = round(ub / (dom[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+    kinfo, ksrc = pmc_kernel(dom[0], workload)
+    if kinfo.get("valu_insts") and dom[0].startswith("render"):
+        # The tile passes are bound by VALU issue (the PMC counters show their HBM traffic at
+        # ~0.3x the algorithmic bytes): instruction throughput against the spec issue rate,
+        # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md).
+        n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        peak = n_simd * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST
+        ach = kinfo["valu_insts"] / (dom[1] * 1e-3) / 1e9
+        roofline = {"bound": "valu", "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "Gwave-inst/s",
+                    "frac": round(ach / peak, 4), "traffic": hbm["traffic"], "kernel": dom[0],
+                    "avg_launch_ms": round(dom[1], 4), "valu_insts_per_launch": int(kinfo["valu_insts"]),
+                    "valu_source": ksrc,
+                    "peak_basis": f"{n_simd} SIMDs x {VALU_CLOCK_GHZ} GHz / {VALU_CYCLES_PER_INST} cycles per "
+                                  "wave64 VALU instruction (spec issue rate)",
+                    "hbm": hbm}
+        if kinfo.get("salu_insts"):
+            # the scalar instructions the same waves issue (mask logic, walk bookkeeping,
+            # branches): a co-bound, DESIGN.md §3 (an added SALU op per evaluation costs more
+            # than an added VALU op)
+            roofline["salu_insts_per_launch"] = int(kinfo["salu_insts"])
+            roofline["salu_per_valu"] = round(kinfo["salu_insts"] / kinfo["valu_insts"], 3)
+    elif dom[0].startswith("render"):
+        # a tile pass with no committed instruction count for this workload: its bound is VALU
+        # issue (DESIGN.md §3), and the HBM fraction of its algorithmic bytes is not a roofline
+        # (the R x 40 record reads are served from LDS/L2), so no fraction is claimed
+        roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "Gwave-inst/s", "frac": None,
+                    "traffic": hbm["traffic"], "kernel": dom[0], "avg_launch_ms": round(dom[1], 4),
+                    "frac_null_reason": f"no committed rocprofv3 SQ_INSTS_VALU pass of workload '{workload}' "
+                                        "(profiles/r*_hbm_traffic.json)", "hbm": hbm}
+    else:
+        roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": hbm["frac"], "traffic": hbm["traffic"], "kernel": dom[0],
+                    "avg_launch_ms": round(dom[1], 4), "hbm": hbm}
+    if roofline["bound"] == "hbm" and roofline["frac"] is not None and roofline["frac"] > 1.0:
+        # more algorithmic bytes per second than HBM delivers: part of them came from a cache,
+        # so the figure is no HBM fraction
+        roofline.update(frac=None, frac_null_reason="algorithmic bytes / launch time exceed the HBM peak (served "
+                                                    "from L2 / Infinity Cache)")
+    return roofline
 
 
 def cpu_baseline(cam, gs_cpu, deg, dout_cpu, ntiles=64, seed=2, cfg1=True):
@@ -540,6 +631,87 @@ def dist_setup(args):
     return dist, rank, world, local, backend, int(one.item())
 
 
+def clustered_leg(args, dev, name="cfg2c", V=4, NS=3):
+    """The headline's size on a Trevi-class clustered cloud (gsr.scenes.trevi_like_gaussians:
+    facade sheets with a density gradient, sculpture clusters, a translucent spray volume, the
+    reference's sky band; ~20 % culled, heavy tiles).  Reports the §8d single call (median of 50),
+    the 4-view / 3-stream throughput the headline uses, stage_ms over STAGE_VIEWS one-stream
+    views and the dominant stage's roofline (PMC record of `bench.py --config cfg2c`)."""
+    from diff_gaussian_rasterization import _C
+    from gsr import _lib, scenes
+    cam, gs_cpu, cfg = scenes.build_config(name, device="cpu", seed=0)
+    W, H, deg = cam.image_width, cam.image_height, cfg["sh_degree"]
+    g = {k: v.to(dev) for k, v in gs_cpu.items() if k != "is_sky"}
+    P, M = g["means3D"].shape[0], g["shs"].shape[1]
+    e = torch.empty(0, device=dev)
+    bg = torch.zeros(3, device=dev)
+    dout = torch.randn(3, H, W, generator=torch.Generator().manual_seed(1)).to(dev)
+    cams = [scenes.view_camera(cam, k, look=cfg.get("look")).to(dev) for k in range(V)]
+    mats = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in cams]
+    state = {}
+
+    def view(k=0):
+        vm, pm, cp = mats[k]
+        R, color, radii, geom, binb, img = _C.rasterize_gaussians(
+            bg, g["means3D"], e, g["opacities"], g["scales"], g["rotations"], 1.0, e, vm, pm, cam.tanfovx,
+            cam.tanfovy, H, W, g["shs"], deg, cp, False)
+        _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm, pm,
+                                        cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb, img)
+        if k == 0:
+            state["R"], state["radii"] = R, radii
+
+    main_s = torch.cuda.current_stream(dev)
+    ss = [torch.cuda.Stream(dev) for _ in range(NS)]
+
+    def step():
+        for s_ in ss:
+            s_.wait_stream(main_s)
+        for i in range(V):
+            with torch.cuda.stream(ss[i % NS]):
+                view(i)
+        for s_ in ss:
+            main_s.wait_stream(s_)
+
+    view()
+    torch.cuda.synchronize()
+    stages = stage_breakdown(view, STAGE_VIEWS)
+    dom_name = max(((k, v[0] / v[1]) for k, v in stages.items() if v[1] > 0 and k in STAGE_KERNEL),
+                   key=lambda kv: kv[1])[0]
+    single = single_call_median(view, W, H)
+    for _ in range(SETTLE_STEPS):
+        step()
+    torch.cuda.synchronize()
+    nsteps = max(5, args.steps)
+    t0 = time.perf_counter()
+    for _ in range(nsteps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / nsteps
+    _lib.profile_stages([dom_name])
+    _lib.profile_enable(True)
+    for _ in range(max(1, args.event_steps)):
+        for i in range(V):
+            view(i)
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    live = _lib.profile_read(reset=True).get(dom_name, (0.0, 0))
+    _lib.profile_stages(None)
+    R, Pv = int(state["R"]), int((state["radii"] > 0).sum().item())
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    workload = f"{name}: {P} Gaussians SH{deg}, {W}x{H}"
+    roof = tile_roofline((dom_name, live[0] / max(live[1], 1)), P, Pv, R, T, W, H, M, workload, dev)
+    return {"value": round(V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s", "ms_per_step": round(ms, 4),
+            "steps": nsteps, "views_per_step": V, "streams": NS, "single_call": single,
+            "stage_ms": {k: round(v[0] / max(v[1], 1), 4) for k, v in stages.items() if v[1] > 0},
+            "stage_views": STAGE_VIEWS, "roofline": roof,
+            "measured": {"num_rendered": R, "visible": Pv, "culled_frac": round(1 - Pv / P, 4)},
+            "config": {"workload": workload + ": Trevi-class clustered cloud (gsr.scenes.trevi_like_gaussians: "
+                                              "facade sheets, sculpture clusters, translucent spray, side "
+                                              "buildings, 10 % sky band as augment_with_sky_gaussians), "
+                                              f"{V} views per step on {NS} HIP streams",
+                       "gaussians": P, "width": W, "height": H, "sh_degree": deg}}
+
+
 def refalgo_leg(args, bg, g, e, vm, pm, cp, cam, H, W, deg, dout, ms_ours):
     """The reference rasterizer's stage structure in plain HIP on the same GPU and inputs
     (baseline/refalgo.hip: 64-bit duplicate keys + hipcub radix sort, one thread per pixel,
@@ -595,10 +767,12 @@ def main():
                     help="views per step per GPU (default 4 at every N: the per-GPU mini-batch whose gradients "
                          "cross the ranks in one all-reduce at N > 1)")
     ap.add_argument("--streams", type=int, default=None,
-                    help="HIP streams the views of a step (cfg2, default 1) or a training iteration (cfg4, "
-                         "default 2) alternate over")
+                    help="HIP streams the views of a step (cfg2 / cfg2c, default 3) or a training iteration "
+                         "(cfg4, default 2) alternate over")
     ap.add_argument("--no-minibatch", action="store_true", help="skip the 4-view multi-stream extra leg")
     ap.add_argument("--no-refalgo", action="store_true", help="skip the reference-structure GPU baseline leg")
+    ap.add_argument("--no-clustered", action="store_true",
+                    help="skip the cfg2c leg (cfg2's size on a Trevi-class clustered cloud)")
     ap.add_argument("--no-relit", action="store_true", help="skip the cfg3 / cfg5-relit relight legs of the default line")
     ap.add_argument("--event-steps", type=int, default=5,
                     help="steps (each V views, one stream) run after the timed region with the dominant stage's "
@@ -663,7 +837,7 @@ def main():
     # the step's views alternate over NS HIP streams (default 3): one view's latency-bound
     # geometry passes overlap another's tile passes
     NS = max(1, min(3 if args.streams is None else args.streams, V))
-    cams = [scenes.view_camera(cam, rank * V + k).to(dev) for k in range(V)]
+    cams = [scenes.view_camera(cam, rank * V + k, look=cfg.get("look")).to(dev) for k in range(V)]
     mats = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in cams]
     main_s = torch.cuda.current_stream(dev)
     vstreams = [main_s] if NS == 1 else [torch.cuda.Stream(dev) for _ in range(NS)]
@@ -742,14 +916,7 @@ def main():
     # and starts on a busy GPU's clocks): three profiled views, one at a time on one stream
     # (every stage bracketed by HIP events).  The timed region carries no events; the dominant
     # stage's launch time comes from --event-steps steps on one stream after it.
-    _lib.profile_read(reset=True)
-    _lib.profile_stages(None)
-    _lib.profile_enable(True)
-    for _ in range(3):
-        view()
-    torch.cuda.synchronize()
-    _lib.profile_enable(False)
-    stages = _lib.profile_read(reset=True)
+    stages = stage_breakdown(view, STAGE_VIEWS)
     dom_name = max(((k, v[0] / v[1]) for k, v in stages.items() if v[1] > 0 and k in STAGE_KERNEL),
                    key=lambda kv: kv[1])[0]
     # at least SETTLE_STEPS untimed steps in a row before the timed region (the W warmup steps
@@ -814,23 +981,11 @@ def main():
     if rank == 0 and world == 1:
         # SURVEY §8d's definition: W*H / (t_fwd + t_bwd) of ONE call, the median of >= 50 calls
         # after 10 warm-up, HIP events on the stream the calls run on
-        for _ in range(10):
-            view()
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(50)]
-        for a, b in evs:
-            a.record()
-            view()
-            b.record()
-        torch.cuda.synchronize()
-        t_ms = sorted(a.elapsed_time(b) for a, b in evs)
-        med = t_ms[len(t_ms) // 2]
-        single = {"median_ms": round(med, 4), "p10_ms": round(t_ms[5], 4), "p90_ms": round(t_ms[45], 4),
-                  "calls": len(t_ms), "value": round(W * H / (med * 1e-3) / 1e6, 3), "unit": "MPix/s",
-                  "what": "one rasterizer forward + backward call pair, median of 50 (HIP events, 10 warm-up)"}
+        single = single_call_median(view, W, H)
         if not args.no_minibatch and not (V == 4 and NS == 3):  # (the timed step already is this layout)
             # a 4-view mini-batch of DISTINCT cameras on 3 HIP streams: one view's latency-bound
             # geometry passes overlap another's tile passes (throughput, not the reference's pattern)
-            mcams = [scenes.view_camera(cam, k).to(dev) for k in range(4)]
+            mcams = [scenes.view_camera(cam, k, look=cfg.get("look")).to(dev) for k in range(4)]
             mm = [(c.world_view_transform, c.full_proj_transform, c.camera_center) for c in mcams]
             ss = [torch.cuda.Stream(dev) for _ in range(3)]
             saved = list(mats)
@@ -858,57 +1013,8 @@ def main():
             mini = {"ms_per_4_views": round(mms, 4), "value": round(4 * W * H / (mms * 1e-3) / 1e6, 3),
                     "unit": "MPix/s", "what": "4 distinct cameras of the same scene per step, alternating over 3 "
                                               "HIP streams"}
-    dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
-    achieved_gbs = dom_bytes / (dom[1] * 1e-3) / 1e9
     workload = (f"ply {os.path.basename(args.ply)}" if args.ply else args.config) + f": {P} Gaussians SH{deg}, {W}x{H}"
-    traffic, traffic_src = pmc_traffic(dom[0], workload)
-    hbm = {"achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-           "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes": "algorithmic (SURVEY §8d per-stage figure x "
-                                                                   "this launch's measured P, P_v, R)",
-           "algorithmic_bytes_per_launch": int(dom_bytes),
-           "traffic": None if traffic is None else int(traffic), "traffic_source": traffic_src}
-    ub = unique_bytes(dom[0], P, Pv, R, T, W * H, M)
-    if ub is not None:
-        hbm["unique_bytes_per_launch"] = int(ub)
-        hbm["unique_frac"] = round(ub / (dom[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
-    kinfo, ksrc = pmc_kernel(dom[0], workload)
-    if kinfo.get("valu_insts") and dom[0].startswith("render"):
-        # The tile passes are bound by VALU issue (the PMC counters show their HBM traffic at
-        # ~0.3x the algorithmic bytes): instruction throughput against the spec issue rate,
-        # 1024 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction (MI355X_MICROARCH.md).
-        n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        peak = n_simd * VALU_CLOCK_GHZ / VALU_CYCLES_PER_INST
-        ach = kinfo["valu_insts"] / (dom[1] * 1e-3) / 1e9
-        roofline = {"bound": "valu", "achieved": round(ach, 1), "peak": round(peak, 1), "unit": "Gwave-inst/s",
-                    "frac": round(ach / peak, 4), "traffic": hbm["traffic"], "kernel": dom[0],
-                    "avg_launch_ms": round(dom[1], 4), "valu_insts_per_launch": int(kinfo["valu_insts"]),
-                    "valu_source": ksrc,
-                    "peak_basis": f"{n_simd} SIMDs x {VALU_CLOCK_GHZ} GHz / {VALU_CYCLES_PER_INST} cycles per "
-                                  "wave64 VALU instruction (spec issue rate)",
-                    "hbm": hbm}
-        if kinfo.get("salu_insts"):
-            # the scalar instructions the same waves issue (mask logic, walk bookkeeping,
-            # branches): a co-bound, DESIGN.md §3 (an added SALU op per evaluation costs more
-            # than an added VALU op)
-            roofline["salu_insts_per_launch"] = int(kinfo["salu_insts"])
-            roofline["salu_per_valu"] = round(kinfo["salu_insts"] / kinfo["valu_insts"], 3)
-    elif dom[0].startswith("render"):
-        # a tile pass with no committed instruction count for this workload: its bound is VALU
-        # issue, and the HBM fraction of its algorithmic bytes is not a roofline
-        # (the R x 40 record reads are served from LDS/L2), so no fraction is claimed
-        roofline = {"bound": "valu", "achieved": None, "peak": None, "unit": "Gwave-inst/s", "frac": None,
-                    "traffic": hbm["traffic"], "kernel": dom[0], "avg_launch_ms": round(dom[1], 4),
-                    "frac_null_reason": f"no committed rocprofv3 SQ_INSTS_VALU pass of workload '{workload}' "
-                                        "(profiles/r*_hbm_traffic.json)", "hbm": hbm}
-    else:
-        roofline = {"bound": "hbm", "achieved": hbm["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": hbm["frac"], "traffic": hbm["traffic"], "kernel": dom[0],
-                    "avg_launch_ms": round(dom[1], 4), "hbm": hbm}
-    if roofline["bound"] == "hbm" and roofline["frac"] is not None and roofline["frac"] > 1.0:
-        # more algorithmic bytes per second than HBM delivers: part of them came from a cache,
-        # so the figure is no HBM fraction
-        roofline.update(frac=None, frac_null_reason="algorithmic bytes / launch time exceed the HBM peak (served "
-                                                    "from L2 / Infinity Cache)")
+    roofline = tile_roofline(dom, P, Pv, R, T, W, H, M, workload, dev)
     out = {
         "metric": METRIC, "value": round(world * V * W * H / (ms * 1e-3) / 1e6, 3), "unit": "MPix/s",
         "n_gpus": world, "ranks_joined": joined, "steps": args.steps, "warmup": args.warmup,
@@ -927,7 +1033,7 @@ def main():
                    "parallelism": f"views x{world}" + (f" ({backend})" if backend else "")},
         "roofline": roofline,
         "stage_ms": per_stage,
-        "stage_ms_source": "3 views one at a time on one stream before the timed region (HIP events around every "
+        "stage_ms_source": f"{STAGE_VIEWS} views one at a time on one stream before the timed region (HIP events around every "
                            "stage); roofline.avg_launch_ms is the dominant stage's events over "
                            f"{ev_steps} steps' views run one at a time on one stream right after the timed region",
     }
@@ -945,6 +1051,10 @@ def main():
         state.pop("buckets", None)
         out["train"] = train_leg(args, dev, dist, rank, world, backend,
                                  args.train_steps or min(args.steps, 20), max(3, min(args.warmup, 10)))
+    if rank == 0 and world == 1 and args.config == "cfg2" and not args.no_clustered and not args.ply:
+        # the same size on a Trevi-class clustered cloud (culling, heavy tiles, sky band)
+        out["clustered"] = clustered_leg(args, dev)
+        torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_relit and not args.ply:
         # BASELINE configs[2] and configs[4] at their sizes, timed by the same run: the relight
         # render with backward (cfg3: 1M + 0.1M sky Gaussians at 1080p; cfg5: 4.55M + 0.45M at 4K)

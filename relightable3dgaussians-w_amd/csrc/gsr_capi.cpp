@@ -665,6 +665,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         gsr::TileOrderArgs ord{};
         ord.ntile = (unsigned)T; ord.gx = gx; ord.gsx = gsx; ord.order = at<uint32_t>(img, il.order_fwd);
         ord.nheavy = at<uint32_t>(img, il.nheavy); ord.heavy_bits = gsr::FWD_HEAVY_BITS;
+        ord.heavy_rel8 = GSR_FWD_HEAVY_REL8;
         ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
@@ -955,7 +956,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s,  // det: one writer per row
-                                   at<uint32_t>(img, il.row_cost), gy);
+                                   at<uint32_t>(img, il.row_cost), gy, det ? 0 : GSR_BWD_HEAVY_REL8);
         }
         {
             GSR_STAGE(ST_RENDER_BWD);  // the tile pass alone (roofline.avg_launch_ms in bench.py)

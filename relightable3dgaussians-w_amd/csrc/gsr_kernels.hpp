@@ -117,6 +117,7 @@ struct TileOrderArgs {
     uint32_t* order;
     uint32_t* nheavy;
     int heavy_bits;
+    int heavy_rel8;  // also heavy: cost >= heavy_rel8 / 8 x the band's mean (0: absolute threshold only)
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
     // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
@@ -190,10 +191,22 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
 // cost >= 2^heavy_bits.
 // row_cost [nrows] (optional): the forward's summed cost per tile row (the balanced bands)
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0);
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0,
+                       int heavy_rel8 = 0);
 
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
+// ... or a cost >= REL8 / 8 x the band's mean tile cost (gsr_order.hpp; 0 = off).  Off: on the
+// clustered cfg2c frame splitting the tiles above 2x / 3x the band mean (64-256 per band) made
+// both tile passes slower (render_bwd 494 -> 535 / 592 us at 2x with 64 / 128 per band, 497 at
+// 3x with 256; render_fwd 400 -> 399 / 421 / 464 us): a quadrant unit redoes the list filter,
+// the culling and (backward) the per-survivor reduction (profiles/r5e_heavy_split_ab.txt)
+#ifndef GSR_FWD_HEAVY_REL8
+#define GSR_FWD_HEAVY_REL8 0
+#endif
+#ifndef GSR_BWD_HEAVY_REL8
+#define GSR_BWD_HEAVY_REL8 0
+#endif
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 // The tile passes read each tile's list from its super-tile's entries (TileList):

@@ -130,19 +130,25 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
     } else {
         band_of(band, a.ntile, lo, len);
     }
+    __shared__ unsigned long long s_band_cost;
     for (int i = threadIdx.x; i < NBUCKET; i += blockDim.x) hist[i] = 0;
+    if (threadIdx.x == 0) s_band_cost = 0ull;
     if (a.zero_rows && band == 0)
         for (unsigned i = threadIdx.x; i < a.nrows; i += blockDim.x) a.zero_rows[i] = 0u;
     __syncthreads();
+    unsigned long long csum = 0ull;
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
         const unsigned t = lo + i;
-        atomicAdd(&hist[cost_bucket(tile_cost(t, a))], 1u);
+        const uint32_t c = tile_cost(t, a);
+        csum += c;
+        atomicAdd(&hist[cost_bucket(c)], 1u);
         if (a.zero_a) {
             a.zero_a[t] = 0u;
             a.zero_b[t] = 0u;
             if (a.zero_c) a.zero_c[t] = 0u;
         }
     }
+    if (csum) atomicAdd(&s_band_cost, csum);
     __syncthreads();
     // cur[b] = tiles in buckets above b (heaviest bucket first): a block scan over the
     // buckets in descending order, thread j holding bucket NBUCKET - 1 - j -- wave scans and one
@@ -165,8 +171,15 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int hb = bucket_heavy_from(a.heavy_bits);
-        a.nheavy[band] = hb < NBUCKET ? cur[hb] + hist[hb] : 0u;  // cost >= 2^heavy_bits
+        // heavy: cost >= 2^heavy_bits, or >= heavy_rel8 / 8 x the band's mean tile cost (a
+        // clustered frame's heavy tiles measured against the frame, not an absolute list length)
+        int hb = bucket_heavy_from(a.heavy_bits);
+        if (a.heavy_rel8 && len) {
+            const unsigned long long thr = (s_band_cost * a.heavy_rel8 + 8ull * len - 1) / (8ull * len);
+            const int hr = cost_bucket((uint32_t)min(thr, 0xffffffffull));
+            hb = hr > 0 && hr < hb ? hr : hb;
+        }
+        a.nheavy[band] = hb < NBUCKET ? cur[hb] + hist[hb] : 0u;
     }
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {

@@ -24,7 +24,8 @@ namespace gsr {
 
 #ifdef GSR_RENDER_STATS
 __device__ unsigned long long g_bwd_stats[8];
-__device__ unsigned long long g_bwd_times[4 * 65536];  // per tile: start, end (s_memrealtime), hw id, largest n_contrib
+// per unit (workgroup): start, end (s_memrealtime), hw id, tile, quadrant mask, largest n_contrib, survivors, -
+__device__ unsigned long long g_bwd_times[GSR_UNIT_REC * 65536];
 #ifdef GSR_TIMES_ONLY  // per-tile timing only (tools/xcd_balance.py): no per-evaluation counters
 #define BWD_STAT(k, v)
 #else
@@ -84,6 +85,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
 #ifdef GSR_RENDER_STATS
     unsigned long long st[8] = {};
+    uint32_t nsurv = 0;
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     // the tile's list back to front from its last contributor (the forward's tile_emax and
@@ -121,6 +123,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nb);
         BWD_STAT(1, __popcll(todo));
+#ifdef GSR_RENDER_STATS
+        nsurv += __popcll(todo);
+#endif
         if (!todo) continue;
         // one survivor (record A, B, Cq at batch slot k), back to front
         auto grad_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
@@ -219,12 +224,16 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {
         for (int k = 0; k < 6; k++) atomicAdd(&g_bwd_stats[k], st[k]);
-        if (tile < 65536 && qallow == 15u) {
-            g_bwd_times[4 * tile] = t_start;
-            g_bwd_times[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();
-            g_bwd_times[4 * tile + 3] = nmax;
-            g_bwd_times[4 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
-                                        ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+        if (blockIdx.x < 65536) {
+            unsigned long long* u = g_bwd_times + GSR_UNIT_REC * blockIdx.x;
+            u[0] = t_start;
+            u[1] = __builtin_amdgcn_s_memrealtime();
+            u[2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+            u[3] = tile;
+            u[4] = qallow;
+            u[5] = nmax;
+            u[6] = nsurv;
         }
     }
 #endif
@@ -251,8 +260,14 @@ k_render_bwd(RenderBwdArgs a) {
 }
 
 #ifdef GSR_RENDER_STATS
+// zero the per-unit records (blocks without a unit write none)
+extern "C" int gsr_debug_bwd_times_reset() {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_bwd_times)) != hipSuccess) return -1;
+    return hipMemset(p, 0, sizeof(g_bwd_times)) == hipSuccess ? 0 : -1;
+}
 extern "C" int gsr_debug_bwd_times(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_times), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_times), sizeof(unsigned long long) * GSR_UNIT_REC * n) == hipSuccess ? 0 : -1;
 }
 extern "C" int gsr_debug_bwd_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stats), sizeof(g_bwd_stats)) != hipSuccess) return -1;

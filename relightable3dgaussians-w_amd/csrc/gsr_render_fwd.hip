@@ -25,7 +25,8 @@ namespace gsr {
 
 #ifdef GSR_RENDER_STATS
 __device__ unsigned long long g_fwd_stats[8];
-__device__ unsigned long long g_fwd_times[4 * 65536];  // per tile: start, end (s_memrealtime), hw id, cost estimate
+// per unit (workgroup): start, end (s_memrealtime), hw id, tile, quadrant mask, cost estimate, evaluations, -
+__device__ unsigned long long g_fwd_times[GSR_UNIT_REC * 65536];
 #ifdef GSR_TIMES_ONLY  // per-tile timing only (tools/xcd_balance.py): no per-evaluation counters
 #define FWD_STAT(k, v)
 #else
@@ -171,12 +172,16 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {
         for (int k = 0; k < 7; k++) atomicAdd(&g_fwd_stats[k], st[k]);
-        if (tile < 65536 && qallow == 15u) {
-            g_fwd_times[4 * tile] = t_start;
-            g_fwd_times[4 * tile + 1] = __builtin_amdgcn_s_memrealtime();
-            g_fwd_times[4 * tile + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
-                                        ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
-            g_fwd_times[4 * tile + 3] = a.st_ranges[sti].y - a.st_ranges[sti].x;
+        if (blockIdx.x < 65536) {
+            unsigned long long* u = g_fwd_times + GSR_UNIT_REC * blockIdx.x;
+            u[0] = t_start;
+            u[1] = __builtin_amdgcn_s_memrealtime();
+            u[2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                   ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+            u[3] = tile;
+            u[4] = qallow;
+            u[5] = a.st_ranges[sti].y - a.st_ranges[sti].x;
+            u[6] = nev;
         }
     }
 #endif
@@ -220,8 +225,14 @@ k_render_fwd(RenderFwdArgs a) {
 }
 
 #ifdef GSR_RENDER_STATS
+// zero the per-unit records (blocks without a unit write none)
+extern "C" int gsr_debug_fwd_times_reset() {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_fwd_times)) != hipSuccess) return -1;
+    return hipMemset(p, 0, sizeof(g_fwd_times)) == hipSuccess ? 0 : -1;
+}
 extern "C" int gsr_debug_fwd_times(unsigned long long* out, int n) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_times), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_times), sizeof(unsigned long long) * GSR_UNIT_REC * n) == hipSuccess ? 0 : -1;
 }
 extern "C" int gsr_debug_fwd_stats(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fwd_stats), sizeof(g_fwd_stats)) != hipSuccess) return -1;

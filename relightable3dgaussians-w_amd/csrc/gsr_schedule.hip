@@ -25,10 +25,11 @@ void launch_tile_order_args(const TileOrderArgs& a, hipStream_t s) {
 }
 
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows) {
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows, int heavy_rel8) {
     if (ntile == 0) return;
     TileOrderArgs a{};
     a.ntile = ntile; a.ranges = ranges; a.cost = cost; a.order = order; a.nheavy = nheavy; a.heavy_bits = heavy_bits;
+    a.heavy_rel8 = heavy_rel8;
     a.row_cost = row_cost; a.nrows = nrows;
     a.balance = GSR_BAL_BANDS;  // the backward passes' bands (tile_unit ... bal)
     if (a.balance) hipLaunchKernelGGL(k_tile_order<true>, dim3(8), dim3(512), 0, s, a);

@@ -27,7 +27,12 @@ __device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, un
 // mask; false when the block has nothing to do.  (Four-wave workgroups holding a heavy
 // tile's quadrants measured slower on balanced scenes: a workgroup waits for four free wave
 // slots on one CU, so single waves cannot backfill.)
-constexpr unsigned HEAVY_CAP = 64;  // split heavy tiles per band
+#ifndef GSR_HEAVY_CAP
+#define GSR_HEAVY_CAP 64
+#endif
+constexpr unsigned HEAVY_CAP = GSR_HEAVY_CAP;  // split heavy tiles per band
+// words per unit in the instrumented builds' timing records (g_fwd_times / g_bwd_times)
+#define GSR_UNIT_REC 8
 #ifndef GSR_FWD_TAIL
 #define GSR_FWD_TAIL 128
 #endif

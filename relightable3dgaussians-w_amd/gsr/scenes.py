@@ -97,12 +97,15 @@ def focal_camera(W, H, focal, **kw):
     return make_camera(W, H, 2 * math.atan(W / (2 * focal)), 2 * math.atan(H / (2 * focal)), **kw)
 
 
-def look_at_rotation(cam_pos, target):
+def look_at_rotation(cam_pos, target, upright=False):
     """World->camera rotation R (COLMAP convention: R is stored as camera->world
-    columns transposed by getWorld2View2) looking from cam_pos to target, y down."""
+    columns transposed by getWorld2View2) looking from cam_pos to target.  upright: the
+    image's down axis is world +y (COLMAP's down), so world-up content lands at the top of the
+    frame (cfg2c).  The default keeps the rolled frame every earlier scene and fixture was made
+    with (camera y = world -y: the image is rotated 180 degrees about the view axis)."""
     f = np.asarray(target, np.float64) - np.asarray(cam_pos, np.float64)
     f /= np.linalg.norm(f)
-    up = np.array([0.0, -1.0, 0.0])
+    up = np.array([0.0, 1.0 if upright else -1.0, 0.0])
     r = np.cross(up, f)
     if np.linalg.norm(r) < 1e-6:
         r = np.array([1.0, 0.0, 0.0])
@@ -116,14 +119,21 @@ def look_at_rotation(cam_pos, target):
     return R, T
 
 
-def view_camera(cam, k):
+def view_camera(cam, k, look=None):
     """View k of a multi-view run over one scene: k = 0 is `cam` itself, k > 0 a
     deterministic nearby camera (offset up to +-0.15 and looking at a point 10 units ahead,
     jittered by +-0.2), same intrinsics.  Distinct views of the same Gaussians for the
-    mini-batch and data-parallel benchmarks."""
+    mini-batch and data-parallel benchmarks.  ``look`` = dict(pos, target) of the scene's base
+    camera (cfg2c): views k > 0 then stand within +-0.5 of pos and look at target +-0.5."""
     if k == 0:
         return cam
     rng = np.random.default_rng(100 + k)
+    if look is not None:
+        pos = np.asarray(look["pos"], np.float64) + rng.uniform(-0.5, 0.5, 3)
+        target = np.asarray(look["target"], np.float64) + rng.uniform(-0.5, 0.5, 3)
+        R, T = look_at_rotation(pos, target, upright=True)
+        return make_camera(cam.image_width, cam.image_height, cam.FoVx, cam.FoVy, R=R, T=T,
+                           device=cam.world_view_transform.device)
     pos = rng.uniform(-0.15, 0.15, 3)
     target = np.array([rng.uniform(-0.2, 0.2), rng.uniform(-0.2, 0.2), 10.0])
     R, T = look_at_rotation(pos, target)
@@ -167,12 +177,172 @@ def synthetic_gaussians(P, W, H, tanfovx, tanfovy, sh_degree=0, seed=0, zrange=(
     return {k: v.to(device=device, dtype=dtype).contiguous() for k, v in out.items()}
 
 
+def _rotmat_to_quat(Rm):
+    """Unit quaternions (r, x, y, z) whose build_rotation (general_utils.py:98-119) is ``Rm``
+    [N,3,3] (Shepperd's method, float64)."""
+    m = Rm
+    tr = m[:, 0, 0] + m[:, 1, 1] + m[:, 2, 2]
+    q = np.empty((m.shape[0], 4))
+    cands = np.stack([tr, m[:, 0, 0], m[:, 1, 1], m[:, 2, 2]], 1)
+    k = np.argmax(cands, 1)
+    for i in range(4):
+        s = k == i
+        if not s.any():
+            continue
+        a = m[s]
+        if i == 0:
+            t = np.sqrt(1.0 + tr[s]) * 2
+            q[s] = np.stack([0.25 * t, (a[:, 2, 1] - a[:, 1, 2]) / t, (a[:, 0, 2] - a[:, 2, 0]) / t,
+                             (a[:, 1, 0] - a[:, 0, 1]) / t], 1)
+        elif i == 1:
+            t = np.sqrt(1.0 + a[:, 0, 0] - a[:, 1, 1] - a[:, 2, 2]) * 2
+            q[s] = np.stack([(a[:, 2, 1] - a[:, 1, 2]) / t, 0.25 * t, (a[:, 0, 1] + a[:, 1, 0]) / t,
+                             (a[:, 0, 2] + a[:, 2, 0]) / t], 1)
+        elif i == 2:
+            t = np.sqrt(1.0 + a[:, 1, 1] - a[:, 0, 0] - a[:, 2, 2]) * 2
+            q[s] = np.stack([(a[:, 0, 2] - a[:, 2, 0]) / t, (a[:, 0, 1] + a[:, 1, 0]) / t, 0.25 * t,
+                             (a[:, 1, 2] + a[:, 2, 1]) / t], 1)
+        else:
+            t = np.sqrt(1.0 + a[:, 2, 2] - a[:, 0, 0] - a[:, 1, 1]) * 2
+            q[s] = np.stack([(a[:, 1, 0] - a[:, 0, 1]) / t, (a[:, 0, 2] + a[:, 2, 0]) / t,
+                             (a[:, 1, 2] + a[:, 2, 1]) / t, 0.25 * t], 1)
+    return q / np.linalg.norm(q, axis=1, keepdims=True)
+
+
+def _frames(normals, rng):
+    """Orthonormal frames [N,3,3] whose third column is ``normals`` and whose first two are a
+    random in-plane pair."""
+    n = normals / np.linalg.norm(normals, axis=1, keepdims=True)
+    helper = np.where(np.abs(n[:, 1:2]) < 0.9, np.array([[0.0, 1.0, 0.0]]), np.array([[1.0, 0.0, 0.0]]))
+    t1 = np.cross(helper, n)
+    t1 /= np.linalg.norm(t1, axis=1, keepdims=True)
+    t2 = np.cross(n, t1)
+    a = rng.uniform(0, 2 * np.pi, n.shape[0])[:, None]
+    u, v = np.cos(a) * t1 + np.sin(a) * t2, -np.sin(a) * t1 + np.cos(a) * t2
+    return np.stack([u, v, n], 2)
+
+
+def _trained_opacity(rng, n, lo_frac=0.15, mid_frac=0.25):
+    """Opacities skewed high as after training (most surface splats near 1, a tail of
+    translucent ones; the reference prunes below 0.005, gaussian_model.py:610-624)."""
+    u = rng.uniform(0, 1, n)
+    hi = rng.uniform(0.9, 0.995, n)
+    mid = rng.uniform(0.4, 0.9, n)
+    lo = rng.uniform(0.01, 0.4, n)
+    return np.where(u < lo_frac, lo, np.where(u < lo_frac + mid_frac, mid, hi))
+
+
+TREVI_CAMERA = dict(pos=(0.0, 0.0, 0.0), target=(0.0, -2.5, 20.0))
+
+
+def trevi_like_gaussians(P, sh_degree=3, seed=0):
+    """A Trevi-class clustered cloud (cfg2c; VERDICT r4 "Next" item 1): ``P`` Gaussians, 90 % on
+    surface sheets and clusters of a facade scene seen from a plaza, 10 % on the reference's sky
+    shell.  COLMAP axes (+y down), camera at the origin looking at (0, -2.5, 20) (TREVI_CAMERA):
+
+      * facade (50 % of the foreground): a 32 x 9.6 m wall at z ~ 20 with column relief, density
+        gradient towards the centre and the bottom (Beta-distributed x / y);
+      * ground (20 %): the plaza and basin at y = 1.6, z in [-6, 20] -- its near part lies behind
+        the camera or below the frame (culled);
+      * sculptures (18 %): 14 anisotropic 3D clusters in front of the facade centre, Zipf-sized
+        (the largest ~75k Gaussians): the dense tiles;
+      * water spray (7 %): a translucent volume (opacity 0.02-0.25) in front of the centre: the
+        long-list, late-saturating tiles;
+      * side buildings (5 %): sheets left and right, mostly outside the frustum;
+      * sky (10 % of P): sample_points_on_unit_hemisphere's band (general_utils.py:229-240;
+        y ~ -0.5 U, phi in [-pi/4, pi/4]) scaled by the 0.99-quantile distance of the foreground
+        from its mean and centred on the camera (get_sky_xyz_init, gaussian_model.py:211-230;
+        every band point projects above 2/3 of the frame), isotropic at the shell's point spacing
+        (distCUDA2's role, :249-250), opacity trained high.
+
+    Surface splats are flat (normal axis 0.15x the in-plane scales, in-plane scales 1.2x the
+    local point spacing with a log-normal spread).  Opacities follow _trained_opacity.  Returns
+    the rasterizer inputs plus ``is_sky`` (CPU float32 / bool tensors)."""
+    rng = np.random.default_rng(1000 + seed)
+    P_sky = P // 10
+    P_fg = P - P_sky
+    n_fac, n_gnd, n_scu, n_spr = int(0.50 * P_fg), int(0.20 * P_fg), int(0.18 * P_fg), int(0.07 * P_fg)
+    n_side = P_fg - n_fac - n_gnd - n_scu - n_spr
+    xyz, nrm, s_in, s_n, opa = [], [], [], [], []
+
+    def sheet(pts, normals, spacing, flat=0.15, op=None):
+        xyz.append(pts)
+        nrm.append(normals)
+        si = spacing * 2.0 * np.exp(rng.normal(0.0, 0.5, (pts.shape[0], 2)))
+        s_in.append(si)
+        s_n.append(si.min(1) * flat)
+        opa.append(_trained_opacity(rng, pts.shape[0]) if op is None else op)
+
+    # facade: x in [-16, 16], y in [-8, 1.6] (bottom denser), column relief in z
+    x = 16.0 * (2 * rng.beta(1.6, 1.6, n_fac) - 1)
+    y = 1.6 - 9.6 * rng.beta(1.2, 2.0, n_fac)
+    z = 20.0 - 0.6 * np.sin(x * 1.3) ** 8 + rng.normal(0, 0.08, n_fac)
+    sheet(np.stack([x, y, z], 1), np.tile([0.0, 0.0, -1.0], (n_fac, 1)) + rng.normal(0, 0.15, (n_fac, 3)),
+          math.sqrt(32 * 9.6 / n_fac))
+    # ground: the plaza / basin
+    x = rng.uniform(-18, 18, n_gnd)
+    z = -6.0 + 26.0 * rng.beta(1.0, 1.6, n_gnd)
+    y = 1.6 + rng.normal(0, 0.02, n_gnd)
+    sheet(np.stack([x, y, z], 1), np.tile([0.0, -1.0, 0.0], (n_gnd, 1)) + rng.normal(0, 0.1, (n_gnd, 3)),
+          math.sqrt(36 * 26 / n_gnd))
+    # sculptures: Zipf-sized anisotropic clusters
+    nc = 14
+    w = 1.0 / np.arange(1, nc + 1) ** 1.1
+    cnt = np.floor(w / w.sum() * n_scu).astype(np.int64)
+    cnt[0] += n_scu - cnt.sum()
+    for c in range(nc):
+        ctr = np.array([rng.uniform(-6, 6), rng.uniform(-3.5, 1.0), rng.uniform(16.5, 19.5)])
+        sig = rng.uniform(0.25, 1.0, 3) * np.array([1.0, 1.4, 0.6])
+        pts = ctr + rng.normal(0, 1, (cnt[c], 3)) * sig
+        vol = 4.0 / 3.0 * math.pi * float(np.prod(2 * sig))
+        sheet(pts, rng.normal(0, 1, (cnt[c], 3)), (vol / cnt[c]) ** (1.0 / 3.0), flat=0.3)
+    # water spray: translucent, small, in front of the centre
+    pts = np.stack([rng.normal(0, 1.2, n_spr), rng.uniform(-1.2, 1.6, n_spr), rng.normal(16.0, 0.9, n_spr)], 1)
+    sheet(pts, rng.normal(0, 1, (n_spr, 3)), 0.035, flat=0.6, op=rng.uniform(0.02, 0.25, n_spr))
+    # side buildings
+    side = np.where(rng.uniform(0, 1, n_side) < 0.5, -1.0, 1.0)
+    x = side * rng.uniform(16, 30, n_side)
+    pts = np.stack([x, rng.uniform(-10, 1.6, n_side), rng.uniform(6, 40, n_side)], 1)
+    sheet(pts, np.stack([-side, np.zeros(n_side), np.zeros(n_side)], 1) + rng.normal(0, 0.2, (n_side, 3)),
+          math.sqrt(14 * 11.6 * 34 * 2 / 14 / n_side))
+    fg = np.concatenate(xyz)
+    # the reference's sky band around the camera centre (the only camera)
+    dist = np.linalg.norm(fg - fg.mean(0), axis=1)
+    sky_distance = float(np.quantile(dist, 0.99))
+    yb = -0.5 * rng.uniform(0, 1, P_sky)
+    th = np.arccos(yb)
+    ph = 0.5 * np.pi * rng.uniform(0, 1, P_sky) - np.pi / 4
+    band = np.stack([np.sin(ph) * np.sin(th), yb, np.sin(th) * np.cos(ph)], 1)
+    sky = band * sky_distance + np.asarray(TREVI_CAMERA["pos"])
+    area = sky_distance ** 2 * (0.5 * np.pi) * 0.5
+    sp = math.sqrt(area / P_sky)
+    sky_s = sp * 1.5 * np.exp(rng.normal(0.0, 0.3, P_sky))
+    all_xyz = np.concatenate([fg, sky])
+    frames = _frames(np.concatenate(nrm), rng)
+    scales = np.concatenate([np.concatenate([np.concatenate(s_in), np.concatenate(s_n)[:, None]], 1),
+                             np.repeat(sky_s[:, None], 3, 1)])
+    q = np.concatenate([_rotmat_to_quat(frames), np.tile([1.0, 0.0, 0.0, 0.0], (P_sky, 1))])
+    opac = np.concatenate([np.concatenate(opa), rng.uniform(0.85, 0.99, P_sky)])[:, None]
+    K = (sh_degree + 1) ** 2
+    shs = rng.normal(0, 0.2, (P, K, 3))
+    shs[:, 0, :] = rgb2sh(rng.uniform(0, 1, (P, 3)))
+    colors = rng.uniform(0, 1, (P, 3))
+    is_sky = np.zeros(P, bool)
+    is_sky[P_fg:] = True
+    out = dict(means3D=all_xyz, scales=scales, rotations=q, opacities=opac, shs=shs, colors=colors)
+    out = {k: torch.from_numpy(np.ascontiguousarray(v, dtype=np.float32)) for k, v in out.items()}
+    out["is_sky"] = torch.from_numpy(is_sky)
+    return out
+
+
 CONFIGS = {
     # name: (P, W, H, sh_degree, camera builder, gaussian kwargs)
     "cfg1": dict(P=10_000, W=256, H=256, sh_degree=0, fov=math.radians(60.0), zrange=(2.0, 8.0), log_z=False,
                  scale_mode="cfg1"),
     "cfg2": dict(P=1_500_000, W=1920, H=1080, sh_degree=3, focal=1400.0, zrange=(1.0, 30.0), log_z=True,
                  scale_mode="cfg2"),
+    # cfg2's size on a Trevi-class clustered cloud (trevi_like_gaussians)
+    "cfg2c": dict(P=1_500_000, W=1920, H=1080, sh_degree=3, focal=1400.0, clustered=True, look=TREVI_CAMERA),
     "cfg5": dict(P=5_000_000, W=3840, H=2160, sh_degree=3, focal=2800.0, zrange=(1.0, 30.0), log_z=True,
                  scale_mode="cfg2"),
 }
@@ -186,6 +356,12 @@ def build_config(name, device="cpu", seed=0, P=None, W=None, H=None):
         c["W"] = W
     if H is not None:
         c["H"] = H
+    if c.get("clustered"):
+        R, T = look_at_rotation(TREVI_CAMERA["pos"], TREVI_CAMERA["target"], upright=True)
+        cam = focal_camera(c["W"], c["H"], c["focal"], R=R, T=T, device=device)
+        gs = trevi_like_gaussians(c["P"], c["sh_degree"], seed=seed)
+        gs = {k: v.to(device) for k, v in gs.items()}
+        return cam, gs, c
     if "fov" in c:
         cam = make_camera(c["W"], c["H"], c["fov"], c["fov"], device=device)
     else:

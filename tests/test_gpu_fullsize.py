@@ -38,12 +38,12 @@ def cfg2():
     return _build("cfg2")
 
 
-@pytest.fixture(scope="module", params=["cfg2", "cfg5"])
+@pytest.fixture(scope="module", params=["cfg2", "cfg2c", "cfg5"])
 def full(request, cfg2):
     if request.param == "cfg2":
         yield cfg2
     else:
-        data = _build("cfg5")
+        data = _build(request.param)
         yield data
         del data
 
@@ -111,8 +111,14 @@ def test_cfg2_binning_invariants(cfg2):
     assert inside.all(), inside.mean()
 
 
-def _sample_tiles(gx, gy, seed=5):
-    return np.random.default_rng(seed).choice(gx * gy, size=TILE_SAMPLE, replace=False).astype(np.int32)
+def _sample_tiles(gx, gy, seed=5, ranges=None, heaviest=8):
+    """TILE_SAMPLE random tiles; with ``ranges``, plus the ``heaviest`` tiles by list length (the
+    clustered scene's heavy tiles take the quadrant-split paths of both tile passes)."""
+    t = np.random.default_rng(seed).choice(gx * gy, size=TILE_SAMPLE, replace=False)
+    if ranges is not None:
+        lens = ranges[:, 1].astype(np.int64) - ranges[:, 0]
+        t = np.union1d(t, np.argsort(-lens, kind="stable")[:heaviest])
+    return t.astype(np.int32)
 
 
 def _tile_mask(tiles, gx, W, H):
@@ -127,7 +133,7 @@ def test_full_sampled_tiles_forward(full):
     cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    tiles = _sample_tiles(gx, gy)
+    tiles = _sample_tiles(gx, gy, ranges=st["ranges"])
     rec = st["rec"]
     out, fT, nc = orc.render_fwd(st["ranges"], st["point_list"], rec[:, 0:2], rec[:, 6:9], rec[:, 2:6],
                                  np.zeros(3, np.float32), W, H, tiles=tiles)
@@ -136,7 +142,11 @@ def test_full_sampled_tiles_forward(full):
     assert rel_l2(color[:, m], out[:, m]) <= 1e-6
     # measured: no blend decision differs (tools/parity_margins.py, profiles/r2_parity_margins.log)
     np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
-    assert np.abs(color[:, m] - out[:, m]).max() <= 1e-6
+    # per-pixel rounding grows with the blended count: cfg2/cfg5 pixels blend ~100 Gaussians,
+    # cfg2c's spray and sculpture tiles ~1.5k (its largest difference measured 2.2e-6); both
+    # bars sit far inside north_star's 1e-4 relative
+    bar = 1e-5 if c.get("clustered") else 1e-6
+    assert np.abs(color[:, m] - out[:, m]).max() <= bar
     assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
 
 
@@ -145,7 +155,7 @@ def test_full_sampled_tiles_backward(full):
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
     P = gs["means3D"].shape[0]
-    tiles = _sample_tiles(gx, gy)
+    tiles = _sample_tiles(gx, gy, ranges=st["ranges"])
     m = _tile_mask(tiles, gx, W, H)
     dout = np.random.default_rng(9).standard_normal((3, H, W)).astype(np.float32) * m[None]
     g = _grads(cam, gs, st, torch.tensor(dout, device="cuda"), c["sh_degree"])
@@ -383,7 +393,11 @@ def test_cfg3_relit_render_at_size():
     assert np.abs(out[:, m]).max() > 0.05  # the sampled tiles are lit
     assert rel_l2(color[:, m], out[:, m]) <= 1e-6
     np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
-    assert np.abs(color[:, m] - out[:, m]).max() <= 1e-6
+    # per-pixel rounding grows with the blended count: cfg2/cfg5 pixels blend ~100 Gaussians,
+    # cfg2c's spray and sculpture tiles ~1.5k (its largest difference measured 2.2e-6); both
+    # bars sit far inside north_star's 1e-4 relative
+    bar = 1e-5 if c.get("clustered") else 1e-6
+    assert np.abs(color[:, m] - out[:, m]).max() <= bar
     assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
     del st
     img_errs, errs, errs2, o_f = _fused_vs_calls(scene, view, light_leaves, bg, fix_sky=True)

@@ -50,14 +50,15 @@ def main(cfg="cfg2"):
                      "survivors_reaching_all_quadrants": (v[5] / max(v[6], 1)) if name == "fwd" else None,
                      "queue_wait_us_total": v[6] / 100.0 if name == "bwd" else None,
                      "tiles_via_queue": v[7] if name == "bwd" else None}
-    n = T
-    tb = (C.c_ulonglong * (4 * n))()
+    n = 65536  # per-unit records (GSR_UNIT_REC words each)
+    tb = (C.c_ulonglong * (8 * n))()
     import numpy as np
     if os.environ.get("GSR_STATS_DUMP"):
         L.gsr_debug_fwd_times(tb, n)
-        np.save(os.environ["GSR_STATS_DUMP"] + "_fwd.npy", np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64))
+        np.save(os.environ["GSR_STATS_DUMP"] + "_fwd.npy", np.frombuffer(tb, dtype=np.uint64).reshape(n, 8).astype(np.int64))
     L.gsr_debug_bwd_times(tb, n)
-    t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64)
+    t = np.frombuffer(tb, dtype=np.uint64).reshape(n, 8).astype(np.int64)
+    t = t[t[:, 1] > 0]
     st, en, hw = t[:, 0], t[:, 1], t[:, 2]
     if os.environ.get("GSR_STATS_DUMP"):
         np.save(os.environ["GSR_STATS_DUMP"] + "_bwd.npy", t)

@@ -47,8 +47,8 @@ def main(cfg="cfg2", calls=4):
     bg = torch.zeros(3, device=dev)
     vm, pm, cp = cam.world_view_transform.to(dev), cam.full_proj_transform.to(dev), cam.camera_center.to(dev)
     L = _lib.lib()
-    n = ((W + 15) // 16) * ((H + 15) // 16)
-    tb = (C.c_ulonglong * (4 * n))()
+    n = 65536  # per-unit records (GSR_UNIT_REC words each)
+    tb = (C.c_ulonglong * (8 * n))()
     dout = torch.randn(3, H, W, device=dev)
     for call in range(int(calls)):
         R, color, radii, geom, binb, img = _C.rasterize_gaussians(bg, g["means3D"], e, g["opacities"], g["scales"],
@@ -56,12 +56,12 @@ def main(cfg="cfg2", calls=4):
                                                                   cam.tanfovy, H, W, g["shs"], deg, cp, False)
         torch.cuda.synchronize()
         L.gsr_debug_fwd_times(tb, n)
-        tf = np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64).copy()
+        tf = np.frombuffer(tb, dtype=np.uint64).reshape(n, 8).astype(np.int64).copy()
         _C.rasterize_gaussians_backward(bg, g["means3D"], radii, e, g["scales"], g["rotations"], 1.0, e, vm, pm,
                                         cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb, img)
         torch.cuda.synchronize()
         L.gsr_debug_bwd_times(tb, n)
-        tw = np.frombuffer(tb, dtype=np.uint64).reshape(n, 4).astype(np.int64).copy()
+        tw = np.frombuffer(tb, dtype=np.uint64).reshape(n, 8).astype(np.int64).copy()
         for name, t in (("fwd", tf), ("bwd", tw)):
             ends, durs, bal = per_xcd(t)
             print(f"call {call} {name}: makespan {ends.max():.0f} us, balanced {bal:.0f} us | ends "
