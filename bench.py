@@ -528,8 +528,10 @@ def train_leg(args, dev, dist, rank, world, backend, steps, warmup):
     _lib.profile_enable(False)
     live = _lib.profile_read(reset=True)
     _lib.profile_stages(None)
-    radii = dgr.last_channels_call["radii"]
-    stats = dict(P=scene.P, P_fg=P_fg, Pv=int((radii > 0).sum().item()), R=int(dgr.last_channels_call["num_rendered"]),
+    dgr.record_channels_calls(True)  # one more iteration for the measured R and P_v (after the events)
+    train.train_step(scene, my_views, mine, my_gts, world=world, streams=None)
+    dgr.record_channels_calls(False)
+    stats = dict(P=scene.P, P_fg=P_fg, Pv=int(dgr.last_channels_call["visible"]), R=int(dgr.last_channels_call["num_rendered"]),
                  T=((W + 15) // 16) * ((H + 15) // 16), Npix=W * H, V=vpr, n_params=scene.fp.n)
     roof = train_roofline(live, stats, ms, ev_iters)
     return {"value": round(1e3 / ms, 3), "unit": "iters/s", "ms_per_iter": round(ms, 4), "steps": steps,

@@ -22,6 +22,7 @@
  *                      colour, depth; gaussian_renderer/__init__.py:120-200) fused into
  *                      the composite's feature rows
  *   gsr_adam_step      torch.optim.Adam.step over the per-Gaussian param groups
+ *   gsr_adam_step_range  the same over one element range (the pipelined data-parallel step)
  *                      (train.py:191, relit3DGW_model.py:149) as one fused launch over a
  *                      flat parameter buffer (the data-parallel training step)
  *   gsr_view_loss_forward / gsr_view_loss_backward
@@ -216,6 +217,13 @@ int gsr_relit_epilogue_backward(int width, int height, const float* cam12, const
 int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double* seg_lr, double beta1, double beta2,
                   double eps, int step, float grad_scale, float* param, const float* grad, float* exp_avg,
                   float* exp_avg_sq, void* stream);
+/* The same update over elements [lo, hi) only (lo a multiple of 4): the data-parallel step
+ * runs it chunk by chunk, each chunk right after its slice of the gradient all-reduce lands
+ * (gsr.dp.finish_step), so the update of chunk i overlaps the exchange of chunk i + 1.
+ * gsr_adam_step(...) == gsr_adam_step_range(n, 0, n, ...). */
+int gsr_adam_step_range(long long n, long long lo, long long hi, int nseg, const long long* seg_end,
+                        const double* seg_lr, double beta1, double beta2, double eps, int step, float grad_scale,
+                        float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* stream);
 
 /* SSIM of the training loss (utils/loss_utils.py:53-96: 11x11 Gaussian window, sigma 1.5,
  * zero padding, C1 = 0.01^2, C2 = 0.03^2) over img1, img2 [C,H,W].  window: the 11 normalised

@@ -28,12 +28,14 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
     p = p - s.step_size[k] * (m / denom);
 }
 
-__global__ void __launch_bounds__(256) k_adam(long long n, AdamSegs s, float* __restrict__ p,
+// elements [lo, hi) (lo a multiple of 4): the data-parallel step pipelines the update chunk by
+// chunk behind the gradient all-reduce (gsr.dp.finish_step)
+__global__ void __launch_bounds__(256) k_adam(long long lo, long long hi, AdamSegs s, float* __restrict__ p,
                                               const float* __restrict__ g, float* __restrict__ m,
                                               float* __restrict__ v) {
-    const long long n4 = n >> 2;
+    const long long q0 = lo >> 2, q1 = hi >> 2;
     const long long stride = (long long)gridDim.x * blockDim.x;
-    for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += stride) {
+    for (long long q = q0 + (long long)blockIdx.x * blockDim.x + threadIdx.x; q < q1; q += stride) {
         float4 P = reinterpret_cast<float4*>(p)[q];
         const float4 G = reinterpret_cast<const float4*>(g)[q];
         float4 Mv = reinterpret_cast<float4*>(m)[q];
@@ -47,19 +49,20 @@ __global__ void __launch_bounds__(256) k_adam(long long n, AdamSegs s, float* __
         reinterpret_cast<float4*>(m)[q] = Mv;
         reinterpret_cast<float4*>(v)[q] = V;
     }
-    // tail (n % 4 elements)
-    const long long t = 4 * n4 + (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n && blockIdx.x == 0) adam_one(p[t], g[t], m[t], v[t], s, t);
+    // tail (hi % 4 elements)
+    const long long t = 4 * q1 + (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < hi && blockIdx.x == 0) adam_one(p[t], g[t], m[t], v[t], s, t);
 }
 
-void launch_adam(long long n, const AdamSegs& s, float* p, const float* g, float* m, float* v, hipStream_t st) {
-    if (n <= 0) return;
-    const long long n4 = (n + 3) >> 2;
+void launch_adam(long long lo, long long hi, const AdamSegs& s, float* p, const float* g, float* m, float* v,
+                 hipStream_t st) {
+    if (hi <= lo) return;
+    const long long n4 = (hi - lo + 3) >> 2;
     // ~8 float4 per thread: enough bytes in flight per CU without an oversized grid
     long long blocks = (n4 + 256 * 8 - 1) / (256 * 8);
     if (blocks < 1) blocks = 1;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, st, n, s, p, g, m, v);
+    hipLaunchKernelGGL(k_adam, dim3((unsigned)blocks), dim3(256), 0, st, lo, hi, s, p, g, m, v);
 }
 
 }  // namespace gsr

@@ -166,11 +166,6 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 #define GSR_ST_G 1024
 #endif
 constexpr int ST_G = GSR_ST_G;  // Gaussians per block
-// 1: k_st_hist stores its per-wave counts and k_st_scatter reads them (the round-3 layout, kept
-// for A/B); 0: k_st_scatter counts its waves' entries itself
-#ifndef GSR_ST_WCOUNTS
-#define GSR_ST_WCOUNTS 0
-#endif
 // waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
 // per-wave LDS state of 8 waves would not fit (st_waves)
 
@@ -191,42 +186,106 @@ __device__ __forceinline__ uint2 sorted_rect(const void* r, int p) {
     else return reinterpret_cast<const uint2*>(r)[p];
 }
 
-// k_st_hist's LDS histograms: one per wave when the per-wave counts are stored, else one per
-// block unless GSR_ST_HIST_SHARED=0 (one per wave, summed)
-#ifndef GSR_ST_HIST_SHARED
-#define GSR_ST_HIST_SHARED 1
-#endif
-constexpr int st_hist_count(int st_w) { return (GSR_ST_WCOUNTS || !GSR_ST_HIST_SHARED) ? st_w : 1; }
+// k_st_hist's LDS histograms: one per block.  (Round 3's per-wave counts stored by k_st_hist
+// for the scatter, GSR_ST_WCOUNTS, were retired in round 5: k_st_hist now stores the block's
+// entry-balanced wave cuts instead.)
+constexpr int st_hist_count(int) { return 1; }
 
+// A lane's super-tile rect [sx0, sx1) x [sy0, sy1) is walked by the lane itself when it holds
+// at most ST_BIG super-tiles; larger rects (screen-filling Gaussians right in front of the
+// camera: up to every super-tile of the frame) are walked by the whole wave, one rect at a
+// time, 64 super-tiles per step, so one such Gaussian does not serialise its chunk -- its lane
+// alone issued one LDS atomic per super-tile per pass, and its neighbours' lanes the same
+// addresses (the clustered cfg2c frame: k_st_scatter 32 -> 113 us against cfg2).  f(sx, sy, o,
+// a0, a1, a2) runs once per (lane o, super-tile) pair with lane o's values a0..a2.  Every lane
+// of the wave must call it (a ballot); lanes with nothing to walk pass an empty rect.
+#ifndef GSR_ST_BIG
+#define GSR_ST_BIG 16u
+#endif
+constexpr uint32_t ST_BIG = GSR_ST_BIG;  // (0xffffffffu: every lane walks its own rect, as before round 5)
+template <class F>
+__device__ __forceinline__ void st_rect_walk(uint32_t sx0, uint32_t sx1, uint32_t sy0, uint32_t sy1, uint32_t a0,
+                                             uint32_t a1, uint32_t a2, F&& f) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t w = sx1 > sx0 ? sx1 - sx0 : 0u, n = sy1 > sy0 ? w * (sy1 - sy0) : 0u;
+    const bool big = n > ST_BIG;
+    if (!big)
+        for (uint32_t sy = sy0; sy < sy1; sy++)
+            for (uint32_t sx = sx0; sx < sx1; sx++) f(sx, sy, lane, a0, a1, a2);
+    uint64_t bm = __ballot(big);
+    while (bm) {
+        const int k = __builtin_ctzll(bm);
+        bm &= bm - 1ull;
+        const uint32_t bx = bcast(sx0, k), bw = bcast(w, k), by = bcast(sy0, k), by1 = bcast(sy1, k);
+        const uint32_t b0 = bcast(a0, k), b1 = bcast(a1, k), b2 = bcast(a2, k);
+        if (bw >= 64u) {  // a row per step, 64 columns at a time
+            for (uint32_t sy = by; sy < by1; sy++)
+                for (uint32_t sx = bx + (uint32_t)lane; sx < bx + bw; sx += 64u) f(sx, sy, k, b0, b1, b2);
+        } else {  // floor(64 / bw) rows per step; one division per rect, none per step
+            const uint32_t rps = 64u / bw, ro = (uint32_t)lane / bw, col = (uint32_t)lane - ro * bw;
+            if (ro < rps)
+                for (uint32_t sy = by + ro; sy < by1; sy += rps) f(bx + col, sy, k, b0, b1, b2);
+        }
+    }
+}
+
+// k_st_hist: per block of ST_G depth-sorted Gaussians, its entry count per super-tile (the
+// digit scan's table) and its ST_W wave cuts for k_st_scatter.  Thread t counts Gaussians
+// g0 + PER t .. + PER - 1.  The cuts split the block into contiguous wave ranges of about equal
+// entry counts (super-tiles touched): cuts[blk][w] = the first Gaussian of wave w (w >= 1; wave
+// 0 starts at g0, the last wave ends at the block's end).  Equal Gaussian counts gave the wave
+// holding the block's nearest Gaussians (block 0: screen-filling splats right in front of the
+// camera) most of the block's entries -- a 72 us wave against ~8 us for the rest at cfg2c
+// (tools/unit_times.py).
 template <int ST_W, bool PACKED>
 __global__ void __launch_bounds__(64 * ST_W) k_st_hist(int Pv, const unsigned long long* totals, const void* rect_sorted, unsigned gsx, unsigned sth,
-                                                  int NS, int nb, uint32_t* table, uint32_t* wcounts) {
-    constexpr int NH = st_hist_count(ST_W);
-    extern __shared__ uint32_t hist[];  // [NH][NS]
-    for (int i = threadIdx.x; i < NH * NS; i += (64 * ST_W)) hist[i] = 0;
+                                                  int NS, int nb, uint32_t* table, uint32_t* cuts) {
+    constexpr int PER = ST_G / (64 * ST_W);  // consecutive Gaussians per thread
+    extern __shared__ uint32_t hist[];  // [NS]
+    __shared__ uint32_t s_bscan[ST_W];
+    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) hist[i] = 0;
     Pv = block_visible(Pv, totals);
     __syncthreads();
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // neighbouring blocks share an L2
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int g0 = blk * ST_G;
-    const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
-    uint32_t* wh = hist + (NH > 1 ? wave : 0) * NS;
-    for (int p = p0 + lane; p < p1; p += 64) {
-        const uint2 sr = st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth);
-        for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
-            for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
+    const int t = threadIdx.x;
+    const int g0 = blk * ST_G, g1 = min(Pv, g0 + ST_G);
+    uint32_t n[PER], sum = 0;
+#pragma unroll
+    for (int j = 0; j < PER; j++) {  // wave-uniform trip count (st_rect_walk's ballot)
+        const int p = g0 + t * PER + j;
+        const uint2 sr = p < g1 ? st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth) : make_uint2(0u, 0u);
+        const uint32_t sx0 = sr.x & 0xffffu, sx1 = sr.x >> 16, sy0 = sr.y & 0xffffu, sy1 = sr.y >> 16;
+        n[j] = (sx1 - sx0) * (sy1 - sy0);
+        sum += n[j];
+        st_rect_walk(sx0, sx1, sy0, sy1, 0u, 0u, 0u,
+                     [&](uint32_t sx, uint32_t sy, int, uint32_t, uint32_t, uint32_t) { atomicAdd(&hist[sy * gsx + sx], 1u); });
+    }
+    uint32_t tot;
+    uint32_t run = block_exclusive_scan<ST_W>(sum, s_bscan, &tot);
+    uint32_t* cb = cuts + (size_t)blk * ST_W;
+    // s_bscan[w] = hardware wave w's entries = wave w's under equal Gaussian counts (64 threads x
+    // PER = ST_G / ST_W Gaussians).  Balanced blocks keep the equal cuts: whole 64-Gaussian chunks
+    // per wave (an entry-balanced cut falls mid-chunk and costs its wave a third, partial chunk:
+    // +3 us on the uniform cfg2 scatter); only a block whose heaviest wave holds over twice the
+    // mean is cut by entries.
+    uint32_t wmax = 0;
+#pragma unroll
+    for (int w = 0; w < ST_W; w++) wmax = max(wmax, s_bscan[w]);
+    if (tot == 0 || (unsigned long long)wmax * ST_W <= 2ull * tot) {  // equal Gaussian counts
+        if (t > 0 && t < ST_W) cb[t] = (uint32_t)min(max(g0, g1), g0 + t * (ST_G / ST_W));
+    } else {
+#pragma unroll
+        for (int j = 0; j < PER; j++) {
+            const uint32_t lo = run;
+            run += n[j];
+            for (int w = 1; w < ST_W; w++) {
+                const uint32_t tgt = (uint32_t)(((unsigned long long)w * tot) / ST_W);
+                if (lo <= tgt && tgt < run) cb[w] = (uint32_t)(g0 + t * PER + j);  // the Gaussian holding entry tgt
+            }
+        }
     }
     __syncthreads();
-#if GSR_ST_WCOUNTS
-    uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
-    for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) wc[i] = hist[i];
-#endif
-    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) {
-        uint32_t t = 0;
-#pragma unroll
-        for (int w = 0; w < NH; w++) t += hist[w * NS + i];
-        table[(size_t)i * nb + blk] = t;
-    }
+    for (int i = threadIdx.x; i < NS; i += (64 * ST_W)) table[(size_t)i * nb + blk] = hist[i];
 }
 
 // Segment table of the materialised tile lists (SEG entries per segment, see k_seg_lists),
@@ -285,26 +344,26 @@ __device__ __forceinline__ void st_pass(int p0, int p1, const uint32_t* sorted_i
             gid_nx = sorted_ids[c0 + 64 + lane];
         }
         const uint32_t sx0 = sr.x & 0xffffu, sx1 = sr.x >> 16, sy0 = sr.y & 0xffffu, sy1 = sr.y >> 16;
-        for (uint32_t sy = sy0; sy < sy1; sy++)
-            for (uint32_t sx = sx0; sx < sx1; sx++) atomicOr(&wmask[sy * gsx + sx], bit);
+        st_rect_walk(sx0, sx1, sy0, sy1, 0u, 0u, 0u, [&](uint32_t sx, uint32_t sy, int o, uint32_t, uint32_t, uint32_t) {
+            atomicOr(&wmask[sy * gsx + sx], 1ull << o);
+        });
         lds_order();
-        for (uint32_t sy = sy0; sy < sy1; sy++)
-            for (uint32_t sx = sx0; sx < sx1; sx++) {
-                const uint32_t sid = sy * gsx + sx;
-                const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & lt);
-if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
-                    ent[pos] = make_uint2(sid | (local_rect_code(r, sx, sy, sth) << ST_KEY_BITS), gid);
-            }
+        st_rect_walk(sx0, sx1, sy0, sy1, r.x, r.y, gid,
+                     [&](uint32_t sx, uint32_t sy, int o, uint32_t rx, uint32_t ry, uint32_t g) {
+                         const uint32_t sid = sy * gsx + sx;
+                         const uint32_t pos = wcnt[sid] + (uint32_t)__popcll(wmask[sid] & ((1ull << o) - 1ull));
+                         if (pos < cap)  // S beyond the speculative capacity: the forward redoes the binning
+                             ent[pos] = make_uint2(sid | (local_rect_code(make_uint2(rx, ry), sx, sy, sth) << ST_KEY_BITS), g);
+                     });
         lds_order();
-        for (uint32_t sy = sy0; sy < sy1; sy++)
-            for (uint32_t sx = sx0; sx < sx1; sx++) {
-                const uint32_t sid = sy * gsx + sx;
-                const unsigned long long m = wmask[sid];
-                if ((m & lt) == 0ull) {
-                    wcnt[sid] += (uint32_t)__popcll(m);
-                    wmask[sid] = 0ull;
-                }
+        st_rect_walk(sx0, sx1, sy0, sy1, 0u, 0u, 0u, [&](uint32_t sx, uint32_t sy, int o, uint32_t, uint32_t, uint32_t) {
+            const uint32_t sid = sy * gsx + sx;
+            const unsigned long long m = wmask[sid];
+            if ((m & ((1ull << o) - 1ull)) == 0ull) {  // the lowest lane of the run advances it
+                wcnt[sid] += (uint32_t)__popcll(m);
+                wmask[sid] = 0ull;
             }
+        });
         lds_order();
     }
 }
@@ -313,10 +372,13 @@ if (pos < cap)  // S beyond the speculative capacity: the forward redoes the bin
 // forward's dispatch order, one workgroup per XCD band (costs from the super-tile totals, so
 // neither needs a launch of its own).  Each scatter block scans the super-tile totals into
 // the super-tile bases itself (block 0 also writes the ranges and header[0] = S).
+#ifdef GSR_RENDER_STATS
+__device__ unsigned long long g_st_times[4 * 65536];  // per scatter wave: block start, pass start, end, block
+#endif
 template <int ST_W, bool PACKED>
 __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned long long* totals, const uint32_t* sorted_ids,
                                                      const void* rect_sorted, unsigned gsx, unsigned sth, int NS, int nb,
-                                                     const uint32_t* table, const uint32_t* wcounts,
+                                                     const uint32_t* table, const uint32_t* cuts,
                                                      const uint32_t* tot, uint2* st_ranges, unsigned long long* header,
                                                      uint2* ent, uint32_t cap, FrameTotals ft, TileOrderArgs ord) {
     if ((int)blockIdx.x >= nb) {
@@ -325,6 +387,9 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
         else tile_order_band((unsigned)x, ord);
         return;
     }
+#ifdef GSR_RENDER_STATS
+    const unsigned long long t_block = __builtin_amdgcn_s_memrealtime();
+#endif
     extern __shared__ unsigned long long st_lds[];  // [ST_W][NS] lane masks, then [ST_W][NS] run counters
     __shared__ uint32_t s_scan[ST_W];
     unsigned long long* wmask_all = st_lds;
@@ -333,28 +398,28 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     Pv = block_visible(Pv, totals);
     const unsigned blk = xcd_remap(blockIdx.x, nb);  // as k_st_hist: runs of neighbours merge in L2
     const int g0 = blk * ST_G;
-    const int p0 = min(Pv, g0 + wave * (ST_G / ST_W)), p1 = min(Pv, g0 + (wave + 1) * (ST_G / ST_W));
+    // wave `wave`'s Gaussians: [p0, p1), the entry-balanced cuts k_st_hist stored
+    const int gend = min(Pv, g0 + ST_G);
+    const int p0 = wave == 0 ? g0 : (int)cuts[(size_t)blk * ST_W + wave];
+    const int p1 = wave + 1 == ST_W ? max(g0, gend) : (int)cuts[(size_t)blk * ST_W + wave + 1];
     // super-tile s's base (exclusive scan of the totals); each wave's run of s starts there +
     // the block's offset + the counts of the block's earlier waves.  The waves count their
     // entries per super-tile again here, into the run counters, from the rects k_st_hist read
     // (4 KiB per block, L2-resident): storing k_st_hist's per-wave counts and reading them back
     // moved 4 x ST_W x NS bytes per block through HBM (80 MB each way at cfg5).
-#if GSR_ST_WCOUNTS
-    const uint32_t* wc = wcounts + (size_t)blk * ST_W * NS;
-#else
     for (int i = threadIdx.x; i < ST_W * NS; i += (64 * ST_W)) wcnt_all[i] = 0u;
     __syncthreads();
     {
         const int lane = threadIdx.x & 63;
         uint32_t* wh = wcnt_all + wave * NS;
-        for (int p = p0 + lane; p < p1; p += 64) {
-            const uint2 sr = st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth);
-            for (uint32_t sy = sr.y & 0xffffu; sy < (sr.y >> 16); sy++)
-                for (uint32_t sx = sr.x & 0xffffu; sx < (sr.x >> 16); sx++) atomicAdd(&wh[sy * gsx + sx], 1u);
+        for (int pb = p0; pb < p1; pb += 64) {
+            const int p = pb + lane;
+            const uint2 sr = p < p1 ? st_rect_of(sorted_rect<PACKED>(rect_sorted, p), sth) : make_uint2(0u, 0u);
+            st_rect_walk(sr.x & 0xffffu, sr.x >> 16, sr.y & 0xffffu, sr.y >> 16, 0u, 0u, 0u,
+                         [&](uint32_t sx, uint32_t sy, int, uint32_t, uint32_t, uint32_t) { atomicAdd(&wh[sy * gsx + sx], 1u); });
         }
     }
     __syncthreads();
-#endif
     uint32_t carry = 0;
     for (int c = 0; c < NS; c += 64 * ST_W) {
         const int i = c + (int)threadIdx.x;
@@ -367,11 +432,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
             if (blockIdx.x == 0) st_ranges[i] = v ? make_uint2(min(ex, cap), min(ex + v, cap)) : make_uint2(0u, 0u);
             uint32_t run = ex + table[(size_t)i * nb + blk];
             for (int w = 0; w < ST_W; w++) {
-#if GSR_ST_WCOUNTS
-                const uint32_t c = wc[w * NS + i];
-#else
                 const uint32_t c = wcnt_all[w * NS + i];  // this thread's super-tile only
-#endif
                 wmask_all[w * NS + i] = 0ull;
                 wcnt_all[w * NS + i] = run;
                 run += c;
@@ -381,14 +442,37 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) header[0] = min(carry, cap);
     __syncthreads();
+#ifdef GSR_RENDER_STATS
+    const unsigned long long t_pass = __builtin_amdgcn_s_memrealtime();
+#endif
     st_pass<PACKED>(p0, p1, sorted_ids, rect_sorted, gsx, sth, wcnt_all + wave * NS, wmask_all + wave * NS, ent, cap);
+#ifdef GSR_RENDER_STATS
+    if ((threadIdx.x & 63) == 0 && blockIdx.x * ST_W + wave < 65536) {  // per wave: block start, pass start, end
+        unsigned long long* u = g_st_times + 4 * (blockIdx.x * ST_W + wave);
+        u[0] = t_block;
+        u[1] = t_pass;
+        u[2] = __builtin_amdgcn_s_memrealtime();
+        u[3] = (unsigned long long)blk;
+    }
+#endif
 }
+
+#ifdef GSR_RENDER_STATS
+extern "C" int gsr_debug_st_times(unsigned long long* out, int n) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_st_times), sizeof(unsigned long long) * 4 * n) == hipSuccess ? 0 : -1;
+}
+extern "C" int gsr_debug_st_times_reset() {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_st_times)) != hipSuccess) return -1;
+    return hipMemset(p, 0, sizeof(g_st_times)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 static int st_waves(int NS) { return 12 * 8 * NS <= 65536 ? 8 : 4; }
 
 size_t st_bin_temp_bytes(long long Pv, int NS) {
     const size_t nb = (size_t)((Pv + ST_G - 1) / ST_G);
-    return (4 + (GSR_ST_WCOUNTS ? 4 * (size_t)st_waves(NS) : 0)) * (size_t)NS * nb + 8 * (size_t)NS + 4 * 256 + 1024;
+    return 4 * (size_t)NS * nb + 4 * (size_t)st_waves(NS) * nb + 8 * (size_t)NS + 4 * 256 + 1024 + 256;
 }
 
 // per-wave LDS masks + counters: 12 B x waves x NS within a 64 KiB workgroup allocation
@@ -423,10 +507,10 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     };
     uint32_t* table = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS * nb));
     uint32_t* tot = reinterpret_cast<uint32_t*>(take(4 * (size_t)NS));
-    uint32_t* wcounts = GSR_ST_WCOUNTS ? reinterpret_cast<uint32_t*>(take(4 * (size_t)W * NS * nb)) : nullptr;
+    uint32_t* cuts = reinterpret_cast<uint32_t*>(take(4 * (size_t)W * nb));  // the blocks' wave cuts
     auto hist = [&](auto kern, int threads) {
         hipLaunchKernelGGL(kern, dim3(nb), dim3(threads), 4 * st_hist_count(threads / 64) * NS, s, Pv, totals, rect_sorted, gsx, sth,
-                           NS, nb, table, wcounts);
+                           NS, nb, table, cuts);
     };
     if (W == 8) packed ? hist(k_st_hist<8, true>, 512) : hist(k_st_hist<8, false>, 512);
     else packed ? hist(k_st_hist<4, true>, 256) : hist(k_st_hist<4, false>, 256);
@@ -435,7 +519,7 @@ void launch_st_bin(int Pv, const unsigned long long* totals, const uint32_t* sor
     const dim3 grid(nb + (ftp ? 1 : 0) + (ordp && ord.ntile ? 8 : 0));
     auto scatter = [&](auto kern, int threads) {
         hipLaunchKernelGGL(kern, grid, dim3(threads), 12 * (threads / 64) * NS, s, Pv, totals, sorted_ids, rect_sorted,
-                           gsx, sth, NS, nb, table, wcounts, tot, st_ranges, header, ent, cap, ft, ord);
+                           gsx, sth, NS, nb, table, cuts, tot, st_ranges, header, ent, cap, ft, ord);
     };
     if (W == 8) packed ? scatter(k_st_scatter<8, true>, 512) : scatter(k_st_scatter<8, false>, 512);
     else packed ? scatter(k_st_scatter<4, true>, 256) : scatter(k_st_scatter<4, false>, 256);

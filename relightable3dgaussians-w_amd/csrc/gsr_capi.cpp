@@ -1280,9 +1280,19 @@ int gsr_texture2d_backward(int nb, int npix, int tex_nb, int tex_h, int tex_w, i
 int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double* seg_lr, double beta1, double beta2,
                   double eps, int step, float grad_scale, float* param, const float* grad, float* exp_avg,
                   float* exp_avg_sq, void* stream_) {
+    return gsr_adam_step_range(n, 0, n, nseg, seg_end, seg_lr, beta1, beta2, eps, step, grad_scale, param, grad,
+                               exp_avg, exp_avg_sq, stream_);
+}
+
+int gsr_adam_step_range(long long n, long long lo, long long hi, int nseg, const long long* seg_end,
+                        const double* seg_lr, double beta1, double beta2, double eps, int step, float grad_scale,
+                        float* param, const float* grad, float* exp_avg, float* exp_avg_sq, void* stream_) {
     if (n < 0 || nseg < 1 || nseg > gsr::ADAM_MAX_SEGS || step < 1)
         return fail(GSR_E_ARG, "gsr_adam_step: bad sizes n=%lld nseg=%d step=%d", n, nseg, step);
-    if (n == 0) return GSR_OK;
+    if (lo < 0 || hi > n || lo > hi || (lo & 3))
+        return fail(GSR_E_ARG, "gsr_adam_step_range: bad range [%lld, %lld) of %lld (lo must be a multiple of 4)", lo,
+                    hi, n);
+    if (n == 0 || lo == hi) return GSR_OK;
     if (!seg_end || !seg_lr || !param || !grad || !exp_avg || !exp_avg_sq)
         return fail(GSR_E_ARG, "gsr_adam_step: missing buffers");
     for (const void* q : {(const void*)param, (const void*)grad, (const void*)exp_avg, (const void*)exp_avg_sq})
@@ -1308,7 +1318,7 @@ int gsr_adam_step(long long n, int nseg, const long long* seg_end, const double*
     s.one_minus_b2 = (float)(1.0 - beta2);
     s.eps = (float)eps;
     s.grad_scale = grad_scale;
-    gsr::launch_adam(n, s, param, grad, exp_avg, exp_avg_sq, reinterpret_cast<hipStream_t>(stream_));
+    gsr::launch_adam(lo, hi, s, param, grad, exp_avg, exp_avg_sq, reinterpret_cast<hipStream_t>(stream_));
     GSR_LAUNCH_CHECK();
     return GSR_OK;
 }

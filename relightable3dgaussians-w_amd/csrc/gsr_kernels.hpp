@@ -344,7 +344,8 @@ struct AdamSegs {
     float step_size[ADAM_MAX_SEGS];      // lr / (1 - b1^t) per segment
     float bc2_sqrt, one_minus_b1, b2, one_minus_b2, eps, grad_scale;
 };
-void launch_adam(long long n, const AdamSegs& s, float* p, const float* g, float* m, float* v, hipStream_t st);
+void launch_adam(long long lo, long long hi, const AdamSegs& s, float* p, const float* g, float* m, float* v,
+                 hipStream_t st);  // elements [lo, hi), lo % 4 == 0
 
 // ---- fused SSIM loss (gsr_ssim.hip) ---------------------------------------------------
 struct SsimWindow {

@@ -79,18 +79,22 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     const unsigned long long tp = total + add * a.ntile;
     const unsigned long long tgt[2] = {band * tp / 8, (band + 1) * tp / 8};
     const bool need[2] = {band > 0, band < 7};
-    // the row whose cost' interval (p, p + cost'] holds each target
+    // Each boundary is 1 + the last tile whose cost' interval starts below the target: the row
+    // is the last one starting below it, then the tile the last one of that row.  Every band's
+    // workgroup evaluates the same function of the same costs, so band b's upper bound is band
+    // b + 1's lower bound and the bounds are monotone even if the row sums disagreed with the
+    // tile costs (no per-workgroup fallback that could leave bands overlapping or gapped).
     if (r < n) {
         const unsigned long long p = before + (unsigned long long)r * gx * add, q = p + c + gx * add;
+        const unsigned long long pn = q;  // the next row's start
 #pragma unroll
         for (int k = 0; k < 2; k++)
-            if (need[k] && p < tgt[k] && tgt[k] <= q) {
+            if (need[k] && p < tgt[k] && (r + 1 == n || pn >= tgt[k])) {
                 s_row[k] = r;
                 s_rowp[k] = p;
             }
     }
     __syncthreads();
-    // the tile of that row whose cost' interval holds it: the band boundary follows it
 #pragma unroll
     for (int k = 0; k < 2; k++) {
         if (!need[k]) continue;  // workgroup-uniform
@@ -101,16 +105,13 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
         const unsigned long long bt = block_exclusive_scan<8>(ct, s_scan, &rt);
         if (row < n && threadIdx.x < gx) {
             const unsigned long long p = s_rowp[k] + bt, q = p + ct;
-            if (p < tgt[k] && tgt[k] <= q) s_bound[k] = row * gx + threadIdx.x + 1;
+            if (p < tgt[k] && (threadIdx.x + 1 == gx || q >= tgt[k])) s_bound[k] = row * gx + threadIdx.x + 1;
         }
     }
     __syncthreads();
-    if (s_bound[0] == 0xffffffffu || s_bound[1] == 0xffffffffu) {  // a boundary not found: costs inconsistent
-        band_of(band, a.ntile, lo, len);
-        return;
-    }
-    lo = s_bound[0];
-    len = s_bound[1] - s_bound[0];
+    // (a target at or below the first row's start cannot occur: tgt > 0 = the first start)
+    lo = s_bound[0] == 0xffffffffu ? 0u : s_bound[0];
+    len = (s_bound[1] == 0xffffffffu ? a.ntile : s_bound[1]) - lo;
 }
 
 // BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning

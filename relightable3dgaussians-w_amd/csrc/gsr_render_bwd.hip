@@ -109,8 +109,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
-            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
-            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, r.b.z, r.b.w);
+            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // records to LDS; survivors are read back with broadcast LDS loads (LDS pipe)

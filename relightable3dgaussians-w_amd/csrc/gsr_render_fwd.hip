@@ -82,8 +82,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             const Rec r = a.rec[id];
             qm = wt.reach(r, j, nullptr);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
-            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
-            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, r.b.z, r.b.w);
+            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // the batch's records go to LDS; the walk below reads each survivor's record with

@@ -71,8 +71,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             qm = wt.reach(r, j, nullptr);
-            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
-            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, 0.f, 0.f);
+            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
@@ -232,8 +232,8 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             qm = wt.reach(r, p, qlim);
-            ra = make_float4(r.a.x, r.a.y, TILE_HALF_LOG2E * r.a.z, TILE_NEG_LOG2E * r.a.w);
-            rb = make_float4(TILE_HALF_LOG2E * r.b.x, r.b.y, 0.f, 0.f);
+            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }

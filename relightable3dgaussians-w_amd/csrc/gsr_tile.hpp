@@ -224,12 +224,24 @@ struct TileList {
 // a record is staged (once per record and batch), so exp(power) is one v_exp_f32 (exp2) per
 // evaluation with no multiply.  Forward and backward stage and evaluate identically, so the
 // backward replays exactly the forward's blend decisions.  The backward's conic-weighted
-// position gradients come out scaled by log2(e) and are rescaled by ln 2 once per Gaussian.
+// (The backward accumulates raw sums of G dL/dalpha dx...: G is the same value in either unit.)
+// GSR_REF_EXPONENT=1 builds the reference's order instead (forward.cu:335,343,
+// backward.cu:494-498): the raw conic staged, power = -0.5 (a dx dx + c dy dy) - b dx dy with
+// no contraction, G = expf(power) -- the A/B of VERDICT r4 item 6.
+#ifndef GSR_REF_EXPONENT
+#define GSR_REF_EXPONENT 0
+#endif
 constexpr float TILE_LOG2E = 1.44269504088896340736f;
 constexpr float TILE_LN2 = 0.69314718055994530942f;
-constexpr float TILE_HALF_LOG2E = -0.5f * TILE_LOG2E;  // factor of conic.a and conic.c
-constexpr float TILE_NEG_LOG2E = -TILE_LOG2E;          // factor of conic.b
+#if GSR_REF_EXPONENT
+constexpr float TILE_STAGE_AC = 1.0f;  // factor of conic.a and conic.c as staged
+constexpr float TILE_STAGE_B = 1.0f;   // factor of conic.b
+__device__ __forceinline__ float tile_exp2(float x) { return expf(x); }  // natural units here
+#else
+constexpr float TILE_STAGE_AC = -0.5f * TILE_LOG2E;  // factor of conic.a and conic.c
+constexpr float TILE_STAGE_B = -TILE_LOG2E;          // factor of conic.b
 __device__ __forceinline__ float tile_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+#endif
 
 // Minimum over the pixel box [dx0,dx1]x[dy0,dy1] (offsets from the Gaussian centre) of
 // q(d) = a dx^2 + 2 b dx dy + c dy^2, for a positive-definite conic (a, b, c).
@@ -398,7 +410,12 @@ struct WaveTile {
 // backward tile passes evaluate it with this exact operation sequence, so the backward
 // replays the forward's blend decisions bit for bit.
 __device__ __forceinline__ float gauss_power(float na, float nb, float nc, float dx, float dy) {
+#if GSR_REF_EXPONENT  // (na, nb, nc) = the raw conic (a, b, c); the reference's operation order
+    return __fsub_rn(__fmul_rn(-0.5f, __fadd_rn(__fmul_rn(__fmul_rn(na, dx), dx), __fmul_rn(__fmul_rn(nc, dy), dy))),
+                     __fmul_rn(__fmul_rn(nb, dx), dy));
+#else
     return __builtin_fmaf(na * dx, dx, __builtin_fmaf(nc * dy, dy, (nb * dx) * dy));
+#endif
 }
 
 // Lane masks in SGPR pairs and selects on them (v_cmp_*_e64 / v_cndmask_b32_e64).  On

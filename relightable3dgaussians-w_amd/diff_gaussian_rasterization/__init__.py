@@ -148,9 +148,16 @@ class _RasterizeGaussians(torch.autograd.Function):
         return g_means3D, g_means2D, g_sh, g_colors, g_opacities, g_scales, g_rotations, g_cov3D, None
 
 
-# num_rendered (the reference's R, the sum of tiles touched) of the latest multi-channel call:
-# bench.py's training leg reads it for its algorithmic bytes
-last_channels_call = {"num_rendered": None, "radii": None}
+# num_rendered (the reference's R, the sum of tiles touched) and the visible count of the latest
+# multi-channel call, recorded only while record_channels_calls(True) is on (bench.py's training
+# leg reads them for its algorithmic bytes); scalars, so no device tensor stays alive
+last_channels_call = {"num_rendered": None, "visible": None, "enabled": False}
+
+
+def record_channels_calls(on=True):
+    """Turn the last_channels_call record on or off (off by default; the visible count costs
+    one device reduction and a host sync per call while on)."""
+    last_channels_call["enabled"] = bool(on)
 
 
 def rasterize_channels(means3D, means2D, features, opacities, scales, rotations, cov3Ds_precomp, background,
@@ -178,8 +185,9 @@ class _RasterizeChannels(torch.autograd.Function):
             nch)
         ctx.raster_settings = s
         ctx.num_rendered = num_rendered
-        last_channels_call["num_rendered"] = num_rendered
-        last_channels_call["radii"] = radii
+        if last_channels_call["enabled"]:
+            last_channels_call["num_rendered"] = num_rendered
+            last_channels_call["visible"] = int((radii > 0).sum().item())
         ctx.nch = features.shape[1] if nch is None else int(nch)
         ctx.ncols = features.shape[1]
         ctx.save_for_backward(background, feat, means3D, scales, rotations, cov3Ds_precomp, radii, geom_buf, bin_buf,

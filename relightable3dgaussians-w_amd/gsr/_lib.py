@@ -66,6 +66,9 @@ def _declare(lib):
                                        vp, vp, vp]
     lib.gsr_adam_step.argtypes = [C.c_longlong, i, C.POINTER(C.c_longlong), C.POINTER(C.c_double), C.c_double, C.c_double,
                                   C.c_double, i, f, vp, vp, vp, vp, vp]
+    lib.gsr_adam_step_range.argtypes = [C.c_longlong, C.c_longlong, C.c_longlong, i, C.POINTER(C.c_longlong),
+                                        C.POINTER(C.c_double), C.c_double, C.c_double, C.c_double, i, f, vp, vp, vp,
+                                        vp, vp]
     lib.gsr_view_loss_partials.argtypes = [i]
     lib.gsr_view_loss_forward.argtypes = [i] + [vp] * 9 + [vp]
     lib.gsr_view_loss_backward.argtypes = [i] + [vp] * 9 + [vp] * 5 + [vp]
@@ -106,7 +109,7 @@ def _declare(lib):
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
                "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
-               "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_ssim_forward", "gsr_ssim_backward",
+               "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_adam_step_range", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_ssim_l1_backward",
                "gsr_view_loss_forward", "gsr_view_loss_backward", "gsr_view_objective", "gsr_view_regularisers_forward",
                "gsr_view_regularisers_backward", "gsr_view_regularisers_tail_forward",

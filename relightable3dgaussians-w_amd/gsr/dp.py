@@ -224,18 +224,57 @@ def sync_max_radii(stats: Dict[str, torch.Tensor], group=None) -> None:
     dist.all_reduce(stats["max_radii2D"], op=dist.ReduceOp.MAX, group=group)
 
 
-def finish_step(scene, mean2D_grads, radii, iteration: int, world: int = 1, group=None) -> int:
+def synced_stats(scene, group=None) -> Dict[str, torch.Tensor]:
+    """scene.stats with every field rank-consistent: the one call any reader other than
+    densification (a checkpoint, a statistics export, another pruning path) must make before it
+    reads them at N > 1.  While ``scene.max_radii_local`` is set, max_radii2D holds this rank's
+    views only (finish_step leaves it rank-local); this MAX-reduces it (a collective: every rank
+    must call it) and clears the mark.  The sums are always consistent (they ride in the
+    iteration's exchange)."""
+    if getattr(scene, "max_radii_local", False):
+        if dist.is_available() and dist.is_initialized():
+            sync_max_radii(scene.stats, group)
+        scene.max_radii_local = False
+    return scene.stats
+
+
+EXCHANGE_CHUNKS = 4  # the data-parallel step's all-reduce, in this many pipelined chunks
+EXCHANGE_MIN_CHUNK = 1 << 20  # floats: smaller buckets go out whole
+
+
+def exchange_chunks(n: int, chunks: int = EXCHANGE_CHUNKS, min_chunk: int = EXCHANGE_MIN_CHUNK):
+    """[lo, hi) ranges cutting a bucket of n floats into at most ``chunks`` pieces of at least
+    ``min_chunk`` floats (each start a multiple of 4: the Adam kernel's float4 rows)."""
+    k = max(1, min(int(chunks), n // max(1, int(min_chunk))))
+    step = -(-n // k)
+    step = (step + 3) & ~3
+    out, lo = [], 0
+    while lo < n:
+        out.append((lo, min(n, lo + step)))
+        lo += step
+    return out or [(0, 0)]
+
+
+def finish_step(scene, mean2D_grads, radii, iteration: int, world: int = 1, group=None, on_chunk=None,
+                chunks: int = None, min_chunk: int = None) -> int:
     """The tail of gsr.train.train_step after the views' backward: the densification
-    statistics and the iteration's exchange.  Returns the number of collectives it issued.
+    statistics, the iteration's exchange and (``on_chunk``) the optimizer step.  Returns the
+    number of collectives it issued.
 
     * train.py:130 updates max_radii2D every iteration; train.py:143-144 adds the gradient-norm
       sums only while iteration < densify_until_iter.
-    * One rank: straight into the running statistics.
-    * N ranks: ONE SUM all-reduce per iteration.  The step's sums ride in the flat gradient's
-      tail (step_sums) while they are on, so the bucket is [gradient | accum deltas | denom
-      deltas], and they are folded into the running statistics after; past densify_until_iter
-      the bucket is the gradient alone.  max_radii2D is updated rank-locally (sync_max_radii
-      reduces it when densification needs it); ``scene.max_radii_local`` marks it."""
+    * One rank: straight into the running statistics; on_chunk(0, n) updates every parameter.
+    * N ranks: one SUM all-reduce of the flat bucket per iteration -- the gradient, and while
+      the statistics are on, the step's sums in the bucket's tail (step_sums: [gradient | accum
+      deltas | denom deltas]), folded into the running statistics after; past
+      densify_until_iter the bucket is the gradient alone.  The bucket goes out as ``chunks``
+      (default EXCHANGE_CHUNKS) consecutive slices, all issued at once (asynchronously, in
+      order, on the collective stream); on_chunk(lo, hi) runs the optimizer over the gradient
+      part of slice i as soon as slice i has landed (work.wait orders the current stream after
+      it), so the update of slice i overlaps the exchange of slices i + 1... .  A SUM is
+      elementwise, so the slices reduce exactly as the whole bucket would.  max_radii2D is
+      updated rank-locally (sync_max_radii reduces it when densification needs it);
+      ``scene.max_radii_local`` marks it."""
     st = scene.stats
     stats_on = iteration < DENSIFY_UNTIL_ITER
     fp = scene.fp
@@ -246,12 +285,84 @@ def finish_step(scene, mean2D_grads, radii, iteration: int, world: int = 1, grou
         acc, den = (st["xyz_gradient_accum"], st["denom"]) if stats_on else (None, None)
     add_views(acc, den, st["max_radii2D"], mean2D_grads, radii)
     if world <= 1:
+        if on_chunk is not None:
+            on_chunk(0, fp.n)
         return 0
-    dist.all_reduce(fp.bucket(stats_on), op=dist.ReduceOp.SUM, group=group)
+    bucket = fp.bucket(stats_on)
+    ranges = exchange_chunks(bucket.numel(), EXCHANGE_CHUNKS if chunks is None else chunks,
+                             EXCHANGE_MIN_CHUNK if min_chunk is None else min_chunk)
+    works = [dist.all_reduce(bucket[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True) for lo, hi in ranges]
+    for (lo, hi), w in zip(ranges, works):
+        w.wait()
+        if on_chunk is not None and lo < fp.n:
+            on_chunk(lo, min(hi, fp.n))
     if stats_on:
         st["xyz_gradient_accum"].add_(acc)
         st["denom"].add_(den)
-    return 1
+    return len(ranges)
+
+
+class ReferenceExchange:
+    """The reference's own training loop (train.py:116-163, GaussianModel tensors) under view
+    parallelism with the same single exchange as finish_step: one flat bucket holds every
+    exchanged parameter's gradient and, while densification statistics are on
+    (train.py:143: iteration < densify_until_iter), this iteration's norm-accumulator and view
+    count deltas; one SUM all-reduce (in pipelined slices) per iteration moves both.
+    max_radii2D stays rank-local (train.py:130 MAX is associative): call
+    ``sync_max_radii({"max_radii2D": g.max_radii2D})`` right before densify_and_prune, or
+    ``synced`` before any other reader.
+
+        ex = dp.ReferenceExchange([g._xyz, g._albedo, ...], P=g.get_xyz.shape[0])
+        ...loss.backward()
+        ex.add_views([viewspace_point_tensor.grad], [radii], g.max_radii2D, stats_on)
+        ex.exchange(g, stats_on, world=dist.get_world_size())   # grads summed in place
+    """
+
+    def __init__(self, params: Sequence[torch.Tensor], P: int, device=None):
+        self.params = list(params)
+        dev = device if device is not None else self.params[0].device
+        self.sizes = [p.numel() for p in self.params]
+        self.n = sum(self.sizes)
+        self.P = int(P)
+        self.flat = torch.zeros(self.n + 2 * self.P, device=dev)
+        self.acc = self.flat[self.n:self.n + self.P].view(self.P, 1)
+        self.den = self.flat[self.n + self.P:].view(self.P, 1)
+
+    def add_views(self, mean2D_grads, radii, max_radii2D: torch.Tensor, stats_on: bool) -> None:
+        """This rank's views' densification updates (train.py:130, 143-144)."""
+        add_views(self.acc if stats_on else None, self.den if stats_on else None, max_radii2D, mean2D_grads, radii)
+
+    def exchange(self, gaussians, stats_on: bool, world: int = 1, group=None, chunks: int = None,
+                 min_chunk: int = None) -> int:
+        """Sum the parameters' gradients (in place) and the statistics deltas over the ranks
+        with one all-reduce; fold the deltas into gaussians.xyz_gradient_accum / denom.
+        Returns the number of collectives issued."""
+        o = 0
+        for p, n in zip(self.params, self.sizes):
+            g = p.grad if p.grad is not None else torch.zeros_like(p)
+            self.flat[o:o + n].copy_(g.reshape(-1))
+            o += n
+        bucket = self.flat if stats_on else self.flat[:self.n]
+        issued = 0
+        if world > 1:
+            ranges = exchange_chunks(bucket.numel(), EXCHANGE_CHUNKS if chunks is None else chunks,
+                                     EXCHANGE_MIN_CHUNK if min_chunk is None else min_chunk)
+            works = [dist.all_reduce(bucket[lo:hi], op=dist.ReduceOp.SUM, group=group, async_op=True)
+                     for lo, hi in ranges]
+            for w in works:
+                w.wait()
+            issued = len(ranges)
+        o = 0
+        for p, n in zip(self.params, self.sizes):
+            if p.grad is not None:
+                p.grad.copy_(self.flat[o:o + n].view_as(p.grad))
+            o += n
+        if stats_on:
+            gaussians.xyz_gradient_accum.add_(self.acc)
+            gaussians.denom.add_(self.den)
+            self.acc.zero_()
+            self.den.zero_()
+        return issued
 
 
 def shared_seed(group=None, device="cpu") -> int:

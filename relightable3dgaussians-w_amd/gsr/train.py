@@ -179,17 +179,29 @@ class FlatParams:
         self.lrs[self.names.index(name)] = float(lr)
 
     def step(self, grad_scale: float = 1.0) -> None:
+        self.begin_step(grad_scale)
+        self.step_range(0, self.n)
+
+    def begin_step(self, grad_scale: float = 1.0) -> None:
+        """Start one Adam step (the step count, the groups' learning rates as they are now);
+        step_range then applies it to element ranges, in any order, each exactly once."""
         import ctypes as C
         if self.device.type != "cuda":
             raise RuntimeError("FlatParams.step runs the HIP Adam kernel; parameters must be on the GPU")
         self.t += 1
         nseg = len(self.names)
-        ends = (C.c_longlong * nseg)(*self.ends)
-        lrs = (C.c_double * nseg)(*self.lrs)
-        _lib.check(_lib.lib().gsr_adam_step(self.n, nseg, ends, lrs, self.betas[0], self.betas[1], self.eps, self.t,
-                                            float(grad_scale), self.flat.data_ptr(), self.grad.data_ptr(),
-                                            self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-                                            _lib.stream_of(self.device)), "gsr_adam_step")
+        self._pending = ((C.c_longlong * nseg)(*self.ends), (C.c_double * nseg)(*self.lrs), nseg, float(grad_scale))
+
+    def step_range(self, lo: int, hi: int) -> None:
+        """The current step's update over elements [lo, hi) (lo a multiple of 4)."""
+        ends, lrs, nseg, gs = self._pending
+        hi = min(int(hi), self.n)
+        if hi <= lo:
+            return
+        _lib.check(_lib.lib().gsr_adam_step_range(self.n, int(lo), hi, nseg, ends, lrs, self.betas[0], self.betas[1],
+                                                  self.eps, self.t, gs, self.flat.data_ptr(), self.grad.data_ptr(),
+                                                  self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                                  _lib.stream_of(self.device)), "gsr_adam_step_range")
         # the kernel wrote through a raw pointer: advance the version counter (shared by every
         # view of the flat buffer) so saved-tensor checks and version-keyed caches see it
         torch.autograd.graph.increment_version(self.flat)
@@ -1073,12 +1085,17 @@ def train_step(scene: RelitScene, views: List, view_ids: List[int], gts: List[to
         for n in keep:
             fp.params[n].grad.zero_()
     fp.check_grads_in_place()
-    # densification statistics (train.py:130, 143-144) and the iteration's ONE collective
-    gdp.finish_step(scene, [o["viewspace_points"].grad for o in outs], radii, it, world=world, group=group)
-    del outs
+    # densification statistics (train.py:130, 143-144), the iteration's one exchange and the
+    # Adam step: at N > 1 the bucket's all-reduce goes out in chunks and each chunk's update
+    # runs as soon as that chunk lands (gsr.dp.finish_step), so the update overlaps the exchange
+    on_chunk = None
     if optimizer_step:
         apply_lr_schedule(scene, it)
-        fp.step(grad_scale=1.0 / (len(views) * max(world, 1)))
+        fp.begin_step(grad_scale=1.0 / (len(views) * max(world, 1)))
+        on_chunk = fp.step_range
+    gdp.finish_step(scene, [o["viewspace_points"].grad for o in outs], radii, it, world=world, group=group,
+                    on_chunk=on_chunk)
+    del outs
     return total.detach()
 
 

@@ -200,19 +200,25 @@ def exchange_grad(it, r, n):
     return torch.randn(n, generator=torch.Generator().manual_seed(7919 * it + r))
 
 
-def exchange_run(rank, world):
+EX_CHUNKS = 3  # the exchange's pipelined slices (forced: the test bucket is below the size floor)
+
+
+def exchange_run(rank, world, chunks=EX_CHUNKS):
     """train_step's tail over EX_ITERS: each rank's flat gradient and 2 views' statistics, then
     gsr.dp.finish_step (world 1: both ranks' views in one process, the gradients summed in rank
-    order).  Returns (scene, collectives issued per iteration as counted by wrapping every
-    torch.distributed collective)."""
+    order) with an optimizer stand-in recording the ranges it is handed.  Returns (scene,
+    per iteration (collectives finish_step reports, collectives issued as counted by wrapping
+    every torch.distributed collective), per iteration the (lo, hi) ranges the optimizer got,
+    per iteration the element counts the collectives carried)."""
     from gsr import dp
-    counts, calls = [], []
+    counts, calls, sizes, opt = [], [], [], []
     if world > 1:
         for name in COLLECTIVES:
             orig = getattr(dist, name, None)
             if orig is not None:
                 def wrap(*a, _orig=orig, _n=name, **k):
                     calls.append(_n)
+                    sizes.append(int(a[0].numel()) if a and hasattr(a[0], "numel") else -1)
                     return _orig(*a, **k)
                 setattr(dist, name, wrap)
     scene = small_scene()
@@ -229,11 +235,22 @@ def exchange_run(rank, world):
                 g2d.append(g * 0.02)
                 rad.append(radii)
         n0 = len(calls)
-        ret = dp.finish_step(scene, g2d, rad, it, world=world)
+        got = []
+        ret = dp.finish_step(scene, g2d, rad, it, world=world, on_chunk=lambda lo, hi: got.append((lo, hi)),
+                             chunks=chunks, min_chunk=1)
         counts.append((ret, len(calls) - n0))
+        opt.append(got)
+        sizes.append(None)  # iteration separator
     if world > 1:
         dp.sync_max_radii(scene.stats)
-    return scene, counts
+    per_it, cur = [], []
+    for x in sizes:
+        if x is None:
+            per_it.append(cur)
+            cur = []
+        else:
+            cur.append(x)
+    return scene, counts, opt, per_it
 
 
 def run_exchange(rank, world, port, out_path):
@@ -241,11 +258,60 @@ def run_exchange(rank, world, port, out_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        scene, counts = exchange_run(rank, world)
+        scene, counts, opt, sizes = exchange_run(rank, world)
         if rank == 0:
             out = {k: v.numpy() for k, v in scene.stats.items()}
-            out.update(grad=scene.fp.grad.numpy(), counts=np.array(counts), tail=np.array(scene.fp.tail))
+            out.update(grad=scene.fp.grad.numpy(), counts=np.array(counts), tail=np.array(scene.fp.tail),
+                       opt=np.array([r for it in opt for r in it]), opt_per_it=np.array([len(it) for it in opt]),
+                       sizes=np.array([sum(it) for it in sizes]), nsizes=np.array([len(it) for it in sizes]))
             np.savez(out_path, **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+# ---- the reference loop's exchange helper (gsr.dp.ReferenceExchange) ---------------------
+
+def refex_run(rank, world, P=300):
+    """Two parameters' gradients + each rank's 2 views of statistics per iteration, over two
+    iterations (statistics on, then off), through ReferenceExchange (world 1: both ranks'
+    gradients summed in rank order and all views in one process)."""
+    import types
+    from gsr import dp
+    xyz = torch.zeros(P, 3, requires_grad=True)
+    alb = torch.zeros(P, 3, requires_grad=True)
+    g = types.SimpleNamespace(xyz_gradient_accum=torch.zeros(P, 1), denom=torch.zeros(P, 1), max_radii2D=torch.zeros(P))
+    ex = dp.ReferenceExchange([xyz, alb], P)
+    issued = []
+    grads = []
+    for it, stats_on in ((0, True), (1, False)):
+        ranks = [rank] if world > 1 else list(range(2))
+        xyz.grad = sum(torch.randn(P, 3, generator=torch.Generator().manual_seed(100 * it + r)) for r in ranks)
+        alb.grad = sum(torch.randn(P, 3, generator=torch.Generator().manual_seed(500 + 100 * it + r)) for r in ranks)
+        g2d, rad = [], []
+        for r in ranks:
+            for j in range(VIEWS_PER_RANK):
+                gg, radii = view_stats(it, r * VIEWS_PER_RANK + j, P)
+                g2d.append(gg * 0.02)
+                rad.append(radii)
+        ex.add_views(g2d, rad, g.max_radii2D, stats_on)
+        issued.append(ex.exchange(g, stats_on, world=world, chunks=2, min_chunk=1))
+        grads.append((xyz.grad.clone(), alb.grad.clone()))
+    if world > 1:
+        dp.sync_max_radii({"max_radii2D": g.max_radii2D})
+    return g, grads, issued
+
+
+def run_refex(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g, grads, issued = refex_run(rank, world)
+        if rank == 0:
+            np.savez(out_path, accum=g.xyz_gradient_accum.numpy(), denom=g.denom.numpy(),
+                     max_radii2D=g.max_radii2D.numpy(), xyz0=grads[0][0].numpy(), alb1=grads[1][1].numpy(),
+                     issued=np.array(issued))
         dist.barrier()
     finally:
         dist.destroy_process_group()

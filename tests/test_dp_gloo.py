@@ -99,20 +99,38 @@ def test_replicas_identical_sees_one_bit(tmp_path):
     assert np.load(out).tolist() == [False, True, False]
 
 
-def test_iteration_exchange_is_one_collective(tmp_path):
-    """gsr.dp.finish_step (train_step's tail) issues exactly ONE collective
-    per iteration at world size 2 -- the flat gradient's SUM all-reduce, carrying the step's
-    densification sums in its tail below densify_until_iter and the gradient alone past it --
-    and the result equals the sequential accumulation over both ranks' views: gradient
-    bit-exact (two-rank sums commute), denom and max_radii2D exact (the rank-local maxima
-    MAX-reduced once, as densification does), the norm accumulator to float order; the sums
-    stop at iteration 15000 (train.py:143) while max_radii2D keeps updating (train.py:130)."""
+def test_iteration_exchange_is_one_pipelined_collective(tmp_path):
+    """gsr.dp.finish_step (train_step's tail) issues ONE logical
+    exchange per iteration at world size 2 -- the flat gradient's SUM all-reduce, carrying the
+    step's densification sums in its tail below densify_until_iter and the gradient alone past
+    it -- sent as EX_CHUNKS consecutive slices that together cover the bucket exactly once, and
+    hands the optimizer every gradient element exactly once, slice by slice in order (the
+    pipelined Adam); the result equals the sequential accumulation over both ranks' views:
+    gradient bit-exact (two-rank sums commute, and a SUM is elementwise, so slicing changes no
+    bit), denom and max_radii2D exact (the rank-local maxima MAX-reduced once, as densification
+    does), the norm accumulator to float order; the sums stop at iteration 15000 (train.py:143)
+    while max_radii2D keeps updating (train.py:130)."""
     out = str(tmp_path / "exchange.npz")
     mp.spawn(dp_worker.run_exchange, args=(2, free_port(), out), nprocs=2, join=True)
     got = np.load(out, allow_pickle=False)
-    ref, ref_counts = dp_worker.exchange_run(0, 1)
-    assert got["counts"].tolist() == [[1, 1]] * len(dp_worker.EX_ITERS), got["counts"]
+    ref, ref_counts, ref_opt, _ = dp_worker.exchange_run(0, 1)
+    K = dp_worker.EX_CHUNKS
+    assert got["counts"].tolist() == [[K, K]] * len(dp_worker.EX_ITERS), got["counts"]
     assert [c[0] for c in ref_counts] == [0] * len(dp_worker.EX_ITERS)
+    n, P = ref.fp.n, ref.P
+    # the slices carry the whole bucket: gradient + sums below 15000, the gradient alone after
+    want = [n + 2 * P if it < 15000 else n for it in dp_worker.EX_ITERS]
+    assert got["sizes"].tolist() == want and got["nsizes"].tolist() == [K] * len(want)
+    # the optimizer sees [0, n) once per iteration, in ascending contiguous ranges
+    per = got["opt_per_it"].tolist()
+    rs = got["opt"].tolist()
+    i = 0
+    for k in per:
+        its = rs[i:i + k]
+        i += k
+        assert its[0][0] == 0 and its[-1][1] == n and all(a[1] == b[0] for a, b in zip(its, its[1:]))
+        assert all(lo % 4 == 0 for lo, _ in its)
+    assert all(r == [[0, n]] for r in [[list(x) for x in it] for it in ref_opt])
     assert int(got["tail"]) == 2 * ref.P
     assert np.array_equal(got["grad"], ref.fp.grad.numpy())
     assert np.array_equal(got["denom"], ref.stats["denom"].numpy())
@@ -126,3 +144,20 @@ def test_iteration_exchange_is_one_collective(tmp_path):
     # max_radii2D did take the last iterations' views
     _, r_last = dp_worker.view_stats(dp_worker.EX_ITERS[-1], 0, ref.P)
     assert (ref.stats["max_radii2D"] >= r_last.float()).all()
+
+
+def test_reference_loop_exchange(tmp_path):
+    """gsr.dp.ReferenceExchange (INTEGRATION.md's recipe for the reference's own train.py loop):
+    one exchange per iteration (2 pipelined slices here), gradients summed over the ranks bit
+    for bit, the statistics deltas folded in while they are on, and max_radii2D equal after the
+    one MAX-reduce densification makes."""
+    out = str(tmp_path / "refex.npz")
+    mp.spawn(dp_worker.run_refex, args=(2, free_port(), out), nprocs=2, join=True)
+    got = np.load(out, allow_pickle=False)
+    g, grads, issued = dp_worker.refex_run(0, 1)
+    assert got["issued"].tolist() == [2, 2] and issued == [0, 0]
+    assert np.array_equal(got["xyz0"], grads[0][0].numpy())
+    assert np.array_equal(got["alb1"], grads[1][1].numpy())
+    assert np.array_equal(got["denom"], g.denom.numpy())
+    assert np.array_equal(got["max_radii2D"], g.max_radii2D.numpy())
+    np.testing.assert_allclose(got["accum"], g.xyz_gradient_accum.numpy(), rtol=1e-6, atol=1e-7)

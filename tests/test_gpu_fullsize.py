@@ -140,11 +140,35 @@ def test_full_sampled_tiles_forward(full):
     m = _tile_mask(tiles, gx, W, H)
     color = st["color"].cpu().numpy()
     assert rel_l2(color[:, m], out[:, m]) <= 1e-6
-    # measured: no blend decision differs (tools/parity_margins.py, profiles/r2_parity_margins.log)
-    np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
+    mine_nc, ref_nc = st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m]
+    if c.get("clustered"):
+        # cfg2c's sampled tiles (~10k pixels, up to ~2.7k contributions each) hold a pixel or
+        # two whose last contributor sits where alpha is within ulps of 1/255 or T of 1e-4, so
+        # the GPU's exponent arithmetic (conic pre-scaled by log2 e, FMAs, exp2: gsr_tile.hpp
+        # gauss_power) decides it differently from the oracle's expf -- as on the reference's
+        # own render_large fixture (test_gpu_render_golden.py).  Bar: at most 1 pixel in 2000
+        # differs, each by one position, and the oracle built with the GPU's exponent
+        # (liboracle_gpuexp) reproduces every GPU decision.
+        diff = mine_nc != ref_nc
+        assert diff.sum() <= max(1, m.sum() // 2000), diff.sum()
+        assert (np.abs(mine_nc.astype(np.int64) - ref_nc.astype(np.int64)) <= 1).all()
+        prev = orc.use_variant("gpuexp")
+        try:
+            out, fT_g, nc_g = orc.render_fwd(st["ranges"], st["point_list"], rec[:, 0:2], rec[:, 6:9], rec[:, 2:6],
+                                             np.zeros(3, np.float32), W, H, tiles=tiles)
+        finally:
+            orc.use_variant(prev)
+        np.testing.assert_array_equal(mine_nc, nc_g.reshape(H, W)[m])
+        # a flipped pixel's final T moves by a factor (1 - alpha) or (1 - alpha) ~ T's own
+        # value: north_star's 1e-4 against the canonical oracle, 1e-6 against the gpuexp one
+        assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-4
+        fT = fT_g
+    else:
+        # measured: no blend decision differs (tools/parity_margins.py, profiles/r2_parity_margins.log)
+        np.testing.assert_array_equal(mine_nc, ref_nc)
     # per-pixel rounding grows with the blended count: cfg2/cfg5 pixels blend ~100 Gaussians,
-    # cfg2c's spray and sculpture tiles ~1.5k (its largest difference measured 2.2e-6); both
-    # bars sit far inside north_star's 1e-4 relative
+    # cfg2c's spray and ground tiles up to ~2.7k (its largest difference measured 2.2e-6); both
+    # bars sit far inside north_star's 1e-4 relative (cfg2c: against the gpuexp oracle's colours)
     bar = 1e-5 if c.get("clustered") else 1e-6
     assert np.abs(color[:, m] - out[:, m]).max() <= bar
     assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
@@ -393,11 +417,7 @@ def test_cfg3_relit_render_at_size():
     assert np.abs(out[:, m]).max() > 0.05  # the sampled tiles are lit
     assert rel_l2(color[:, m], out[:, m]) <= 1e-6
     np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
-    # per-pixel rounding grows with the blended count: cfg2/cfg5 pixels blend ~100 Gaussians,
-    # cfg2c's spray and sculpture tiles ~1.5k (its largest difference measured 2.2e-6); both
-    # bars sit far inside north_star's 1e-4 relative
-    bar = 1e-5 if c.get("clustered") else 1e-6
-    assert np.abs(color[:, m] - out[:, m]).max() <= bar
+    assert np.abs(color[:, m] - out[:, m]).max() <= 1e-6
     assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
     del st
     img_errs, errs, errs2, o_f = _fused_vs_calls(scene, view, light_leaves, bg, fix_sky=True)

@@ -66,6 +66,7 @@ def main(cfg="cfg2c", calls=3):
     for call in range(int(calls)):
         L.gsr_debug_fwd_times_reset()
         L.gsr_debug_bwd_times_reset()
+        L.gsr_debug_st_times_reset()
         torch.cuda.synchronize()
         R, color, radii, geom, binb, img = _C.rasterize_gaussians(bg, g["means3D"], e, g["opacities"], g["scales"],
                                                                   g["rotations"], 1.0, e, vm, pm, cam.tanfovx,
@@ -74,6 +75,22 @@ def main(cfg="cfg2c", calls=3):
                                         cam.tanfovx, cam.tanfovy, dout, g["shs"], deg, cp, geom, R, binb, img)
         torch.cuda.synchronize()
         print(f"{cfg} call {call}")
+        sb = (C.c_ulonglong * (4 * MAXU))()
+        L.gsr_debug_st_times(sb, MAXU)
+        t = np.frombuffer(sb, dtype=np.uint64).reshape(MAXU, 4).astype(np.int64).copy()
+        t = t[t[:, 2] > 0]
+        if len(t):
+            t0 = t[:, 0].min()
+            setup = (t[:, 1] - t[:, 0]) / 100.0
+            pas = (t[:, 2] - t[:, 1]) / 100.0
+            end = (t[:, 2] - t0) / 100.0
+            o = np.argsort(-pas)[:5]
+            print(f"  st_scatter: span {end.max():.1f} us over {len(t)} waves; set-up p50/max {np.median(setup):.1f}/"
+                  f"{setup.max():.1f} us; ranking pass p50/p99/max {np.median(pas):.1f}/{np.percentile(pas, 99):.1f}/"
+                  f"{pas.max():.1f} us; longest passes (us, block, start): "
+                  + "; ".join(f"{pas[i]:.0f} b{t[i, 3]} @{(t[i, 1] - t0) / 100:.0f}" for i in o))
+            if os.environ.get("GSR_STATS_DUMP"):
+                np.save(f"{os.environ['GSR_STATS_DUMP']}_st{call}.npy", t)
         for name, fn in (("fwd", L.gsr_debug_fwd_times), ("bwd", L.gsr_debug_bwd_times)):
             fn(tb, MAXU)
             t = np.frombuffer(tb, dtype=np.uint64).reshape(MAXU, REC).astype(np.int64).copy()
