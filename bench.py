@@ -43,10 +43,14 @@ METRIC = "MPix/s fwd+bwd, 1.5M Gaussians @1080p; train iters/s at 1/2/4/8 GPUs"
 def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
     """SURVEY §8d per-stage compulsory HBM bytes (each array touched once)."""
     S = 12 * M if M else 12
+    F = 4 * TRAIN_NCH  # the relit composite's float channels per Gaussian (gsr.relit.RELIT_CHANNELS)
     return {
         "preprocess": P * 12 + Pv * (32 + S) + P * 8 + Pv * 67,
         "render_fwd": T * 8 + R * 40 + Npix * 20,
         "render_bwd": T * 8 + R * 40 + Npix * 20 + Pv * 44,
+        # the multi-channel composite: §8d's terms with nch channels in place of 3 colours
+        "render_fwd_mc": T * 8 + R * (28 + F) + Npix * (F + 8),
+        "render_bwd_mc": T * 8 + R * (28 + F) + Npix * (8 + F) + Pv * (44 + F),
         # this design's compulsory bytes (DESIGN §3): reads radii, the 9-float accumulator line,
         # means, scales, rotations, SH; writes every output row of every Gaussian (the reference's
         # zero-filled buffers: dmean2D, dcolor, dopacity, dmean3D, dcov3D, dscale, drot, dsh)
@@ -55,7 +59,11 @@ def algorithmic_bytes(stage, P, Pv, R, T, Npix, M):
 
 
 STAGE_KERNEL = {"preprocess": "k_preprocess", "render_fwd": "k_render_fwd", "render_bwd": "k_render_bwd",
-                "preprocess_bwd": "k_preprocess_bwd"}
+                "preprocess_bwd": "k_preprocess_bwd", "render_fwd_mc": "k_render_fwd_mc",
+                "render_bwd_mc": "k_render_bwd_mc", "shade_fwd": "k_shade_fwd", "shade_bwd": "k_shade_bwd"}
+# the relit legs' kernel-level stages (render_fwd / render_bwd also hold the order launch)
+RELIT_STAGES = ("preprocess", "depth_sort", "st_emit", "render_fwd_mc", "render_bwd_mc", "preprocess_bwd",
+                "shade_fwd", "shade_bwd")
 
 
 # spec VALU issue rate: a wave64 VALU instruction issues over 2 cycles on a SIMD-32, 2.4 GHz
@@ -144,8 +152,12 @@ def single_call_median(view, W, H, n=50, warm=10):
 def tile_roofline(dom, P, Pv, R, T, W, H, M, workload, dev):
     """The roofline object of the dominant stage ``dom`` = (stage, avg launch ms)."""
     dom_bytes = algorithmic_bytes(dom[0], P, Pv, R, T, W * H, M)
-    achieved_gbs = dom_bytes / (dom[1] * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(dom[0], workload)
+    if dom_bytes is None or dom[1] <= 0:  # a stage without a §8d byte count (or not timed)
+        return {"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
+                "traffic": None if traffic is None else int(traffic), "kernel": dom[0],
+                "avg_launch_ms": round(dom[1], 4), "frac_null_reason": f"no SURVEY §8d byte count for stage {dom[0]}"}
+    achieved_gbs = dom_bytes / (dom[1] * 1e-3) / 1e9
     hbm = {"achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
            "frac": round(achieved_gbs / HBM_PEAK_GBS, 5), "bytes": "algorithmic (SURVEY §8d per-stage figure x "
                                                                    "this launch's measured P, P_v, R)",
@@ -260,6 +272,33 @@ class _RelitModel:
         self.__dict__.update(kw)
 
 
+class _WeightedSum(torch.autograd.Function):
+    """The relit legs' training-style loss: sum over render()'s images of <image, weights>
+    (fixed random weights), as one dot product per image instead of a product image, a sum
+    and a scalar add per image; the backward writes weights x dL into the composite's gradient
+    rows when render() reserved them (gsr.relit.slab_take), so its channel split copies
+    nothing.  Same value and gradient as sum((out[k] * w[k]).sum())."""
+
+    @staticmethod
+    def forward(ctx, weights, *imgs):
+        ctx.weights, ctx.imgs = weights, imgs
+        return torch.stack([torch.dot(i.reshape(-1), w.reshape(-1)) for i, w in zip(imgs, weights)]).sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        from gsr import relit
+        grads = []
+        for i, w in zip(ctx.imgs, ctx.weights):
+            dst = relit.slab_take(i) if i.is_contiguous() else None
+            if dst is not None and dst.shape == w.shape:
+                torch.mul(w, g, out=dst)
+                grads.append(dst)
+            else:
+                grads.append(w * g)
+        ctx.imgs = None
+        return (None, *grads)
+
+
 def bench_relight(args, dev):
     """--config cfg3 / cfg5-relit: relight_leg as the JSON line."""
     print(json.dumps(relight_leg(args, dev, args.config == "cfg5-relit", args.steps, args.warmup,
@@ -306,6 +345,7 @@ def relight_leg(args, dev, stress, steps, warmup, with_calls=True, P_fg=None):
     bg = torch.zeros(3, device=dev)
     names = ("render", "diffuse_color", "specular_color", "depth", "normal", "alpha", "normal_ref")
     dweights = {k: torch.randn(3, H, W, generator=gen).to(dev) for k in names}
+    dweights_t = tuple(dweights[k] for k in names)
 
     is_sky_dev = is_sky.to(dev)[:, None]  # one device tensor: render()'s foreground index stays cached
     # consecutive views (the relight sequence of relit_novel_view.py renders one view per env
@@ -329,7 +369,7 @@ def relight_leg(args, dev, stress, steps, warmup, with_calls=True, P_fg=None):
                              get_opacity=t["opacity"], get_is_sky=is_sky_dev, get_albedo=t["albedo"],
                              get_roughness=t["roughness"], get_metalness=t["metalness"])
             out = fn(view, pc, light, sky_sh, 1, pipe, bg, debug=False, fix_sky=True)
-            loss = sum((out[k] * dweights[k]).sum() for k in names)
+            loss = _WeightedSum.apply(dweights_t, *[out[k] for k in names])
             loss.backward()
 
     def timed(fn):
@@ -343,6 +383,32 @@ def relight_leg(args, dev, stress, steps, warmup, with_calls=True, P_fg=None):
         return (time.perf_counter() - t0) * 1e3 / steps
 
     ms = timed(relit.render)
+    # the dominant kernel's live launch time (HIP events on its stream, views one at a time on
+    # one stream after the timed region) and the measured R, P_v of one more view
+    from gsr import _lib
+    saved = rstreams[:]
+    rstreams[:] = [main_s]
+    _lib.profile_read(reset=True)
+    _lib.profile_stages(list(RELIT_STAGES))
+    _lib.profile_enable(True)
+    for _ in range(max(1, args.event_steps)):
+        step(relit.render)
+    torch.cuda.synchronize()
+    _lib.profile_enable(False)
+    live = _lib.profile_read(reset=True)
+    _lib.profile_stages(None)
+    dgr.record_channels_calls(True)
+    step(relit.render)
+    torch.cuda.synchronize()
+    dgr.record_channels_calls(False)
+    rstreams[:] = saved
+    R, Pv = int(dgr.last_channels_call["num_rendered"]), int(dgr.last_channels_call["visible"])
+    stage_ms = {k: v[0] / v[1] for k, v in live.items() if v[1] > 0}
+    dom = max(((k, v) for k, v in stage_ms.items() if k in RELIT_STAGES), key=lambda kv: kv[1],
+              default=("render_bwd_mc", 0.0))
+    workload = f"{'cfg5 (relit stress)' if stress else 'cfg3'}: {P_fg} foreground + {P - P_fg} sky Gaussians"
+    roof = tile_roofline(dom, P, Pv, R, ((W + 15) // 16) * ((H + 15) // 16), W, H, 0, workload, dev)
+    roof["stage_ms"] = {k: round(v, 4) for k, v in stage_ms.items()}
     res = {True: float("nan"), False: float("nan")}
     if with_calls and not stress:
         for cached in (True, False):
@@ -358,6 +424,7 @@ def relight_leg(args, dev, stress, steps, warmup, with_calls=True, P_fg=None):
                                "angles (one per view), fix_sky=True, debug=False", "gaussians": P,
                    "width": W, "height": H},
         "mpix_per_s": round(W * H / (ms * 1e-3) / 1e6, 3),
+        "roofline": roof, "measured": {"num_rendered": R, "visible": Pv},
         "implementation": f"gsr.relit.render: fused relit features + one 14-channel composite; views on {nsr} "
                           "HIP streams",
         "render_calls": None if res[True] != res[True] else {
@@ -1064,7 +1131,7 @@ def main():
         for key, stress in (("cfg3", False), ("cfg5_relit", True)):
             r = relight_leg(args, dev, stress, 10, 3, with_calls=False, P_fg=4_545_455 if stress else 1_000_000)
             rl[key] = {k: r[k] for k in ("value", "unit", "ms_per_step", "steps", "warmup", "mpix_per_s", "config",
-                                          "implementation")}
+                                          "roofline", "measured", "implementation")}
             torch.cuda.empty_cache()
         out["relit"] = rl
     if rank == 0 and world == 1 and not args.no_refalgo and not args.ply:

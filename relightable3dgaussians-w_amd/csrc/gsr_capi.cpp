@@ -22,6 +22,8 @@
 #include <vector>
 
 #include "../../include/gsr.h"
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "gsr_kernels.hpp"
 #include "gsr_shade.hpp"
 
@@ -311,14 +313,36 @@ struct Prof {
 };
 Prof g_prof;
 
+// roctx ranges: every stage is also a named range ("gsr:<stage>") for external
+// rocprofv3 --marker-trace timelines of the reference's own train.py on this path; on unless
+// GSR_ROCTX=0 (a call into librocprofiler-sdk-roctx, a no-op without a tool attached)
+static bool roctx_on() {
+    static const bool on = [] {
+        const char* e = getenv("GSR_ROCTX");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+extern const char* kStageNames[];
 struct StageTimer {
     hipEvent_t a = nullptr;
     int stage;
     hipStream_t s;
+    bool rx = false;
     StageTimer(int st, hipStream_t ss) : stage(st), s(ss) {
+        if (roctx_on()) {
+            static const std::vector<std::string> names = [] {
+                std::vector<std::string> v;
+                for (int i = 0; i < ST_COUNT; i++) v.push_back(std::string("gsr:") + kStageNames[i]);
+                return v;
+            }();
+            roctxRangePushA(names[st].c_str());
+            rx = true;
+        }
         if (g_prof.on && ((g_prof.mask >> st) & 1u)) { a = g_prof.get(); (void)hipEventRecord(a, s); }
     }
     ~StageTimer() {
+        if (rx) roctxRangePop();
         if (a) {
             hipEvent_t b = g_prof.get();
             (void)hipEventRecord(b, s);
