@@ -35,7 +35,9 @@ __device__ unsigned long long g_bwd_times[GSR_UNIT_REC * 65536];
 #define BWD_STAT(k, v)
 #endif
 
-template <bool DET>
+// BG: the background is not all zero (its dL/dalpha term is carried); with a zero background
+// (render()'s default, the bench) the term and its per-evaluation multiply-add are dropped
+template <bool DET, bool BG = true>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -162,7 +164,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 const float dch = ae * Tn;
                 const float cdp = __builtin_fmaf(c2, dp2[q], __builtin_fmaf(c1, dp1[q], c0 * dp0[q]));
                 const float dcs = cdp - Sr[q];
-                const float dLda = __builtin_fmaf(Tn, dcs, inv * Tb[q]);
+                const float dLda = BG ? __builtin_fmaf(Tn, dcs, inv * Tb[q]) : Tn * dcs;
                 Sr[q] = __builtin_fmaf(ae, dcs, Sr[q]);
                 const float Gd = Ge * dLda;
                 S5 += Gd;
@@ -249,6 +251,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 #ifndef GSR_BWD_WAVES
 #define GSR_BWD_WAVES 4
 #endif
+#ifndef GSR_BWD_BG_SPEC
+#define GSR_BWD_BG_SPEC 0
+#endif
 template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
 k_render_bwd(RenderBwdArgs a) {
@@ -256,7 +261,13 @@ k_render_bwd(RenderBwdArgs a) {
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
         return;  // det: one writer per row
+#if GSR_BWD_BG_SPEC
+    // a zero background (wave-uniform scalar loads) takes the walk without its dL/dalpha term
+    if (a.bg[0] == 0.f && a.bg[1] == 0.f && a.bg[2] == 0.f) render_bwd_tile<DET, false>(a, tile, qallow);
+    else render_bwd_tile<DET, true>(a, tile, qallow);
+#else
     render_bwd_tile<DET>(a, tile, qallow);
+#endif
 }
 
 #ifdef GSR_RENDER_STATS
