@@ -83,8 +83,13 @@ __host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned
     return 8u * ((ntile + 7u) / 8u + 3u * HEAVY_CAP + 3u * ntail);
 }
 // the same with cost-balanced bands: a band holds at most 3 ntile / 8 + 2 tiles (balanced_band)
+// (GSR_BAL_GRID_X4: the bound in quarters of the mean band, 12 = 3x; a timing experiment only:
+// any other value can drop the tiles of a band longer than it)
+#ifndef GSR_BAL_GRID_X4
+#define GSR_BAL_GRID_X4 12u
+#endif
 __host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsigned ntail) {
-    return 8u * (3u * ((ntile + 7u) / 8u) + 2u + 3u * HEAVY_CAP + 3u * ntail);
+    return 8u * ((GSR_BAL_GRID_X4 * ((ntile + 7u) / 8u) + 3u) / 4u + 2u + 3u * HEAVY_CAP + 3u * ntail);
 }
 // The backward passes' bands: 1 (default) -- cost-balanced (each band a contiguous tile range
 // holding an eighth of the estimated cost: balanced_band), 0 -- equal tile counts
