@@ -161,3 +161,21 @@ def test_reference_loop_exchange(tmp_path):
     assert np.array_equal(got["denom"], g.denom.numpy())
     assert np.array_equal(got["max_radii2D"], g.max_radii2D.numpy())
     np.testing.assert_allclose(got["accum"], g.xyz_gradient_accum.numpy(), rtol=1e-6, atol=1e-7)
+
+
+def test_exchange_chunks_cover_aligned():
+    """gsr.dp.exchange_chunks: contiguous ascending slices covering [0, n) exactly once, every
+    start a multiple of 4 floats (the ranged Adam's float4 rows), at most `chunks` of them,
+    none below the size floor unless the bucket itself is smaller."""
+    from gsr import dp
+    for n, k, floor in ((23_316_836 + 3_000_000, 4, 1 << 20), (10, 4, 1 << 20), (1001, 3, 1), (4096, 8, 100),
+                        (7, 8, 1), (0, 4, 1)):
+        r = dp.exchange_chunks(n, k, floor)
+        if n == 0:
+            assert r == [(0, 0)]
+            continue
+        assert r[0][0] == 0 and r[-1][1] == n and all(a[1] == b[0] for a, b in zip(r, r[1:]))
+        assert all(lo % 4 == 0 and hi > lo for lo, hi in r)
+        assert 1 <= len(r) <= k
+        if n >= k * floor:
+            assert len(r) == k

@@ -99,7 +99,7 @@ def main(tag="r01", workload=None):
                     f"{'' if v['valu_insts'] is None else round(v['valu_insts'] / 1e6, 2)} | "
                     f"{'' if v['salu_insts'] is None else round(v['salu_insts'] / 1e6, 2)} |\n")
         if bench:
-            f.write(f"\nbench line under the profiler: value {bench['value']} MPix/s, ms/step {bench['ms_per_step']}"
+            f.write(f"\nbench line under the profiler: value {bench['value']} {bench.get('unit', 'MPix/s')}, ms/step {bench['ms_per_step']}"
                     f"\n\nstage_ms (HIP events): {json.dumps(bench.get('stage_ms'))}\n")
     print(open(os.path.join(out_dir, f"{tag}_summary.md")).read())
 
