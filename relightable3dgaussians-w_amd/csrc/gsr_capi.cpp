@@ -65,7 +65,8 @@ struct GeomLayout {
         offsets, scan_tmp, sort_tmp, total;
 };
 struct ImgLayout {
-    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, total;
+    size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, surv_n,
+        surv, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -117,6 +118,10 @@ ImgLayout img_layout(int W, int H) {
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
     L.nheavy = c.take(4 * 32);  // forward [0..8), backward [8..16), the backward's band bounds [16..25)
+    // the forward's survivor lists for the backward (RenderFwdArgs::surv): 8 B x SURV_CAP per tile,
+    // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
+    L.surv_n = c.take(4 * T);
+    L.surv = c.take(8 * (size_t)gsr::SURV_CAP * T);
     L.total = c.o + 256;
     return L;
 }
@@ -693,6 +698,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
+        ord.unset = gsr::SURV_CAP ? at<uint32_t>(img, il.surv_n) : nullptr;  // no list unless this forward stores one
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, rect_packed, gsx, st_h(width, height), NS,
@@ -742,6 +748,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
     ra.row_cost = at<uint32_t>(img, il.row_cost);
+    if (gsr::SURV_CAP && !mc) {  // the single-channel backward walks the forward's survivor lists
+        ra.surv = at<uint2>(img, il.surv);
+        ra.surv_n = at<uint32_t>(img, il.surv_n);
+    }
     // the forward tile pass over the binning in `bin`; its workgroups also zero the backward's
     // accumulator lines (zero_slice; the depth sort's digit scans did it up to round 3)
     ra.zero = reinterpret_cast<float4*>(at<float>(geom, gl.acc));
@@ -765,6 +775,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                     ma.n_contrib = ra.n_contrib;
                     ma.zero = ra.zero;
                     ma.zero_n4 = ra.zero_n4;
+                    if (gsr::SURV_CAP) {  // the survivors (the same for every group)
+                        ma.surv = at<uint2>(img, il.surv);
+                        ma.surv_n = at<uint32_t>(img, il.surv_n);
+                    }
                 } else {
                     ma.tile_nmax = nullptr;
                 }
@@ -897,6 +911,10 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = nullptr;  // already summed by the cached call's forward
+    if (gsr::SURV_CAP) {  // the same survivors again (the lists of the cached call are rewritten)
+        ra.surv = at<uint2>(img, il.surv);
+        ra.surv_n = at<uint32_t>(img, il.surv_n);
+    }
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {
         GSR_STAGE(ST_RENDER_FWD);
@@ -976,6 +994,10 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.order = at<uint32_t>(img, il.order_bwd);
         ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         ra.partial = partial;
+        if (gsr::SURV_CAP) {
+            ra.surv = at<uint2>(img, il.surv);
+            ra.surv_n = at<uint32_t>(img, il.surv_n);
+        }
         {
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
@@ -993,6 +1015,8 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
                                                    ra.nheavy, at<uint32_t>(img, il.tile_nmax),
                                                    at<uint32_t>(img, il.tile_emax), *mc, c0);
                     ma.ranges = det_ranges;
+                    ma.surv = const_cast<uint2*>(ra.surv);
+                    ma.surv_n = const_cast<uint32_t*>(ra.surv_n);
                     ma.final_T = const_cast<float*>(ra.final_T);
                     ma.n_contrib = const_cast<uint32_t*>(ra.n_contrib);
                     ma.dL_dout = mc->dL_dout + (size_t)c0 * width * height;

@@ -80,6 +80,15 @@ struct __align__(16) Rec {
 constexpr int ACC_STRIDE = GSR_ACC_STRIDE;
 static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9 floats, 16-B aligned");
 
+// The forward tile pass's survivor lists (RenderFwdArgs::surv): at most SURV_CAP entries per
+// tile (cfg2: 285 at most, the clustered cfg2c 749), a count of SURV_NONE sends the backward
+// back to its super-tile list.  GSR_SURV_CAP=0 builds without them.
+#ifndef GSR_SURV_CAP
+#define GSR_SURV_CAP 1024
+#endif
+constexpr uint32_t SURV_CAP = GSR_SURV_CAP;
+constexpr uint32_t SURV_NONE = 0xffffffffu;
+
 // Gradient outputs added into (instead of overwritten): the backward kernels' accumulate
 // bits (include/gsr.h GSR_ACC_*), so several views' gradients are summed where they are made.
 constexpr unsigned ACC_MEAN3D = 1u, ACC_SCALE = 2u, ACC_ROT = 4u, ACC_OPACITY = 8u, ACC_ALBEDO = 16u, ACC_ROUGH = 32u,

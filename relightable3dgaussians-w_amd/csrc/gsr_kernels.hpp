@@ -119,6 +119,7 @@ struct TileOrderArgs {
     int heavy_bits;
     int heavy_rel8;  // also heavy: cost >= heavy_rel8 / 8 x the band's mean (0: absolute threshold only)
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
+    uint32_t* unset;  // optional per-tile words set to SURV_NONE (survivor counts the forward may not write)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
     // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
     // forward's order for its tile pass to raise (zero_rows); nrows = tile rows
@@ -233,6 +234,12 @@ struct RenderFwdArgs {
     // write bandwidth to spare
     float4* zero;
     long long zero_n4;
+    // when non-null: each whole-tile unit stores its survivors (entries reaching a live
+    // quadrant), front to back, to surv[tile * SURV_CAP ...) as (Gaussian, position << 4 | reach
+    // mask) and their count to surv_n[tile] (SURV_NONE past SURV_CAP); the backward walks them
+    // instead of re-filtering the super-tile list
+    uint2* surv;
+    uint32_t* surv_n;
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -257,6 +264,10 @@ struct RenderBwdArgs {
     // deterministic mode (non-null): each (tile, Gaussian) writes its partial sums to row
     // [instance] of DET_ROW3 floats instead of adding them into acc (k_det_gather sums them)
     float* partial;
+    // the forward's survivor lists (RenderFwdArgs::surv); tiles whose count is SURV_NONE (or
+    // all tiles when null) filter their super-tile list
+    const uint2* surv;
+    const uint32_t* surv_n;
 };
 constexpr int DET_ROW3 = 12;  // 8 sums + the ninth's four row partials
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
@@ -292,6 +303,9 @@ struct RenderMcArgs {
     int pstride, pc0;
     float4* zero;  // forward: as RenderFwdArgs::zero
     long long zero_n4;
+    // survivor lists as RenderFwdArgs::surv (forward: stored when non-null) and RenderBwdArgs::surv
+    uint2* surv;
+    uint32_t* surv_n;
 };
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);

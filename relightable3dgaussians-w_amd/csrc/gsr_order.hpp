@@ -148,6 +148,7 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
             a.zero_b[t] = 0u;
             if (a.zero_c) a.zero_c[t] = 0u;
         }
+        if (a.unset) a.unset[t] = SURV_NONE;
     }
     if (csum) atomicAdd(&s_band_cost, csum);
     __syncthreads();

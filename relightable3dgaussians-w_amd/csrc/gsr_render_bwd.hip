@@ -95,21 +95,46 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const unsigned sth = st_sth(a.grid_x, a.grid_y);
     const unsigned sti = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
+    // the forward's survivor list when it stored one (wave-uniform): batches of 64 back to front,
+    // each lane's entry loaded a batch ahead (its record one batch ahead too measured the same
+    // call and a slower 3-stream headline: 113 VGPRs); else the super-tile list, filtered and
+    // culled again
+    const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
+    const bool lst = sn != SURV_NONE;
+    uint32_t li = lst ? sn : 0u;  // list entries left
+    const uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);
     TileList<false> tl;
-    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    if (!lst)
+        tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
-        tl.fill(s_list);
-        uint32_t id = 0, ei = 0, p0 = 0;
-        const uint32_t nb = tl.take(s_list, id, ei, p0);
-        if (nb == 0) break;
-        const uint32_t p = p0 - (uint32_t)lane;  // list position (back to front)
-        uint32_t qm = 0;
+        uint32_t id = 0, nb, p, qm = 0;  // p: list position (back to front)
+        if (lst) {
+            nb = min(64u, li);
+            if (nb == 0) break;
+            const uint2 v = nv;
+            li -= nb;
+            nv = sl[max((int)li - 1 - lane, 0)];
+            id = v.x;
+            p = v.y >> 4;
+            if ((uint32_t)lane < nb) {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (p < qlim[q]) qm |= v.y & (1u << q);
+            }
+        } else {
+            tl.fill(s_list);
+            uint32_t ei = 0, p0 = 0;
+            nb = tl.take(s_list, id, ei, p0);
+            if (nb == 0) break;
+            p = p0 - (uint32_t)lane;
+        }
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float rc = 0.f;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, p, qlim);
+            if (!lst) qm = wt.reach(r, p, qlim);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
@@ -120,7 +145,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
+        // (position << 4 | reach mask): one word, one readfirstlane per survivor for both
+        s_c[lane] = make_float4(rc, __uint_as_float((p << 4) | qm), __uint_as_float(id), 0.f);
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         BWD_STAT(0, nb);
@@ -131,10 +157,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         if (!todo) continue;
         // one survivor (record A, B, Cq at batch slot k), back to front
         auto grad_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
-            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
+            const uint32_t mp = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y));
+            const uint32_t m = mp & 15u;
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
             const float c0 = B.z, c1 = B.w, c2 = Cq.x;
-            const uint32_t pos = p0 - (uint32_t)k;
+            const uint32_t pos = mp >> 4;  // list position
             // per-lane sums over the quadrants: M1 = sum G dL/dalpha dx, M2 = ... dy,
             // S2/S3/S4 = sum G dL/dalpha (dx dx, dx dy, dy dy), S5 = sum G dL/dalpha,
             // S6..8 = sum alpha T dL/dpix

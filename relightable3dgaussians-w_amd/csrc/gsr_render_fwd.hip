@@ -68,6 +68,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
+    // survivors stored so far (whole-tile units; SURV_NONE: none stored, or past SURV_CAP)
+    uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
+    uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
     uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
         tl.fill(s_list);
@@ -96,6 +99,19 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         s_e[lane] = ei;
         wave_lds_sync();
         const uint64_t todo0 = __ballot((qm & live) != 0);
+        if (scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
+            const uint32_t n = (uint32_t)__popcll(todo0);
+            if (scnt + n > SURV_CAP) {
+                scnt = SURV_NONE;
+            } else {
+                if ((qm & live) != 0) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(todo0 >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)todo0, 0u));
+                    sl[scnt + r] = make_uint2(id, (j << 4) | qm);
+                }
+                scnt += n;
+            }
+        }
         FWD_STAT(0, nb);
         FWD_STAT(1, __popcll(todo0));
         if (!todo0) continue;
@@ -197,6 +213,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
         }
     }
+    if (lane == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
     uint32_t nm = 0, nsum = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {

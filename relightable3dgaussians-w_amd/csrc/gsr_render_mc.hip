@@ -57,6 +57,9 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     }
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere
     uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
+    // the backward's survivor list (as gsr_render_fwd.hip): whole-tile units only
+    uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
+    uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
     while (live) {
         tl.fill(s_list);
         uint32_t id = 0, ei = 0, p0 = 0;
@@ -85,6 +88,19 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         for (int g = 0; g < NC4; g++) s_f[g][lane] = f[g];
         wave_lds_sync();
         uint64_t todo = __ballot((qm & live) != 0);
+        if (scnt != SURV_NONE) {
+            const uint32_t n = (uint32_t)__popcll(todo);
+            if (scnt + n > SURV_CAP) {
+                scnt = SURV_NONE;
+            } else {
+                if ((qm & live) != 0) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(todo >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)todo, 0u));
+                    sl[scnt + r] = make_uint2(id, (j << 4) | qm);
+                }
+                scnt += n;
+            }
+        }
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
         while (todo && live) {
             const int k = sgpr_ff1(todo);
@@ -132,6 +148,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         }
         if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }
+    if (threadIdx.x == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
     const int HW = a.H * a.W;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -168,7 +185,7 @@ template <int NC4>
 struct McBwdLds {
     float4 a[64], b[64];
     float4 f[NC4][64];
-    uint2 q[64];  // (quadrant mask, Gaussian id)
+    uint2 q[64];  // (list position << 4 | quadrant mask, Gaussian id)
     TileListLds list;
 };
 
@@ -215,23 +232,45 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     // back to front from the tile's last contributor (as gsr_render_bwd.hip)
     const unsigned sth = st_sth(a.grid_x, a.grid_y);
     const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
+    // the forward's survivor list when it stored one, else the super-tile list (as gsr_render_bwd.hip)
+    const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
+    const bool lst = sn != SURV_NONE;
+    uint32_t li = lst ? sn : 0u;
+    const uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);
     TileList<false> tl;
-    tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
+    if (!lst)
+        tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
     for (;;) {
-        tl.fill(sm.list);
-        uint32_t id = 0, ei = 0, p0 = 0;
-        const uint32_t nb = tl.take(sm.list, id, ei, p0);
-        if (nb == 0) break;
-        const uint32_t p = p0 - (uint32_t)lane;
-        uint32_t qm = 0;
+        uint32_t id = 0, nb, p, qm = 0;  // p: list position (back to front)
+        if (lst) {
+            nb = min(64u, li);
+            if (nb == 0) break;
+            const uint2 v = nv;
+            li -= nb;
+            nv = sl[max((int)li - 1 - lane, 0)];
+            id = v.x;
+            p = v.y >> 4;
+            if ((uint32_t)lane < nb) {
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    if (p < qlim[q]) qm |= v.y & (1u << q);
+            }
+        } else {
+            tl.fill(sm.list);
+            uint32_t ei = 0, p0 = 0;
+            nb = tl.take(sm.list, id, ei, p0);
+            if (nb == 0) break;
+            p = p0 - (uint32_t)lane;
+        }
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra;
         float4 f[NC4];
 #pragma unroll
         for (int g = 0; g < NC4; g++) f[g] = ra;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, p, qlim);
+            if (!lst) qm = wt.reach(r, p, qlim);
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
@@ -240,7 +279,7 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
         wave_lds_sync();
         sm.a[lane] = ra;
         sm.b[lane] = rb;
-        sm.q[lane] = make_uint2(qm, id);
+        sm.q[lane] = make_uint2((p << 4) | qm, id);
 #pragma unroll
         for (int g = 0; g < NC4; g++) sm.f[g][lane] = f[g];
         if constexpr (COMPACT) {
@@ -270,9 +309,10 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
                 F[4 * g + 2] = v.z;
                 F[4 * g + 3] = v.w;
             }
-            const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)Q2.x);
+            const uint32_t mp = (uint32_t)__builtin_amdgcn_readfirstlane((int)Q2.x);
+            const uint32_t m = mp & 15u;
             const float ax = A.x, ay = A.y, ka = A.z, kb = A.w, kc = B.x, op = B.y;
-            const uint32_t pos = p0 - (uint32_t)k;
+            const uint32_t pos = mp >> 4;  // list position
             float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f;
             float SF[NL];
 #pragma unroll

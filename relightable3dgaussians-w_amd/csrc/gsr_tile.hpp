@@ -448,6 +448,11 @@ __device__ __forceinline__ lmask m_ult(uint32_t a, uint32_t b) {  // a < b, a wa
     asm("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "s"(a), "v"(b));
     return m;
 }
+__device__ __forceinline__ lmask m_ultv(uint32_t a, uint32_t b) {  // a < b, a in a VGPR
+    lmask m;
+    asm("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
 __device__ __forceinline__ float sel(lmask m, float t, float f) {  // m ? t : f per lane
     float r;
     asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(f), "v"(t), "s"(m));
