@@ -415,6 +415,13 @@ int gsr_profile_read(double* ms, long long* counts, int n, int reset);
  * Set it before the forward whose backward should be deterministic. */
 int gsr_set_deterministic(int on);
 int gsr_get_deterministic(void);
+/* Survivor lists (default on; GSR_SURV_LISTS=0 in the environment turns them off): the forward
+ * tile pass stores each tile's surviving list entries in the image buffer and the backward walks
+ * them instead of filtering the tile's super-tile list again.  Results are identical either way
+ * (the same evaluations in the same order); a switch for tests and A/B timing.  Set it before
+ * the forward. */
+int gsr_set_survivor_lists(int on);
+int gsr_get_survivor_lists(void);
 /* 1 when this library was built with -DGSR_DEBUG (`make debug` -> lib/debug/libgsr.so): every
  * forward then verifies its tile lists against the preprocess (ids, culling, rect coverage,
  * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a

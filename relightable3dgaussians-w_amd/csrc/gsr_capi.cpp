@@ -225,6 +225,18 @@ bool det_on() {
     }
     return v != 0;
 }
+// The forward's survivor lists for the backward (gsr_set_survivor_lists / GSR_SURV_LISTS=0 to
+// turn off; on by default in builds with SURV_CAP > 0)
+std::atomic<int> g_surv{-1};
+bool surv_on() {
+    int v = g_surv.load();
+    if (v < 0) {
+        const char* e = getenv("GSR_SURV_LISTS");
+        v = (e && e[0] == '0') ? 0 : 1;
+        g_surv.store(v);
+    }
+    return gsr::SURV_CAP > 0 && v != 0;
+}
 // grow-only device scratch of one thread (the deterministic rows, the debug checks); the
 // calls that use it synchronise their stream before returning, so it is free again
 struct Scratch {
@@ -461,6 +473,11 @@ int gsr_set_deterministic(int on) {
 }
 
 int gsr_get_deterministic(void) { return det_on() ? 1 : 0; }
+int gsr_set_survivor_lists(int on) {
+    g_surv.store(on ? 1 : 0);
+    return GSR_OK;
+}
+int gsr_get_survivor_lists(void) { return surv_on() ? 1 : 0; }
 
 int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
                       void* img_buffer, void* stream_) {
@@ -748,7 +765,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
     ra.row_cost = at<uint32_t>(img, il.row_cost);
-    if (gsr::SURV_CAP && !mc) {  // the single-channel backward walks the forward's survivor lists
+    if (surv_on() && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
     }
@@ -775,7 +792,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                     ma.n_contrib = ra.n_contrib;
                     ma.zero = ra.zero;
                     ma.zero_n4 = ra.zero_n4;
-                    if (gsr::SURV_CAP) {  // the survivors (the same for every group)
+                    if (surv_on()) {  // the survivors (the same for every group)
                         ma.surv = at<uint2>(img, il.surv);
                         ma.surv_n = at<uint32_t>(img, il.surv_n);
                     }
@@ -911,7 +928,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = nullptr;  // already summed by the cached call's forward
-    if (gsr::SURV_CAP) {  // the same survivors again (the lists of the cached call are rewritten)
+    if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
     }

@@ -17,6 +17,11 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
+// 1: the survivor list holds only the survivors that blended in some quadrant (the others
+// contribute nothing in the backward)
+#ifndef GSR_SURV_BLENDED
+#define GSR_SURV_BLENDED 0
+#endif
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
@@ -95,11 +100,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         wave_lds_sync();
         s_a[lane] = ra;
         s_b[lane] = rb;
-        s_c[lane] = make_float4(rc, __uint_as_float(qm), 0.f, 0.f);
+        s_c[lane] = make_float4(rc, __uint_as_float(qm), __uint_as_float(id), 0.f);
         s_e[lane] = ei;
         wave_lds_sync();
         const uint64_t todo0 = __ballot((qm & live) != 0);
-        if (scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
+        if (!GSR_SURV_BLENDED && scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
             const uint32_t n = (uint32_t)__popcll(todo0);
             if (scnt + n > SURV_CAP) {
                 scnt = SURV_NONE;
@@ -117,6 +122,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         if (!todo0) continue;
         // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
+        uint64_t bmask = 0;  // batch slots of the survivors that blended anywhere (GSR_SURV_BLENDED)
+        uint32_t qbl = 0;    // GSR_SURV_BLENDED 2: lane k = the quadrants batch slot k blended in
         uint64_t todo = todo0;
         auto blend_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
@@ -126,6 +133,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             uint32_t pos1;
             asm("v_mov_b32 %0, %1" : "=v"(pos1) : "s"(p0 + (uint32_t)k + 1u));
             lmask blended = 0;
+            uint32_t qb = 0;
             FWD_STAT(5, m == 15u);
             FWD_STAT(6, m != 0u);
 #pragma unroll
@@ -151,6 +159,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
                 blended |= blend;
+                if (GSR_SURV_BLENDED == 2 && blend) qb |= 1u << q;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) {
@@ -159,7 +168,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                     }
                 }
             }
-            if (blended) klast = k;
+            if (blended) {
+                klast = k;
+                if (GSR_SURV_BLENDED) bmask |= 1ull << k;
+                if (GSR_SURV_BLENDED == 2) {
+                    uint32_t v;
+                    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(qb));
+                    qbl = sel((lmask)1ull << k, v, qbl);
+                }
+            }
         };
         // survivors in pairs over two register sets (the next survivor's record is read
         // while the current one blends, and no register copies between them); the walk's
@@ -184,6 +201,20 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             if (k < 0) break;
         }
         if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
+        if (GSR_SURV_BLENDED && scnt != SURV_NONE) {  // only the survivors that blended somewhere
+            const uint32_t n = (uint32_t)__popcll(bmask);
+            if (scnt + n > SURV_CAP) {
+                scnt = SURV_NONE;
+            } else {
+                if ((bmask >> lane) & 1u) {
+                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bmask >> 32),
+                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bmask, 0u));
+                    const float4 c = s_c[lane];
+                    sl[scnt + r] = make_uint2(__float_as_uint(c.z), (j << 4) | (GSR_SURV_BLENDED == 2 ? qbl : __float_as_uint(c.y)));
+                }
+                scnt += n;
+            }
+        }
     }
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {

@@ -102,6 +102,7 @@ def _declare(lib):
     lib.gsr_profile_stage_name.restype = C.c_char_p
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_set_deterministic.argtypes = [i]
+    lib.gsr_set_survivor_lists.argtypes = [i]
     lib.gsr_check_buffers.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
     lib.gsr_materialize_lists.argtypes = [i, i, i, vp, vp, vp, vp]
     lib.gsr_last_error.restype = C.c_char_p
@@ -116,7 +117,7 @@ def _declare(lib):
                "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
                "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
-               "gsr_get_deterministic", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
+               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
 
 
@@ -179,6 +180,16 @@ def set_deterministic(on=True):
 
 def deterministic():
     return bool(lib().gsr_get_deterministic())
+
+
+def set_survivor_lists(on=True):
+    """Survivor lists (gsr_set_survivor_lists): the backward walks the forward's per-tile
+    survivors instead of re-filtering the super-tile lists (default on; identical results)."""
+    check(lib().gsr_set_survivor_lists(int(bool(on))), "gsr_set_survivor_lists")
+
+
+def survivor_lists():
+    return bool(lib().gsr_get_survivor_lists())
 
 
 def debug_build():

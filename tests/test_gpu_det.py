@@ -27,7 +27,7 @@ DET_CASES = [c for c in CASES if c["name"] in ("cfg1_small_sh0", "sh3_orbit_bg",
                                                 "opaque_stack", "heavy_tiles")]
 
 
-def _backward(case, det):
+def _backward(case, det, surv=True):
     from diff_gaussian_rasterization import _C
     from gsr import _lib
     cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
@@ -35,8 +35,9 @@ def _backward(case, det):
     gs = mutate(gs, case.get("mutate"))
     kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), sh_degree=case.get("sh_degree", 0))
     _lib.set_deterministic(det)
+    _lib.set_survivor_lists(surv)
     try:
-        assert _lib.deterministic() == det
+        assert _lib.deterministic() == det and _lib.survivor_lists() == surv
         st = run_gpu(cam, gs, **kw)
         dout = torch.randn(3, cam.image_height, cam.image_width, generator=torch.Generator().manual_seed(1))
         grads = _C.rasterize_gaussians_backward(
@@ -46,6 +47,7 @@ def _backward(case, det):
         torch.cuda.synchronize()
     finally:
         _lib.set_deterministic(False)
+        _lib.set_survivor_lists(True)
     return [g.detach().cpu() for g in grads]
 
 
@@ -63,6 +65,17 @@ def test_deterministic_backward(case):
         assert e <= 1e-6, (k, e)
 
 
+@pytest.mark.parametrize("case", DET_CASES, ids=[c["name"] for c in DET_CASES])
+def test_survivor_lists_change_nothing(case):
+    """The backward over the forward's survivor lists evaluates the same (Gaussian, quadrant)
+    pairs in the same order as the one that filters the super-tile lists again: in
+    deterministic mode (no atomics) every gradient is bit-identical."""
+    with_lists = _backward(case, True, surv=True)
+    without = _backward(case, True, surv=False)
+    for k, (x, y) in enumerate(zip(with_lists, without)):
+        assert torch.equal(x, y), f"gradient {k} differs with the survivor lists"
+
+
 def test_deterministic_multichannel():
     """render_channels' 14-channel composite backward: deterministic runs bit-identical, and
     within 1e-6 of the atomic composite."""
@@ -76,18 +89,21 @@ def test_deterministic_multichannel():
     gen = torch.Generator(device="cuda").manual_seed(4)
     weights = [torch.randn(k, 100, 150, device="cuda", generator=gen) for k in ks]
 
-    def run(det):
+    def run(det, surv=True):
         _lib.set_deterministic(det)
+        _lib.set_survivor_lists(surv)
         try:
             _, _, grads, cgrads = _multi(dgr, g, s, cols, bgs, weights)
             torch.cuda.synchronize()
         finally:
             _lib.set_deterministic(False)
+            _lib.set_survivor_lists(True)
         return [t.detach().cpu() for t in grads + cgrads]
 
-    a, d1, d2 = run(False), run(True), run(True)
-    for k, (x, y, z) in enumerate(zip(a, d1, d2)):
+    a, d1, d2, d3 = run(False), run(True), run(True), run(True, surv=False)
+    for k, (x, y, z, w) in enumerate(zip(a, d1, d2, d3)):
         assert torch.equal(y, z), k
+        assert torch.equal(y, w), f"{k}: the survivor lists changed a deterministic gradient"
         if x.abs().max() > 0:
             assert rel_l2(y.numpy(), x.numpy()) <= 1e-6, (k, rel_l2(y.numpy(), x.numpy()))
 
