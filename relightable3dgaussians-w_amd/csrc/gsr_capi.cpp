@@ -66,7 +66,7 @@ struct GeomLayout {
 };
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, surv_n,
-        surv, total;
+        surv, ck_n, ck_pos, ck_state, cfin, units, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -117,11 +117,19 @@ ImgLayout img_layout(int W, int H) {
     L.row_cost = c.take(4 * (size_t)tiles_y(H));  // the same per tile row (the backward's balanced bands)
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    L.nheavy = c.take(4 * 32);  // forward [0..8), backward [8..16), the backward's band bounds [16..25)
+    // forward [0..8), backward [8..16), the backward's band bounds [16..25), its unit counts [32..40)
+    L.nheavy = c.take(4 * 48);
     // the forward's survivor lists for the backward (RenderFwdArgs::surv): 8 B x SURV_CAP per tile,
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
     L.surv_n = c.take(4 * T);
     L.surv = c.take(8 * (size_t)gsr::SURV_CAP * T);
+    // the backward's chunks (GSR_CK_SURV): checkpoints, final colours, the expanded unit order
+    const size_t ck = gsr::CK_SURV ? 1 : 0;
+    L.ck_n = c.take(ck * 4 * T);
+    L.ck_pos = c.take(ck * 4 * gsr::CK_MAX * T);
+    L.ck_state = c.take(ck * 16 * 4 * 64 * gsr::CK_MAX * T);
+    L.cfin = c.take(ck * 16 * 3 * 64 * T);
+    L.units = c.take(ck * 4 * gsr::UNITS_MAX * T);
     L.total = c.o + 256;
     return L;
 }
@@ -716,6 +724,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
         ord.unset = gsr::SURV_CAP ? at<uint32_t>(img, il.surv_n) : nullptr;  // no list unless this forward stores one
+        ord.zero_d = gsr::CK_SURV ? at<uint32_t>(img, il.ck_n) : nullptr;     // nor chunks
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, rect_packed, gsx, st_h(width, height), NS,
@@ -768,6 +777,12 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     if (surv_on() && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
+        if (gsr::CK_SURV) {  // ... in chunks from the forward's checkpoints
+            ra.ck_state = at<float4>(img, il.ck_state);
+            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
+            ra.ck_n = at<uint32_t>(img, il.ck_n);
+            ra.cfin = at<float4>(img, il.cfin);
+        }
     }
     // the forward tile pass over the binning in `bin`; its workgroups also zero the backward's
     // accumulator lines (zero_slice; the depth sort's digit scans did it up to round 3)
@@ -931,6 +946,12 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
+        if (gsr::CK_SURV) {
+            ra.ck_state = at<float4>(img, il.ck_state);
+            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
+            ra.ck_n = at<uint32_t>(img, il.ck_n);
+            ra.cfin = at<float4>(img, il.cfin);
+        }
     }
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {
@@ -1015,11 +1036,23 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
             ra.surv = at<uint2>(img, il.surv);
             ra.surv_n = at<uint32_t>(img, il.surv_n);
         }
+        // the single-channel backward's units: chunks of the survivor lists (every forward sets
+        // ck_n for its list tiles; the composite forward stores no checkpoints)
+        const bool chunks = gsr::CK_SURV && !mc;
+        if (chunks) {
+            ra.ck_state = at<float4>(img, il.ck_state);
+            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
+            ra.ck_n = at<uint32_t>(img, il.ck_n);
+            ra.cfin = at<float4>(img, il.cfin);
+            ra.units = at<uint32_t>(img, il.units);
+        }
         {
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s,  // det: one writer per row
-                                   at<uint32_t>(img, il.row_cost), gy, det ? 0 : GSR_BWD_HEAVY_REL8);
+                                   at<uint32_t>(img, il.row_cost), gy, det ? 0 : GSR_BWD_HEAVY_REL8,
+                                   chunks ? ra.surv_n : nullptr, chunks ? ra.ck_n : nullptr,
+                                   chunks ? at<uint32_t>(img, il.units) : nullptr);
         }
         {
             GSR_STAGE(ST_RENDER_BWD);  // the tile pass alone (roofline.avg_launch_ms in bench.py)

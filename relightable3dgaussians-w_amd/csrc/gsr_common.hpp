@@ -88,6 +88,22 @@ static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9
 #endif
 constexpr uint32_t SURV_CAP = GSR_SURV_CAP;
 constexpr uint32_t SURV_NONE = 0xffffffffu;
+// Backward chunks (GSR_CK_SURV > 0): the forward checkpoints a whole tile's per-pixel state (T and
+// the colour so far) after the batch at which another CK_SURV survivors have been stored, at most
+// CK_MAX times; the backward then runs a tile as one unit per chunk of its survivor list, each
+// starting from its checkpoint (T, and the recurrence from the final colour), in parallel.
+#ifndef GSR_CK_SURV
+#define GSR_CK_SURV 0
+#endif
+#ifndef GSR_CK_MAX
+#define GSR_CK_MAX 3
+#endif
+constexpr uint32_t CK_SURV = GSR_CK_SURV;
+constexpr uint32_t CK_MAX = GSR_CK_MAX;
+// backward units per tile at most: its chunks, or four quadrants of a heavy tile without a list
+constexpr uint32_t UNITS_MAX = (CK_MAX + 1) > 4 ? (CK_MAX + 1) : 4;
+// unit codes (the top 8 bits of an expanded order entry): chunk index, a quadrant, the whole tile
+constexpr uint32_t UNIT_QUAD = 0xF0u, UNIT_WHOLE = 0xFFu;
 
 // Gradient outputs added into (instead of overwritten): the backward kernels' accumulate
 // bits (include/gsr.h GSR_ACC_*), so several views' gradients are summed where they are made.

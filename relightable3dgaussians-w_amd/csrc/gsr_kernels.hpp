@@ -120,12 +120,18 @@ struct TileOrderArgs {
     int heavy_rel8;  // also heavy: cost >= heavy_rel8 / 8 x the band's mean (0: absolute threshold only)
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
     uint32_t* unset;  // optional per-tile words set to SURV_NONE (survivor counts the forward may not write)
+    uint32_t* zero_d;  // optional per-tile words zeroed (chunk counts the composite forward does not write)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
     // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
     // forward's order for its tile pass to raise (zero_rows); nrows = tile rows
     const uint32_t* row_cost;
     uint32_t* zero_rows;
     unsigned nrows;
+    // the backward with survivor lists and chunks: each band's tiles in order expanded into units
+    // (units[band start x UNITS_MAX + i] = tile | code << 24; the count to nheavy[24 + band])
+    const uint32_t* surv_n;
+    const uint32_t* ck_n;
+    uint32_t* units;
 };
 
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
@@ -193,7 +199,8 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
 // row_cost [nrows] (optional): the forward's summed cost per tile row (the balanced bands)
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
                        int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0,
-                       int heavy_rel8 = 0);
+                       int heavy_rel8 = 0, const uint32_t* surv_n = nullptr, const uint32_t* ck_n = nullptr,
+                       uint32_t* units = nullptr);
 
 constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
 constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
@@ -240,6 +247,12 @@ struct RenderFwdArgs {
     // instead of re-filtering the super-tile list
     uint2* surv;
     uint32_t* surv_n;
+    // GSR_CK_SURV: the chunk checkpoints (per tile: CK_MAX x [T, C0, C1, C2] rows of 64 float4, the
+    // boundaries' survivor counts, their number) and the final colours ([C0, C1, C2] rows)
+    float4* ck_state;
+    uint32_t* ck_pos;
+    uint32_t* ck_n;
+    float4* cfin;
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -268,6 +281,14 @@ struct RenderBwdArgs {
     // all tiles when null) filter their super-tile list
     const uint2* surv;
     const uint32_t* surv_n;
+    // the forward's chunk checkpoints (RenderFwdArgs::ck_state ...) and the expanded unit order
+    // (k_tile_order: per band, entries tile | code << 24 from band start x UNITS_MAX; counts at
+    // nheavy[24 + band]); units null: tile_unit's order
+    const float4* ck_state;
+    const uint32_t* ck_pos;
+    const uint32_t* ck_n;
+    const float4* cfin;
+    const uint32_t* units;
 };
 constexpr int DET_ROW3 = 12;  // 8 sums + the ninth's four row partials
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);

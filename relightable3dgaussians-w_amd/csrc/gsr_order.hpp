@@ -114,6 +114,35 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     len = (s_bound[1] == 0xffffffffu ? a.ntile : s_bound[1]) - lo;
 }
 
+// The backward's units of a band in its order: a tile with a survivor list runs as one unit per
+// chunk (codes 0..ck_n), a heavy tile without one (the first nheavy[band] of the order) as four
+// quadrant units, any other as one whole-tile unit.  512-thread workgroups (k_tile_order).
+__device__ __noinline__ void expand_units(unsigned band, unsigned lo, unsigned len, const TileOrderArgs& a) {
+    __shared__ uint32_t s_scan[8];
+    __syncthreads();  // this workgroup's order entries are written
+    const uint32_t nh = a.nheavy[band];
+    uint32_t* const out = a.units + (size_t)lo * UNITS_MAX;
+    uint32_t run = 0;
+    for (unsigned i0 = 0; i0 < len; i0 += blockDim.x) {
+        const unsigned i = i0 + threadIdx.x;
+        uint32_t t = 0, nu = 0;
+        bool lst = false;
+        if (i < len) {
+            t = a.order[lo + i];
+            lst = a.surv_n[t] != SURV_NONE;
+            nu = lst ? 1u + (a.ck_n ? a.ck_n[t] : 0u) : (i < nh ? 4u : 1u);
+        }
+        uint32_t tot;
+        const uint32_t off = run + block_exclusive_scan<8>(nu, s_scan, &tot);
+        for (uint32_t j = 0; j < nu; j++) {
+            const uint32_t code = lst ? j : (nu == 4u ? UNIT_QUAD + j : UNIT_WHOLE);
+            out[off + j] = t | (code << 24);
+        }
+        run += tot;
+    }
+    if (threadIdx.x == 0) a.nheavy[24 + band] = run;
+}
+
 // BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning
 // scatter's order workgroups carry none of its LDS)
 template <bool BAL = false>
@@ -149,6 +178,7 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
             if (a.zero_c) a.zero_c[t] = 0u;
         }
         if (a.unset) a.unset[t] = SURV_NONE;
+        if (a.zero_d) a.zero_d[t] = 0u;
     }
     if (csum) atomicAdd(&s_band_cost, csum);
     __syncthreads();
@@ -192,6 +222,7 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
         a.order[lo + atomicAdd(&cur[cost_bucket(tile_cost(t, a))], 1u)] = t;
 #endif
     }
+    if (a.units) expand_units(band, lo, len, a);
 }
 
 }  // namespace gsr

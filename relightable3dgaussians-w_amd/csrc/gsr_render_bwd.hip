@@ -38,7 +38,8 @@ __device__ unsigned long long g_bwd_times[GSR_UNIT_REC * 65536];
 // BG: the background is not all zero (its dL/dalpha term is carried); with a zero background
 // (render()'s default, the bench) the term and its per-evaluation multiply-add are dropped
 template <bool DET, bool BG = true>
-__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow,
+                                                const uint32_t chunk = 0) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -102,7 +103,33 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
     const bool lst = sn != SURV_NONE;
     uint32_t li = lst ? sn : 0u;  // list entries left
-    const uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    const uint2* sl = a.surv + (size_t)tile * SURV_CAP;
+    if (CK_SURV && lst && a.ck_n) {
+        // chunk `chunk` of the list: survivors [ck_pos[chunk - 1], ck_pos[chunk]) (the last chunk up
+        // to sn), from the forward's checkpoint after its last survivor: T there, and the recurrence
+        // Sr = dL/dpix . (C_final - C_there) / T_there (the colour of everything behind, per unit T)
+        const uint32_t nck = a.ck_n[tile];
+        const uint32_t* cp = a.ck_pos + (size_t)tile * CK_MAX;
+        const uint32_t lo = chunk ? cp[chunk - 1] : 0u, hi = chunk < nck ? cp[chunk] : sn;
+        sl += lo;
+        li = hi - lo;
+        if (chunk < nck) {
+            const float4* ck = a.ck_state + ((size_t)tile * CK_MAX + chunk) * 256 + lane;
+            const float4* cf = a.cfin + (size_t)tile * 192 + lane;
+            const float4 kT = ck[0], k0 = ck[64], k1 = ck[128], k2 = ck[192];
+            const float4 f0 = cf[0], f1 = cf[64], f2 = cf[128];
+            const float tq[4] = {kT.x, kT.y, kT.z, kT.w};
+            const float d0[4] = {f0.x - k0.x, f0.y - k0.y, f0.z - k0.z, f0.w - k0.w};
+            const float d1[4] = {f1.x - k1.x, f1.y - k1.y, f1.z - k1.z, f1.w - k1.w};
+            const float d2[4] = {f2.x - k2.x, f2.y - k2.y, f2.z - k2.z, f2.w - k2.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const bool ok = wt.inside(q, a.W, a.H) && tq[q] > 0.f;
+                T[q] = ok ? tq[q] : 0.f;
+                Sr[q] = ok ? (dp0[q] * d0[q] + dp1[q] * d1[q] + dp2[q] * d2[q]) / tq[q] : 0.f;
+            }
+        }
+    }
     uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);
     TileList<false> tl;
     if (!lst)
@@ -285,15 +312,27 @@ template <bool DET>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
 k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
-    uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
+    uint32_t qallow, chunk = 0;
+    if (CK_SURV && a.units) {  // the expanded order: chunk / quadrant / whole-tile units (expand_units)
+        const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
+        if (u >= a.nheavy[24 + band]) return;
+        unsigned lo = a.nheavy[8 + band], len;
+        if (!GSR_BAL_BANDS) band_of(band, a.grid_x * a.grid_y, lo, len);
+        const uint32_t e = a.units[(size_t)lo * UNITS_MAX + u];
+        tile = e & 0xffffffu;
+        const uint32_t code = e >> 24;
+        qallow = (code & UNIT_QUAD) == UNIT_QUAD && code != UNIT_WHOLE ? 1u << (code & 3u) : 15u;
+        chunk = code < UNIT_QUAD ? code : 0u;
+    } else if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT,
+                          GSR_BAL_BANDS)) {
         return;  // det: one writer per row
+    }
 #if GSR_BWD_BG_SPEC
     // a zero background (wave-uniform scalar loads) takes the walk without its dL/dalpha term
-    if (a.bg[0] == 0.f && a.bg[1] == 0.f && a.bg[2] == 0.f) render_bwd_tile<DET, false>(a, tile, qallow);
-    else render_bwd_tile<DET, true>(a, tile, qallow);
+    if (a.bg[0] == 0.f && a.bg[1] == 0.f && a.bg[2] == 0.f) render_bwd_tile<DET, false>(a, tile, qallow, chunk);
+    else render_bwd_tile<DET, true>(a, tile, qallow, chunk);
 #else
-    render_bwd_tile<DET>(a, tile, qallow);
+    render_bwd_tile<DET>(a, tile, qallow, chunk);
 #endif
 }
 
@@ -321,7 +360,10 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    // (expanded units: up to UNITS_MAX per tile of a band of at most 3 ntile / 8 + 2 tiles)
+    const dim3 grid(CK_SURV && a.units ? 8u * (UNITS_MAX * (3u * ((ntile + 7u) / 8u) + 2u))
+                    : GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT)
+                                    : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }

@@ -76,6 +76,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     // survivors stored so far (whole-tile units; SURV_NONE: none stored, or past SURV_CAP)
     uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
     uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    uint32_t nck = 0, ck_last = 0;  // chunk checkpoints stored, the survivor count at the last one
     uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
         tl.fill(s_list);
@@ -215,6 +216,28 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 scnt += n;
             }
         }
+        if (CK_SURV && a.ck_state && scnt != SURV_NONE && nck < CK_MAX && scnt - ck_last >= CK_SURV) {
+            // the state after this batch: the backward's chunk of the survivors before scnt starts here
+            float4* ck = a.ck_state + ((size_t)tile * CK_MAX + nck) * 256 + lane;
+            ck[0] = make_float4(T[0], T[1], T[2], T[3]);
+            ck[64] = make_float4(C0[0], C0[1], C0[2], C0[3]);
+            ck[128] = make_float4(C1[0], C1[1], C1[2], C1[3]);
+            ck[192] = make_float4(C2[0], C2[1], C2[2], C2[3]);
+            if (lane == 0) a.ck_pos[(size_t)tile * CK_MAX + nck] = scnt;
+            nck++;
+            ck_last = scnt;
+        }
+    }
+    if (CK_SURV && a.ck_state && qallow == 15u) {
+        if (scnt == SURV_NONE) nck = 0;
+        if (nck && ck_last == scnt) nck--;  // no survivors after the last checkpoint
+        if (nck) {  // the final colours (the chunks' recurrence starts from their difference)
+            float4* cf = a.cfin + (size_t)tile * 192 + lane;
+            cf[0] = make_float4(C0[0], C0[1], C0[2], C0[3]);
+            cf[64] = make_float4(C1[0], C1[1], C1[2], C1[3]);
+            cf[128] = make_float4(C2[0], C2[1], C2[2], C2[3]);
+        }
+        if (lane == 0) a.ck_n[tile] = nck;
     }
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {

@@ -25,9 +25,11 @@ void launch_tile_order_args(const TileOrderArgs& a, hipStream_t s) {
 }
 
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows, int heavy_rel8) {
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows, int heavy_rel8,
+                       const uint32_t* surv_n, const uint32_t* ck_n, uint32_t* units) {
     if (ntile == 0) return;
     TileOrderArgs a{};
+    a.surv_n = surv_n; a.ck_n = ck_n; a.units = units;
     a.ntile = ntile; a.ranges = ranges; a.cost = cost; a.order = order; a.nheavy = nheavy; a.heavy_bits = heavy_bits;
     a.heavy_rel8 = heavy_rel8;
     a.row_cost = row_cost; a.nrows = nrows;
