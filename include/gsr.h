@@ -422,6 +422,11 @@ int gsr_get_deterministic(void);
  * the forward. */
 int gsr_set_survivor_lists(int on);
 int gsr_get_survivor_lists(void);
+/* The backward's chunk size in survivors (0: each tile's list is one unit).  With chunks the
+ * backward runs a long list as several units, each starting from a checkpoint the forward stored
+ * (T and the colour so far per pixel); their gradients then differ from the one-unit walk's by
+ * float rounding only. */
+int gsr_backward_chunk_size(void);
 /* 1 when this library was built with -DGSR_DEBUG (`make debug` -> lib/debug/libgsr.so): every
  * forward then verifies its tile lists against the preprocess (ids, culling, rect coverage,
  * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a

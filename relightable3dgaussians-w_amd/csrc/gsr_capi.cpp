@@ -486,6 +486,7 @@ int gsr_set_survivor_lists(int on) {
     return GSR_OK;
 }
 int gsr_get_survivor_lists(void) { return surv_on() ? 1 : 0; }
+int gsr_backward_chunk_size(void) { return (int)gsr::CK_SURV; }
 
 int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
                       void* img_buffer, void* stream_) {
