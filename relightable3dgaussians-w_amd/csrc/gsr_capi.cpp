@@ -947,12 +947,9 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
-        if (gsr::CK_SURV) {
-            ra.ck_state = at<float4>(img, il.ck_state);
-            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
-            ra.ck_n = at<uint32_t>(img, il.ck_n);
-            ra.cfin = at<float4>(img, il.cfin);
-        }
+        // no chunks: the image buffer is the cached call's, shared by calls of other colours, and
+        // a checkpoint holds one call's colours; the chunk counts are cleared
+        if (gsr::CK_SURV) ra.ck_n = at<uint32_t>(img, il.ck_n);
     }
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {

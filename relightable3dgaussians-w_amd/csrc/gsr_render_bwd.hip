@@ -313,20 +313,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
 k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow, chunk = 0;
-    if (CK_SURV && a.units) {  // the expanded order: chunk / quadrant / whole-tile units (expand_units)
-        const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
-        if (u >= a.nheavy[24 + band]) return;
+    if (CK_SURV && a.units) {
+        // the expanded order (expand_units): chunk / quadrant / whole-tile units; the grid is the
+        // tile order's, so a band with more units than the grid's share loops (grid stride)
+        const unsigned band = blockIdx.x & 7u, stride = gridDim.x >> 3;
+        const uint32_t nu = a.nheavy[24 + band];
         unsigned lo = a.nheavy[8 + band], len;
         if (!GSR_BAL_BANDS) band_of(band, a.grid_x * a.grid_y, lo, len);
-        const uint32_t e = a.units[(size_t)lo * UNITS_MAX + u];
-        tile = e & 0xffffffu;
-        const uint32_t code = e >> 24;
-        qallow = (code & UNIT_QUAD) == UNIT_QUAD && code != UNIT_WHOLE ? 1u << (code & 3u) : 15u;
-        chunk = code < UNIT_QUAD ? code : 0u;
-    } else if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT,
-                          GSR_BAL_BANDS)) {
-        return;  // det: one writer per row
+        for (unsigned u = blockIdx.x >> 3; u < nu; u += stride) {
+            const uint32_t e = a.units[(size_t)lo * UNITS_MAX + u];
+            tile = e & 0xffffffu;
+            const uint32_t code = e >> 24;
+            qallow = (code & UNIT_QUAD) == UNIT_QUAD && code != UNIT_WHOLE ? 1u << (code & 3u) : 15u;
+            chunk = code < UNIT_QUAD ? code : 0u;
+            render_bwd_tile<DET>(a, tile, qallow, chunk);
+        }
+        return;
     }
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
+        return;  // det: one writer per row
 #if GSR_BWD_BG_SPEC
     // a zero background (wave-uniform scalar loads) takes the walk without its dL/dalpha term
     if (a.bg[0] == 0.f && a.bg[1] == 0.f && a.bg[2] == 0.f) render_bwd_tile<DET, false>(a, tile, qallow, chunk);
@@ -360,10 +365,7 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    // (expanded units: up to UNITS_MAX per tile of a band of at most 3 ntile / 8 + 2 tiles)
-    const dim3 grid(CK_SURV && a.units ? 8u * (UNITS_MAX * (3u * ((ntile + 7u) / 8u) + 2u))
-                    : GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT)
-                                    : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
     if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }

@@ -228,8 +228,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             ck_last = scnt;
         }
     }
-    if (CK_SURV && a.ck_state && qallow == 15u) {
-        if (scnt == SURV_NONE) nck = 0;
+    if (CK_SURV && a.ck_n && qallow == 15u) {
+        // (no checkpoints without ck_state: a re-coloured forward over a cached call's buffers,
+        // gsr_forward_reuse, whose colours differ from the checkpoints the buffers may hold)
+        if (scnt == SURV_NONE || !a.ck_state) nck = 0;
         if (nck && ck_last == scnt) nck--;  // no survivors after the last checkpoint
         if (nck) {  // the final colours (the chunks' recurrence starts from their difference)
             float4* cf = a.cfin + (size_t)tile * 192 + lane;
