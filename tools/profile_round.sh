@@ -12,18 +12,18 @@ mkdir -p "$R/gpurun_out"
 rm -rf "$R/gpurun_out/prof_${TAG}_kt" "$R/gpurun_out/prof_${TAG}_fetch" "$R/gpurun_out/prof_${TAG}_write" \
   "$R/gpurun_out/prof_${TAG}_valu"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof_${TAG}_kt" \
-  -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --streams 1 $EXTRA > "$R/gpurun_out/prof_${TAG}_kt.log" 2>&1
+  -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --no-clustered --streams 1 $EXTRA > "$R/gpurun_out/prof_${TAG}_kt.log" 2>&1
 rc=$?; echo "kernel-trace rc=$rc"; grep '^{"metric"' "$R/gpurun_out/prof_${TAG}_kt.log"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-  -d "$R/gpurun_out/prof_${TAG}_fetch" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --streams 1 $EXTRA \
+  -d "$R/gpurun_out/prof_${TAG}_fetch" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --no-clustered --streams 1 $EXTRA \
   > "$R/gpurun_out/prof_${TAG}_fetch.log" 2>&1
 rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-  -d "$R/gpurun_out/prof_${TAG}_write" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --streams 1 $EXTRA \
+  -d "$R/gpurun_out/prof_${TAG}_write" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --no-clustered --streams 1 $EXTRA \
   > "$R/gpurun_out/prof_${TAG}_write.log" 2>&1
 rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES --output-format csv \
-  -d "$R/gpurun_out/prof_${TAG}_valu" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --streams 1 $EXTRA \
+  -d "$R/gpurun_out/prof_${TAG}_valu" -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-refalgo --no-relit --no-train --no-minibatch --no-clustered --streams 1 $EXTRA \
   > "$R/gpurun_out/prof_${TAG}_valu.log" 2>&1
 rc=$?; echo "valu rc=$rc"; [ $rc -eq 0 ] || exit $rc
 python3 "$R/tools/profile_summary.py" "$TAG"
