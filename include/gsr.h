@@ -390,6 +390,9 @@ typedef struct gsr_layout {
      * [T] and its per-tile-row sums [tiles_y], the order [T], and the band table (u32 [32]:
      * forward band heavy counts [0..8), backward [8..16), backward band bounds [16..25)) */
     size_t img_tile_cost, img_row_cost, img_order_bwd, img_nheavy;
+    /* the forward's survivor lists (appended in round 5): per tile the count (u32 [T],
+     * 0xFFFFFFFF: none stored) and the list (u32 pairs [T][surv_cap]) */
+    size_t img_surv_n, img_surv, surv_cap;
 } gsr_layout;
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
 

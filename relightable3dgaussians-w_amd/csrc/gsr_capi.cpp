@@ -583,6 +583,9 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     out->img_row_cost = im.row_cost;
     out->img_order_bwd = im.order_bwd;
     out->img_nheavy = im.nheavy;
+    out->img_surv_n = im.surv_n;
+    out->img_surv = im.surv;
+    out->surv_cap = gsr::SURV_CAP;
     return GSR_OK;
 }
 

@@ -24,7 +24,8 @@ class Layout(C.Structure):
     _fields_ = [(n, C.c_size_t) for n in (
         "geom_bytes", "img_bytes", "bin_bytes", "geom_radii", "geom_tiles", "geom_depth_key", "geom_rect",
         "geom_rec", "geom_acc", "img_final_T", "img_n_contrib", "img_ranges", "img_tile_nmax", "img_tile_emax",
-        "bin_st_ranges", "bin_entries", "img_tile_cost", "img_row_cost", "img_order_bwd", "img_nheavy")]
+        "bin_st_ranges", "bin_entries", "img_tile_cost", "img_row_cost", "img_order_bwd", "img_nheavy",
+        "img_surv_n", "img_surv", "surv_cap")]
 
 
 DEBUG_LIB_PATH = os.path.join(PKG_DIR, "lib", "debug", "libgsr.so")
