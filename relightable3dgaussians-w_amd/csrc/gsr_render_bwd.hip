@@ -20,6 +20,10 @@
 #include "gsr_tile.hpp"
 
 
+#ifndef GSR_BWD_QPAIR
+#define GSR_BWD_QPAIR 0
+#endif
+
 namespace gsr {
 
 #ifdef GSR_RENDER_STATS
@@ -194,23 +198,23 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             // S6..8 = sum alpha T dL/dpix
             float M1 = 0.f, M2 = 0.f, S2 = 0.f, S3 = 0.f, S4 = 0.f, S5 = 0.f, S6 = 0.f, S7 = 0.f, S8 = 0.f;
             bool any = false;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (!((m >> q) & 1u)) continue;
+            // one reachable quadrant: the exponent and the blend decision (pre), then the
+            // recurrence and this Gaussian's sums (post); inactive lanes run post with alpha =
+            // G = 0, leaving T, the sums and the gradients unchanged
+            auto pre = [&](int q, float& dx, float& dy, float& G, float& alpha, lmask& act) __attribute__((always_inline)) {
                 BWD_STAT(2, 1);
-                const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
+                dx = ax - pxq[q & 1];
+                dy = ay - pyq[q >> 1];
                 const float power = gauss_power(ka, kb, kc, dx, dy);
-                const float G = tile_exp2(power);
-                const float alpha = fminf(0.99f, op * G);
+                G = tile_exp2(power);
+                alpha = fminf(0.99f, op * G);
                 // active: pos < last && !(power > 0) && !(alpha < 1/255)
                 // (compare results are 0 on inactive lanes, and every lane is on: no exec masking)
-                const lmask act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
-                if (act == 0ull) continue;  // wave-uniform
+                act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
+            };
+            auto post = [&](int q, float dx, float dy, float G, float alpha, lmask act) __attribute__((always_inline)) {
                 BWD_STAT(3, 1);
                 BWD_STAT(4, __popcll(act));
-                any = true;
-                // inactive lanes run the same code with alpha = G = 0: T, the sums and
-                // the gradients stay unchanged
                 const float ae = sel(act, alpha, 0.f);
                 const float Ge = sel(act, G, 0.f);
                 const float inv = __builtin_amdgcn_rcpf(1.f - ae);
@@ -232,7 +236,46 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 S7 = __builtin_fmaf(dch, dp1[q], S7);
                 S8 = __builtin_fmaf(dch, dp2[q], S8);
                 T[q] = Tn;
+            };
+#if GSR_BWD_QPAIR
+            // GSR_BWD_QPAIR: both quadrants of a row reached -> one straight-line block, so the
+            // two independent chains (exponent, blend test, recurrence) interleave; the sums are
+            // still added quadrant by quadrant, in order
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int q0 = 2 * h, q1 = 2 * h + 1;
+                const uint32_t pm = (m >> q0) & 3u;
+                if (pm == 3u) {
+                    float dx0, dy0, G0, a0, dx1, dy1, G1, a1;
+                    lmask k0, k1;
+                    pre(q0, dx0, dy0, G0, a0, k0);
+                    pre(q1, dx1, dy1, G1, a1, k1);
+                    if ((k0 | k1) == 0ull) continue;
+                    any = true;
+                    post(q0, dx0, dy0, G0, a0, k0);
+                    post(q1, dx1, dy1, G1, a1, k1);
+                } else if (pm) {
+                    const int q = pm == 1u ? q0 : q1;
+                    float dx, dy, G, al;
+                    lmask k;
+                    pre(q, dx, dy, G, al, k);
+                    if (k == 0ull) continue;
+                    any = true;
+                    post(q, dx, dy, G, al, k);
+                }
             }
+#else
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!((m >> q) & 1u)) continue;
+                float dx, dy, G, al;
+                lmask k;
+                pre(q, dx, dy, G, al, k);
+                if (k == 0ull) continue;  // wave-uniform
+                any = true;
+                post(q, dx, dy, G, al, k);
+            }
+#endif
             if (any) {
             BWD_STAT(5, 1);
             // raw sums (the line's layout, acc_raw): M1, M2 -- dL/dmean2D is -(a M1 + b M2),
