@@ -22,6 +22,11 @@
 #ifndef GSR_SURV_BLENDED
 #define GSR_SURV_BLENDED 0
 #endif
+// 1: the forward finds its latest blend per batch from last[] (a wave max) instead of tracking
+// which survivors blended
+#ifndef GSR_FWD_LASTMAX
+#define GSR_FWD_LASTMAX 0
+#endif
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
@@ -159,7 +164,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 C2[q] += Cq.x * w;
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
-                blended |= blend;
+                if (!GSR_FWD_LASTMAX || GSR_SURV_BLENDED) blended |= blend;
                 if (GSR_SURV_BLENDED == 2 && blend) qb |= 1u << q;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
@@ -169,7 +174,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                     }
                 }
             }
-            if (blended) {
+            if ((!GSR_FWD_LASTMAX || GSR_SURV_BLENDED) && blended) {
                 klast = k;
                 if (GSR_SURV_BLENDED) bmask |= 1ull << k;
                 if (GSR_SURV_BLENDED == 2) {
@@ -201,7 +206,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             blend_one(An, Bn, Cn, kn);
             if (k < 0) break;
         }
-        if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
+        if (GSR_FWD_LASTMAX) {
+            // the latest blend so far (the tile's largest n_contrib): if it lies in this batch, its
+            // entry is the backward's start (a wave max per batch instead of a mask OR per
+            // evaluation and a test per survivor: SALU issue is as scarce as VALU here)
+            const uint32_t mx = wave_max_u32(max(max(last[0], last[1]), max(last[2], last[3])));
+            if (mx > p0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[mx - 1u - p0]);
+        } else if (klast >= 0) {
+            elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
+        }
         if (GSR_SURV_BLENDED && scnt != SURV_NONE) {  // only the survivors that blended somewhere
             const uint32_t n = (uint32_t)__popcll(bmask);
             if (scnt + n > SURV_CAP) {
