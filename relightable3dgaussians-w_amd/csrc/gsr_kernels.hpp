@@ -202,8 +202,14 @@ void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost
                        int heavy_rel8 = 0, const uint32_t* surv_n = nullptr, const uint32_t* ck_n = nullptr,
                        uint32_t* units = nullptr);
 
-constexpr int FWD_HEAVY_BITS = 14;  // super-tile entries >= 16384 (its tiles' lists ~8k)
-constexpr int BWD_HEAVY_BITS = 13;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
+#ifndef GSR_FWD_HEAVY_BITS
+#define GSR_FWD_HEAVY_BITS 14
+#endif
+#ifndef GSR_BWD_HEAVY_BITS
+#define GSR_BWD_HEAVY_BITS 13
+#endif
+constexpr int FWD_HEAVY_BITS = GSR_FWD_HEAVY_BITS;  // super-tile entries >= 16384 (its tiles' lists ~8k)
+constexpr int BWD_HEAVY_BITS = GSR_BWD_HEAVY_BITS;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
 // ... or a cost >= REL8 / 8 x the band's mean tile cost (gsr_order.hpp; 0 = off).  Off: on the
 // clustered cfg2c frame splitting the tiles above 2x / 3x the band mean (64-256 per band) made
 // both tile passes slower (render_bwd 494 -> 535 / 592 us at 2x with 64 / 128 per band, 497 at
