@@ -66,7 +66,7 @@ struct GeomLayout {
 };
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, surv_n,
-        surv, surv_q, ck_n, ck_pos, ck_state, cfin, units, total;
+        surv, ck_n, ck_pos, ck_state, cfin, units, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -123,7 +123,6 @@ ImgLayout img_layout(int W, int H) {
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
     L.surv_n = c.take(4 * T);
     L.surv = c.take(8 * (size_t)gsr::SURV_CAP * T);
-    L.surv_q = c.take(GSR_SURV_QUAD ? 16 * T : 0);  // quadrant list counts of split tiles
     // the backward's chunks (GSR_CK_SURV): checkpoints, final colours, the expanded unit order
     const size_t ck = gsr::CK_SURV ? 1 : 0;
     L.ck_n = c.take(ck * 4 * T);
@@ -729,7 +728,6 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
         ord.unset = gsr::SURV_CAP ? at<uint32_t>(img, il.surv_n) : nullptr;  // no list unless this forward stores one
-        ord.unset_q = (gsr::SURV_CAP && GSR_SURV_QUAD) ? at<uint32_t>(img, il.surv_q) : nullptr;
         ord.zero_d = gsr::CK_SURV ? at<uint32_t>(img, il.ck_n) : nullptr;     // nor chunks
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
@@ -783,7 +781,6 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     if (surv_on() && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
-        if (GSR_SURV_QUAD) ra.surv_q = at<uint32_t>(img, il.surv_q);
         if (gsr::CK_SURV) {  // ... in chunks from the forward's checkpoints
             ra.ck_state = at<float4>(img, il.ck_state);
             ra.ck_pos = at<uint32_t>(img, il.ck_pos);
@@ -953,7 +950,6 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
-        if (GSR_SURV_QUAD) ra.surv_q = at<uint32_t>(img, il.surv_q);
         // no chunks: the image buffer is the cached call's, shared by calls of other colours, and
         // a checkpoint holds one call's colours; the chunk counts are cleared
         if (gsr::CK_SURV) ra.ck_n = at<uint32_t>(img, il.ck_n);
@@ -1040,7 +1036,6 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         if (gsr::SURV_CAP) {
             ra.surv = at<uint2>(img, il.surv);
             ra.surv_n = at<uint32_t>(img, il.surv_n);
-            if (GSR_SURV_QUAD) ra.surv_q = at<uint32_t>(img, il.surv_q);
         }
         // the single-channel backward's units: chunks of the survivor lists (every forward sets
         // ck_n for its list tiles; the composite forward stores no checkpoints)

@@ -87,11 +87,6 @@ static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9
 #define GSR_SURV_CAP 1024
 #endif
 constexpr uint32_t SURV_CAP = GSR_SURV_CAP;
-// 1: the forward's quadrant units (tiles it splits) store per-quadrant lists too, and the
-// backward walks a split tile's four lists one quadrant after the other
-#ifndef GSR_SURV_QUAD
-#define GSR_SURV_QUAD 0
-#endif
 constexpr uint32_t SURV_NONE = 0xffffffffu;
 // Backward chunks (GSR_CK_SURV > 0): the forward checkpoints a whole tile's per-pixel state (T and
 // the colour so far) after the batch at which another CK_SURV survivors have been stored, at most

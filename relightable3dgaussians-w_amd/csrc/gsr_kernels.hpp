@@ -120,7 +120,6 @@ struct TileOrderArgs {
     int heavy_rel8;  // also heavy: cost >= heavy_rel8 / 8 x the band's mean (0: absolute threshold only)
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
     uint32_t* unset;  // optional per-tile words set to SURV_NONE (survivor counts the forward may not write)
-    uint32_t* unset_q;  // the same, four per tile (GSR_SURV_QUAD's quadrant list counts)
     uint32_t* zero_d;  // optional per-tile words zeroed (chunk counts the composite forward does not write)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
     // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
@@ -254,7 +253,6 @@ struct RenderFwdArgs {
     // instead of re-filtering the super-tile list
     uint2* surv;
     uint32_t* surv_n;
-    uint32_t* surv_q;  // GSR_SURV_QUAD: per tile and quadrant, a split tile's quadrant list counts
     // GSR_CK_SURV: the chunk checkpoints (per tile: CK_MAX x [T, C0, C1, C2] rows of 64 float4, the
     // boundaries' survivor counts, their number) and the final colours ([C0, C1, C2] rows)
     float4* ck_state;
@@ -289,7 +287,6 @@ struct RenderBwdArgs {
     // all tiles when null) filter their super-tile list
     const uint2* surv;
     const uint32_t* surv_n;
-    const uint32_t* surv_q;  // GSR_SURV_QUAD: the quadrant lists' counts (SURV_NONE: none)
     // the forward's chunk checkpoints (RenderFwdArgs::ck_state ...) and the expanded unit order
     // (k_tile_order: per band, entries tile | code << 24 from band start x UNITS_MAX; counts at
     // nheavy[24 + band]); units null: tile_unit's order

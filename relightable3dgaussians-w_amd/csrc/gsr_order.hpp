@@ -178,8 +178,6 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
             if (a.zero_c) a.zero_c[t] = 0u;
         }
         if (a.unset) a.unset[t] = SURV_NONE;
-        if constexpr (GSR_SURV_QUAD != 0)
-            if (a.unset_q) reinterpret_cast<uint4*>(a.unset_q)[t] = make_uint4(SURV_NONE, SURV_NONE, SURV_NONE, SURV_NONE);
         if constexpr (CK_SURV != 0)
             if (a.zero_d) a.zero_d[t] = 0u;
     }

@@ -105,52 +105,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     // call and a slower 3-stream headline: 113 VGPRs); else the super-tile list, filtered and
     // culled again
     const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
-#if GSR_SURV_QUAD
-    bool lst = sn != SURV_NONE;
-    uint32_t li = lst ? sn : 0u;  // list entries left (of the current segment)
-    const uint2* const sbase = a.surv + (size_t)tile * SURV_CAP;
-    const uint2* sl = sbase;
-    // GSR_SURV_QUAD: a tile the forward split has one list per quadrant; walked one quadrant after
-    // the other (segments), each entry restricted to the segment's quadrant (smask).  Not in
-    // deterministic mode: a Gaussian's rows would then be written once per quadrant.
-    uint32_t smask = 15u, qsegs = 0u;
-    uint4 cq = make_uint4(0u, 0u, 0u, 0u);
-    if (!DET && !lst && a.surv_q) {
-        const uint4 c4 = reinterpret_cast<const uint4*>(a.surv_q)[tile];
-        cq = make_uint4((uint32_t)__builtin_amdgcn_readfirstlane((int)c4.x), (uint32_t)__builtin_amdgcn_readfirstlane((int)c4.y),
-                        (uint32_t)__builtin_amdgcn_readfirstlane((int)c4.z), (uint32_t)__builtin_amdgcn_readfirstlane((int)c4.w));
-        uint32_t need = 0;
-        bool ok = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t c = q == 0 ? cq.x : q == 1 ? cq.y : q == 2 ? cq.z : cq.w;
-            if (qlim[q]) {
-                need |= 1u << q;
-                ok = ok && c != SURV_NONE;
-            }
-        }
-        if (ok) {
-            lst = true;
-            qsegs = need;  // li = 0: next_segment below takes the first non-empty one
-        }
-    }
-    // the next non-empty quadrant list, when the current segment is done
-    auto next_segment = [&]() __attribute__((always_inline)) {
-        while (li == 0 && qsegs) {
-            const uint32_t q = (uint32_t)__builtin_ctz(qsegs);
-            qsegs &= qsegs - 1u;
-            sl = sbase + q * (SURV_CAP / 4u);
-            li = q == 0 ? cq.x : q == 1 ? cq.y : q == 2 ? cq.z : cq.w;
-            smask = 1u << q;
-        }
-    };
-    next_segment();
-#else
     const bool lst = sn != SURV_NONE;
     uint32_t li = lst ? sn : 0u;  // list entries left
     const uint2* sl = a.surv + (size_t)tile * SURV_CAP;
-    constexpr uint32_t smask = 15u;
-#endif
     if (CK_SURV && lst && a.ck_n) {
         // chunk `chunk` of the list: survivors [ck_pos[chunk - 1], ck_pos[chunk]) (the last chunk up
         // to sn), from the forward's checkpoint after its last survivor: T there, and the recurrence
@@ -189,18 +146,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             if (nb == 0) break;
             const uint2 v = nv;
             li -= nb;
-            if (!GSR_SURV_QUAD) nv = sl[max((int)li - 1 - lane, 0)];
+            nv = sl[max((int)li - 1 - lane, 0)];
             id = v.x;
             p = v.y >> 4;
             if ((uint32_t)lane < nb) {
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    if (p < qlim[q]) qm |= v.y & smask & (1u << q);
+                    if (p < qlim[q]) qm |= v.y & (1u << q);
             }
-#if GSR_SURV_QUAD
-            next_segment();  // the next segment's prefetch once this one is done
-            nv = sl[max((int)li - 1 - lane, 0)];
-#endif
         } else {
             tl.fill(s_list);
             uint32_t ei = 0, p0 = 0;

@@ -79,19 +79,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
     // survivors stored so far (whole-tile units; SURV_NONE: none stored, or past SURV_CAP)
-    // a whole-tile unit stores the tile's list (up to SURV_CAP entries); a quadrant unit (a split
-    // tile) stores its quadrant's in a quarter of the tile's region (up to SURV_CAP / 4)
-    const bool whole = qallow == 15u;
-#if GSR_SURV_QUAD
-    const uint32_t qi = whole ? 0u : (uint32_t)__builtin_ctz(qallow);
-    const uint32_t scap = whole ? SURV_CAP : SURV_CAP / 4u;
-    uint32_t scnt = a.surv ? 0u : SURV_NONE;
-    uint2* const sl = a.surv + (size_t)tile * SURV_CAP + qi * (SURV_CAP / 4u);
-#else
-    constexpr uint32_t scap = SURV_CAP;
-    uint32_t scnt = (a.surv && whole) ? 0u : SURV_NONE;
+    uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
     uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
-#endif
     uint32_t nck = 0, ck_last = 0;  // chunk checkpoints stored, the survivor count at the last one
     uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
@@ -123,7 +112,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         const uint64_t todo0 = __ballot((qm & live) != 0);
         if (!GSR_SURV_BLENDED && scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
             const uint32_t n = (uint32_t)__popcll(todo0);
-            if (scnt + n > scap) {
+            if (scnt + n > SURV_CAP) {
                 scnt = SURV_NONE;
             } else {
                 if ((qm & live) != 0) {
@@ -228,7 +217,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         }
         if (GSR_SURV_BLENDED && scnt != SURV_NONE) {  // only the survivors that blended somewhere
             const uint32_t n = (uint32_t)__popcll(bmask);
-            if (scnt + n > scap) {
+            if (scnt + n > SURV_CAP) {
                 scnt = SURV_NONE;
             } else {
                 if ((bmask >> lane) & 1u) {
@@ -240,7 +229,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 scnt += n;
             }
         }
-        if (CK_SURV && a.ck_state && whole && scnt != SURV_NONE && nck < CK_MAX && scnt - ck_last >= CK_SURV) {
+        if (CK_SURV && a.ck_state && scnt != SURV_NONE && nck < CK_MAX && scnt - ck_last >= CK_SURV) {
             // the state after this batch: the backward's chunk of the survivors before scnt starts here
             float4* ck = a.ck_state + ((size_t)tile * CK_MAX + nck) * 256 + lane;
             ck[0] = make_float4(T[0], T[1], T[2], T[3]);
@@ -293,12 +282,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
         }
     }
-    if (lane == 0 && a.surv) {
-        if (whole) a.surv_n[tile] = scnt;
-#if GSR_SURV_QUAD
-        else a.surv_q[4u * tile + qi] = scnt;
-#endif
-    }
+    if (lane == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
     uint32_t nm = 0, nsum = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
