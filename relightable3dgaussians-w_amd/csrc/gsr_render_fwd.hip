@@ -27,6 +27,11 @@
 #ifndef GSR_FWD_LASTMAX
 #define GSR_FWD_LASTMAX 0
 #endif
+// 1 (default): a quadrant unit culls its batch against its own quadrant only (its survivors are
+// never stored): k_render_fwd 238.1 -> 236.9 us, headline / cfg2c / train +0.5-1 % (profiles/r5z_reach_own_ab.txt)
+#ifndef GSR_FWD_REACH_OWN
+#define GSR_FWD_REACH_OWN 1
+#endif
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 6
 #endif
@@ -94,7 +99,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         float rc = 0.f;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, j, nullptr);
+            qm = wt.reach(r, j, nullptr, GSR_FWD_REACH_OWN ? qallow : 15u);  // (a quadrant unit tests its own only)
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);

@@ -23,6 +23,10 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
+#ifndef GSR_FWD_REACH_OWN
+#define GSR_FWD_REACH_OWN 1
+#endif
+
 namespace gsr {
 
 // NCH: channels composited (<= 4 NC4; render()'s layout has 14, so its group skips the two
@@ -73,7 +77,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         for (int g = 0; g < NC4; g++) f[g] = ra;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, j, nullptr);
+            qm = wt.reach(r, j, nullptr, GSR_FWD_REACH_OWN ? qallow : 15u);
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll

@@ -396,10 +396,13 @@ struct WaveTile {
 
     // Quadrants (bit q) the record can reach with alpha >= 1/255 (conservative, see
     // box_reachable); `limit[q]`: only positions < limit[q] are kept for quadrant q.
-    __device__ __forceinline__ uint32_t reach(const Rec& r, uint32_t position, const uint32_t* limit) const {
+    // `qmask` (wave-uniform): the quadrants worth testing (a quadrant unit's own)
+    __device__ __forceinline__ uint32_t reach(const Rec& r, uint32_t position, const uint32_t* limit,
+                                              uint32_t qmask = 15u) const {
         uint32_t m = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
+            if (!((qmask >> q) & 1u)) continue;
             const float qx0 = tx0 + (q & 1) * 8.f, qy0 = ty0 + (q >> 1) * 8.f;
             const float qx1 = fminf(qx0 + 7.f, wmax), qy1 = fminf(qy0 + 7.f, hmax);
             if (qx0 <= wmax && qy0 <= hmax && (!limit || position < limit[q]) &&
