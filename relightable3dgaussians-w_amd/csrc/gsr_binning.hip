@@ -384,6 +384,7 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     if ((int)blockIdx.x >= nb) {
         const int x = (int)blockIdx.x - nb - (ft.host ? 1 : 0);
         if (x < 0) frame_totals(ft);  // the extra workgroup: the host's frame totals
+        else if (GSR_FWD_BAL) tile_order_band<true>((unsigned)x, ord);  // (equal bands below 512 threads)
         else tile_order_band((unsigned)x, ord);
         return;
     }

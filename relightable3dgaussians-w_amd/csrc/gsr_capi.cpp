@@ -103,6 +103,8 @@ GeomLayout geom_layout(long long P) {
 unsigned tiles_x(int W) { return (unsigned)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X); }
 unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y); }
 
+constexpr int FWD_NHEAVY = 40;  // the forward's band table within the image buffer's nheavy words
+
 ImgLayout img_layout(int W, int H) {
     Carver c;
     ImgLayout L;
@@ -117,8 +119,9 @@ ImgLayout img_layout(int W, int H) {
     L.row_cost = c.take(4 * (size_t)tiles_y(H));  // the same per tile row (the backward's balanced bands)
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    // forward [0..8), backward [8..16), the backward's band bounds [16..25), its unit counts [32..40)
-    L.nheavy = c.take(4 * 48);
+    // backward band counts [8..16), bounds [16..25), unit counts [32..40); forward band counts
+    // [40..48), bounds [48..57) (the forward's table starts at 40: FWD_NHEAVY)
+    L.nheavy = c.take(4 * 64);
     // the forward's survivor lists for the backward (RenderFwdArgs::surv): 8 B x SURV_CAP per tile,
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
     L.surv_n = c.take(4 * T);
@@ -722,7 +725,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         // the tile maxima and summed cost the tile pass raises
         gsr::TileOrderArgs ord{};
         ord.ntile = (unsigned)T; ord.gx = gx; ord.gsx = gsx; ord.order = at<uint32_t>(img, il.order_fwd);
-        ord.nheavy = at<uint32_t>(img, il.nheavy); ord.heavy_bits = gsr::FWD_HEAVY_BITS;
+        ord.nheavy = at<uint32_t>(img, il.nheavy) + FWD_NHEAVY; ord.heavy_bits = gsr::FWD_HEAVY_BITS;
+        ord.balance = GSR_FWD_BAL;  // (the large-frame path's own order launch)
         ord.heavy_rel8 = GSR_FWD_HEAVY_REL8;
         ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
@@ -773,7 +777,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.gsx = gsx; ra.rec = pa.rec; ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
-    ra.nheavy = at<uint32_t>(img, il.nheavy);
+    ra.nheavy = at<uint32_t>(img, il.nheavy) + FWD_NHEAVY;
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
@@ -943,7 +947,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.rec = at<gsr::Rec>(geom, gl.rec); ra.bg = background;
     ra.out_color = out_color; ra.final_T = at<float>(img, il.final_T); ra.n_contrib = at<uint32_t>(img, il.n_contrib);
     ra.order = at<uint32_t>(img, il.order_fwd);
-    ra.nheavy = at<uint32_t>(img, il.nheavy);
+    ra.nheavy = at<uint32_t>(img, il.nheavy) + FWD_NHEAVY;
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = nullptr;  // already summed by the cached call's forward

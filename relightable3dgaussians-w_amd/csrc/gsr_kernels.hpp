@@ -202,6 +202,11 @@ void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost
                        int heavy_rel8 = 0, const uint32_t* surv_n = nullptr, const uint32_t* ck_n = nullptr,
                        uint32_t* units = nullptr);
 
+// The forward passes' bands: 1 -- cost-balanced by the super-tile entry counts (summed per row;
+// bounds stored after the forward's band counts as the backward's are), 0 -- equal tile counts
+#ifndef GSR_FWD_BAL
+#define GSR_FWD_BAL 0
+#endif
 #ifndef GSR_FWD_HEAVY_BITS
 #define GSR_FWD_HEAVY_BITS 14
 #endif

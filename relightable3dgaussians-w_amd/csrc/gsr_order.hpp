@@ -57,12 +57,24 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     __shared__ unsigned long long s_rowp[2];  // cost' before the boundary rows
     __shared__ unsigned s_row[2], s_bound[2];
     const unsigned n = a.nrows, gx = n ? a.ntile / n : 0u;
-    if (!a.row_cost || n == 0 || n > blockDim.x || gx > blockDim.x || gx * n != a.ntile) {
+    // the forward's order has no row sums: a row's cost is summed from its super-tiles' entry
+    // counts (its tiles' costs), a handful of loads per row
+    const bool strow = !a.row_cost && !a.cost && (a.st_ranges || a.st_tot);
+    if ((!a.row_cost && !strow) || n == 0 || n > blockDim.x || gx > blockDim.x || gx * n != a.ntile ||
+        blockDim.x != 512) {
         band_of(band, a.ntile, lo, len);
         return;
     }
     const unsigned r = threadIdx.x;
-    const unsigned long long c = r < n ? a.row_cost[r] : 0ull;
+    unsigned long long c = 0ull;
+    if (r < n) {
+        if (strow) {
+            for (unsigned x0 = 0; x0 < gx; x0 += GSR_ST_W)  // one super-tile's tiles of this row at a time
+                c += (unsigned long long)tile_cost(r * gx + x0, a) * (gx - x0 < GSR_ST_W ? gx - x0 : GSR_ST_W);
+        } else {
+            c = a.row_cost[r];
+        }
+    }
     if (threadIdx.x < 2) {
         s_row[threadIdx.x] = 0xffffffffu;
         s_bound[threadIdx.x] = threadIdx.x == 0 ? (band > 0 ? 0xffffffffu : 0u) : (band < 7 ? 0xffffffffu : a.ntile);
@@ -99,8 +111,7 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     for (int k = 0; k < 2; k++) {
         if (!need[k]) continue;  // workgroup-uniform
         const unsigned row = s_row[k];
-        const unsigned long long ct =
-            (row < n && threadIdx.x < gx) ? a.cost[(size_t)row * gx + threadIdx.x] + add : 0ull;
+        const unsigned long long ct = (row < n && threadIdx.x < gx) ? tile_cost(row * gx + threadIdx.x, a) + add : 0ull;
         unsigned long long rt;
         const unsigned long long bt = block_exclusive_scan<8>(ct, s_scan, &rt);
         if (row < n && threadIdx.x < gx) {

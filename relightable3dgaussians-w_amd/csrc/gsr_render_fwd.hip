@@ -311,7 +311,7 @@ k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL)) return;
     render_fwd_tile(a, tile, qallow);
 }
 
@@ -339,7 +339,8 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    hipLaunchKernelGGL(k_render_fwd, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(GSR_FWD_BAL ? tile_pass_blocks_bal(ntile, FWD_TAIL_SPLIT) : tile_pass_blocks(ntile, FWD_TAIL_SPLIT)),
+                       dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

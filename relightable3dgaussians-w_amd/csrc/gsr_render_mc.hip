@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcAr
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
@@ -543,7 +543,7 @@ __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcAr
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
+    const dim3 grid(GSR_FWD_BAL ? tile_pass_blocks_bal(ntile, FWD_TAIL_SPLIT) : tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
     switch ((a.nch + 3) / 4) {
         case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;

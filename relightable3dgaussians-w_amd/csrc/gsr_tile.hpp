@@ -39,11 +39,14 @@ constexpr unsigned HEAVY_CAP = GSR_HEAVY_CAP;  // split heavy tiles per band
 #ifndef GSR_BWD_TAIL
 #define GSR_BWD_TAIL 0
 #endif
-// The backward's per-tile cost estimate (its dispatch order, heaviest first), written by the
-// forward: 1 -- the forward's (survivor, quadrant) evaluations, 0 -- the sum of the quadrants'
-// largest n_contrib
+// The backward's per-tile cost estimate (its dispatch order, heaviest first, and its balanced
+// bands), written by the forward: 1 (default) -- the forward's (survivor, quadrant) evaluations,
+// 0 -- the sum of the quadrants' largest n_contrib.  Measured in round 5 (profiles/
+// r5z_eval_cost_ab.txt): cfg2c render_bwd 0.465 -> 0.429 ms (its bands balance by the work the
+// backward repeats, not by list positions; no tile reaches the quadrant split's 8192 any more),
+// cfg2 and training unchanged
 #ifndef GSR_EVAL_COST
-#define GSR_EVAL_COST 0
+#define GSR_EVAL_COST 1
 #endif
 constexpr unsigned FWD_TAIL_SPLIT = GSR_FWD_TAIL;  // split tail tiles per band, forward passes
 constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
