@@ -119,9 +119,10 @@ ImgLayout img_layout(int W, int H) {
     L.row_cost = c.take(4 * (size_t)tiles_y(H));  // the same per tile row (the backward's balanced bands)
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    // backward band counts [8..16), bounds [16..25), unit counts [32..40); forward band counts
-    // [40..48), bounds [48..57) (the forward's table starts at 40: FWD_NHEAVY)
-    L.nheavy = c.take(4 * 64);
+    // two band tables, the backward's at 8 and the forward's at 40 (FWD_NHEAVY), each (relative
+    // to its start): heavy counts [0..8), balanced bounds [8..17), unit counts (backward chunks)
+    // or band costs (the forward's rotated bands) [24..32)
+    L.nheavy = c.take(4 * 80);
     // the forward's survivor lists for the backward (RenderFwdArgs::surv): 8 B x SURV_CAP per tile,
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
     L.surv_n = c.take(4 * T);

@@ -224,6 +224,9 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
             hb = hr > 0 && hr < hb ? hr : hb;
         }
         a.nheavy[band] = hb < NBUCKET ? cur[hb] + hist[hb] : 0u;
+        // the band's estimated cost (the forward's rotated bands: tile_unit); the slot holds
+        // the unit count instead when the order expands units
+        if (!a.units) a.nheavy[24 + band] = (uint32_t)min(s_band_cost, 0xffffffffull);
     }
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {

@@ -311,7 +311,7 @@ k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true)) return;
     render_fwd_tile(a, tile, qallow);
 }
 

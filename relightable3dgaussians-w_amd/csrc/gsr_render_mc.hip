@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcAr
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 

@@ -52,9 +52,29 @@ constexpr unsigned FWD_TAIL_SPLIT = GSR_FWD_TAIL;  // split tail tiles per band,
 constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 // bal: the bands are the cost-balanced ranges k_tile_order stored after the band counts
 // (nheavy[8 + b] = band b's first tile, nheavy[16] = ntile; GSR_BAL_BANDS); else equal bands.
+// rot: rotated bands -- block b takes unit b / 8 of band (b + b / 8) mod 8 instead of band b mod
+// 8, so each XCD (b mod 8) works through every band's order in turn -- when the bands' estimated
+// costs (nheavy[24 + b], written by the order) are uneven: the largest above GSR_ROT_THR8 / 8 x
+// their mean (0: never).  A skewed frame then no longer waits for one XCD's band; an even one
+// keeps each band's L2 locality (rotating unconditionally measured cfg2c +1.5 %, cfg2 -0.9 %)
+#ifndef GSR_ROT_THR8
+#define GSR_ROT_THR8 10u
+#endif
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
-                                          unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false) {
-    const unsigned band = blockIdx.x & 7u, u = blockIdx.x >> 3;
+                                          unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
+                                          bool rot = false) {
+    unsigned u = blockIdx.x >> 3, band = blockIdx.x & 7u;
+    if (rot && GSR_ROT_THR8 != 0u) {
+        uint32_t mx = 0u;
+        unsigned long long sum = 0ull;
+#pragma unroll
+        for (int b = 0; b < 8; b++) {
+            const uint32_t c = nheavy[24 + b];
+            mx = max(mx, c);
+            sum += c;
+        }
+        if (64ull * mx > (unsigned long long)GSR_ROT_THR8 * sum) band = (band + u) & 7u;
+    }
     unsigned lo, len;
     if (bal) {
         lo = nheavy[8 + band];
