@@ -60,6 +60,12 @@ constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 #ifndef GSR_ROT_THR8
 #define GSR_ROT_THR8 10u
 #endif
+// the rotation steps every 2^GSR_ROT_SHIFT units: an XCD walks runs of 32 units of one band's
+// order, so its L2 still serves neighbouring tiles (cfg2c render_fwd 0.385 -> 0.370 ms against a
+// step per unit, whose forward fetched 3.4x the bytes of unrotated bands: r5z_band_rotate_ab.txt)
+#ifndef GSR_ROT_SHIFT
+#define GSR_ROT_SHIFT 5
+#endif
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
                                           unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
                                           bool rot = false) {
@@ -73,7 +79,7 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
             mx = max(mx, c);
             sum += c;
         }
-        if (64ull * mx > (unsigned long long)GSR_ROT_THR8 * sum) band = (band + u) & 7u;
+        if (64ull * mx > (unsigned long long)GSR_ROT_THR8 * sum) band = (band + (u >> GSR_ROT_SHIFT)) & 7u;
     }
     unsigned lo, len;
     if (bal) {
