@@ -66,7 +66,7 @@ struct GeomLayout {
 };
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, surv_n,
-        surv, ck_n, ck_pos, ck_state, cfin, units, total;
+        surv, qsurv_n, qsurv, ck_n, ck_pos, ck_state, cfin, units, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -127,6 +127,10 @@ ImgLayout img_layout(int W, int H) {
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
     L.surv_n = c.take(4 * T);
     L.surv = c.take(8 * (size_t)gsr::SURV_CAP * T);
+    // the forward's quadrant lists (GSR_QLIST): SURV_CAP entries per (quadrant-unit slot, quadrant)
+    const size_t nql = GSR_QLIST && gsr::SURV_CAP ? 4 * (size_t)gsr::QL_SLOTS : 0;
+    L.qsurv_n = c.take(4 * nql);
+    L.qsurv = c.take(8 * (size_t)gsr::SURV_CAP * nql);
     // the backward's chunks (GSR_CK_SURV): checkpoints, final colours, the expanded unit order
     const size_t ck = gsr::CK_SURV ? 1 : 0;
     L.ck_n = c.take(ck * 4 * T);
@@ -786,6 +790,10 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     if (surv_on() && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
+        if (GSR_QLIST) {
+            ra.qsurv = at<uint2>(img, il.qsurv);
+            ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
+        }
         if (gsr::CK_SURV) {  // ... in chunks from the forward's checkpoints
             ra.ck_state = at<float4>(img, il.ck_state);
             ra.ck_pos = at<uint32_t>(img, il.ck_pos);
@@ -955,6 +963,10 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
+        if (GSR_QLIST) {
+            ra.qsurv = at<uint2>(img, il.qsurv);
+            ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
+        }
         // no chunks: the image buffer is the cached call's, shared by calls of other colours, and
         // a checkpoint holds one call's colours; the chunk counts are cleared
         if (gsr::CK_SURV) ra.ck_n = at<uint32_t>(img, il.ck_n);
@@ -1041,6 +1053,10 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         if (gsr::SURV_CAP) {
             ra.surv = at<uint2>(img, il.surv);
             ra.surv_n = at<uint32_t>(img, il.surv_n);
+            if (GSR_QLIST) {
+                ra.qsurv = at<uint2>(img, il.qsurv);
+                ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
+            }
         }
         // the single-channel backward's units: chunks of the survivor lists (every forward sets
         // ck_n for its list tiles; the composite forward stores no checkpoints)

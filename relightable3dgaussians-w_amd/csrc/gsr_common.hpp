@@ -88,6 +88,32 @@ static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9
 #endif
 constexpr uint32_t SURV_CAP = GSR_SURV_CAP;
 constexpr uint32_t SURV_NONE = 0xffffffffu;
+// Quadrant lists (GSR_QLIST): the forward's quadrant units of a tile whose super-tile list holds
+// at least GSR_QL_MIN entries store their own quadrant's survivors, each to a list of SURV_CAP
+// slots of their own (qsurv, indexed by the unit's slot: tile_unit), and the tile's count word
+// becomes SURV_QFLAG | slot; the backward merges the four lists in windows of 64 positions
+// instead of re-filtering the whole super-tile list (cfg2c: its slowest backward units are these
+// tiles, 400+ us each).  Measured in round 5 (profiles/r5z_qlist_ab.txt): cfg2c render_bwd 0.432
+// -> 0.418 ms, cfg2 0.314 -> 0.311, single calls unchanged, but the 3-stream throughput -3.8 %
+// (cfg2) / -2.6 % (cfg2c): the backward at 110 VGPRs (104 without) and the forward's extra
+// stores; walked one quadrant after another instead (each survivor reduced per quadrant):
+// render_bwd 0.31 -> 0.41 ms.  Off.
+#ifndef GSR_QLIST
+#define GSR_QLIST 0
+#endif
+#ifndef GSR_QL_MIN
+#define GSR_QL_MIN 4096
+#endif
+constexpr uint32_t SURV_QFLAG = 0x80000000u;
+// (the tile passes' split counts, gsr_tile.hpp, here for the host's layout)
+#ifndef GSR_HEAVY_CAP
+#define GSR_HEAVY_CAP 64
+#endif
+#ifndef GSR_FWD_TAIL
+#define GSR_FWD_TAIL 128
+#endif
+// the forward's quadrant-unit slots (tile_unit's qslot)
+constexpr unsigned QL_SLOTS = 8u * (GSR_HEAVY_CAP + GSR_FWD_TAIL);
 // Backward chunks (GSR_CK_SURV > 0): the forward checkpoints a whole tile's per-pixel state (T and
 // the colour so far) after the batch at which another CK_SURV survivors have been stored, at most
 // CK_MAX times; the backward then runs a tile as one unit per chunk of its survivor list, each

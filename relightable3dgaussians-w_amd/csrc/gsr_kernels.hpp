@@ -258,6 +258,10 @@ struct RenderFwdArgs {
     // instead of re-filtering the super-tile list
     uint2* surv;
     uint32_t* surv_n;
+    // when non-null (GSR_QLIST): quadrant units' lists, SURV_CAP slots per (slot, quadrant), and
+    // their counts [QL_SLOTS][4] (SURV_NONE past SURV_CAP)
+    uint2* qsurv;
+    uint32_t* qsurv_n;
     // GSR_CK_SURV: the chunk checkpoints (per tile: CK_MAX x [T, C0, C1, C2] rows of 64 float4, the
     // boundaries' survivor counts, their number) and the final colours ([C0, C1, C2] rows)
     float4* ck_state;
@@ -292,6 +296,8 @@ struct RenderBwdArgs {
     // all tiles when null) filter their super-tile list
     const uint2* surv;
     const uint32_t* surv_n;
+    const uint2* qsurv;  // the forward's quadrant lists (RenderFwdArgs::qsurv)
+    const uint32_t* qsurv_n;
     // the forward's chunk checkpoints (RenderFwdArgs::ck_state ...) and the expanded unit order
     // (k_tile_order: per band, entries tile | code << 24 from band start x UNITS_MAX; counts at
     // nheavy[24 + band]); units null: tile_unit's order

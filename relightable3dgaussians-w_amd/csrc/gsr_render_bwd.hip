@@ -104,10 +104,36 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     // each lane's entry loaded a batch ahead (its record one batch ahead too measured the same
     // call and a slower 3-stream headline: 113 VGPRs); else the super-tile list, filtered and
     // culled again
-    const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
+    uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
+    const uint2* sl = a.surv + (size_t)tile * SURV_CAP;
+    // the forward's quadrant lists (GSR_QLIST; not in deterministic mode: its partial rows take one
+    // write per survivor), merged: windows of 64 list positions, lane k holding position base - k,
+    // its Gaussian and the OR of the quadrant bits the four lists hold for it (an LDS table), so
+    // each survivor is evaluated over all its quadrants and reduced once, as from a whole list.
+    // qptr[q]: quadrant q's entries left (back to front), cv[q]: each lane's candidate entry of it
+    bool qwin = false;
+    uint32_t qbase = 0, qptr[4] = {0u, 0u, 0u, 0u};
+    __shared__ uint32_t s_wq[64], s_wid[64];
+    if (GSR_QLIST && !DET && a.qsurv && sn != SURV_NONE && (sn & SURV_QFLAG)) {
+        qbase = 4u * (sn & ~SURV_QFLAG);
+        bool ok = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (qlim[q]) {
+                qptr[q] = a.qsurv_n[qbase + q];
+                ok = ok && qptr[q] != SURV_NONE;
+            }
+        qwin = ok;
+        if (ok) {
+            s_wq[lane] = 0u;
+            wave_lds_sync();
+        }
+        sn = SURV_NONE;
+    } else if (sn & SURV_QFLAG) {
+        sn = SURV_NONE;
+    }
     const bool lst = sn != SURV_NONE;
     uint32_t li = lst ? sn : 0u;  // list entries left
-    const uint2* sl = a.surv + (size_t)tile * SURV_CAP;
     if (CK_SURV && lst && a.ck_n) {
         // chunk `chunk` of the list: survivors [ck_pos[chunk - 1], ck_pos[chunk]) (the last chunk up
         // to sn), from the forward's checkpoint after its last survivor: T there, and the recurrence
@@ -141,7 +167,46 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
         uint32_t id = 0, nb, p, qm = 0;  // p: list position (back to front)
-        if (lst) {
+        if (GSR_QLIST && qwin) {
+            // the window below the highest position any list still holds (each lane's candidate
+            // entries loaded here: prefetching them across the walk took 14 more VGPRs)
+            uint2 cv[4];
+            uint32_t base = 0;
+            bool more = false;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                cv[q] = qptr[q] ? a.qsurv[(size_t)(qbase + q) * SURV_CAP + max((int)qptr[q] - 1 - lane, 0)] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (qptr[q]) {
+                    base = max(base, (uint32_t)__builtin_amdgcn_readfirstlane((int)cv[q].y) >> 4);
+                    more = true;
+                }
+            if (!more) break;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!qptr[q]) continue;  // wave-uniform
+                const uint2 c = cv[q];
+                const uint32_t cp = c.y >> 4;
+                const bool in = (int)qptr[q] - 1 - lane >= 0 && cp + 64u > base;  // (entries are a prefix of lanes)
+                const uint32_t n = (uint32_t)__popcll(__ballot(in));
+                if (in) {
+                    atomicOr(&s_wq[base - cp], 1u << q);
+                    s_wid[base - cp] = c.x;
+                }
+                qptr[q] -= n;
+            }
+            wave_lds_sync();
+            const uint32_t wq = s_wq[lane];
+            id = wq ? s_wid[lane] : 0u;
+            s_wq[lane] = 0u;  // (this lane's slot: read above; the next window writes after two syncs)
+            p = base - (uint32_t)lane;
+            nb = base + 1u < 64u ? base + 1u : 64u;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                if (p < qlim[q]) qm |= wq & (1u << q);
+        } else if (lst) {
             nb = min(64u, li);
             if (nb == 0) break;
             const uint2 v = nv;
@@ -165,7 +230,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         float rc = 0.f;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            if (!lst) qm = wt.reach(r, p, qlim);
+            if (!lst && !qwin) qm = wt.reach(r, p, qlim);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
@@ -294,7 +359,11 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             if (DET) {  // one row per instance, summed per Gaussian in tile order (k_det_gather)
                 if (vidx >= 0 && v != 0.f) a.partial[(size_t)(rbase + pos) * DET_ROW3 + pslot] = v;
             } else if (vidx >= 0 && v != 0.f) {
+#ifdef GSR_DIAG_NOATOMIC  // timing diagnostic only (wrong gradients): plain stores to a private line
+                if (v == 1234.5f) a.acc[(size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx] = v;
+#else
                 atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
+#endif
             }
             }
         };

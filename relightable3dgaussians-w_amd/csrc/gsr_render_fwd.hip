@@ -51,7 +51,8 @@ __device__ unsigned long long g_fwd_times[GSR_UNIT_REC * 65536];
 #define FWD_STAT(k, v)
 #endif
 
-__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow) {
+__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow,
+                                                const uint32_t qslot = SURV_NONE) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -59,7 +60,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     const unsigned sti = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     __shared__ TileListLds s_list;
     TileList<true> tl;
-    tl.init(a.ent, a.st_ranges[sti], tile, a.grid_x, sth, 0u, 0u);
+    const uint2 str = a.st_ranges[sti];
+    tl.init(a.ent, str, tile, a.grid_x, sth, 0u, 0u);
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64];
@@ -84,8 +86,11 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
     // survivors stored so far (whole-tile units; SURV_NONE: none stored, or past SURV_CAP)
-    uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
-    uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    // (a quadrant unit of a tile with a long super-tile list: its own quadrant's list, GSR_QLIST)
+    const bool ql = GSR_QLIST && a.qsurv && qslot != SURV_NONE && str.y - str.x >= GSR_QL_MIN;
+    const uint32_t qcode = ql ? 4u * qslot + (uint32_t)__builtin_ctz(qallow) : 0u;
+    uint32_t scnt = ((a.surv && qallow == 15u) || ql) ? 0u : SURV_NONE;
+    uint2* const sl = ql ? a.qsurv + (size_t)qcode * SURV_CAP : a.surv + (size_t)tile * SURV_CAP;
     uint32_t nck = 0, ck_last = 0;  // chunk checkpoints stored, the survivor count at the last one
     uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
     while (live) {
@@ -288,6 +293,10 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         }
     }
     if (lane == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
+    if (lane == 0 && ql) {
+        a.qsurv_n[qcode] = scnt;
+        a.surv_n[tile] = SURV_QFLAG | qslot;  // (the same word from all four quadrant units)
+    }
     uint32_t nm = 0, nsum = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
@@ -311,8 +320,9 @@ k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true)) return;
-    render_fwd_tile(a, tile, qallow);
+    uint32_t qslot;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true, &qslot)) return;
+    render_fwd_tile(a, tile, qallow, qslot);
 }
 
 #ifdef GSR_RENDER_STATS

@@ -238,7 +238,7 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     // the forward's survivor list when it stored one, else the super-tile list (as gsr_render_bwd.hip)
     const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
-    const bool lst = sn != SURV_NONE;
+    const bool lst = sn < SURV_QFLAG;  // (quadrant lists: the single-channel backward's only)
     uint32_t li = lst ? sn : 0u;
     const uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
     uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);

@@ -66,9 +66,12 @@ constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 #ifndef GSR_ROT_SHIFT
 #define GSR_ROT_SHIFT 5
 #endif
+// qslot (when non-null): a quadrant unit's tile slot, unique per frame -- band x (HEAVY_CAP +
+// ntail) + the heavy tile's rank, or HEAVY_CAP + the tail tile's rank (QL_SLOTS with the
+// forward's ntail); SURV_NONE for a whole-tile unit
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
                                           unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
-                                          bool rot = false) {
+                                          bool rot = false, uint32_t* qslot = nullptr) {
     unsigned u = blockIdx.x >> 3, band = blockIdx.x & 7u;
     if (rot && GSR_ROT_THR8 != 0u) {
         uint32_t mx = 0u;
@@ -92,9 +95,11 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
     const unsigned t = min(ntail, len - h);
     const unsigned whole = len - h - t;
     unsigned pos;
+    uint32_t slot = SURV_NONE;
     if (u < 4u * h) {
         pos = u >> 2;
         qallow = 1u << (u & 3u);
+        slot = band * (HEAVY_CAP + ntail) + pos;
     } else if (u < 4u * h + whole) {
         pos = h + (u - 4u * h);
         qallow = 15u;
@@ -102,7 +107,9 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
         const unsigned v = u - 4u * h - whole;
         pos = h + whole + (v >> 2);
         qallow = 1u << (v & 3u);
+        slot = band * (HEAVY_CAP + ntail) + HEAVY_CAP + (v >> 2);
     }
+    if (qslot) *qslot = slot;
     if (pos >= len) return false;
     tile = order[lo + pos];
     return true;
