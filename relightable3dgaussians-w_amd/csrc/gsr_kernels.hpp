@@ -207,13 +207,20 @@ void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost
 #ifndef GSR_FWD_BAL
 #define GSR_FWD_BAL 0
 #endif
+// The forward splits a tile for being heavy from 2^16 super-tile entries (round 4: 2^14): at
+// cfg2c, whose heaviest super-tiles hold 30-45k entries in hundreds of similar tiles, the whole
+// heavy tiles beyond the split cap ran as long as the split ones anyway, and a split tile
+// stores no survivor list, so its backward re-filtered the whole super-tile list.  Round 5
+// (profiles/r5z_fwd_heavy_ab.txt): no split there took cfg2c render_fwd 0.369 -> 0.359 ms, its
+// call 1.227 -> 1.217 ms, its throughput +2.3 %; cfg2 has no such tiles.  The test PLY scene's
+// few 86k-entry tiles (a dense centre, DESIGN §3 "Heavy tiles") still split
 #ifndef GSR_FWD_HEAVY_BITS
-#define GSR_FWD_HEAVY_BITS 14
+#define GSR_FWD_HEAVY_BITS 16
 #endif
 #ifndef GSR_BWD_HEAVY_BITS
 #define GSR_BWD_HEAVY_BITS 13
 #endif
-constexpr int FWD_HEAVY_BITS = GSR_FWD_HEAVY_BITS;  // super-tile entries >= 16384 (its tiles' lists ~8k)
+constexpr int FWD_HEAVY_BITS = GSR_FWD_HEAVY_BITS;  // super-tile entries >= 65536
 constexpr int BWD_HEAVY_BITS = GSR_BWD_HEAVY_BITS;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
 // ... or a cost >= REL8 / 8 x the band's mean tile cost (gsr_order.hpp; 0 = off).  Off: on the
 // clustered cfg2c frame splitting the tiles above 2x / 3x the band mean (64-256 per band) made
