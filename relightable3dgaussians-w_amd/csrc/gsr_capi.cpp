@@ -104,6 +104,7 @@ unsigned tiles_x(int W) { return (unsigned)((W + GSR_BLOCK_X - 1) / GSR_BLOCK_X)
 unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y); }
 
 constexpr int FWD_NHEAVY = 40;  // the forward's band table within the image buffer's nheavy words
+static_assert(FWD_NHEAVY == 8 + 32, "the backward (table at 8) reads the forward's band costs 32 words on (gsr_tile.hpp BWD_ROT_COST)");
 
 ImgLayout img_layout(int W, int H) {
     Carver c;

@@ -321,7 +321,7 @@ k_render_fwd(RenderFwdArgs a) {
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
     uint32_t qslot;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true, &qslot)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, GSR_ROT_THR8, &qslot)) return;
     render_fwd_tile(a, tile, qallow, qslot);
 }
 

@@ -498,7 +498,7 @@ __global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcAr
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, true)) return;
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, GSR_ROT_THR8)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
@@ -523,7 +523,8 @@ template <int NC4, int NCH = 4 * NC4, bool DET = false, int CLS = -1>
 __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS))
+    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS,
+                   DET ? 0u : GSR_BWD_ROT_THR8, nullptr, BWD_ROT_COST))
         return;  // det: one writer per row
 #ifdef GSR_RENDER_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();

@@ -60,6 +60,17 @@ constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 #ifndef GSR_ROT_THR8
 #define GSR_ROT_THR8 10u
 #endif
+// The backward passes rotate their (cost-balanced) bands when the *forward's* equal bands had
+// uneven costs, by the same threshold (0: never): balancing by the estimate left cfg2c's
+// backward XCDs ending 305-450 us apart (a balanced split: 381).  Measured in round 5
+// (profiles/r5z_band_rotate_ab.txt, s36: rotating every frame): cfg2c render_bwd 0.434 ->
+// 0.397 ms, call 1.215 -> 1.182 ms, throughput +2 %, but cfg2's call +0.5 %
+#ifndef GSR_BWD_ROT_THR8
+#define GSR_BWD_ROT_THR8 GSR_ROT_THR8
+#endif
+// the backward's table (nheavy) starts 32 words before the forward's: the forward's band costs
+// are at nheavy[BWD_ROT_COST + b] there
+constexpr unsigned BWD_ROT_COST = 32u + 24u;
 // the rotation steps every 2^GSR_ROT_SHIFT units: an XCD walks runs of 32 units of one band's
 // order, so its L2 still serves neighbouring tiles (cfg2c render_fwd 0.385 -> 0.370 ms against a
 // step per unit, whose forward fetched 3.4x the bytes of unrotated bands: r5z_band_rotate_ab.txt)
@@ -71,18 +82,18 @@ constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 // forward's ntail); SURV_NONE for a whole-tile unit
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
                                           unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
-                                          bool rot = false, uint32_t* qslot = nullptr) {
+                                          unsigned rot = 0u, uint32_t* qslot = nullptr, unsigned rcost = 24u) {
     unsigned u = blockIdx.x >> 3, band = blockIdx.x & 7u;
-    if (rot && GSR_ROT_THR8 != 0u) {
+    if (rot != 0u) {  // (rot: the threshold, GSR_ROT_THR8 / GSR_BWD_ROT_THR8; the costs at nheavy[rcost + b])
         uint32_t mx = 0u;
         unsigned long long sum = 0ull;
 #pragma unroll
         for (int b = 0; b < 8; b++) {
-            const uint32_t c = nheavy[24 + b];
+            const uint32_t c = nheavy[rcost + b];
             mx = max(mx, c);
             sum += c;
         }
-        if (64ull * mx > (unsigned long long)GSR_ROT_THR8 * sum) band = (band + (u >> GSR_ROT_SHIFT)) & 7u;
+        if (64ull * mx > (unsigned long long)rot * sum) band = (band + (u >> GSR_ROT_SHIFT)) & 7u;
     }
     unsigned lo, len;
     if (bal) {
