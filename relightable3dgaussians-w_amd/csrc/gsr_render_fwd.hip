@@ -307,8 +307,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     if (lane == 0 && nm) {
         atomicMax(&a.tile_nmax[tile], nm);
         atomicMax(&a.tile_emax[tile], elast + 1u);
-        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
-        if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], GSR_EVAL_COST ? nev : nsum);
+        uint32_t cost = GSR_EVAL_COST ? nev : nsum;
+#ifdef GSR_NOLIST_SPLIT
+        // experiment: a unit without a survivor list whose backward re-filters at least
+        // GSR_NOLIST_SPLIT super-tile entries marks its tile heavy (the backward splits it)
+        if (scnt == SURV_NONE && elast + 1u - str.x >= (uint32_t)GSR_NOLIST_SPLIT)
+            cost += (1u << GSR_BWD_HEAVY_BITS) / (uint32_t)__popc(qallow);
+#endif
+        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], cost);
+        if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], cost);
     }
 }
 
