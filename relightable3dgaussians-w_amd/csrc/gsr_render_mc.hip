@@ -519,12 +519,16 @@ extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n, int reset) {
 }
 #endif
 
+// the composite backward's band rotation threshold (gsr_tile.hpp; the single-channel pass's by default)
+#ifndef GSR_MC_BWD_ROT_THR8
+#define GSR_MC_BWD_ROT_THR8 GSR_BWD_ROT_THR8
+#endif
 template <int NC4, int NCH = 4 * NC4, bool DET = false, int CLS = -1>
 __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS,
-                   DET ? 0u : GSR_BWD_ROT_THR8, nullptr, BWD_ROT_COST))
+                   DET ? 0u : GSR_MC_BWD_ROT_THR8, nullptr, BWD_ROT_COST))
         return;  // det: one writer per row
 #ifdef GSR_RENDER_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();

@@ -30,9 +30,19 @@ def short(name):
     return name.split("(")[0].replace("gsr::", "").replace("void ", "")
 
 
+def newest_run(files):
+    """The files of the newest rocprofv3 run among files (gpurun_out/ keeps earlier calls' runs of
+    the same tag beside it: <pid>_*.csv, one pid per run)."""
+    if not files:
+        return []
+    last = max(files, key=os.path.getmtime)
+    pid = os.path.basename(last).split("_")[0]
+    return [f for f in files if os.path.dirname(f) == os.path.dirname(last) and os.path.basename(f).split("_")[0] == pid]
+
+
 def counters(pattern):
     acc = defaultdict(list)
-    for f in glob.glob(pattern):
+    for f in newest_run(glob.glob(pattern)):
         for r in csv.DictReader(open(f)):
             acc[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
     return acc
@@ -42,7 +52,7 @@ def main(tag="r01", workload=None):
     out_dir = os.path.join(ROOT, "profiles")
     os.makedirs(out_dir, exist_ok=True)
     g = os.path.join(ROOT, "gpurun_out")
-    ks = sorted(glob.glob(os.path.join(g, f"prof_{tag}_kt", "*", "*_kernel_stats.csv")))
+    ks = newest_run(glob.glob(os.path.join(g, f"prof_{tag}_kt", "*", "*_kernel_stats.csv")))
     if not ks:
         sys.exit(f"no kernel stats for {tag}")
     rows = list(csv.DictReader(open(ks[-1])))
