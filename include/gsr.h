@@ -425,6 +425,11 @@ int gsr_get_deterministic(void);
  * the forward. */
 int gsr_set_survivor_lists(int on);
 int gsr_get_survivor_lists(void);
+/* The backward's heavy-tile threshold: tiles whose estimated cost (the forward's evaluation
+ * count) reaches 2^bits run as four quadrant units (a negative value restores the build's
+ * default, 13).  Results agree either way within the atomic-order tolerance; a switch for tests
+ * (the parity cases' tiles stay below the default) and A/B timing.  Set it before the backward. */
+int gsr_set_backward_heavy_bits(int bits);
 /* The backward's chunk size in survivors (0: each tile's list is one unit).  With chunks the
  * backward runs a long list as several units, each starting from a checkpoint the forward stored
  * (T and the colour so far per pixel); their gradients then differ from the one-unit walk's by

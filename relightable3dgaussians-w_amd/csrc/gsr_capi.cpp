@@ -495,6 +495,13 @@ int gsr_set_survivor_lists(int on) {
     return GSR_OK;
 }
 int gsr_get_survivor_lists(void) { return surv_on() ? 1 : 0; }
+// the backward's heavy-tile threshold (log2 of the estimate; < 0: the build's BWD_HEAVY_BITS)
+static std::atomic<int> g_bwd_heavy_bits{-1};
+int gsr_set_backward_heavy_bits(int bits) {
+    if (bits > 32) return fail(GSR_E_ARG, "gsr_set_backward_heavy_bits: bits %d > 32", bits);
+    g_bwd_heavy_bits.store(bits < 0 ? -1 : bits);
+    return GSR_OK;
+}
 int gsr_backward_chunk_size(void) { return (int)gsr::CK_SURV; }
 
 int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
@@ -1072,7 +1079,9 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         {
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
-                                   at<uint32_t>(img, il.nheavy) + 8, det ? 32 : gsr::BWD_HEAVY_BITS, s,  // det: one writer per row
+                                   at<uint32_t>(img, il.nheavy) + 8,
+                                   det ? 32 : (g_bwd_heavy_bits.load() >= 0 ? g_bwd_heavy_bits.load() : gsr::BWD_HEAVY_BITS),
+                                   s,  // det: one writer per row
                                    at<uint32_t>(img, il.row_cost), gy, det ? 0 : GSR_BWD_HEAVY_REL8,
                                    chunks ? ra.surv_n : nullptr, chunks ? ra.ck_n : nullptr,
                                    chunks ? at<uint32_t>(img, il.units) : nullptr);

@@ -104,6 +104,7 @@ def _declare(lib):
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_set_deterministic.argtypes = [i]
     lib.gsr_set_survivor_lists.argtypes = [i]
+    lib.gsr_set_backward_heavy_bits.argtypes = [i]
     lib.gsr_check_buffers.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
     lib.gsr_materialize_lists.argtypes = [i, i, i, vp, vp, vp, vp]
     lib.gsr_last_error.restype = C.c_char_p
@@ -118,7 +119,7 @@ def _declare(lib):
                "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
                "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
-               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_backward_chunk_size", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
+               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_set_backward_heavy_bits", "gsr_backward_chunk_size", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
 
 
@@ -191,6 +192,12 @@ def set_survivor_lists(on=True):
 
 def survivor_lists():
     return bool(lib().gsr_get_survivor_lists())
+
+
+def set_backward_heavy_bits(bits=-1):
+    """The backward's heavy-tile split threshold, log2 of the estimated cost
+    (gsr_set_backward_heavy_bits; -1: the build's default)."""
+    check(lib().gsr_set_backward_heavy_bits(int(bits)), "gsr_set_backward_heavy_bits")
 
 
 def debug_build():

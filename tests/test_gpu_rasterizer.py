@@ -234,6 +234,20 @@ def test_backward_parity(case):
     assert not bad, f"gradient rel L2 errors above {GRAD_TOL}: {bad} (all: {errs})"
 
 
+@pytest.mark.parametrize("name,bits", [("heavy_tiles", 8), ("dense_small", 6), ("sh3_orbit_bg", 5)])
+def test_backward_parity_quadrant_units(name, bits):
+    """The backward's quadrant units: its split threshold lowered (gsr_set_backward_heavy_bits)
+    so that the parity cases' tiles -- below the default 2^13 evaluations -- run as four
+    quadrant units each, against the same oracle and tolerance as test_backward_parity."""
+    _, _, _lib = _dgr()
+    case = next(c for c in CASES if c["name"] == name)
+    _lib.set_backward_heavy_bits(bits)
+    try:
+        test_backward_parity(case)
+    finally:
+        _lib.set_backward_heavy_bits(-1)
+
+
 def test_autograd_module_path():
     """The drop-in GaussianRasterizer as gaussian_renderer.render() uses it (colors_precomp,
     sh_degree=-1, scales/rotations, means2D with retain_grad)."""
