@@ -443,7 +443,7 @@ k_render_bwd(RenderBwdArgs a) {
         return;
     }
     if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS,
-                   DET ? 0u : GSR_BWD_ROT_THR8, nullptr, BWD_ROT_COST))
+                   DET ? 0u : GSR_BWD_ROT_THR8, nullptr, BWD_ROT_COST, GSR_BWD_ROT_SHIFT))
         return;  // det: one writer per row
 #if GSR_BWD_BG_SPEC
     // a zero background (wave-uniform scalar loads) takes the walk without its dL/dalpha term

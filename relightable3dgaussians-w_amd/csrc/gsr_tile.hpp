@@ -71,6 +71,9 @@ constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
 // the backward's table (nheavy) starts 32 words before the forward's: the forward's band costs
 // are at nheavy[BWD_ROT_COST + b] there
 constexpr unsigned BWD_ROT_COST = 32u + 24u;
+#ifndef GSR_BWD_ROT_SHIFT
+#define GSR_BWD_ROT_SHIFT GSR_ROT_SHIFT
+#endif
 // the rotation steps every 2^GSR_ROT_SHIFT units: an XCD walks runs of 32 units of one band's
 // order, so its L2 still serves neighbouring tiles (cfg2c render_fwd 0.385 -> 0.370 ms against a
 // step per unit, whose forward fetched 3.4x the bytes of unrotated bands: r5z_band_rotate_ab.txt)
@@ -82,7 +85,8 @@ constexpr unsigned BWD_ROT_COST = 32u + 24u;
 // forward's ntail); SURV_NONE for a whole-tile unit
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
                                           unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
-                                          unsigned rot = 0u, uint32_t* qslot = nullptr, unsigned rcost = 24u) {
+                                          unsigned rot = 0u, uint32_t* qslot = nullptr, unsigned rcost = 24u,
+                                          unsigned rshift = GSR_ROT_SHIFT) {
     unsigned u = blockIdx.x >> 3, band = blockIdx.x & 7u;
     if (rot != 0u) {  // (rot: the threshold, GSR_ROT_THR8 / GSR_BWD_ROT_THR8; the costs at nheavy[rcost + b])
         uint32_t mx = 0u;
@@ -93,7 +97,7 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
             mx = max(mx, c);
             sum += c;
         }
-        if (64ull * mx > (unsigned long long)rot * sum) band = (band + (u >> GSR_ROT_SHIFT)) & 7u;
+        if (64ull * mx > (unsigned long long)rot * sum) band = (band + (u >> rshift)) & 7u;
     }
     unsigned lo, len;
     if (bal) {
