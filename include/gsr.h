@@ -387,11 +387,13 @@ typedef struct gsr_layout {
     size_t img_final_T, img_n_contrib, img_ranges, img_tile_nmax, img_tile_emax;
     size_t bin_st_ranges, bin_entries;
     /* the backward's dispatch order (appended in round 4): the forward's per-tile cost estimate
-     * [T] and its per-tile-row sums [tiles_y], the order [T], and the band table (u32 [32]:
-     * forward band heavy counts [0..8), backward [8..16), backward band bounds [16..25)) */
+     * [T] and its per-tile-row sums [tiles_y], the order [T], and the band tables (u32 [80]: the
+     * backward's table at word 8 and the forward's at word 40, each relative to its start: band
+     * heavy counts [0..8), balanced band bounds [8..17), band costs [24..32)) */
     size_t img_tile_cost, img_row_cost, img_order_bwd, img_nheavy;
     /* the forward's survivor lists (appended in round 5): per tile the count (u32 [T],
-     * 0xFFFFFFFF: none stored) and the list (u32 pairs [T][surv_cap]) */
+     * 0xFFFFFFFF: none stored) and the list (u32 pairs [T][surv_cap]), the last region of the
+     * image buffer, reserved only while the survivor lists are on (img_bytes counts them then) */
     size_t img_surv_n, img_surv, surv_cap;
 } gsr_layout;
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out);
@@ -430,11 +432,6 @@ int gsr_get_survivor_lists(void);
  * default, 13).  Results agree either way within the atomic-order tolerance; a switch for tests
  * (the parity cases' tiles stay below the default) and A/B timing.  Set it before the backward. */
 int gsr_set_backward_heavy_bits(int bits);
-/* The backward's chunk size in survivors (0: each tile's list is one unit).  With chunks the
- * backward runs a long list as several units, each starting from a checkpoint the forward stored
- * (T and the colour so far per pixel); their gradients then differ from the one-unit walk's by
- * float rounding only. */
-int gsr_backward_chunk_size(void);
 /* 1 when this library was built with -DGSR_DEBUG (`make debug` -> lib/debug/libgsr.so): every
  * forward then verifies its tile lists against the preprocess (ids, culling, rect coverage,
  * (depth, index) order, per-Gaussian instance counts, total R, n_contrib bounds) with a

@@ -162,10 +162,7 @@ void launch_frame_totals(const FrameTotals& ft, hipStream_t s) {
 // ranks them per super-tile with wave ballots, writing each entry at its final position.
 // Equivalent to emit + a stable counting sort by super-tile (the entry order within a
 // super-tile is the depth order), in four launches and no entry round trip through HBM.
-#ifndef GSR_ST_G
-#define GSR_ST_G 1024
-#endif
-constexpr int ST_G = GSR_ST_G;  // Gaussians per block
+constexpr int ST_G = 1024;  // Gaussians per block
 // waves per block in k_st_hist / k_st_scatter (ST_G / W Gaussians each): 8, or 4 when the
 // per-wave LDS state of 8 waves would not fit (st_waves)
 
@@ -187,8 +184,8 @@ __device__ __forceinline__ uint2 sorted_rect(const void* r, int p) {
 }
 
 // k_st_hist's LDS histograms: one per block.  (Round 3's per-wave counts stored by k_st_hist
-// for the scatter, GSR_ST_WCOUNTS, were retired in round 5: k_st_hist now stores the block's
-// entry-balanced wave cuts instead.)
+// for the scatter were retired in round 5: k_st_hist now stores the block's entry-balanced wave
+// cuts instead.)
 constexpr int st_hist_count(int) { return 1; }
 
 // A lane's super-tile rect [sx0, sx1) x [sy0, sy1) is walked by the lane itself when it holds
@@ -199,10 +196,7 @@ constexpr int st_hist_count(int) { return 1; }
 // addresses (the clustered cfg2c frame: k_st_scatter 32 -> 113 us against cfg2).  f(sx, sy, o,
 // a0, a1, a2) runs once per (lane o, super-tile) pair with lane o's values a0..a2.  Every lane
 // of the wave must call it (a ballot); lanes with nothing to walk pass an empty rect.
-#ifndef GSR_ST_BIG
-#define GSR_ST_BIG 16u
-#endif
-constexpr uint32_t ST_BIG = GSR_ST_BIG;  // (0xffffffffu: every lane walks its own rect, as before round 5)
+constexpr uint32_t ST_BIG = 16u;
 template <class F>
 __device__ __forceinline__ void st_rect_walk(uint32_t sx0, uint32_t sx1, uint32_t sy0, uint32_t sy1, uint32_t a0,
                                              uint32_t a1, uint32_t a2, F&& f) {
@@ -384,7 +378,6 @@ __global__ void __launch_bounds__(64 * ST_W) k_st_scatter(int Pv, const unsigned
     if ((int)blockIdx.x >= nb) {
         const int x = (int)blockIdx.x - nb - (ft.host ? 1 : 0);
         if (x < 0) frame_totals(ft);  // the extra workgroup: the host's frame totals
-        else if (GSR_FWD_BAL) tile_order_band<true>((unsigned)x, ord);  // (equal bands below 512 threads)
         else tile_order_band((unsigned)x, ord);
         return;
     }

@@ -22,7 +22,9 @@
 #include <vector>
 
 #include "../../include/gsr.h"
+#ifdef GSR_WITH_ROCTX
 #include <rocprofiler-sdk-roctx/roctx.h>
+#endif
 
 #include "gsr_kernels.hpp"
 #include "gsr_shade.hpp"
@@ -66,7 +68,7 @@ struct GeomLayout {
 };
 struct ImgLayout {
     size_t final_T, n_contrib, ranges, tile_nmax, tile_emax, tile_cost, row_cost, order_fwd, order_bwd, nheavy, surv_n,
-        surv, qsurv_n, qsurv, ck_n, ck_pos, ck_state, cfin, units, total;
+        surv, total;
 };
 // The binning buffer: a header (S), the super-tile ranges and entries at offsets independent of
 // S (all the backward needs), then the forward's binning scratch.
@@ -106,7 +108,10 @@ unsigned tiles_y(int H) { return (unsigned)((H + GSR_BLOCK_Y - 1) / GSR_BLOCK_Y)
 constexpr int FWD_NHEAVY = 40;  // the forward's band table within the image buffer's nheavy words
 static_assert(FWD_NHEAVY == 8 + 32, "the backward (table at 8) reads the forward's band costs 32 words on (gsr_tile.hpp BWD_ROT_COST)");
 
-ImgLayout img_layout(int W, int H) {
+// surv: reserve the survivor lists (the forward stores them: surv_on()).  They sit last, so every
+// other offset (and the lists' own) is the same either way: a backward over a buffer made without
+// them finds every tile's count SURV_NONE (the forward's order sets it) and never reads the lists.
+ImgLayout img_layout(int W, int H, bool surv) {
     Carver c;
     ImgLayout L;
     const size_t N = (size_t)W * H;
@@ -116,29 +121,17 @@ ImgLayout img_layout(int W, int H) {
     L.ranges = c.take(8 * T);  // the reference's tile ranges: filled only by the list materialisation
     L.tile_nmax = c.take(4 * T);
     L.tile_emax = c.take(4 * T);
-    L.tile_cost = c.take(4 * T);  // the backward's cost estimate: sum of the quadrants' largest n_contrib
+    L.tile_cost = c.take(4 * T);  // the backward's cost estimate: (survivor, quadrant) evaluations
     L.row_cost = c.take(4 * (size_t)tiles_y(H));  // the same per tile row (the backward's balanced bands)
     L.order_fwd = c.take(4 * T);
     L.order_bwd = c.take(4 * T);
-    // two band tables, the backward's at 8 and the forward's at 40 (FWD_NHEAVY), each (relative
-    // to its start): heavy counts [0..8), balanced bounds [8..17), unit counts (backward chunks)
-    // or band costs (the forward's rotated bands) [24..32)
+    // two band tables of 40 words, the backward's at 8 and the forward's at 40 (FWD_NHEAVY), each
+    // (relative to its start): heavy counts [0..8), balanced bounds [8..17), band costs [24..32)
     L.nheavy = c.take(4 * 80);
+    L.surv_n = c.take(4 * T);
     // the forward's survivor lists for the backward (RenderFwdArgs::surv): 8 B x SURV_CAP per tile,
     // written only as far as each tile's survivors reach (cfg2: ~1.4 KB of the 8 KB)
-    L.surv_n = c.take(4 * T);
-    L.surv = c.take(8 * (size_t)gsr::SURV_CAP * T);
-    // the forward's quadrant lists (GSR_QLIST): SURV_CAP entries per (quadrant-unit slot, quadrant)
-    const size_t nql = GSR_QLIST && gsr::SURV_CAP ? 4 * (size_t)gsr::QL_SLOTS : 0;
-    L.qsurv_n = c.take(4 * nql);
-    L.qsurv = c.take(8 * (size_t)gsr::SURV_CAP * nql);
-    // the backward's chunks (GSR_CK_SURV): checkpoints, final colours, the expanded unit order
-    const size_t ck = gsr::CK_SURV ? 1 : 0;
-    L.ck_n = c.take(ck * 4 * T);
-    L.ck_pos = c.take(ck * 4 * gsr::CK_MAX * T);
-    L.ck_state = c.take(ck * 16 * 4 * 64 * gsr::CK_MAX * T);
-    L.cfin = c.take(ck * 16 * 3 * 64 * T);
-    L.units = c.take(ck * 4 * gsr::UNITS_MAX * T);
+    L.surv = c.take(surv ? 8 * (size_t)gsr::SURV_CAP * T : 0);
     L.total = c.o + 256;
     return L;
 }
@@ -347,15 +340,19 @@ struct Prof {
 };
 Prof g_prof;
 
-// roctx ranges: every stage is also a named range ("gsr:<stage>") for external
-// rocprofv3 --marker-trace timelines of the reference's own train.py on this path; on unless
-// GSR_ROCTX=0 (a call into librocprofiler-sdk-roctx, a no-op without a tool attached)
+// roctx ranges: with GSR_ROCTX=1 in the environment, every stage is also a named
+// range ("gsr:<stage>") for external rocprofv3 --marker-trace timelines of the reference's own
+// train.py on this path.  Builds without rocprofiler-sdk (make ROCTX=0) have no ranges.
 static bool roctx_on() {
+#ifdef GSR_WITH_ROCTX
     static const bool on = [] {
         const char* e = getenv("GSR_ROCTX");
-        return !(e && e[0] == '0');
+        return e && e[0] && e[0] != '0';
     }();
     return on;
+#else
+    return false;
+#endif
 }
 extern const char* kStageNames[];
 struct StageTimer {
@@ -370,13 +367,17 @@ struct StageTimer {
                 for (int i = 0; i < ST_COUNT; i++) v.push_back(std::string("gsr:") + kStageNames[i]);
                 return v;
             }();
+#ifdef GSR_WITH_ROCTX
             roctxRangePushA(names[st].c_str());
             rx = true;
+#endif
         }
         if (g_prof.on && ((g_prof.mask >> st) & 1u)) { a = g_prof.get(); (void)hipEventRecord(a, s); }
     }
     ~StageTimer() {
+#ifdef GSR_WITH_ROCTX
         if (rx) roctxRangePop();
+#endif
         if (a) {
             hipEvent_t b = g_prof.get();
             (void)hipEventRecord(b, s);
@@ -502,14 +503,13 @@ int gsr_set_backward_heavy_bits(int bits) {
     g_bwd_heavy_bits.store(bits < 0 ? -1 : bits);
     return GSR_OK;
 }
-int gsr_backward_chunk_size(void) { return (int)gsr::CK_SURV; }
 
 int gsr_check_buffers(int P, int R, int width, int height, const int* radii, void* geom_buffer, void* binning_buffer,
                       void* img_buffer, void* stream_) {
     if (P < 0 || R < 0 || width <= 0 || height <= 0 || !radii || !geom_buffer || !img_buffer || (R > 0 && !binning_buffer))
         return fail(GSR_E_ARG, "gsr_check_buffers: bad arguments");
     const GeomLayout gl = geom_layout(P);
-    const ImgLayout il = img_layout(width, height);
+    const ImgLayout il = img_layout(width, height, false);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
     char* bin = binning_buffer ? align_base(binning_buffer) : nullptr;
@@ -576,7 +576,7 @@ int gsr_profile_read(double* ms, long long* counts, int n, int reset) {
 int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     if (!out || P < 0 || R < 0 || width < 0 || height < 0) return fail(GSR_E_ARG, "gsr_get_layout: bad arguments");
     const GeomLayout g = geom_layout(P);
-    const ImgLayout im = img_layout(width, height);
+    const ImgLayout im = img_layout(width, height, surv_on());
     const BinLayout b = bin_layout(0, width, height, 0);
     (void)R;
     out->geom_bytes = g.total;
@@ -628,7 +628,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     const float focal_y = height / (2.0f * tan_fovy);
     const float focal_x = width / (2.0f * tan_fovx);
     const GeomLayout gl = geom_layout(P);
-    const ImgLayout il = img_layout(width, height);
+    const bool surv = surv_on();
+    const ImgLayout il = img_layout(width, height, surv);
     char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
     char* img = reinterpret_cast<char*>(image_buffer(image_ctx, il.total));
     if (!geom || !img) return fail(GSR_E_ALLOC, "gsr_forward: buffer allocation failed");
@@ -739,13 +740,11 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         gsr::TileOrderArgs ord{};
         ord.ntile = (unsigned)T; ord.gx = gx; ord.gsx = gsx; ord.order = at<uint32_t>(img, il.order_fwd);
         ord.nheavy = at<uint32_t>(img, il.nheavy) + FWD_NHEAVY; ord.heavy_bits = gsr::FWD_HEAVY_BITS;
-        ord.balance = GSR_FWD_BAL;  // (the large-frame path's own order launch)
-        ord.heavy_rel8 = GSR_FWD_HEAVY_REL8;
+        ord.balance = 0;  // equal bands (tile_unit_fwd)
         ord.zero_a = at<uint32_t>(img, il.tile_nmax); ord.zero_b = at<uint32_t>(img, il.tile_emax);
         ord.zero_c = at<uint32_t>(img, il.tile_cost);
         ord.zero_rows = at<uint32_t>(img, il.row_cost); ord.nrows = gy;
-        ord.unset = gsr::SURV_CAP ? at<uint32_t>(img, il.surv_n) : nullptr;  // no list unless this forward stores one
-        ord.zero_d = gsr::CK_SURV ? at<uint32_t>(img, il.ck_n) : nullptr;     // nor chunks
+        ord.unset = at<uint32_t>(img, il.surv_n);  // no list unless this forward stores one
         if (fused_bin) {  // the order runs in extra workgroups of the binning's scatter
             GSR_STAGE(ST_DUPLICATE);
             gsr::launch_st_bin(dev ? P : (int)Pv, dev ? tot_dev : nullptr, sorted_ids, rect_sorted, rect_packed, gsx, st_h(width, height), NS,
@@ -795,19 +794,9 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
     ra.row_cost = at<uint32_t>(img, il.row_cost);
-    if (surv_on() && !mc) {  // the single-channel backward walks the forward's survivor lists
+    if (surv && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
-        if (GSR_QLIST) {
-            ra.qsurv = at<uint2>(img, il.qsurv);
-            ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
-        }
-        if (gsr::CK_SURV) {  // ... in chunks from the forward's checkpoints
-            ra.ck_state = at<float4>(img, il.ck_state);
-            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
-            ra.ck_n = at<uint32_t>(img, il.ck_n);
-            ra.cfin = at<float4>(img, il.cfin);
-        }
     }
     // the forward tile pass over the binning in `bin`; its workgroups also zero the backward's
     // accumulator lines (zero_slice; the depth sort's digit scans did it up to round 3)
@@ -832,7 +821,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                     ma.n_contrib = ra.n_contrib;
                     ma.zero = ra.zero;
                     ma.zero_n4 = ra.zero_n4;
-                    if (surv_on()) {  // the survivors (the same for every group)
+                    if (surv) {  // the survivors (the same for every group)
                         ma.surv = at<uint2>(img, il.surv);
                         ma.surv_n = at<uint32_t>(img, il.surv_n);
                     }
@@ -935,7 +924,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
         !binning_buffer)
         return fail(GSR_E_ARG, "gsr_forward_reuse: missing buffers");
     const GeomLayout gl = geom_layout(P);
-    const ImgLayout il = img_layout(width, height);
+    const ImgLayout il = img_layout(width, height, false);
     const BinLayout bl = bin_layout(0, width, height, 0);
     char* geom = reinterpret_cast<char*>(geometry_buffer(geometry_ctx, gl.total));
     if (!geom) return fail(GSR_E_ALLOC, "gsr_forward_reuse: buffer allocation failed");
@@ -968,17 +957,8 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = nullptr;  // already summed by the cached call's forward
-    if (surv_on()) {  // the same survivors again (the lists of the cached call are rewritten)
-        ra.surv = at<uint2>(img, il.surv);
-        ra.surv_n = at<uint32_t>(img, il.surv_n);
-        if (GSR_QLIST) {
-            ra.qsurv = at<uint2>(img, il.qsurv);
-            ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
-        }
-        // no chunks: the image buffer is the cached call's, shared by calls of other colours, and
-        // a checkpoint holds one call's colours; the chunk counts are cleared
-        if (gsr::CK_SURV) ra.ck_n = at<uint32_t>(img, il.ck_n);
-    }
+    // no survivor lists: the cached call's stay (its survivors are this call's -- they depend on the
+    // geometry only -- and its buffer holds lists only if that forward stored them)
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
     {
         GSR_STAGE(ST_RENDER_FWD);
@@ -1003,7 +983,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
     const float focal_y = height / (2.0f * tan_fovy);
     const float focal_x = width / (2.0f * tan_fovx);
     const GeomLayout gl = geom_layout(P);
-    const ImgLayout il = img_layout(width, height);
+    const ImgLayout il = img_layout(width, height, true);  // (the lists are read only where stored)
     const BinLayout bl = bin_layout(0, width, height, 0);
     char* geom = align_base(geom_buffer);
     char* img = align_base(img_buffer);
@@ -1058,33 +1038,15 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.order = at<uint32_t>(img, il.order_bwd);
         ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         ra.partial = partial;
-        if (gsr::SURV_CAP) {
-            ra.surv = at<uint2>(img, il.surv);
-            ra.surv_n = at<uint32_t>(img, il.surv_n);
-            if (GSR_QLIST) {
-                ra.qsurv = at<uint2>(img, il.qsurv);
-                ra.qsurv_n = at<uint32_t>(img, il.qsurv_n);
-            }
-        }
-        // the single-channel backward's units: chunks of the survivor lists (every forward sets
-        // ck_n for its list tiles; the composite forward stores no checkpoints)
-        const bool chunks = gsr::CK_SURV && !mc;
-        if (chunks) {
-            ra.ck_state = at<float4>(img, il.ck_state);
-            ra.ck_pos = at<uint32_t>(img, il.ck_pos);
-            ra.ck_n = at<uint32_t>(img, il.ck_n);
-            ra.cfin = at<float4>(img, il.cfin);
-            ra.units = at<uint32_t>(img, il.units);
-        }
+        ra.surv = at<uint2>(img, il.surv);
+        ra.surv_n = at<uint32_t>(img, il.surv_n);
         {
             GSR_STAGE(ST_RANGES);  // "tile_order": the backward's dispatch order
             gsr::launch_tile_order(gx * gy, nullptr, at<uint32_t>(img, il.tile_cost), at<uint32_t>(img, il.order_bwd),
                                    at<uint32_t>(img, il.nheavy) + 8,
                                    det ? 32 : (g_bwd_heavy_bits.load() >= 0 ? g_bwd_heavy_bits.load() : gsr::BWD_HEAVY_BITS),
                                    s,  // det: one writer per row
-                                   at<uint32_t>(img, il.row_cost), gy, det ? 0 : GSR_BWD_HEAVY_REL8,
-                                   chunks ? ra.surv_n : nullptr, chunks ? ra.ck_n : nullptr,
-                                   chunks ? at<uint32_t>(img, il.units) : nullptr);
+                                   at<uint32_t>(img, il.row_cost), gy);
         }
         {
             GSR_STAGE(ST_RENDER_BWD);  // the tile pass alone (roofline.avg_launch_ms in bench.py)

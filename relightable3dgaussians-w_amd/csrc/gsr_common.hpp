@@ -30,17 +30,11 @@ constexpr int ST_TILES = 64;  // tiles of the tallest super-tile (8 x 8), one la
 // frames (4K: 1020 8x4 super-tiles) take 8x8 (sth = 3): fewer entries per Gaussian (cfg5:
 // 3.2 instead of 4.7) and half the per-wave scatter state, for a little more filtering in
 // the tile passes.  A pure function of the tile grid, evaluated on the host and in the
-// kernels alike.  GSR_ST_STH forces one height (experiments).
+// kernels alike.
 constexpr unsigned ST_SMALL_MAX = 682;
 __host__ __device__ __forceinline__ unsigned st_sth(unsigned gx, unsigned gy) {
-#ifdef GSR_ST_STH
-    (void)gx;
-    (void)gy;
-    return GSR_ST_STH;
-#else
     const unsigned long long ns4 = (unsigned long long)((gx + GSR_ST_W - 1u) / GSR_ST_W) * ((gy + 3u) / 4u);
     return ns4 > ST_SMALL_MAX ? 3u : 2u;
-#endif
 }
 
 // auxiliary.h:22-39 (same decimal literals as the reference)
@@ -72,64 +66,14 @@ struct __align__(16) Rec {
 // requests: with 48-B lines half of a Gaussian's 9-value atomics straddled two 64-B segments.
 // 64-B lines (measured at cfg2, rocprofv3 kernel trace): render_bwd 351 -> 334 us, the
 // preprocess backward 122 -> 131 us (33 % more accumulator bytes to read; a coalesced LDS
-// hand-out of the lines measured the same), the call pair -16 us.  GSR_ACC_STRIDE=12 builds
-// the 48-B layout.
-#ifndef GSR_ACC_STRIDE
-#define GSR_ACC_STRIDE 16
-#endif
-constexpr int ACC_STRIDE = GSR_ACC_STRIDE;
-static_assert(ACC_STRIDE % 4 == 0 && ACC_STRIDE >= 12, "accumulator lines hold 9 floats, 16-B aligned");
+// hand-out of the lines measured the same), the call pair -16 us.
+constexpr int ACC_STRIDE = 16;
 
 // The forward tile pass's survivor lists (RenderFwdArgs::surv): at most SURV_CAP entries per
 // tile (cfg2: 285 at most, the clustered cfg2c 749), a count of SURV_NONE sends the backward
-// back to its super-tile list.  GSR_SURV_CAP=0 builds without them.
-#ifndef GSR_SURV_CAP
-#define GSR_SURV_CAP 1024
-#endif
-constexpr uint32_t SURV_CAP = GSR_SURV_CAP;
+// back to its super-tile list.
+constexpr uint32_t SURV_CAP = 1024;
 constexpr uint32_t SURV_NONE = 0xffffffffu;
-// Quadrant lists (GSR_QLIST): the forward's quadrant units of a tile whose super-tile list holds
-// at least GSR_QL_MIN entries store their own quadrant's survivors, each to a list of SURV_CAP
-// slots of their own (qsurv, indexed by the unit's slot: tile_unit), and the tile's count word
-// becomes SURV_QFLAG | slot; the backward merges the four lists in windows of 64 positions
-// instead of re-filtering the whole super-tile list (cfg2c: its slowest backward units are these
-// tiles, 400+ us each).  Measured in round 5 (profiles/r5z_qlist_ab.txt): cfg2c render_bwd 0.432
-// -> 0.418 ms, cfg2 0.314 -> 0.311, single calls unchanged, but the 3-stream throughput -3.8 %
-// (cfg2) / -2.6 % (cfg2c): the backward at 110 VGPRs (104 without) and the forward's extra
-// stores; walked one quadrant after another instead (each survivor reduced per quadrant):
-// render_bwd 0.31 -> 0.41 ms.  Off.
-#ifndef GSR_QLIST
-#define GSR_QLIST 0
-#endif
-#ifndef GSR_QL_MIN
-#define GSR_QL_MIN 4096
-#endif
-constexpr uint32_t SURV_QFLAG = 0x80000000u;
-// (the tile passes' split counts, gsr_tile.hpp, here for the host's layout)
-#ifndef GSR_HEAVY_CAP
-#define GSR_HEAVY_CAP 64
-#endif
-#ifndef GSR_FWD_TAIL
-#define GSR_FWD_TAIL 128
-#endif
-// the forward's quadrant-unit slots (tile_unit's qslot)
-constexpr unsigned QL_SLOTS = 8u * (GSR_HEAVY_CAP + GSR_FWD_TAIL);
-// Backward chunks (GSR_CK_SURV > 0): the forward checkpoints a whole tile's per-pixel state (T and
-// the colour so far) after the batch at which another CK_SURV survivors have been stored, at most
-// CK_MAX times; the backward then runs a tile as one unit per chunk of its survivor list, each
-// starting from its checkpoint (T, and the recurrence from the final colour), in parallel.
-#ifndef GSR_CK_SURV
-#define GSR_CK_SURV 0
-#endif
-#ifndef GSR_CK_MAX
-#define GSR_CK_MAX 3
-#endif
-constexpr uint32_t CK_SURV = GSR_CK_SURV;
-constexpr uint32_t CK_MAX = GSR_CK_MAX;
-// backward units per tile at most: its chunks, or four quadrants of a heavy tile without a list
-constexpr uint32_t UNITS_MAX = (CK_MAX + 1) > 4 ? (CK_MAX + 1) : 4;
-// unit codes (the top 8 bits of an expanded order entry): chunk index, a quadrant, the whole tile
-constexpr uint32_t UNIT_QUAD = 0xF0u, UNIT_WHOLE = 0xFFu;
 
 // Gradient outputs added into (instead of overwritten): the backward kernels' accumulate
 // bits (include/gsr.h GSR_ACC_*), so several views' gradients are summed where they are made.

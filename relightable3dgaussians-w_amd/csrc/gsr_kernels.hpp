@@ -62,10 +62,7 @@ void launch_exclusive_scan_u32(long long n, const uint32_t* in, const uint32_t* 
 
 // ---- radix sort (gsr_sort.hip) ---------------------------------------------------------
 constexpr int SORT_THREADS = 256;
-#ifndef GSR_SORT_ITEMS
-#define GSR_SORT_ITEMS 8
-#endif
-constexpr int SORT_ITEMS = GSR_SORT_ITEMS;
+constexpr int SORT_ITEMS = 8;
 constexpr int SORT_TILE = SORT_THREADS * SORT_ITEMS;  // 2048 keys per block
 inline int sort_blocks(long long n) { return (int)((n + SORT_TILE - 1) / SORT_TILE); }
 // scratch bytes for sort of n items
@@ -117,21 +114,14 @@ struct TileOrderArgs {
     uint32_t* order;
     uint32_t* nheavy;
     int heavy_bits;
-    int heavy_rel8;  // also heavy: cost >= heavy_rel8 / 8 x the band's mean (0: absolute threshold only)
     uint32_t *zero_a, *zero_b, *zero_c;  // optional per-tile words zeroed (the forward's targets)
     uint32_t* unset;  // optional per-tile words set to SURV_NONE (survivor counts the forward may not write)
-    uint32_t* zero_d;  // optional per-tile words zeroed (chunk counts the composite forward does not write)
     int balance;  // cost-balanced bands, their first tiles stored to nheavy[8..17) (tile_unit's bal)
     // per tile row: the summed cost the balanced bands read (row_cost), or zeroed by the
     // forward's order for its tile pass to raise (zero_rows); nrows = tile rows
     const uint32_t* row_cost;
     uint32_t* zero_rows;
     unsigned nrows;
-    // the backward with survivor lists and chunks: each band's tiles in order expanded into units
-    // (units[band start x UNITS_MAX + i] = tile | code << 24; the count to nheavy[24 + band])
-    const uint32_t* surv_n;
-    const uint32_t* ck_n;
-    uint32_t* units;
 };
 
 // The forward's frame totals for the host: one workgroup sums the preprocess's per-workgroup
@@ -198,41 +188,20 @@ void launch_materialize(long long S, int nst, const uint2* st_ranges, const uint
 // cost >= 2^heavy_bits.
 // row_cost [nrows] (optional): the forward's summed cost per tile row (the balanced bands)
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0,
-                       int heavy_rel8 = 0, const uint32_t* surv_n = nullptr, const uint32_t* ck_n = nullptr,
-                       uint32_t* units = nullptr);
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost = nullptr, unsigned nrows = 0);
 
-// The forward passes' bands: 1 -- cost-balanced by the super-tile entry counts (summed per row;
-// bounds stored after the forward's band counts as the backward's are), 0 -- equal tile counts
-#ifndef GSR_FWD_BAL
-#define GSR_FWD_BAL 0
-#endif
-// The forward splits a tile for being heavy from 2^16 super-tile entries (round 4: 2^14): at
-// cfg2c, whose heaviest super-tiles hold 30-45k entries in hundreds of similar tiles, the whole
-// heavy tiles beyond the split cap ran as long as the split ones anyway, and a split tile
-// stores no survivor list, so its backward re-filtered the whole super-tile list.  Round 5
-// (profiles/r5z_fwd_heavy_ab.txt): no split there took cfg2c render_fwd 0.369 -> 0.359 ms, its
-// call 1.227 -> 1.217 ms, its throughput +2.3 %; cfg2 has no such tiles.  The test PLY scene's
-// few 86k-entry tiles (a dense centre, DESIGN §3 "Heavy tiles") still split
-#ifndef GSR_FWD_HEAVY_BITS
-#define GSR_FWD_HEAVY_BITS 16
-#endif
-#ifndef GSR_BWD_HEAVY_BITS
-#define GSR_BWD_HEAVY_BITS 13
-#endif
-constexpr int FWD_HEAVY_BITS = GSR_FWD_HEAVY_BITS;  // super-tile entries >= 65536
-constexpr int BWD_HEAVY_BITS = GSR_BWD_HEAVY_BITS;  // quadrant maxima of n_contrib summing to >= 8192 (one ~2048)
-// ... or a cost >= REL8 / 8 x the band's mean tile cost (gsr_order.hpp; 0 = off).  Off: on the
-// clustered cfg2c frame splitting the tiles above 2x / 3x the band mean (64-256 per band) made
-// both tile passes slower (render_bwd 494 -> 535 / 592 us at 2x with 64 / 128 per band, 497 at
-// 3x with 256; render_fwd 400 -> 399 / 421 / 464 us): a quadrant unit redoes the list filter,
-// the culling and (backward) the per-survivor reduction (profiles/r5e_heavy_split_ab.txt)
-#ifndef GSR_FWD_HEAVY_REL8
-#define GSR_FWD_HEAVY_REL8 0
-#endif
-#ifndef GSR_BWD_HEAVY_REL8
-#define GSR_BWD_HEAVY_REL8 0
-#endif
+// Heavy tiles (split into four quadrant units, gsr_tile.hpp tile_unit): the forward splits a
+// tile from 2^16 super-tile entries (round 4: 2^14): at cfg2c, whose heaviest super-tiles hold
+// 30-45k entries in hundreds of similar tiles, the whole heavy tiles beyond the split cap ran as
+// long as the split ones anyway, and a split tile stores no survivor list, so its backward
+// re-filtered the whole super-tile list.  Round 5 (profiles/r5z_fwd_heavy_ab.txt): no split there
+// took cfg2c render_fwd 0.369 -> 0.359 ms, its call 1.227 -> 1.217 ms, its throughput +2.3 %;
+// cfg2 has no such tiles.  The test PLY scene's few 86k-entry tiles (a dense centre, DESIGN §3
+// "Heavy tiles") still split.  Thresholds relative to the band's mean cost measured slower on
+// cfg2c (profiles/r5e_heavy_split_ab.txt): a quadrant unit redoes the list filter, the culling
+// and (backward) the per-survivor reduction.
+constexpr int FWD_HEAVY_BITS = 16;  // super-tile entries >= 65536
+constexpr int BWD_HEAVY_BITS = 13;  // (survivor, quadrant) evaluations >= 8192
 
 // ---- render (gsr_render_fwd.hip / gsr_render_bwd.hip) --------------------------------
 // The tile passes read each tile's list from its super-tile's entries (TileList):
@@ -252,7 +221,7 @@ struct RenderFwdArgs {
     const uint32_t* nheavy;
     uint32_t* tile_nmax;  // out: per tile, the largest n_contrib (the backward's cost; atomicMax, zeroed)
     uint32_t* tile_emax;  // out: per tile, 1 + the entry index of that last contributor (where the backward starts)
-    uint32_t* tile_cost;  // out (when non-null): per tile, the sum of its quadrants' largest n_contrib (atomicAdd, zeroed)
+    uint32_t* tile_cost;  // out (when non-null): per tile, its (survivor, quadrant) evaluations (atomicAdd, zeroed)
     uint32_t* row_cost;   // out (when non-null): the same summed per tile row (the backward's balanced bands)
     // when non-null: zero_n4 float4s the backward needs zeroed (the gradient accumulator lines),
     // cleared by the pass's workgroups a slice each (zero_slice): VALU-bound waves have the HBM
@@ -265,16 +234,6 @@ struct RenderFwdArgs {
     // instead of re-filtering the super-tile list
     uint2* surv;
     uint32_t* surv_n;
-    // when non-null (GSR_QLIST): quadrant units' lists, SURV_CAP slots per (slot, quadrant), and
-    // their counts [QL_SLOTS][4] (SURV_NONE past SURV_CAP)
-    uint2* qsurv;
-    uint32_t* qsurv_n;
-    // GSR_CK_SURV: the chunk checkpoints (per tile: CK_MAX x [T, C0, C1, C2] rows of 64 float4, the
-    // boundaries' survivor counts, their number) and the final colours ([C0, C1, C2] rows)
-    float4* ck_state;
-    uint32_t* ck_pos;
-    uint32_t* ck_n;
-    float4* cfin;
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -303,16 +262,6 @@ struct RenderBwdArgs {
     // all tiles when null) filter their super-tile list
     const uint2* surv;
     const uint32_t* surv_n;
-    const uint2* qsurv;  // the forward's quadrant lists (RenderFwdArgs::qsurv)
-    const uint32_t* qsurv_n;
-    // the forward's chunk checkpoints (RenderFwdArgs::ck_state ...) and the expanded unit order
-    // (k_tile_order: per band, entries tile | code << 24 from band start x UNITS_MAX; counts at
-    // nheavy[24 + band]); units null: tile_unit's order
-    const float4* ck_state;
-    const uint32_t* ck_pos;
-    const uint32_t* ck_n;
-    const float4* cfin;
-    const uint32_t* units;
 };
 constexpr int DET_ROW3 = 12;  // 8 sums + the ninth's four row partials
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
@@ -335,7 +284,7 @@ struct RenderMcArgs {
     float* final_T;      // forward: written when non-null
     uint32_t* n_contrib;
     uint32_t* tile_nmax;  // forward: atomicMax when non-null
-    uint32_t* tile_cost;  // forward: atomicAdd of the quadrants' largest n_contrib when non-null
+    uint32_t* tile_cost;  // forward: atomicAdd of its (survivor, quadrant) evaluations when non-null
     uint32_t* row_cost;   // forward: the same per tile row when non-null
     const uint32_t* order;
     const uint32_t* nheavy;

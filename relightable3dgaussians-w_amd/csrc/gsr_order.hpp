@@ -20,16 +20,10 @@ __device__ __forceinline__ uint32_t tile_cost(unsigned t, const TileOrderArgs& a
     return a.ranges ? a.ranges[t].y - a.ranges[t].x : 0u;
 }
 
-// Cost bucket: the bit length of c and its next two bits (4 buckets per octave), 0 for c = 0.
-#ifdef GSR_COARSE_BUCKETS
-constexpr int NBUCKET = 33;
-__device__ __forceinline__ int cost_bucket(uint32_t c) { return c ? 32 - __clz(c) : 0; }
-__device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return heavy_bits + 1; }
-#else
-#ifndef GSR_BUCKET_BITS
-#define GSR_BUCKET_BITS 3
-#endif
-constexpr int BUCKET_FRAC = GSR_BUCKET_BITS;  // 2^BUCKET_FRAC buckets per octave
+// Cost bucket: the bit length of c and its next three bits (8 buckets per octave), 0 for c = 0.
+// (One bucket per octave took the backward tile pass to 0.40 ms at cfg2, eight 0.38 ms; four and
+// sixteen measured the same as eight.)
+constexpr int BUCKET_FRAC = 3;  // 2^BUCKET_FRAC buckets per octave
 constexpr int NBUCKET = 33 << BUCKET_FRAC;
 __device__ __forceinline__ int cost_bucket(uint32_t c) {
     if (!c) return 0;
@@ -39,7 +33,6 @@ __device__ __forceinline__ int cost_bucket(uint32_t c) {
     return (L << BUCKET_FRAC) + (int)f;
 }
 __device__ __forceinline__ int bucket_heavy_from(int heavy_bits) { return (heavy_bits + 1) << BUCKET_FRAC; }
-#endif
 
 // One band's order (any block size): order[lo .. lo+len) = the band's tiles, cost buckets
 // descending; nheavy[band] = how many lead the order with a cost >= 2^heavy_bits (split 4
@@ -87,7 +80,7 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     }
     // the per-tile floor, rounded up so that total <= 2 ntile add: a band's tiles then number at
     // most 3 ntile / 8 + 2 (tile_pass_blocks_bal)
-    const unsigned long long add = (total + GSR_BAL_FLOOR_DIV * a.ntile - 1) / (GSR_BAL_FLOOR_DIV * a.ntile);
+    const unsigned long long add = (total + BAL_FLOOR_DIV * a.ntile - 1) / (BAL_FLOOR_DIV * a.ntile);
     const unsigned long long tp = total + add * a.ntile;
     const unsigned long long tgt[2] = {band * tp / 8, (band + 1) * tp / 8};
     const bool need[2] = {band > 0, band < 7};
@@ -125,35 +118,6 @@ __device__ __forceinline__ void balanced_band(unsigned band, const TileOrderArgs
     len = (s_bound[1] == 0xffffffffu ? a.ntile : s_bound[1]) - lo;
 }
 
-// The backward's units of a band in its order: a tile with a survivor list runs as one unit per
-// chunk (codes 0..ck_n), a heavy tile without one (the first nheavy[band] of the order) as four
-// quadrant units, any other as one whole-tile unit.  512-thread workgroups (k_tile_order).
-__device__ __noinline__ void expand_units(unsigned band, unsigned lo, unsigned len, const TileOrderArgs& a) {
-    __shared__ uint32_t s_scan[8];
-    __syncthreads();  // this workgroup's order entries are written
-    const uint32_t nh = a.nheavy[band];
-    uint32_t* const out = a.units + (size_t)lo * UNITS_MAX;
-    uint32_t run = 0;
-    for (unsigned i0 = 0; i0 < len; i0 += blockDim.x) {
-        const unsigned i = i0 + threadIdx.x;
-        uint32_t t = 0, nu = 0;
-        bool lst = false;
-        if (i < len) {
-            t = a.order[lo + i];
-            lst = a.surv_n[t] != SURV_NONE;
-            nu = lst ? 1u + (a.ck_n ? a.ck_n[t] : 0u) : (i < nh ? 4u : 1u);
-        }
-        uint32_t tot;
-        const uint32_t off = run + block_exclusive_scan<8>(nu, s_scan, &tot);
-        for (uint32_t j = 0; j < nu; j++) {
-            const uint32_t code = lst ? j : (nu == 4u ? UNIT_QUAD + j : UNIT_WHOLE);
-            out[off + j] = t | (code << 24);
-        }
-        run += tot;
-    }
-    if (threadIdx.x == 0) a.nheavy[24 + band] = run;
-}
-
 // BAL: the band is cost-balanced (balanced_band; a template argument, so that the binning
 // scatter's order workgroups carry none of its LDS)
 template <bool BAL = false>
@@ -189,8 +153,6 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
             if (a.zero_c) a.zero_c[t] = 0u;
         }
         if (a.unset) a.unset[t] = SURV_NONE;
-        if constexpr (CK_SURV != 0)
-            if (a.zero_d) a.zero_d[t] = 0u;
     }
     if (csum) atomicAdd(&s_band_cost, csum);
     __syncthreads();
@@ -215,30 +177,17 @@ __device__ __forceinline__ void tile_order_band(unsigned band, const TileOrderAr
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        // heavy: cost >= 2^heavy_bits, or >= heavy_rel8 / 8 x the band's mean tile cost (a
-        // clustered frame's heavy tiles measured against the frame, not an absolute list length)
-        int hb = bucket_heavy_from(a.heavy_bits);
-        if (a.heavy_rel8 && len) {
-            const unsigned long long thr = (s_band_cost * a.heavy_rel8 + 8ull * len - 1) / (8ull * len);
-            const int hr = cost_bucket((uint32_t)min(thr, 0xffffffffull));
-            hb = hr > 0 && hr < hb ? hr : hb;
-        }
+        // heavy: cost >= 2^heavy_bits
+        const int hb = bucket_heavy_from(a.heavy_bits);
         a.nheavy[band] = hb < NBUCKET ? cur[hb] + hist[hb] : 0u;
-        // the band's estimated cost (the forward's rotated bands: tile_unit); the slot holds
-        // the unit count instead when the order expands units
-        if (!a.units) a.nheavy[24 + band] = (uint32_t)min(s_band_cost, 0xffffffffull);
+        // the band's estimated cost (the rotated bands: tile_unit)
+        a.nheavy[24 + band] = (uint32_t)min(s_band_cost, 0xffffffffull);
     }
     __syncthreads();
     for (unsigned i = threadIdx.x; i < len; i += blockDim.x) {
         const unsigned t = lo + i;
-#ifdef GSR_NATURAL_ORDER
-        a.order[lo + i] = t;
-#else
         a.order[lo + atomicAdd(&cur[cost_bucket(tile_cost(t, a))], 1u)] = t;
-#endif
     }
-    if constexpr (CK_SURV != 0)  // (compiled out otherwise: its call cost the binning scatter 18 us)
-        if (a.units) expand_units(band, lo, len, a);
 }
 
 }  // namespace gsr

@@ -212,16 +212,10 @@ __global__ void __launch_bounds__(256) k_preprocess(PreprocessArgs a) {
     preprocess_block_out(a, tiles, stc, err);
 }
 
-// GSR_PRE_WAVE_SH: the wave-staged SH rows (k_preprocess_wavesh) for M = 16, with GSR_PRE_SH_NT
-// its loads non-temporal.  Off by default: its single call is faster (preprocess 0.107 ->
-// 0.094 ms at cfg2), but its 53 KB of LDS per workgroup starves the overlapping views' kernels
-// and the default 3-stream bench drops 3 % (profiles/r4zj_ab_preprocess_default_bench.txt)
-#ifndef GSR_PRE_WAVE_SH
-#define GSR_PRE_WAVE_SH 0
-#endif
-#ifndef GSR_PRE_SH_NT
-#define GSR_PRE_SH_NT 1
-#endif
+// (Round 4 also measured the SH rows staged per wave through LDS with coalesced 16-B loads: its
+// single call was faster -- preprocess 0.107 -> 0.094 ms at cfg2 -- but its 53 KB of LDS per
+// workgroup starved the overlapping views' kernels and the default 3-stream bench dropped 3 %,
+// profiles/r4zj_ab_preprocess_default_bench.txt.)
 // SH path with M in {1, 4, 9, 16}: each thread loads its own SH row into registers with
 // the other inputs (16-B loads when 3M is a multiple of 4) -- no LDS, so occupancy is
 // bounded by registers only (16 coefficients: 102 vs 130 us at cfg2 against the
@@ -246,125 +240,6 @@ __global__ void __launch_bounds__(256) k_preprocess_regsh(PreprocessArgs a) {
         } else {
 #pragma unroll
             for (int k = 0; k < 3 * M; k++) shr[k] = a.shs[(size_t)idx * 3 * M + k];
-        }
-    }
-    uint32_t tiles = 0, stc = 0, key = 0;
-    bool err = false;
-    if (idx < a.P)
-        preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr, key, err);
-    preprocess_block_out(a, tiles, stc, err);
-}
-
-// SH path with 3M a multiple of 4 (M in {4, 16}): each wave loads its 64 Gaussians' SH rows
-// (contiguous, 64 * 3M floats) with coalesced 16-B loads -- every lane's 3M/4 loads in flight
-// at once, each instruction one contiguous 1 KiB -- into wave-private LDS rows padded to 3M + 4
-// floats (16-B aligned; the row reads below then hit distinct banks), and each lane reads its
-// own row back.  The register-row kernel's per-lane 16-B loads touch 64 scattered lines per
-// instruction.  No barrier: the rows are wave-private.
-template <int M>
-__global__ void __launch_bounds__(256) k_preprocess_wavesh(PreprocessArgs a) {
-    static_assert((3 * M) % 4 == 0, "16-B rows");
-    constexpr int F4 = 3 * M / 4, RS4 = F4 + 1;  // float4s per row, per padded LDS row
-    __shared__ float4 s_rows[4][64 * RS4];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    const long long g0 = (long long)blockIdx.x * blockDim.x + wave * 64;  // the wave's first Gaussian
-    const int nf = (int)(a.P - g0 < 64 ? (a.P - g0 > 0 ? a.P - g0 : 0) : 64) * F4;
-    GaussIn gin;
-    if (idx < a.P) load_gauss(a, idx, gin);
-    {
-        const float4* src = reinterpret_cast<const float4*>(a.shs) + g0 * F4;
-        float4 v[F4];
-#pragma unroll
-        for (int j = 0; j < F4; j++) {
-            const int f = j * 64 + lane;
-#if GSR_PRE_SH_NT  // non-temporal: the rows are read once per call (the backward reads the Jacobian)
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            if (f < nf) {
-                const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + f));
-                v[j] = make_float4(t.x, t.y, t.z, t.w);
-            } else {
-                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-#else
-            v[j] = f < nf ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
-#endif
-        }
-        float4* rows = s_rows[wave];
-#pragma unroll
-        for (int j = 0; j < F4; j++) {
-            const int f = j * 64 + lane, r = f / F4;
-            rows[r * RS4 + (f - r * F4)] = v[j];
-        }
-    }
-    wave_lds_fence();
-    float shr[3 * M];
-#pragma unroll
-    for (int k = 0; k < F4; k++) {
-        const float4 t = s_rows[wave][lane * RS4 + k];
-        shr[4 * k] = t.x;
-        shr[4 * k + 1] = t.y;
-        shr[4 * k + 2] = t.z;
-        shr[4 * k + 3] = t.w;
-    }
-    uint32_t tiles = 0, stc = 0, key = 0;
-    bool err = false;
-    if (idx < a.P)
-        preprocess_one<(M >= 16 ? 3 : M >= 9 ? 2 : M >= 4 ? 1 : 0)>(a, idx, gin, tiles, stc, shr, key, err);
-    preprocess_block_out(a, tiles, stc, err);
-}
-
-// The same staged in two half-wave rounds of 32 rows (half the LDS: 26.6 KB per workgroup),
-// GSR_PRE_WAVE_SH == 2: each round's 32 rows are 6 KiB contiguous (6 coalesced 16-B loads per
-// lane), and the lanes of that half read their rows.
-template <int M>
-__global__ void __launch_bounds__(256) k_preprocess_halfsh(PreprocessArgs a) {
-    static_assert((3 * M) % 4 == 0 && (3 * M / 4 * 32) % 64 == 0, "16-B rows, whole loads per round");
-    constexpr int F4 = 3 * M / 4, RS4 = F4 + 1, NJ = F4 * 32 / 64;
-    __shared__ float4 s_rows[4][32 * RS4];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-    GaussIn gin;
-    if (idx < a.P) load_gauss(a, idx, gin);
-    float shr[3 * M];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-        const long long g0 = (long long)blockIdx.x * blockDim.x + wave * 64 + 32 * h;
-        const int nf = (int)(a.P - g0 < 32 ? (a.P - g0 > 0 ? a.P - g0 : 0) : 32) * F4;
-        const float4* src = reinterpret_cast<const float4*>(a.shs) + g0 * F4;
-        float4 v[NJ];
-#pragma unroll
-        for (int j = 0; j < NJ; j++) {
-            const int f = j * 64 + lane;
-            typedef float f4v __attribute__((ext_vector_type(4)));
-            if (f < nf) {
-#if GSR_PRE_SH_NT
-                const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(src + f));
-#else
-                const f4v t = *reinterpret_cast<const f4v*>(src + f);
-#endif
-                v[j] = make_float4(t.x, t.y, t.z, t.w);
-            } else {
-                v[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
-        }
-        wave_lds_fence();  // the previous round's row reads are done
-        float4* rows = s_rows[wave];
-#pragma unroll
-        for (int j = 0; j < NJ; j++) {
-            const int f = j * 64 + lane, r = f / F4;
-            rows[r * RS4 + (f - r * F4)] = v[j];
-        }
-        wave_lds_fence();
-        if ((lane >> 5) == h) {
-#pragma unroll
-            for (int k = 0; k < F4; k++) {
-                const float4 t = rows[(lane & 31) * RS4 + k];
-                shr[4 * k] = t.x;
-                shr[4 * k + 1] = t.y;
-                shr[4 * k + 2] = t.z;
-                shr[4 * k + 3] = t.w;
-            }
         }
     }
     uint32_t tiles = 0, stc = 0, key = 0;
@@ -416,8 +291,6 @@ void launch_preprocess(const PreprocessArgs& a, hipStream_t s) {
             case 4: if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<4>, grid, blk, 0, s, a); return; } break;
             case 9: hipLaunchKernelGGL(k_preprocess_regsh<9>, grid, blk, 0, s, a); return;
             case 16:
-                if (al16 && GSR_PRE_WAVE_SH == 2) { hipLaunchKernelGGL(k_preprocess_halfsh<16>, grid, blk, 0, s, a); return; }
-                if (al16 && GSR_PRE_WAVE_SH) { hipLaunchKernelGGL(k_preprocess_wavesh<16>, grid, blk, 0, s, a); return; }
                 if (al16) { hipLaunchKernelGGL(k_preprocess_regsh<16>, grid, blk, 0, s, a); return; }
                 break;
             default: break;

@@ -31,18 +31,11 @@ struct BwdIn {
 };
 
 // The accumulator lines and the Jacobian rows are read for the last time here: non-temporal
-// loads (GSR_PREBWD_NT=1) were measured neutral at cfg2 and slower at cfg5 (+20 us a call,
-// profiles/r4zi_ab_prebwd_nt.txt): off.
-#ifndef GSR_PREBWD_NT
-#define GSR_PREBWD_NT 0
-#endif
+// loads were measured neutral at cfg2 and slower at cfg5 (+20 us a call,
+// profiles/r4zi_ab_prebwd_nt.txt), so these are plain loads.
 template <typename T>
 __device__ __forceinline__ T last_load(const T* p) {
-#if GSR_PREBWD_NT
-    return __builtin_nontemporal_load(p);
-#else
     return *p;
-#endif
 }
 __device__ __forceinline__ float4 last_load4(const float* p) {
     typedef float f4v __attribute__((ext_vector_type(4)));

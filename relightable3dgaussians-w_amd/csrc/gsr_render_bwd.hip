@@ -20,10 +20,6 @@
 #include "gsr_tile.hpp"
 
 
-#ifndef GSR_BWD_QPAIR
-#define GSR_BWD_QPAIR 0
-#endif
-
 namespace gsr {
 
 #ifdef GSR_RENDER_STATS
@@ -39,11 +35,8 @@ __device__ unsigned long long g_bwd_times[GSR_UNIT_REC * 65536];
 #define BWD_STAT(k, v)
 #endif
 
-// BG: the background is not all zero (its dL/dalpha term is carried); with a zero background
-// (render()'s default, the bench) the term and its per-evaluation multiply-add are dropped
-template <bool DET, bool BG = true>
-__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow,
-                                                const uint32_t chunk = 0) {
+template <bool DET>
+__device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -104,62 +97,10 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     // each lane's entry loaded a batch ahead (its record one batch ahead too measured the same
     // call and a slower 3-stream headline: 113 VGPRs); else the super-tile list, filtered and
     // culled again
-    uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
+    const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
     const uint2* sl = a.surv + (size_t)tile * SURV_CAP;
-    // the forward's quadrant lists (GSR_QLIST; not in deterministic mode: its partial rows take one
-    // write per survivor), merged: windows of 64 list positions, lane k holding position base - k,
-    // its Gaussian and the OR of the quadrant bits the four lists hold for it (an LDS table), so
-    // each survivor is evaluated over all its quadrants and reduced once, as from a whole list.
-    // qptr[q]: quadrant q's entries left (back to front), cv[q]: each lane's candidate entry of it
-    bool qwin = false;
-    uint32_t qbase = 0, qptr[4] = {0u, 0u, 0u, 0u};
-    __shared__ uint32_t s_wq[64], s_wid[64];
-    if (GSR_QLIST && !DET && a.qsurv && sn != SURV_NONE && (sn & SURV_QFLAG)) {
-        qbase = 4u * (sn & ~SURV_QFLAG);
-        bool ok = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            if (qlim[q]) {
-                qptr[q] = a.qsurv_n[qbase + q];
-                ok = ok && qptr[q] != SURV_NONE;
-            }
-        qwin = ok;
-        if (ok) {
-            s_wq[lane] = 0u;
-            wave_lds_sync();
-        }
-        sn = SURV_NONE;
-    } else if (sn & SURV_QFLAG) {
-        sn = SURV_NONE;
-    }
     const bool lst = sn != SURV_NONE;
     uint32_t li = lst ? sn : 0u;  // list entries left
-    if (CK_SURV && lst && a.ck_n) {
-        // chunk `chunk` of the list: survivors [ck_pos[chunk - 1], ck_pos[chunk]) (the last chunk up
-        // to sn), from the forward's checkpoint after its last survivor: T there, and the recurrence
-        // Sr = dL/dpix . (C_final - C_there) / T_there (the colour of everything behind, per unit T)
-        const uint32_t nck = a.ck_n[tile];
-        const uint32_t* cp = a.ck_pos + (size_t)tile * CK_MAX;
-        const uint32_t lo = chunk ? cp[chunk - 1] : 0u, hi = chunk < nck ? cp[chunk] : sn;
-        sl += lo;
-        li = hi - lo;
-        if (chunk < nck) {
-            const float4* ck = a.ck_state + ((size_t)tile * CK_MAX + chunk) * 256 + lane;
-            const float4* cf = a.cfin + (size_t)tile * 192 + lane;
-            const float4 kT = ck[0], k0 = ck[64], k1 = ck[128], k2 = ck[192];
-            const float4 f0 = cf[0], f1 = cf[64], f2 = cf[128];
-            const float tq[4] = {kT.x, kT.y, kT.z, kT.w};
-            const float d0[4] = {f0.x - k0.x, f0.y - k0.y, f0.z - k0.z, f0.w - k0.w};
-            const float d1[4] = {f1.x - k1.x, f1.y - k1.y, f1.z - k1.z, f1.w - k1.w};
-            const float d2[4] = {f2.x - k2.x, f2.y - k2.y, f2.z - k2.z, f2.w - k2.w};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool ok = wt.inside(q, a.W, a.H) && tq[q] > 0.f;
-                T[q] = ok ? tq[q] : 0.f;
-                Sr[q] = ok ? (dp0[q] * d0[q] + dp1[q] * d1[q] + dp2[q] * d2[q]) / tq[q] : 0.f;
-            }
-        }
-    }
     uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);
     TileList<false> tl;
     if (!lst)
@@ -167,46 +108,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;  // deterministic rows: the materialised list start
     for (;;) {
         uint32_t id = 0, nb, p, qm = 0;  // p: list position (back to front)
-        if (GSR_QLIST && qwin) {
-            // the window below the highest position any list still holds (each lane's candidate
-            // entries loaded here: prefetching them across the walk took 14 more VGPRs)
-            uint2 cv[4];
-            uint32_t base = 0;
-            bool more = false;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                cv[q] = qptr[q] ? a.qsurv[(size_t)(qbase + q) * SURV_CAP + max((int)qptr[q] - 1 - lane, 0)] : make_uint2(0u, 0u);
-            }
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (qptr[q]) {
-                    base = max(base, (uint32_t)__builtin_amdgcn_readfirstlane((int)cv[q].y) >> 4);
-                    more = true;
-                }
-            if (!more) break;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (!qptr[q]) continue;  // wave-uniform
-                const uint2 c = cv[q];
-                const uint32_t cp = c.y >> 4;
-                const bool in = (int)qptr[q] - 1 - lane >= 0 && cp + 64u > base;  // (entries are a prefix of lanes)
-                const uint32_t n = (uint32_t)__popcll(__ballot(in));
-                if (in) {
-                    atomicOr(&s_wq[base - cp], 1u << q);
-                    s_wid[base - cp] = c.x;
-                }
-                qptr[q] -= n;
-            }
-            wave_lds_sync();
-            const uint32_t wq = s_wq[lane];
-            id = wq ? s_wid[lane] : 0u;
-            s_wq[lane] = 0u;  // (this lane's slot: read above; the next window writes after two syncs)
-            p = base - (uint32_t)lane;
-            nb = base + 1u < 64u ? base + 1u : 64u;
-#pragma unroll
-            for (int q = 0; q < 4; q++)
-                if (p < qlim[q]) qm |= wq & (1u << q);
-        } else if (lst) {
+        if (lst) {
             nb = min(64u, li);
             if (nb == 0) break;
             const uint2 v = nv;
@@ -230,7 +132,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         float rc = 0.f;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            if (!lst && !qwin) qm = wt.reach(r, p, qlim);
+            if (!lst) qm = wt.reach(r, p, qlim);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
@@ -287,7 +189,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 const float dch = ae * Tn;
                 const float cdp = __builtin_fmaf(c2, dp2[q], __builtin_fmaf(c1, dp1[q], c0 * dp0[q]));
                 const float dcs = cdp - Sr[q];
-                const float dLda = BG ? __builtin_fmaf(Tn, dcs, inv * Tb[q]) : Tn * dcs;
+                const float dLda = __builtin_fmaf(Tn, dcs, inv * Tb[q]);
                 Sr[q] = __builtin_fmaf(ae, dcs, Sr[q]);
                 const float Gd = Ge * dLda;
                 S5 += Gd;
@@ -302,34 +204,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 S8 = __builtin_fmaf(dch, dp2[q], S8);
                 T[q] = Tn;
             };
-#if GSR_BWD_QPAIR
-            // GSR_BWD_QPAIR: both quadrants of a row reached -> one straight-line block, so the
-            // two independent chains (exponent, blend test, recurrence) interleave; the sums are
-            // still added quadrant by quadrant, in order
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int q0 = 2 * h, q1 = 2 * h + 1;
-                const uint32_t pm = (m >> q0) & 3u;
-                if (pm == 3u) {
-                    float dx0, dy0, G0, a0, dx1, dy1, G1, a1;
-                    lmask k0, k1;
-                    pre(q0, dx0, dy0, G0, a0, k0);
-                    pre(q1, dx1, dy1, G1, a1, k1);
-                    if ((k0 | k1) == 0ull) continue;
-                    any = true;
-                    post(q0, dx0, dy0, G0, a0, k0);
-                    post(q1, dx1, dy1, G1, a1, k1);
-                } else if (pm) {
-                    const int q = pm == 1u ? q0 : q1;
-                    float dx, dy, G, al;
-                    lmask k;
-                    pre(q, dx, dy, G, al, k);
-                    if (k == 0ull) continue;
-                    any = true;
-                    post(q, dx, dy, G, al, k);
-                }
-            }
-#else
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
@@ -340,7 +214,6 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 any = true;
                 post(q, dx, dy, G, al, k);
             }
-#endif
             if (any) {
             BWD_STAT(5, 1);
             // raw sums (the line's layout, acc_raw): M1, M2 -- dL/dmean2D is -(a M1 + b M2),
@@ -359,11 +232,7 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
             if (DET) {  // one row per instance, summed per Gaussian in tile order (k_det_gather)
                 if (vidx >= 0 && v != 0.f) a.partial[(size_t)(rbase + pos) * DET_ROW3 + pslot] = v;
             } else if (vidx >= 0 && v != 0.f) {
-#ifdef GSR_DIAG_NOATOMIC  // timing diagnostic only (wrong gradients): plain stores to a private line
-                if (v == 1234.5f) a.acc[(size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx] = v;
-#else
                 atomicAdd(a.acc + (size_t)__float_as_uint(Cq.z) * ACC_STRIDE + vidx, v);
-#endif
             }
             }
         };
@@ -414,44 +283,14 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 // 3 HIP streams, this pass overlapping other views' forward and geometry kernels -- four leave
 // them room: the headline +0.9 % at cfg2 and +1.3 % at cfg5, the isolated call pair +7 / +22 us
 // (profiles/r4zo_ab_bwd_waves_default_bench.txt).
-#ifndef GSR_BWD_WAVES
-#define GSR_BWD_WAVES 4
-#endif
-#ifndef GSR_BWD_BG_SPEC
-#define GSR_BWD_BG_SPEC 0
-#endif
+constexpr int BWD_WAVES = 4;
 template <bool DET>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD_WAVES, GSR_BWD_WAVES)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(BWD_WAVES, BWD_WAVES)))
 k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
-    uint32_t qallow, chunk = 0;
-    if (CK_SURV && a.units) {
-        // the expanded order (expand_units): chunk / quadrant / whole-tile units; the grid is the
-        // tile order's, so a band with more units than the grid's share loops (grid stride)
-        const unsigned band = blockIdx.x & 7u, stride = gridDim.x >> 3;
-        const uint32_t nu = a.nheavy[24 + band];
-        unsigned lo = a.nheavy[8 + band], len;
-        if (!GSR_BAL_BANDS) band_of(band, a.grid_x * a.grid_y, lo, len);
-        for (unsigned u = blockIdx.x >> 3; u < nu; u += stride) {
-            const uint32_t e = a.units[(size_t)lo * UNITS_MAX + u];
-            tile = e & 0xffffffu;
-            const uint32_t code = e >> 24;
-            qallow = (code & UNIT_QUAD) == UNIT_QUAD && code != UNIT_WHOLE ? 1u << (code & 3u) : 15u;
-            chunk = code < UNIT_QUAD ? code : 0u;
-            render_bwd_tile<DET>(a, tile, qallow, chunk);
-        }
-        return;
-    }
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS,
-                   DET ? 0u : GSR_BWD_ROT_THR8, nullptr, BWD_ROT_COST, GSR_BWD_ROT_SHIFT))
-        return;  // det: one writer per row
-#if GSR_BWD_BG_SPEC
-    // a zero background (wave-uniform scalar loads) takes the walk without its dL/dalpha term
-    if (a.bg[0] == 0.f && a.bg[1] == 0.f && a.bg[2] == 0.f) render_bwd_tile<DET, false>(a, tile, qallow, chunk);
-    else render_bwd_tile<DET, true>(a, tile, qallow, chunk);
-#else
-    render_bwd_tile<DET>(a, tile, qallow, chunk);
-#endif
+    uint32_t qallow;
+    if (!tile_unit_bwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET)) return;
+    render_bwd_tile<DET>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -478,7 +317,7 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    const dim3 grid(tile_pass_blocks_bal(ntile, 0u));
     if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
 }

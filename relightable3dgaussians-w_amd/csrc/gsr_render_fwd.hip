@@ -17,24 +17,8 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
-// 1: the survivor list holds only the survivors that blended in some quadrant (the others
-// contribute nothing in the backward)
-#ifndef GSR_SURV_BLENDED
-#define GSR_SURV_BLENDED 0
-#endif
-// 1: the forward finds its latest blend per batch from last[] (a wave max) instead of tracking
-// which survivors blended
-#ifndef GSR_FWD_LASTMAX
-#define GSR_FWD_LASTMAX 0
-#endif
-// 1 (default): a quadrant unit culls its batch against its own quadrant only (its survivors are
-// never stored): k_render_fwd 238.1 -> 236.9 us, headline / cfg2c / train +0.5-1 % (profiles/r5z_reach_own_ab.txt)
-#ifndef GSR_FWD_REACH_OWN
-#define GSR_FWD_REACH_OWN 1
-#endif
-#ifndef GSR_FWD_WAVES
-#define GSR_FWD_WAVES 6
-#endif
+// six waves per SIMD
+constexpr int FWD_WAVES = 6;
 
 namespace gsr {
 
@@ -51,8 +35,7 @@ __device__ unsigned long long g_fwd_times[GSR_UNIT_REC * 65536];
 #define FWD_STAT(k, v)
 #endif
 
-__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow,
-                                                const uint32_t qslot = SURV_NONE) {
+__device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
     const int lane = threadIdx.x;
@@ -86,13 +69,13 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
 #endif
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere (wave-uniform)
     // survivors stored so far (whole-tile units; SURV_NONE: none stored, or past SURV_CAP)
-    // (a quadrant unit of a tile with a long super-tile list: its own quadrant's list, GSR_QLIST)
-    const bool ql = GSR_QLIST && a.qsurv && qslot != SURV_NONE && str.y - str.x >= GSR_QL_MIN;
-    const uint32_t qcode = ql ? 4u * qslot + (uint32_t)__builtin_ctz(qallow) : 0u;
-    uint32_t scnt = ((a.surv && qallow == 15u) || ql) ? 0u : SURV_NONE;
-    uint2* const sl = ql ? a.qsurv + (size_t)qcode * SURV_CAP : a.surv + (size_t)tile * SURV_CAP;
-    uint32_t nck = 0, ck_last = 0;  // chunk checkpoints stored, the survivor count at the last one
-    uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
+    uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
+    uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
+    // (survivor, quadrant) evaluations: the backward's cost estimate (its dispatch order, heaviest
+    // first, and its balanced bands).  Round 5 (profiles/r5z_eval_cost_ab.txt): against the sum of
+    // the quadrants' largest n_contrib, cfg2c render_bwd 0.465 -> 0.429 ms (its bands balance by the
+    // work the backward repeats, not by list positions), cfg2 and training unchanged
+    uint32_t nev = 0;
     while (live) {
         tl.fill(s_list);
         uint32_t id = 0, ei = 0, p0 = 0;
@@ -104,7 +87,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         float rc = 0.f;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, j, nullptr, GSR_FWD_REACH_OWN ? qallow : 15u);  // (a quadrant unit tests its own only)
+            // a quadrant unit culls its batch against its own quadrant only (k_render_fwd 238.1 ->
+            // 236.9 us, profiles/r5z_reach_own_ab.txt)
+            qm = wt.reach(r, j, nullptr, qallow);
             // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
@@ -120,7 +105,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         s_e[lane] = ei;
         wave_lds_sync();
         const uint64_t todo0 = __ballot((qm & live) != 0);
-        if (!GSR_SURV_BLENDED && scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
+        if (scnt != SURV_NONE) {  // the backward's list: (Gaussian, position << 4 | reach mask)
             const uint32_t n = (uint32_t)__popcll(todo0);
             if (scnt + n > SURV_CAP) {
                 scnt = SURV_NONE;
@@ -138,8 +123,6 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         if (!todo0) continue;
         // blend one survivor (record A, B, Cq at batch slot k) into the four quadrants
         int klast = -1;  // batch slot of the latest survivor that blended anywhere
-        uint64_t bmask = 0;  // batch slots of the survivors that blended anywhere (GSR_SURV_BLENDED)
-        uint32_t qbl = 0;    // GSR_SURV_BLENDED 2: lane k = the quadrants batch slot k blended in
         uint64_t todo = todo0;
         auto blend_one = [&](const float4& A, const float4& B, const float4& Cq, int k) __attribute__((always_inline)) {
             const uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)__float_as_uint(Cq.y)) & live;
@@ -149,7 +132,6 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             uint32_t pos1;
             asm("v_mov_b32 %0, %1" : "=v"(pos1) : "s"(p0 + (uint32_t)k + 1u));
             lmask blended = 0;
-            uint32_t qb = 0;
             FWD_STAT(5, m == 15u);
             FWD_STAT(6, m != 0u);
 #pragma unroll
@@ -174,8 +156,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 C2[q] += Cq.x * w;
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
-                if (!GSR_FWD_LASTMAX || GSR_SURV_BLENDED) blended |= blend;
-                if (GSR_SURV_BLENDED == 2 && blend) qb |= 1u << q;
+                blended |= blend;
                 if (sat) {  // rare: pixels finish
                     lim[q] = sel(sat, __builtin_inff(), lim[q]);
                     if (!(m_lt(lim[q], 1.f) & exec_mask())) {
@@ -184,15 +165,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                     }
                 }
             }
-            if ((!GSR_FWD_LASTMAX || GSR_SURV_BLENDED) && blended) {
-                klast = k;
-                if (GSR_SURV_BLENDED) bmask |= 1ull << k;
-                if (GSR_SURV_BLENDED == 2) {
-                    uint32_t v;
-                    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(qb));
-                    qbl = sel((lmask)1ull << k, v, qbl);
-                }
-            }
+            if (blended) klast = k;
         };
         // survivors in pairs over two register sets (the next survivor's record is read
         // while the current one blends, and no register copies between them); the walk's
@@ -216,53 +189,7 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             blend_one(An, Bn, Cn, kn);
             if (k < 0) break;
         }
-        if (GSR_FWD_LASTMAX) {
-            // the latest blend so far (the tile's largest n_contrib): if it lies in this batch, its
-            // entry is the backward's start (a wave max per batch instead of a mask OR per
-            // evaluation and a test per survivor: SALU issue is as scarce as VALU here)
-            const uint32_t mx = wave_max_u32(max(max(last[0], last[1]), max(last[2], last[3])));
-            if (mx > p0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[mx - 1u - p0]);
-        } else if (klast >= 0) {
-            elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
-        }
-        if (GSR_SURV_BLENDED && scnt != SURV_NONE) {  // only the survivors that blended somewhere
-            const uint32_t n = (uint32_t)__popcll(bmask);
-            if (scnt + n > SURV_CAP) {
-                scnt = SURV_NONE;
-            } else {
-                if ((bmask >> lane) & 1u) {
-                    const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(bmask >> 32),
-                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bmask, 0u));
-                    const float4 c = s_c[lane];
-                    sl[scnt + r] = make_uint2(__float_as_uint(c.z), (j << 4) | (GSR_SURV_BLENDED == 2 ? qbl : __float_as_uint(c.y)));
-                }
-                scnt += n;
-            }
-        }
-        if (CK_SURV && a.ck_state && scnt != SURV_NONE && nck < CK_MAX && scnt - ck_last >= CK_SURV) {
-            // the state after this batch: the backward's chunk of the survivors before scnt starts here
-            float4* ck = a.ck_state + ((size_t)tile * CK_MAX + nck) * 256 + lane;
-            ck[0] = make_float4(T[0], T[1], T[2], T[3]);
-            ck[64] = make_float4(C0[0], C0[1], C0[2], C0[3]);
-            ck[128] = make_float4(C1[0], C1[1], C1[2], C1[3]);
-            ck[192] = make_float4(C2[0], C2[1], C2[2], C2[3]);
-            if (lane == 0) a.ck_pos[(size_t)tile * CK_MAX + nck] = scnt;
-            nck++;
-            ck_last = scnt;
-        }
-    }
-    if (CK_SURV && a.ck_n && qallow == 15u) {
-        // (no checkpoints without ck_state: a re-coloured forward over a cached call's buffers,
-        // gsr_forward_reuse, whose colours differ from the checkpoints the buffers may hold)
-        if (scnt == SURV_NONE || !a.ck_state) nck = 0;
-        if (nck && ck_last == scnt) nck--;  // no survivors after the last checkpoint
-        if (nck) {  // the final colours (the chunks' recurrence starts from their difference)
-            float4* cf = a.cfin + (size_t)tile * 192 + lane;
-            cf[0] = make_float4(C0[0], C0[1], C0[2], C0[3]);
-            cf[64] = make_float4(C1[0], C1[1], C1[2], C1[3]);
-            cf[128] = make_float4(C2[0], C2[1], C2[2], C2[3]);
-        }
-        if (lane == 0) a.ck_n[tile] = nck;
+        if (klast >= 0) elast = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_e[klast]);
     }
 #ifdef GSR_RENDER_STATS
     if (lane == 0) {
@@ -293,43 +220,30 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
         }
     }
     if (lane == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
-    if (lane == 0 && ql) {
-        a.qsurv_n[qcode] = scnt;
-        a.surv_n[tile] = SURV_QFLAG | qslot;  // (the same word from all four quadrant units)
-    }
-    uint32_t nm = 0, nsum = 0;
+    uint32_t nm = 0;
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const uint32_t m = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nm = m > nm ? m : nm;
-        nsum += m;
     }
     if (lane == 0 && nm) {
         atomicMax(&a.tile_nmax[tile], nm);
         atomicMax(&a.tile_emax[tile], elast + 1u);
-        uint32_t cost = GSR_EVAL_COST ? nev : nsum;
-#ifdef GSR_NOLIST_SPLIT
-        // experiment: a unit without a survivor list whose backward re-filters at least
-        // GSR_NOLIST_SPLIT super-tile entries marks its tile heavy (the backward splits it)
-        if (scnt == SURV_NONE && elast + 1u - str.x >= (uint32_t)GSR_NOLIST_SPLIT)
-            cost += (1u << GSR_BWD_HEAVY_BITS) / (uint32_t)__popc(qallow);
-#endif
-        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], cost);
-        if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], cost);
+        if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nev);
+        if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], nev);
     }
 }
 
 
 // One wave per unit of the dispatch order (tile_unit): a quadrant of a heavy tile or a
 // whole tile.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES, GSR_FWD_WAVES)))
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(FWD_WAVES, FWD_WAVES)))
 k_render_fwd(RenderFwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    uint32_t qslot;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, GSR_ROT_THR8, &qslot)) return;
-    render_fwd_tile(a, tile, qallow, qslot);
+    if (!tile_unit_fwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_fwd_tile(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -356,8 +270,7 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    hipLaunchKernelGGL(k_render_fwd, dim3(GSR_FWD_BAL ? tile_pass_blocks_bal(ntile, FWD_TAIL_SPLIT) : tile_pass_blocks(ntile, FWD_TAIL_SPLIT)),
-                       dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_render_fwd, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

@@ -23,10 +23,6 @@
 #include "gsr_kernels.hpp"
 #include "gsr_tile.hpp"
 
-#ifndef GSR_FWD_REACH_OWN
-#define GSR_FWD_REACH_OWN 1
-#endif
-
 namespace gsr {
 
 // NCH: channels composited (<= 4 NC4; render()'s layout has 14, so its group skips the two
@@ -60,7 +56,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         if (((qallow >> q) & 1u) && __ballot(in)) live |= 1u << q;
     }
     uint32_t elast = 0;  // entry index of the latest Gaussian that blended anywhere
-    uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate (GSR_EVAL_COST)
+    uint32_t nev = 0;    // (survivor, quadrant) evaluations: the backward's cost estimate
     // the backward's survivor list (as gsr_render_fwd.hip): whole-tile units only
     uint32_t scnt = (a.surv && qallow == 15u) ? 0u : SURV_NONE;
     uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
@@ -77,7 +73,7 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         for (int g = 0; g < NC4; g++) f[g] = ra;
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
-            qm = wt.reach(r, j, nullptr, GSR_FWD_REACH_OWN ? qallow : 15u);
+            qm = wt.reach(r, j, nullptr, qallow);  // (a quadrant unit tests its own only)
             ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
             rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
@@ -168,18 +164,17 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         }
     }
     if (a.tile_nmax) {
-        uint32_t nm = 0, nsum = 0;
+        uint32_t nm = 0;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t mq = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
             nm = mq > nm ? mq : nm;
-            nsum += mq;
         }
         if (lane == 0 && nm) {
             atomicMax(&a.tile_nmax[tile], nm);
             atomicMax(&a.tile_emax[tile], elast + 1u);
-            if (a.tile_cost) atomicAdd(&a.tile_cost[tile], GSR_EVAL_COST ? nev : nsum);
-            if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], GSR_EVAL_COST ? nev : nsum);
+            if (a.tile_cost) atomicAdd(&a.tile_cost[tile], nev);
+            if (a.row_cost) atomicAdd(&a.row_cost[tile / a.grid_x], nev);
         }
     }
 }
@@ -193,20 +188,14 @@ struct McBwdLds {
     TileListLds list;
 };
 
-// The back-to-front walk of one tile over NL channels.  COMPACT: the channels are the tile's
-// live ones (lch[i], i < L; -1 past them), the others have dL/dout == 0 at every pixel of the
-// tile, so every term they would add -- to cdp, to their feature sums -- is exactly zero and
-// is skipped; dpl[q][i] holds dL/dout of channel lch[i].  Otherwise channel i is i (NL = NCH).
-template <int NC4, int NCH, int NL, bool COMPACT, bool DET>
+// The back-to-front walk of one tile over its NL = NCH channels.
+template <int NC4, int NCH, bool DET>
 __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigned tile, const WaveTile& wt,
                                             McBwdLds<NC4>& sm, float (&T)[4], const float (&Tb)[4],
-                                            const float (&dpl)[4][NL], const uint32_t (&last)[4],
-                                            const uint32_t (&qlim)[4], const uint32_t nmax, const int (&lch)[NL]) {
-#ifdef GSR_MC_DIAG_NOFEAT  // timing diagnostic only (wrong dL/dfeatures): no feature sums
-    constexpr int V = 6;
-#else
+                                            const float (&dpl)[4][NCH], const uint32_t (&last)[4],
+                                            const uint32_t (&qlim)[4], const uint32_t nmax) {
+    constexpr int NL = NCH;
     constexpr int V = 6 + NL;         // 6 geometric sums + the feature sums
-#endif
     constexpr int NP = (V + 1) / 2;   // after the permlane32 stage
     constexpr int NQ = (NP + 1) / 2;  // after the permlane16 stage: registers reduced by DPP rows
     constexpr int NL4 = (NL + 3) / 4;
@@ -224,13 +213,7 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     // Gaussian by the preprocess backward (acc_raw), as in gsr_render_bwd.hip
     const bool vop = vidx >= 0 && vidx <= 4;
     // the channel of this lane's feature sum
-    int fch = vidx - 6;
-    if constexpr (COMPACT) {
-        int c = -1;
-#pragma unroll
-        for (int i = 0; i < NL; i++) c = (vidx - 6 == i) ? lch[i] : c;
-        fch = vidx >= 6 ? c : -1;
-    }
+    const int fch = vidx - 6;
     const bool vfeat = vidx >= 6 && fch >= 0 && fch < a.nch;
 
     // back to front from the tile's last contributor (as gsr_render_bwd.hip)
@@ -238,7 +221,7 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     const unsigned st = ((tile / a.grid_x) >> sth) * a.gsx + (tile % a.grid_x) / GSR_ST_W;
     // the forward's survivor list when it stored one, else the super-tile list (as gsr_render_bwd.hip)
     const uint32_t sn = a.surv ? a.surv_n[tile] : SURV_NONE;
-    const bool lst = sn < SURV_QFLAG;  // (quadrant lists: the single-channel backward's only)
+    const bool lst = sn != SURV_NONE;
     uint32_t li = lst ? sn : 0u;
     const uint2* const sl = a.surv + (size_t)tile * SURV_CAP;
     uint2 nv = lst ? sl[max((int)li - 1 - lane, 0)] : make_uint2(0u, 0u);
@@ -286,17 +269,6 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
         sm.q[lane] = make_uint2((p << 4) | qm, id);
 #pragma unroll
         for (int g = 0; g < NC4; g++) sm.f[g][lane] = f[g];
-        if constexpr (COMPACT) {
-            // the record's live channels, in order, back into its first NL4 rows (each lane
-            // rewrites only its own column, after reading it: no other lane's data involved)
-            wave_lds_sync();
-            float v[4 * NL4];
-#pragma unroll
-            for (int i = 0; i < 4 * NL4; i++)
-                v[i] = (i < NL && lch[i] >= 0) ? reinterpret_cast<const float*>(&sm.f[lch[i] >> 2][lane])[lch[i] & 3] : 0.f;
-#pragma unroll
-            for (int g = 0; g < NL4; g++) sm.f[g][lane] = make_float4(v[4 * g], v[4 * g + 1], v[4 * g + 2], v[4 * g + 3]);
-        }
         wave_lds_sync();
         uint64_t todo = __ballot(qm != 0);
         while (todo) {
@@ -352,12 +324,8 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
                 S2 = __builtin_fmaf(wdx, dx, S2);
                 S3 = __builtin_fmaf(wdx, dy, S3);
                 S4 = __builtin_fmaf(wdy, dy, S4);
-#ifndef GSR_MC_DIAG_NOFEAT
 #pragma unroll
                 for (int c = 0; c < NL; c++) SF[c] = __builtin_fmaf(dch, dpl[q][c], SF[c]);
-#else
-                SF[0] += dch;
-#endif
                 T[q] = Tn;
             }
             if (any) {
@@ -396,28 +364,11 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     }
 }
 
-// GSR_MC_LIVE: 1 -- the backward runs as two launches over the same dispatch order: one walks
-// the tiles whose dL/dout is nonzero in at most MC_NL_SMALL channels, over those channels only
-// (training: the sky-BRDF loss reaches diffuse / specular only on sky pixels, the
-// normal-consistency term the normal and depth channels only off them, and alpha never: 7
-// live channels of 14 off the sky, 9 on it); the other walks the remaining tiles over every
-// channel.  0 (default): one launch, every channel of every tile.  (Measured in round 5 on the
-// cfg4 training iteration: k_render_bwd_mc 0.60 -> 0.79 ms per view, 132 -> 120 iters/s,
-// profiles/r5x_mc_live_ab.txt.)
-#ifndef GSR_MC_LIVE
-#define GSR_MC_LIVE 0
-#endif
-#ifndef GSR_MC_NL_SMALL
-#define GSR_MC_NL_SMALL 10
-#endif
-constexpr int MC_NL_SMALL = GSR_MC_NL_SMALL;
-
 // The tile's state (T, the background term, dL/dout, the last contributors), then the walk.
-// CLS < 0: every tile, every channel; CLS == 0: the tiles with more than MC_NL_SMALL live
-// channels, every channel; CLS == MC_NL_SMALL: the other tiles, their live channels only.
-// (Two launches, not one kernel with two walks: the two walks inlined together took 166-213
-// VGPRs against 151, non-inlined 197 + scratch.)
-template <int NC4, int NCH, bool DET, int CLS>
+// (Round 5 also measured a split into two launches, one walking the tiles with at most 10 live
+// channels over those only: k_render_bwd_mc 0.60 -> 0.79 ms per view at cfg4,
+// profiles/r5x_mc_live_ab.txt.)
+template <int NC4, int NCH, bool DET>
 __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -443,62 +394,15 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
-    if constexpr (CLS >= 0) {
-        // the tile's live channels (wave-uniform)
-        uint32_t live = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; c++)
-            if (__ballot(dp[0][c] != 0.f || dp[1][c] != 0.f || dp[2][c] != 0.f || dp[3][c] != 0.f)) live |= 1u << c;
-        const bool small = __popc(live) <= MC_NL_SMALL;
-        if (small != (CLS == MC_NL_SMALL)) return;  // the other launch's tile
-        if constexpr (CLS == MC_NL_SMALL) {
-            constexpr int NL = MC_NL_SMALL;
-            int lch[NL];
-            uint32_t rest = live;
-#pragma unroll
-            for (int i = 0; i < NL; i++) {
-                lch[i] = rest ? __builtin_ctz(rest) : -1;
-                rest &= rest - 1u;
-            }
-            // dL/dout of the live channels loaded again (L2-hot) rather than selected from dp
-            float dpl[4][NL];
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const bool in = wt.inside(q, a.W, a.H);
-                const int pix = in ? wt.pixel(q, a.W) : 0;
-#pragma unroll
-                for (int i = 0; i < NL; i++) dpl[q][i] = (in && lch[i] >= 0) ? a.dL_dout[(size_t)lch[i] * HW + pix] : 0.f;
-            }
-            mc_bwd_walk<NC4, NCH, NL, true, DET>(a, tile, wt, sm, T, Tb, dpl, last, qlim, nmax, lch);
-            return;
-        }
-    }
-    if constexpr (CLS != MC_NL_SMALL) {
-        int lch[NCH];
-#pragma unroll
-        for (int i = 0; i < NCH; i++) lch[i] = i;
-        mc_bwd_walk<NC4, NCH, NCH, false, DET>(a, tile, wt, sm, T, Tb, dp, last, qlim, nmax, lch);
-    }
+    mc_bwd_walk<NC4, NCH, DET>(a, tile, wt, sm, T, Tb, dp, last, qlim, nmax);
 }
 
-// occupancy experiments (waves per SIMD the compiler must fit; unset: its own choice)
-#ifdef GSR_MC_FWD_WAVES
-#define GSR_MC_FWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MC_FWD_WAVES, GSR_MC_FWD_WAVES)))
-#else
-#define GSR_MC_FWD_ATTR
-#endif
-#ifdef GSR_MC_BWD_WAVES
-#define GSR_MC_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_MC_BWD_WAVES, GSR_MC_BWD_WAVES)))
-#else
-#define GSR_MC_BWD_ATTR
-#endif
-
 template <int NC4, int NCH = 4 * NC4>
-__global__ void __launch_bounds__(64) GSR_MC_FWD_ATTR k_render_fwd_mc(RenderMcArgs a) {
+__global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, FWD_TAIL_SPLIT, GSR_FWD_BAL, GSR_ROT_THR8)) return;
+    if (!tile_unit_fwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
     render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
 }
 
@@ -519,27 +423,21 @@ extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n, int reset) {
 }
 #endif
 
-// the composite backward's band rotation threshold (gsr_tile.hpp; the single-channel pass's by default)
-#ifndef GSR_MC_BWD_ROT_THR8
-#define GSR_MC_BWD_ROT_THR8 GSR_BWD_ROT_THR8
-#endif
-template <int NC4, int NCH = 4 * NC4, bool DET = false, int CLS = -1>
-__global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcArgs a) {
+template <int NC4, int NCH = 4 * NC4, bool DET = false>
+__global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
-    if (!tile_unit(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET ? 0u : BWD_TAIL_SPLIT, GSR_BAL_BANDS,
-                   DET ? 0u : GSR_MC_BWD_ROT_THR8, nullptr, BWD_ROT_COST))
-        return;  // det: one writer per row
+    if (!tile_unit_bwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET)) return;
 #ifdef GSR_RENDER_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    render_bwd_mc_tile<NC4, NCH, DET, CLS>(a, tile, qallow);
+    render_bwd_mc_tile<NC4, NCH, DET>(a, tile, qallow);
 #ifdef GSR_RENDER_STATS
     if (threadIdx.x == 0 && blockIdx.x < (unsigned)MCB_UNITS) {
-        unsigned long long* r = g_mcb_times[CLS == 0 ? 1 : 0] + 4 * (size_t)blockIdx.x;
+        unsigned long long* r = g_mcb_times[0] + 4 * (size_t)blockIdx.x;
         r[0] = t0;
         r[1] = __builtin_amdgcn_s_memrealtime();
-        r[2] = tile | ((unsigned long long)qallow << 20) | ((unsigned long long)(CLS == 0 ? 1 : 0) << 28);
+        r[2] = tile | ((unsigned long long)qallow << 20);
         r[3] = a.tile_nmax[tile];
     }
 #endif
@@ -548,7 +446,7 @@ __global__ void __launch_bounds__(64) GSR_MC_BWD_ATTR k_render_bwd_mc(RenderMcAr
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(GSR_FWD_BAL ? tile_pass_blocks_bal(ntile, FWD_TAIL_SPLIT) : tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
+    const dim3 grid(tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
     switch ((a.nch + 3) / 4) {
         case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
         case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;
@@ -567,10 +465,7 @@ static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s)
         case 2: hipLaunchKernelGGL((k_render_bwd_mc<2, 8, DET>), grid, dim3(64), 0, s, a); break;
         case 3: hipLaunchKernelGGL((k_render_bwd_mc<3, 12, DET>), grid, dim3(64), 0, s, a); break;
         default:
-            if (a.nch == 14 && GSR_MC_LIVE && !DET) {  // the few-channel tiles, then the rest
-                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, false, MC_NL_SMALL>), grid, dim3(64), 0, s, a);
-                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, false, 0>), grid, dim3(64), 0, s, a);
-            } else if (a.nch == 14) {
+            if (a.nch == 14) {
                 hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET>), grid, dim3(64), 0, s, a);
             } else {
                 hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET>), grid, dim3(64), 0, s, a);
@@ -582,7 +477,7 @@ static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s)
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(GSR_BAL_BANDS ? tile_pass_blocks_bal(ntile, BWD_TAIL_SPLIT) : tile_pass_blocks(ntile, BWD_TAIL_SPLIT));
+    const dim3 grid(tile_pass_blocks_bal(ntile, 0u));
     if (a.partial) launch_bwd_mc<true>(a, grid, s);
     else launch_bwd_mc<false>(a, grid, s);
 }

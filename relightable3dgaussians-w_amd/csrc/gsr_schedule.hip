@@ -25,17 +25,13 @@ void launch_tile_order_args(const TileOrderArgs& a, hipStream_t s) {
 }
 
 void launch_tile_order(unsigned ntile, const uint2* ranges, const uint32_t* cost, uint32_t* order, uint32_t* nheavy,
-                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows, int heavy_rel8,
-                       const uint32_t* surv_n, const uint32_t* ck_n, uint32_t* units) {
+                       int heavy_bits, hipStream_t s, const uint32_t* row_cost, unsigned nrows) {
     if (ntile == 0) return;
     TileOrderArgs a{};
-    a.surv_n = surv_n; a.ck_n = ck_n; a.units = units;
     a.ntile = ntile; a.ranges = ranges; a.cost = cost; a.order = order; a.nheavy = nheavy; a.heavy_bits = heavy_bits;
-    a.heavy_rel8 = heavy_rel8;
     a.row_cost = row_cost; a.nrows = nrows;
-    a.balance = GSR_BAL_BANDS;  // the backward passes' bands (tile_unit ... bal)
-    if (a.balance) hipLaunchKernelGGL(k_tile_order<true>, dim3(8), dim3(512), 0, s, a);
-    else hipLaunchKernelGGL(k_tile_order<false>, dim3(8), dim3(512), 0, s, a);
+    a.balance = 1;  // the backward passes' bands are cost-balanced (tile_unit_bwd)
+    hipLaunchKernelGGL(k_tile_order<true>, dim3(8), dim3(512), 0, s, a);
 }
 
 }  // namespace gsr

@@ -22,11 +22,9 @@ namespace gsr {
 
 constexpr int WAVE_ITEMS = SORT_TILE / 4;  // contiguous keys per wave
 
-// The depth sort's digit width (4 passes of 8 bits by default; GSR_DEPTH_BITS = 11 sorts the
-// 32-bit keys in 3 passes of 11 + 11 + 10 bits).
-#ifndef GSR_DEPTH_BITS
-#define GSR_DEPTH_BITS 8
-#endif
+// The depth sort's digit width: 4 passes of 8 bits (3 passes of 11 + 11 + 10 bits measured
+// slower, profiles/r4r_ab_depth_sort.txt).
+constexpr int DEPTH_BITS = 8;
 
 template <int BITS>
 __device__ __forceinline__ uint64_t peer_mask(uint32_t d, bool valid) {
@@ -311,7 +309,7 @@ int radix_sort_pairs_from(long long n, const uint32_t* keys_in, const uint32_t* 
 }
 
 size_t depth_sort_temp_bytes(long long P) {
-    const size_t nb = (size_t)sort_blocks(P), NB = (size_t)1 << GSR_DEPTH_BITS;
+    const size_t nb = (size_t)sort_blocks(P), NB = (size_t)1 << DEPTH_BITS;
     return 4 * (NB * nb + NB) + 256;
 }
 
@@ -319,7 +317,7 @@ int depth_sort(long long P, const uint32_t* keys_in, uint32_t* keys, uint32_t* v
                uint32_t* vals_alt, const uint2* aux_in, uint2* aux, uint2* aux_alt, void* temp,
                unsigned long long* pv_out, hipStream_t s, void* zero, size_t zero_bytes, bool pack) {
     if (P <= 0) return -1;
-    constexpr int BITS = GSR_DEPTH_BITS, NB = 1 << BITS, NPASS = (32 + BITS - 1) / BITS;
+    constexpr int BITS = DEPTH_BITS, NB = 1 << BITS, NPASS = (32 + BITS - 1) / BITS;
     const int nb = sort_blocks(P);
     uint32_t* hist = reinterpret_cast<uint32_t*>(temp);
     uint32_t* digit_tot = hist + (long long)NB * nb;

@@ -44,16 +44,10 @@ __device__ __forceinline__ float ld_zero(const float* p, int x, int y, int W, in
 // 3x1080x1920 (tools/bench_ssim.py): one chunk per workgroup 77.7 / 61.5 us (forward /
 // backward), four chunks 78.0 / 66.6 us, four without the prefetch 79.6 / 64.6 us; the
 // single-tile kernel that staged its window with interleaved loads and LDS stores took 89.3 /
-// 64.6 us.  The gain is the window's loads issued all at once into registers; the strip is
-// kept as an option (GSR_SSIM_STRIP).  Per output the arithmetic and its order are the same
-// in every variant.
-#ifndef GSR_SSIM_STRIP
-#define GSR_SSIM_STRIP 1
-#endif
-#ifndef GSR_SSIM_PREFETCH  // load the next chunk during the vertical pass (registers) or at its start
-#define GSR_SSIM_PREFETCH 1
-#endif
-constexpr int SS_CH = GSR_SSIM_STRIP;
+// 64.6 us.  The gain is the window's loads issued all at once into registers: one chunk per
+// workgroup (SS_CH; the loops below serve any strip length, with the next chunk's rows loaded
+// during the vertical pass).  Per output the arithmetic and its order are the same either way.
+constexpr int SS_CH = 1;
 constexpr int SS_NEW = SS_TH * SS_LW;                            // raw values of one chunk's new rows
 constexpr int SS_PF = (SS_NEW + 255) / 256;                      // per thread
 
@@ -110,7 +104,6 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
         const int ty = ty_first + j * SS_TH;
         if (ty >= H) break;  // block-uniform
         const int r0 = j == 0 ? 0 : SS_LH - SS_TH;  // window rows [r0, SS_LH) are new
-        if (!GSR_SSIM_PREFETCH && j > 0) ss_fetch<2>(src, x0, ty - SS_R, SS_LH - SS_TH, W, H, pf);
         ss_stage<2>(sr, SS_LH - SS_TH, pf);
         __syncthreads();
         // horizontal pass over the new window rows: the five moments over 11 columns
@@ -143,7 +136,7 @@ __global__ void __launch_bounds__(256) k_ssim_fwd(int H, int W, const float* __r
         }
         __syncthreads();
         // the next chunk's new rows load while this chunk's vertical pass runs
-        if (GSR_SSIM_PREFETCH && j + 1 < SS_CH && ty + SS_TH < H)
+        if (j + 1 < SS_CH && ty + SS_TH < H)
             ss_fetch<2>(src, x0, ty + SS_TH - SS_R, SS_LH - SS_TH, W, H, pf);
         {
             const int tx = threadIdx.x % SS_TW, ty0 = (threadIdx.x / SS_TW) * SS_VY;
@@ -246,7 +239,6 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
         const int ty = ty_first + j * SS_TH;
         if (ty >= H) break;  // block-uniform
         const int r0 = j == 0 ? 0 : SS_LH - SS_TH;
-        if (!GSR_SSIM_PREFETCH && j > 0) ss_fetch<3>(src, x0, ty - SS_R, SS_LH - SS_TH, W, H, pf);
         ss_stage<3>(sr, SS_LH - SS_TH, pf);
         __syncthreads();
         for (int t = threadIdx.x; t < (SS_LH - r0) * (SS_TW / SS_HX); t += 256) {
@@ -273,7 +265,7 @@ __global__ void __launch_bounds__(256) k_ssim_bwd(int H, int W, const float* __r
             }
         }
         __syncthreads();
-        if (GSR_SSIM_PREFETCH && j + 1 < SS_CH && ty + SS_TH < H)
+        if (j + 1 < SS_CH && ty + SS_TH < H)
             ss_fetch<3>(src, x0, ty + SS_TH - SS_R, SS_LH - SS_TH, W, H, pf);
         {
             const int tx = threadIdx.x % SS_TW, ty0 = (threadIdx.x / SS_TW) * SS_VY;

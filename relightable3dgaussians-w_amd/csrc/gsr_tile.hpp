@@ -27,68 +27,31 @@ __device__ __forceinline__ void band_of(unsigned x, unsigned n, unsigned& lo, un
 // mask; false when the block has nothing to do.  (Four-wave workgroups holding a heavy
 // tile's quadrants measured slower on balanced scenes: a workgroup waits for four free wave
 // slots on one CU, so single waves cannot backfill.)
-#ifndef GSR_HEAVY_CAP
-#define GSR_HEAVY_CAP 64
-#endif
-constexpr unsigned HEAVY_CAP = GSR_HEAVY_CAP;  // split heavy tiles per band
+constexpr unsigned HEAVY_CAP = 64;  // split heavy tiles per band
 // words per unit in the instrumented builds' timing records (g_fwd_times / g_bwd_times)
 #define GSR_UNIT_REC 8
-#ifndef GSR_FWD_TAIL
-#define GSR_FWD_TAIL 128
-#endif
-#ifndef GSR_BWD_TAIL
-#define GSR_BWD_TAIL 0
-#endif
-// The backward's per-tile cost estimate (its dispatch order, heaviest first, and its balanced
-// bands), written by the forward: 1 (default) -- the forward's (survivor, quadrant) evaluations,
-// 0 -- the sum of the quadrants' largest n_contrib.  Measured in round 5 (profiles/
-// r5z_eval_cost_ab.txt): cfg2c render_bwd 0.465 -> 0.429 ms (its bands balance by the work the
-// backward repeats, not by list positions; no tile reaches the quadrant split's 8192 any more),
-// cfg2 and training unchanged
-#ifndef GSR_EVAL_COST
-#define GSR_EVAL_COST 1
-#endif
-constexpr unsigned FWD_TAIL_SPLIT = GSR_FWD_TAIL;  // split tail tiles per band, forward passes
-constexpr unsigned BWD_TAIL_SPLIT = GSR_BWD_TAIL;  // backward passes
-// bal: the bands are the cost-balanced ranges k_tile_order stored after the band counts
-// (nheavy[8 + b] = band b's first tile, nheavy[16] = ntile; GSR_BAL_BANDS); else equal bands.
-// rot: rotated bands -- block b takes unit b / 8 of band (b + b / 8) mod 8 instead of band b mod
-// 8, so each XCD (b mod 8) works through every band's order in turn -- when the bands' estimated
-// costs (nheavy[24 + b], written by the order) are uneven: the largest above GSR_ROT_THR8 / 8 x
-// their mean (0: never).  A skewed frame then no longer waits for one XCD's band; an even one
-// keeps each band's L2 locality (rotating unconditionally measured cfg2c +1.5 %, cfg2 -0.9 %)
-#ifndef GSR_ROT_THR8
-#define GSR_ROT_THR8 10u
-#endif
-// The backward passes rotate their (cost-balanced) bands when the *forward's* equal bands had
-// uneven costs, by the same threshold (0: never): balancing by the estimate left cfg2c's
-// backward XCDs ending 305-450 us apart (a balanced split: 381).  Measured in round 5
-// (profiles/r5z_band_rotate_ab.txt, s36: rotating every frame): cfg2c render_bwd 0.434 ->
-// 0.397 ms, call 1.215 -> 1.182 ms, throughput +2 %, but cfg2's call +0.5 %
-#ifndef GSR_BWD_ROT_THR8
-#define GSR_BWD_ROT_THR8 GSR_ROT_THR8
-#endif
-// the backward's table (nheavy) starts 32 words before the forward's: the forward's band costs
-// are at nheavy[BWD_ROT_COST + b] there
+// Split tail tiles per band: the forward passes split their 128 lightest (render_fwd 0.247 ->
+// 0.233 ms at cfg2); the backward passes none (splitting its lightest 32 / 96 per band cost 1.5 /
+// 3.5 % of the throughput: a quadrant unit repeats the per-survivor reduction,
+// profiles/r5z_bwd_tail_ab.txt)
+constexpr unsigned FWD_TAIL_SPLIT = 128;
+// Rotated bands: block b takes unit b / 8 of band (b + (b / 8 >> ROT_SHIFT)) mod 8 instead of band
+// b mod 8, so each XCD (b mod 8) works through every band's order in runs of 2^ROT_SHIFT units,
+// when the bands' estimated costs (nheavy[rcost + b], written by the order) are uneven: the
+// largest above ROT_THR8 / 8 x their mean.  A skewed frame then no longer waits for one XCD's
+// band; an even one keeps each band's L2 locality (rotating unconditionally measured cfg2c
+// +1.5 %, cfg2 -0.9 %; a step per unit instead of per 32 fetched 3.4x the bytes,
+// profiles/r5z_band_rotate_ab.txt).  The backward passes rotate their cost-balanced bands when
+// the *forward's* equal bands had uneven costs (cfg2c render_bwd 0.434 -> 0.397 ms): the
+// backward's table (nheavy) starts 32 words before the forward's, so those costs are at
+// nheavy[BWD_ROT_COST + b] there.
+constexpr unsigned ROT_THR8 = 10u, ROT_SHIFT = 5u;
 constexpr unsigned BWD_ROT_COST = 32u + 24u;
-#ifndef GSR_BWD_ROT_SHIFT
-#define GSR_BWD_ROT_SHIFT GSR_ROT_SHIFT
-#endif
-// the rotation steps every 2^GSR_ROT_SHIFT units: an XCD walks runs of 32 units of one band's
-// order, so its L2 still serves neighbouring tiles (cfg2c render_fwd 0.385 -> 0.370 ms against a
-// step per unit, whose forward fetched 3.4x the bytes of unrotated bands: r5z_band_rotate_ab.txt)
-#ifndef GSR_ROT_SHIFT
-#define GSR_ROT_SHIFT 5
-#endif
-// qslot (when non-null): a quadrant unit's tile slot, unique per frame -- band x (HEAVY_CAP +
-// ntail) + the heavy tile's rank, or HEAVY_CAP + the tail tile's rank (QL_SLOTS with the
-// forward's ntail); SURV_NONE for a whole-tile unit
 __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
-                                          unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal = false,
-                                          unsigned rot = 0u, uint32_t* qslot = nullptr, unsigned rcost = 24u,
-                                          unsigned rshift = GSR_ROT_SHIFT) {
+                                          unsigned& tile, uint32_t& qallow, unsigned ntail, bool bal, unsigned rot,
+                                          unsigned rcost) {
     unsigned u = blockIdx.x >> 3, band = blockIdx.x & 7u;
-    if (rot != 0u) {  // (rot: the threshold, GSR_ROT_THR8 / GSR_BWD_ROT_THR8; the costs at nheavy[rcost + b])
+    if (rot != 0u) {
         uint32_t mx = 0u;
         unsigned long long sum = 0ull;
 #pragma unroll
@@ -97,7 +60,7 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
             mx = max(mx, c);
             sum += c;
         }
-        if (64ull * mx > (unsigned long long)rot * sum) band = (band + (u >> rshift)) & 7u;
+        if (64ull * mx > (unsigned long long)rot * sum) band = (band + (u >> ROT_SHIFT)) & 7u;
     }
     unsigned lo, len;
     if (bal) {
@@ -110,11 +73,9 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
     const unsigned t = min(ntail, len - h);
     const unsigned whole = len - h - t;
     unsigned pos;
-    uint32_t slot = SURV_NONE;
     if (u < 4u * h) {
         pos = u >> 2;
         qallow = 1u << (u & 3u);
-        slot = band * (HEAVY_CAP + ntail) + pos;
     } else if (u < 4u * h + whole) {
         pos = h + (u - 4u * h);
         qallow = 15u;
@@ -122,36 +83,35 @@ __device__ __forceinline__ bool tile_unit(unsigned ntile, const uint32_t* order,
         const unsigned v = u - 4u * h - whole;
         pos = h + whole + (v >> 2);
         qallow = 1u << (v & 3u);
-        slot = band * (HEAVY_CAP + ntail) + HEAVY_CAP + (v >> 2);
     }
-    if (qslot) *qslot = slot;
     if (pos >= len) return false;
     tile = order[lo + pos];
     return true;
+}
+// The forward passes' units: equal bands, their 128 lightest tiles split
+__device__ __forceinline__ bool tile_unit_fwd(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
+                                              unsigned& tile, uint32_t& qallow) {
+    return tile_unit(ntile, order, nheavy, tile, qallow, FWD_TAIL_SPLIT, false, ROT_THR8, 24u);
+}
+// The backward passes' units: cost-balanced bands (balanced_band), no tail split; det: one
+// writer per partial row, so no band rotation either
+__device__ __forceinline__ bool tile_unit_bwd(unsigned ntile, const uint32_t* order, const uint32_t* nheavy,
+                                              unsigned& tile, uint32_t& qallow, bool det) {
+    return tile_unit(ntile, order, nheavy, tile, qallow, 0u, true, det ? 0u : ROT_THR8, BWD_ROT_COST);
 }
 // blocks of a tile pass launch: the longest band's units (heavy and tail tiles count four)
 __host__ __device__ constexpr unsigned tile_pass_blocks(unsigned ntile, unsigned ntail) {
     return 8u * ((ntile + 7u) / 8u + 3u * HEAVY_CAP + 3u * ntail);
 }
-// the same with cost-balanced bands: a band holds at most 3 ntile / 8 + 2 tiles (balanced_band)
-// (GSR_BAL_GRID_X4: the bound in quarters of the mean band, 12 = 3x; a timing experiment only:
-// any other value can drop the tiles of a band longer than it)
-#ifndef GSR_BAL_GRID_X4
-#define GSR_BAL_GRID_X4 12u
-#endif
+// the same with cost-balanced bands: a band holds at most 3 ntile / 8 + 2 tiles (balanced_band;
+// the grid launches 12/4 workgroups per 8 tiles of a band: blocks past a band's units exit at
+// once, and a grid of 5/4 measured the same within noise, profiles/r5q_ab_grid.txt)
 __host__ __device__ constexpr unsigned tile_pass_blocks_bal(unsigned ntile, unsigned ntail) {
-    return 8u * ((GSR_BAL_GRID_X4 * ((ntile + 7u) / 8u) + 3u) / 4u + 2u + 3u * HEAVY_CAP + 3u * ntail);
+    return 8u * ((12u * ((ntile + 7u) / 8u) + 3u) / 4u + 2u + 3u * HEAVY_CAP + 3u * ntail);
 }
-// The backward passes' bands: 1 (default) -- cost-balanced (each band a contiguous tile range
-// holding an eighth of the estimated cost: balanced_band), 0 -- equal tile counts
-#ifndef GSR_BAL_BANDS
-#define GSR_BAL_BANDS 1
-#endif
-// the balanced bands' per-tile floor: the mean tile cost / GSR_BAL_FLOOR_DIV (1 or 2; the grid
-// bound of tile_pass_blocks_bal holds for both)
-#ifndef GSR_BAL_FLOOR_DIV
-#define GSR_BAL_FLOOR_DIV 2ull
-#endif
+// the balanced bands' per-tile floor: the mean tile cost / BAL_FLOOR_DIV (the grid bound of
+// tile_pass_blocks_bal holds for 1 and 2)
+constexpr unsigned long long BAL_FLOOR_DIV = 2ull;
 // LDS ordering within one wave (the tile passes' waves share no LDS)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -279,25 +239,13 @@ struct TileList {
 // The tile passes evaluate Gaussians in log2 units: the conic is pre-scaled by log2(e) when
 // a record is staged (once per record and batch), so exp(power) is one v_exp_f32 (exp2) per
 // evaluation with no multiply.  Forward and backward stage and evaluate identically, so the
-// backward replays exactly the forward's blend decisions.  The backward's conic-weighted
+// backward replays exactly the forward's blend decisions.
 // (The backward accumulates raw sums of G dL/dalpha dx...: G is the same value in either unit.)
-// GSR_REF_EXPONENT=1 builds the reference's order instead (forward.cu:335,343,
-// backward.cu:494-498): the raw conic staged, power = -0.5 (a dx dx + c dy dy) - b dx dy with
-// no contraction, G = expf(power) -- the A/B of VERDICT r4 item 6.
-#ifndef GSR_REF_EXPONENT
-#define GSR_REF_EXPONENT 0
-#endif
 constexpr float TILE_LOG2E = 1.44269504088896340736f;
 constexpr float TILE_LN2 = 0.69314718055994530942f;
-#if GSR_REF_EXPONENT
-constexpr float TILE_STAGE_AC = 1.0f;  // factor of conic.a and conic.c as staged
-constexpr float TILE_STAGE_B = 1.0f;   // factor of conic.b
-__device__ __forceinline__ float tile_exp2(float x) { return expf(x); }  // natural units here
-#else
 constexpr float TILE_STAGE_AC = -0.5f * TILE_LOG2E;  // factor of conic.a and conic.c
 constexpr float TILE_STAGE_B = -TILE_LOG2E;          // factor of conic.b
 __device__ __forceinline__ float tile_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
-#endif
 
 // Minimum over the pixel box [dx0,dx1]x[dy0,dy1] (offsets from the Gaussian centre) of
 // q(d) = a dx^2 + 2 b dx dy + c dy^2, for a positive-definite conic (a, b, c).
@@ -469,12 +417,7 @@ struct WaveTile {
 // backward tile passes evaluate it with this exact operation sequence, so the backward
 // replays the forward's blend decisions bit for bit.
 __device__ __forceinline__ float gauss_power(float na, float nb, float nc, float dx, float dy) {
-#if GSR_REF_EXPONENT  // (na, nb, nc) = the raw conic (a, b, c); the reference's operation order
-    return __fsub_rn(__fmul_rn(-0.5f, __fadd_rn(__fmul_rn(__fmul_rn(na, dx), dx), __fmul_rn(__fmul_rn(nc, dy), dy))),
-                     __fmul_rn(__fmul_rn(nb, dx), dy));
-#else
     return __builtin_fmaf(na * dx, dx, __builtin_fmaf(nc * dy, dy, (nb * dx) * dy));
-#endif
 }
 
 // Lane masks in SGPR pairs and selects on them (v_cmp_*_e64 / v_cndmask_b32_e64).  On

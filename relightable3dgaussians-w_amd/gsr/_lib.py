@@ -119,7 +119,7 @@ def _declare(lib):
                "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
                "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
-               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_set_backward_heavy_bits", "gsr_backward_chunk_size", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
+               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_set_backward_heavy_bits", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
 
 

@@ -38,12 +38,24 @@ def test_layout_query_is_consistent():
     assert L.geom_bytes > 1000 * (48 + 64) and L.bin_bytes >= 8 * 255 and L.img_bytes >= 1920 * 1080 * 8
     for off in (L.geom_rec, L.geom_acc, L.img_ranges, L.bin_st_ranges, L.bin_entries):
         assert off % 256 == 0
-    # the backward's order buffers (appended fields): disjoint, in order, inside the image buffer
+    # the backward's order buffers and the survivor lists (appended fields): disjoint, in order,
+    # inside the image buffer; the lists (the last region) are reserved only while they are on
     T, gy = 120 * 68, 68
-    spans = [(L.img_tile_cost, 4 * T), (L.img_row_cost, 4 * gy), (L.img_order_bwd, 4 * T), (L.img_nheavy, 4 * 32)]
+    spans = [(L.img_tile_cost, 4 * T), (L.img_row_cost, 4 * gy), (L.img_order_bwd, 4 * T), (L.img_nheavy, 4 * 80),
+             (L.img_surv_n, 4 * T), (L.img_surv, 8 * L.surv_cap * T)]
     for (a, n), (b, _) in zip(spans, spans[1:]):
         assert a + n <= b
-    assert spans[-1][0] + spans[-1][1] <= L.img_bytes
+    before = _lib.survivor_lists()
+    try:
+        _lib.set_survivor_lists(True)
+        on = _lib.layout(1000, 12345, 1920, 1080)
+        assert on.img_surv + 8 * on.surv_cap * T <= on.img_bytes
+        _lib.set_survivor_lists(False)
+        off = _lib.layout(1000, 12345, 1920, 1080)
+        assert off.img_surv == on.img_surv and off.img_surv_n == on.img_surv_n  # the same offsets
+        assert off.img_surv <= off.img_bytes < on.img_bytes - 8 * on.surv_cap * T + 4096
+    finally:
+        _lib.set_survivor_lists(before)
 
 
 def test_cpu_tensors_are_rejected():

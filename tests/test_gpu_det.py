@@ -69,17 +69,11 @@ def test_deterministic_backward(case):
 def test_survivor_lists_change_nothing(case):
     """The backward over the forward's survivor lists evaluates the same (Gaussian, quadrant)
     pairs in the same order as the one that filters the super-tile lists again: in
-    deterministic mode (no atomics) every gradient is bit-identical (within 1e-6 when the
-    backward runs long lists in chunks from the forward's checkpoints)."""
-    from gsr import _lib
+    deterministic mode (no atomics) every gradient is bit-identical."""
     with_lists = _backward(case, True, surv=True)
     without = _backward(case, True, surv=False)
-    chunks = _lib.lib().gsr_backward_chunk_size() > 0  # chunks start from checkpoints: rounding only
     for k, (x, y) in enumerate(zip(with_lists, without)):
-        if not chunks:
-            assert torch.equal(x, y), f"gradient {k} differs with the survivor lists"
-        elif y.numel() and y.abs().max() > 0:
-            assert rel_l2(x.numpy(), y.numpy()) <= 1e-6, (k, rel_l2(x.numpy(), y.numpy()))
+        assert torch.equal(x, y), f"gradient {k} differs with the survivor lists"
 
 
 def test_deterministic_multichannel():
