@@ -312,36 +312,90 @@ class ReferenceExchange:
     ``sync_max_radii({"max_radii2D": g.max_radii2D})`` right before densify_and_prune, or
     ``synced`` before any other reader.
 
-        ex = dp.ReferenceExchange([g._xyz, g._albedo, ...], P=g.get_xyz.shape[0])
+        ex = dp.ReferenceExchange(optimizer=g.optimizer)
         ...loss.backward()
         ex.add_views([viewspace_point_tensor.grad], [radii], g.max_radii2D, stats_on)
         ex.exchange(g, stats_on, world=dist.get_world_size())   # grads summed in place
-    """
 
-    def __init__(self, params: Sequence[torch.Tensor], P: int, device=None):
-        self.params = list(params)
-        dev = device if device is not None else self.params[0].device
-        self.sizes = [p.numel() for p in self.params]
-        self.n = sum(self.sizes)
-        self.P = int(P)
-        self.flat = torch.zeros(self.n + 2 * self.P, device=dev)
-        self.acc = self.flat[self.n:self.n + self.P].view(self.P, 1)
-        self.den = self.flat[self.n + self.P:].view(self.P, 1)
+    With ``optimizer`` (the recommended form) the exchanged parameters are, on every call, every
+    tensor with requires_grad in its param_groups -- the Gaussians' attributes, the sky radius
+    (gaussian_model.py:272) and, in the relightable model, the MLP and appearance embeddings
+    (relit3DGW_model.py:144-145) -- so nothing drifts apart across ranks, and the
+    densify_and_prune that replaces the Parameters and resizes the statistics
+    (gaussian_model.py:471-542) needs no rebuild: the bucket is re-laid out for the new sizes.
+    With a fixed ``params`` list and ``P`` the exchange checks on every call that the statistics
+    still hold P rows and that every listed tensor is still the size it was, and raises
+    otherwise (rebuild it after densify_and_prune)."""
+
+    def __init__(self, params: Optional[Sequence[torch.Tensor]] = None, P: Optional[int] = None, device=None,
+                 optimizer=None):
+        if (params is None) == (optimizer is None):
+            raise ValueError("ReferenceExchange: give either the optimizer (recommended) or a fixed params list")
+        if params is not None and P is None:
+            raise ValueError("ReferenceExchange: a fixed params list needs P")
+        self.optimizer = optimizer
+        self.fixed = None if params is None else list(params)
+        self.fixed_sizes = None if params is None else [p.numel() for p in self.fixed]
+        self.fixed_P = None if P is None else int(P)
+        self.device = device
+        self.flat = None
+        self.params, self.sizes, self.n, self.P = [], [], -1, -1
+        self.pending = False  # statistics deltas added since the last exchange
+        if self.fixed is not None:
+            self._bind(self.fixed_P)
+
+    def _current(self) -> List[torch.Tensor]:
+        if self.optimizer is not None:
+            return [p for grp in self.optimizer.param_groups for p in grp["params"] if p.requires_grad]
+        if any(p.numel() != n for p, n in zip(self.fixed, self.fixed_sizes)):
+            raise RuntimeError("ReferenceExchange: a listed parameter changed size (densify_and_prune replaced "
+                               "it): rebuild the exchange, or build it from the optimizer")
+        return self.fixed
+
+    def _bind(self, P: int) -> None:
+        """(Re)lay out the bucket [gradients | one has-gradient flag per parameter | accum deltas |
+        denom deltas] for the current parameters and P statistics rows."""
+        if self.fixed_P is not None and P != self.fixed_P:
+            raise RuntimeError(f"ReferenceExchange: the statistics hold {P} rows, the exchange was built for "
+                               f"{self.fixed_P} (densify_and_prune resized them): rebuild it, or build it from the "
+                               "optimizer")
+        params = self._current()
+        sizes = [p.numel() for p in params]
+        n = sum(sizes) + len(params)
+        if self.flat is None or n != self.n or P != self.P:
+            if self.pending:
+                raise RuntimeError("ReferenceExchange: the parameters or the statistics changed size between "
+                                   "add_views and exchange")
+            dev = self.device if self.device is not None else (params[0].device if params else "cpu")
+            self.flat = torch.zeros(n + 2 * P, device=dev)
+            self.acc = self.flat[n:n + P].view(P, 1)
+            self.den = self.flat[n + P:].view(P, 1)
+        self.params, self.sizes, self.n, self.P = params, sizes, n, P
+        self.flags = self.flat[n - len(params):n]
 
     def add_views(self, mean2D_grads, radii, max_radii2D: torch.Tensor, stats_on: bool) -> None:
         """This rank's views' densification updates (train.py:130, 143-144)."""
+        self._bind(int(max_radii2D.shape[0]))
         add_views(self.acc if stats_on else None, self.den if stats_on else None, max_radii2D, mean2D_grads, radii)
+        self.pending = self.pending or stats_on
 
     def exchange(self, gaussians, stats_on: bool, world: int = 1, group=None, chunks: int = None,
                  min_chunk: int = None) -> int:
         """Sum the parameters' gradients (in place) and the statistics deltas over the ranks
         with one all-reduce; fold the deltas into gaussians.xyz_gradient_accum / denom.
         Returns the number of collectives issued."""
+        P = int(gaussians.max_radii2D.shape[0])
+        self._bind(P)
+        if stats_on and (gaussians.xyz_gradient_accum.shape[0] != P or gaussians.denom.shape[0] != P):
+            raise RuntimeError("ReferenceExchange: xyz_gradient_accum / denom do not hold max_radii2D's rows")
         o = 0
-        for p, n in zip(self.params, self.sizes):
-            g = p.grad if p.grad is not None else torch.zeros_like(p)
-            self.flat[o:o + n].copy_(g.reshape(-1))
+        for i, (p, n) in enumerate(zip(self.params, self.sizes)):
+            if p.grad is not None:
+                self.flat[o:o + n].copy_(p.grad.reshape(-1))
+            else:  # no gradient on this rank (e.g. an embedding no local view used): adds zero
+                self.flat[o:o + n].zero_()
             o += n
+        self.flags.copy_(torch.tensor([0.0 if p.grad is None else 1.0 for p in self.params]))
         bucket = self.flat if stats_on else self.flat[:self.n]
         issued = 0
         if world > 1:
@@ -353,15 +407,20 @@ class ReferenceExchange:
                 w.wait()
             issued = len(ranges)
         o = 0
-        for p, n in zip(self.params, self.sizes):
+        anyg = self.flags.tolist() if world > 1 else None
+        for i, (p, n) in enumerate(zip(self.params, self.sizes)):
+            summed = self.flat[o:o + n].view_as(p)
             if p.grad is not None:
-                p.grad.copy_(self.flat[o:o + n].view_as(p.grad))
+                p.grad.copy_(summed)
+            elif anyg is not None and anyg[i] > 0:  # another rank's views reached it: every replica steps
+                p.grad = summed.clone()
             o += n
         if stats_on:
             gaussians.xyz_gradient_accum.add_(self.acc)
             gaussians.denom.add_(self.den)
-            self.acc.zero_()
-            self.den.zero_()
+        self.acc.zero_()
+        self.den.zero_()
+        self.pending = False
         return issued
 
 

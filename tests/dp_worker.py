@@ -315,3 +315,70 @@ def run_refex(rank, world, port, out_path):
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def refex_resize_run(rank, world, P1=200, P2=260):
+    """ReferenceExchange built from the optimizer across a densify_and_prune-style resize: the
+    Gaussians' Parameter replaced by a larger one (its optimizer state dropped, as
+    gaussian_model.py:471-542 rebuilds it) and the statistics resized to P2 between two
+    exchanges; an MLP weight that only rank 0's views reach and a sky radius ride in the same
+    exchange (world 1: both ranks' gradients summed in rank order).  Returns the final
+    parameters, the statistics, and whether a fixed-list exchange refused the resize."""
+    import types
+    from gsr import dp
+    ranks = [rank] if world > 1 else list(range(2))
+    gen = lambda s: torch.Generator().manual_seed(s)
+    xyz = torch.nn.Parameter(torch.randn(P1, 3, generator=gen(1)))
+    mlp = torch.nn.Parameter(torch.randn(8, 8, generator=gen(2)))
+    sky = torch.nn.Parameter(torch.ones(1))
+    opt = torch.optim.Adam([{"params": [xyz]}, {"params": [mlp]}, {"params": [sky]}], lr=0.01)
+    g = types.SimpleNamespace(xyz_gradient_accum=torch.zeros(P1, 1), denom=torch.zeros(P1, 1),
+                              max_radii2D=torch.zeros(P1))
+    ex = dp.ReferenceExchange(optimizer=opt)
+    fixed = dp.ReferenceExchange([xyz], P1)
+    refused = False
+    for it in range(2):
+        P = xyz.shape[0]
+        opt.zero_grad(set_to_none=True)
+        xyz.grad = sum(torch.randn(P, 3, generator=gen(100 * it + r)) for r in ranks)
+        if 0 in ranks:
+            mlp.grad = torch.randn(8, 8, generator=gen(700 + it))
+        sky.grad = sum(torch.randn(1, generator=gen(900 + 10 * it + r)) for r in ranks)
+        g2d, rad = [], []
+        for r in ranks:
+            for j in range(VIEWS_PER_RANK):
+                gg, radii = view_stats(it, r * VIEWS_PER_RANK + j, P)
+                g2d.append(gg * 0.02)
+                rad.append(radii)
+        ex.add_views(g2d, rad, g.max_radii2D, True)
+        ex.exchange(g, True, world=world, chunks=2, min_chunk=1)
+        opt.step()
+        if it == 0:  # densify: a new, larger Parameter (state rebuilt) and resized statistics
+            new = torch.nn.Parameter(torch.cat([xyz.detach(), xyz.detach()[:P2 - P1] * 0.5]))
+            del opt.state[xyz]
+            opt.param_groups[0]["params"] = [new]
+            xyz = new
+            g.xyz_gradient_accum = torch.cat([g.xyz_gradient_accum, torch.zeros(P2 - P1, 1)])
+            g.denom = torch.cat([g.denom, torch.zeros(P2 - P1, 1)])
+            g.max_radii2D = torch.cat([g.max_radii2D, torch.zeros(P2 - P1)])
+            try:
+                fixed.add_views(g2d, rad, g.max_radii2D, True)
+            except RuntimeError:
+                refused = True
+    return {"xyz": xyz.detach().numpy(), "mlp": mlp.detach().numpy(), "sky": sky.detach().numpy(),
+            "accum": g.xyz_gradient_accum.numpy(), "denom": g.denom.numpy(), "refused": np.array(refused)}
+
+
+def run_refex_resize(rank, world, port, out_path):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsr import dp
+        out = refex_resize_run(rank, world)
+        same = dp.replicas_identical([torch.from_numpy(out[k]) for k in ("xyz", "mlp", "sky", "accum", "denom")])
+        if rank == 0:
+            np.savez(out_path, same=np.array(same), **out)
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

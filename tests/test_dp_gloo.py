@@ -163,6 +163,22 @@ def test_reference_loop_exchange(tmp_path):
     np.testing.assert_allclose(got["accum"], g.xyz_gradient_accum.numpy(), rtol=1e-6, atol=1e-7)
 
 
+def test_reference_exchange_follows_densify(tmp_path):
+    """ReferenceExchange(optimizer=...) across a densify_and_prune-style resize: the
+    replaced, larger Gaussian Parameter and the resized statistics are exchanged in the next
+    iteration without a rebuild, an MLP weight that only one rank's views reach and the sky radius
+    stay identical on every rank, everything equals the one-process run over both ranks' views,
+    and a fixed-list exchange built for the old size refuses the resized statistics."""
+    out = str(tmp_path / "refex_resize.npz")
+    mp.spawn(dp_worker.run_refex_resize, args=(2, free_port(), out), nprocs=2, join=True)
+    got = np.load(out, allow_pickle=False)
+    assert got["same"].all(), got["same"]
+    want = dp_worker.refex_resize_run(0, 1)
+    assert want["xyz"].shape == (260, 3) and bool(got["refused"]) and bool(want["refused"])
+    for k in ("xyz", "mlp", "sky", "accum", "denom"):
+        np.testing.assert_allclose(got[k], want[k], rtol=1e-6, atol=1e-7, err_msg=k)
+
+
 def test_exchange_chunks_cover_aligned():
     """gsr.dp.exchange_chunks: contiguous ascending slices covering [0, n) exactly once, every
     start a multiple of 4 floats (the ranged Adam's float4 rows), at most `chunks` of them,
