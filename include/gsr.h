@@ -427,6 +427,16 @@ int gsr_get_deterministic(void);
  * the forward. */
 int gsr_set_survivor_lists(int on);
 int gsr_get_survivor_lists(void);
+/* Exact blend mode (default off; GSR_EXACT_BLEND=1 in the environment turns it on): the tile passes
+ * evaluate every (pixel, Gaussian) pair with the reference's float arithmetic bit for bit -- the
+ * exponent in forward.cu:335's operation order, glibc's expf (the oracle's libm), alpha =
+ * min(0.99, o G), the colour sum in forward.cu:359's order -- so the forward's colours,
+ * transmittance and n_contrib equal the canonical oracle's exactly (the default arithmetic
+ * differs by rounding, and decides a pair or two per frame within ulps of a threshold the other
+ * way).  The backward replays the forward's mode (recorded per image buffer).  Slower: a
+ * double-precision exp per evaluation.  Set it before the forward. */
+int gsr_set_exact_blend(int on);
+int gsr_get_exact_blend(void);
 /* The backward's heavy-tile threshold: tiles whose estimated cost (the forward's evaluation
  * count) reaches 2^bits run as four quadrant units (a negative value restores the build's
  * default, 13).  Results agree either way within the atomic-order tolerance; a switch for tests

@@ -247,6 +247,35 @@ bool surv_on() {
     }
     return gsr::SURV_CAP > 0 && v != 0;
 }
+// Exact blend mode (gsr_set_exact_blend / GSR_EXACT_BLEND=1; gsr_tile.hpp "exact mode"): the tile
+// passes evaluate every pair with the reference's float arithmetic bit for bit.  Each forward records
+// its mode against its image buffer, so its backward (and a geometry-cache forward over the same
+// buffers) replays the same arithmetic whatever the switch says by then.
+std::atomic<int> g_exact{-1};
+bool exact_on() {
+    int v = g_exact.load();
+    if (v < 0) {
+        const char* e = getenv("GSR_EXACT_BLEND");
+        v = (e && e[0] && e[0] != '0') ? 1 : 0;
+        g_exact.store(v);
+    }
+    return v != 0;
+}
+std::mutex g_exact_mu;
+std::unordered_set<const void*> g_exact_imgs;
+void exact_set(const void* img, bool on) {
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    if (on) {
+        if (g_exact_imgs.size() >= 65536) g_exact_imgs.clear();  // (far beyond any live set of buffers)
+        g_exact_imgs.insert(img);
+    } else {
+        g_exact_imgs.erase(img);
+    }
+}
+bool exact_get(const void* img) {
+    std::lock_guard<std::mutex> lk(g_exact_mu);
+    return g_exact_imgs.count(img) > 0;
+}
 // grow-only device scratch of one thread (the deterministic rows, the debug checks); the
 // calls that use it synchronise their stream before returning, so it is free again
 struct Scratch {
@@ -496,6 +525,11 @@ int gsr_set_survivor_lists(int on) {
     return GSR_OK;
 }
 int gsr_get_survivor_lists(void) { return surv_on() ? 1 : 0; }
+int gsr_set_exact_blend(int on) {
+    g_exact.store(on ? 1 : 0);
+    return GSR_OK;
+}
+int gsr_get_exact_blend(void) { return exact_on() ? 1 : 0; }
 // the backward's heavy-tile threshold (log2 of the estimate; < 0: the build's BWD_HEAVY_BITS)
 static std::atomic<int> g_bwd_heavy_bits{-1};
 int gsr_set_backward_heavy_bits(int bits) {
@@ -635,6 +669,8 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     if (!geom || !img) return fail(GSR_E_ALLOC, "gsr_forward: buffer allocation failed");
     geom = align_base(geom);
     img = align_base(img);
+    const bool exact = exact_on();
+    exact_set(img, exact);
     const unsigned gx = tiles_x(width), gy = tiles_y(height);
     const int T = (int)(gx * gy);
     if (!radii) radii = at<int>(geom, gl.radii);
@@ -794,6 +830,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = at<uint32_t>(img, il.tile_cost);
     ra.row_cost = at<uint32_t>(img, il.row_cost);
+    ra.exact = exact ? 1 : 0;
     if (surv && !mc) {  // the single-channel backward walks the forward's survivor lists
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
@@ -815,6 +852,7 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
                                                ra.nheavy, ra.tile_nmax, ra.tile_emax, *mc, c0);
                 ma.tile_cost = ra.tile_cost;
                 ma.row_cost = ra.row_cost;
+                ma.exact = ra.exact;
                 ma.out = mc->out + (size_t)c0 * width * height;
                 if (c0 == 0) {  // the other groups would write the same values
                     ma.final_T = ra.final_T;
@@ -957,6 +995,7 @@ int gsr_forward_reuse(gsr_resize_fn geometry_buffer, void* geometry_ctx, const v
     ra.tile_nmax = at<uint32_t>(img, il.tile_nmax);  // re-maxed with identical values
     ra.tile_emax = at<uint32_t>(img, il.tile_emax);
     ra.tile_cost = nullptr;  // already summed by the cached call's forward
+    ra.exact = exact_get(img) ? 1 : 0;  // the cached call's arithmetic
     // no survivor lists: the cached call's stay (its survivors are this call's -- they depend on the
     // geometry only -- and its buffer holds lists only if that forward stored them)
     if (!bin) return fail(GSR_E_ARG, "gsr_forward_reuse: missing binning buffer");
@@ -1038,6 +1077,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
         ra.order = at<uint32_t>(img, il.order_bwd);
         ra.nheavy = at<uint32_t>(img, il.nheavy) + 8;
         ra.partial = partial;
+        ra.exact = exact_get(img) ? 1 : 0;  // the forward's arithmetic
         ra.surv = at<uint2>(img, il.surv);
         ra.surv_n = at<uint32_t>(img, il.surv_n);
         {
@@ -1069,6 +1109,7 @@ static int backward_impl(int P, int D, int M, int R, const float* background, in
                     ma.partial = partial;
                     ma.pstride = pstride;
                     ma.pc0 = c0;
+                    ma.exact = ra.exact;
                     gsr::launch_render_bwd_mc(ma, s);
                 }
             }

@@ -234,6 +234,7 @@ struct RenderFwdArgs {
     // instead of re-filtering the super-tile list
     uint2* surv;
     uint32_t* surv_n;
+    int exact;  // the reference's blend arithmetic bit for bit (gsr_tile.hpp "exact mode")
 };
 void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s);
 
@@ -262,6 +263,7 @@ struct RenderBwdArgs {
     // all tiles when null) filter their super-tile list
     const uint2* surv;
     const uint32_t* surv_n;
+    int exact;  // the forward's exact mode, replayed
 };
 constexpr int DET_ROW3 = 12;  // 8 sums + the ninth's four row partials
 void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s);
@@ -300,6 +302,7 @@ struct RenderMcArgs {
     // survivor lists as RenderFwdArgs::surv (forward: stored when non-null) and RenderBwdArgs::surv
     uint2* surv;
     uint32_t* surv_n;
+    int exact;  // exact mode (RenderFwdArgs::exact)
 };
 void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s);
 void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s);

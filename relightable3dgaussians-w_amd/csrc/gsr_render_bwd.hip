@@ -35,7 +35,8 @@ __device__ unsigned long long g_bwd_times[GSR_UNIT_REC * 65536];
 #define BWD_STAT(k, v)
 #endif
 
-template <bool DET>
+// EXACT: the forward's exact mode replayed (gsr_tile.hpp): the same power, G and alpha bits
+template <bool DET, bool EXACT>
 __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -44,6 +45,8 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
 
     const float pxq[2] = {wt.pfx, wt.pfx + 8.f}, pyq[2] = {wt.pfy, wt.pfy + 8.f};
     __shared__ float4 s_a[64], s_b[64], s_c[64];
+    __shared__ unsigned long long s_gexp[EXACT ? 32 : 1];  // exact mode: glibc_expf's table
+    if (EXACT) gexp_table_init(s_gexp);
     // per quadrant pixel state: T, dL/dpix, the background term, and the recurrence of
     // backward.cu:514-537 carried as one dot product with dL/dpix: Sr = accum_rec . dL/dpix
     // of the Gaussians behind the current one.  The reference updates accum_rec one step
@@ -133,9 +136,9 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             if (!lst) qm = wt.reach(r, p, qlim);
-            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
-            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
-            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e) (exact mode: raw)
+            ra = EXACT ? r.a : make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = EXACT ? r.b : make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // records to LDS; survivors are read back with broadcast LDS loads (LDS pipe)
@@ -172,9 +175,17 @@ __device__ __forceinline__ void render_bwd_tile(const RenderBwdArgs& a, const un
                 BWD_STAT(2, 1);
                 dx = ax - pxq[q & 1];
                 dy = ay - pyq[q >> 1];
-                const float power = gauss_power(ka, kb, kc, dx, dy);
-                G = tile_exp2(power);
-                alpha = fminf(0.99f, op * G);
+                float power;
+                if (EXACT) {  // backward.cu:494-500 with the forward's exact bits
+#pragma clang fp contract(off)
+                    power = ref_power(ka, kb, kc, dx, dy);
+                    G = glibc_expf(power, s_gexp);
+                    alpha = fminf(0.99f, op * G);
+                } else {
+                    power = gauss_power(ka, kb, kc, dx, dy);
+                    G = tile_exp2(power);
+                    alpha = fminf(0.99f, op * G);
+                }
                 // active: pos < last && !(power > 0) && !(alpha < 1/255)
                 // (compare results are 0 on inactive lanes, and every lane is on: no exec masking)
                 act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
@@ -290,7 +301,14 @@ k_render_bwd(RenderBwdArgs a) {
     unsigned tile;
     uint32_t qallow;
     if (!tile_unit_bwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET)) return;
-    render_bwd_tile<DET>(a, tile, qallow);
+    render_bwd_tile<DET, false>(a, tile, qallow);
+}
+template <bool DET>
+__global__ void __launch_bounds__(64) k_render_bwd_exact(RenderBwdArgs a) {
+    unsigned tile;
+    uint32_t qallow;
+    if (!tile_unit_bwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow, DET)) return;
+    render_bwd_tile<DET, true>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -318,8 +336,13 @@ void launch_render_bwd(const RenderBwdArgs& a, hipStream_t s) {
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
     const dim3 grid(tile_pass_blocks_bal(ntile, 0u));
-    if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
-    else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
+    if (a.exact) {
+        if (a.partial) hipLaunchKernelGGL(k_render_bwd_exact<true>, grid, dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(k_render_bwd_exact<false>, grid, dim3(64), 0, s, a);
+    } else {
+        if (a.partial) hipLaunchKernelGGL(k_render_bwd<true>, grid, dim3(64), 0, s, a);
+        else hipLaunchKernelGGL(k_render_bwd<false>, grid, dim3(64), 0, s, a);
+    }
 }
 
 }  // namespace gsr

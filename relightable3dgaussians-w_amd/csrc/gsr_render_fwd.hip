@@ -35,6 +35,9 @@ __device__ unsigned long long g_fwd_times[GSR_UNIT_REC * 65536];
 #define FWD_STAT(k, v)
 #endif
 
+// EXACT: the reference's blend arithmetic bit for bit (gsr_tile.hpp "exact mode"): the raw conic
+// staged, the reference-order power, glibc's expf, the reference's colour order
+template <bool EXACT>
 __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -50,6 +53,8 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_c[64];  // (colour b, quadrant mask, -, -): 16-B rows, one LDS address for all three reads
     __shared__ uint32_t s_e[64];  // entry index
+    __shared__ unsigned long long s_gexp[EXACT ? 32 : 1];  // exact mode: glibc_expf's table
+    if (EXACT) gexp_table_init(s_gexp);
     float T[4], C0[4], C1[4], C2[4];
     float lim[4];  // alpha a Gaussian must reach to blend: 1/255, or +inf once the pixel is done
     uint32_t last[4];
@@ -90,9 +95,9 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             // a quadrant unit culls its batch against its own quadrant only (k_render_fwd 238.1 ->
             // 236.9 us, profiles/r5z_reach_own_ab.txt)
             qm = wt.reach(r, j, nullptr, qallow);
-            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e)
-            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
-            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
+            // conic as gauss_power takes it: (-a/2, -b, -c/2) log2(e) (exact mode: raw)
+            ra = EXACT ? r.a : make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = EXACT ? r.b : make_float4(TILE_STAGE_AC * r.b.x, r.b.y, r.b.z, r.b.w);
             rc = r.c.x;
         }
         // the batch's records go to LDS; the walk below reads each survivor's record with
@@ -138,8 +143,15 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
-                const float power = gauss_power(A.z, A.w, B.x, dx, dy);
-                const float alpha = fminf(0.99f, B.y * tile_exp2(power));
+                float power, alpha;
+                if (EXACT) {  // forward.cu:335-343
+#pragma clang fp contract(off)
+                    power = ref_power(A.z, A.w, B.x, dx, dy);
+                    alpha = fminf(0.99f, B.y * glibc_expf(power, s_gexp));
+                } else {
+                    power = gauss_power(A.z, A.w, B.x, dx, dy);
+                    alpha = fminf(0.99f, B.y * tile_exp2(power));
+                }
                 // hit: !(power > 0) && alpha >= lim (masks and selects in SGPR pairs, see m_ge)
                 // (compare results are 0 on inactive lanes, and the walk runs with every lane on:
                 // no exec masking; each mask op below is one SALU instruction)
@@ -150,10 +162,17 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
                 const float test_T = T[q] * (1 - alpha);
                 const lmask lt = m_lt(test_T, 0.0001f);  // saturating Gaussian is not blended
                 const lmask blend = hit & ~lt, sat = hit & lt;
-                const float w = sel(blend, alpha * T[q], 0.f);
-                C0[q] += B.z * w;
-                C1[q] += B.w * w;
-                C2[q] += Cq.x * w;
+                if (EXACT) {  // forward.cu:359: C += feature * alpha * T, left to right
+#pragma clang fp contract(off)
+                    C0[q] = sel(blend, C0[q] + B.z * alpha * T[q], C0[q]);
+                    C1[q] = sel(blend, C1[q] + B.w * alpha * T[q], C1[q]);
+                    C2[q] = sel(blend, C2[q] + Cq.x * alpha * T[q], C2[q]);
+                } else {
+                    const float w = sel(blend, alpha * T[q], 0.f);
+                    C0[q] += B.z * w;
+                    C1[q] += B.w * w;
+                    C2[q] += Cq.x * w;
+                }
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
                 blended |= blend;
@@ -214,9 +233,16 @@ __device__ __forceinline__ void render_fwd_tile(const RenderFwdArgs& a, const un
             const int pix = wt.pixel(q, a.W);
             a.final_T[pix] = T[q];
             a.n_contrib[pix] = last[q];
-            a.out_color[pix] = C0[q] + T[q] * a.bg[0];
-            a.out_color[HW + pix] = C1[q] + T[q] * a.bg[1];
-            a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
+            if (EXACT) {  // forward.cu:372
+#pragma clang fp contract(off)
+                a.out_color[pix] = C0[q] + T[q] * a.bg[0];
+                a.out_color[HW + pix] = C1[q] + T[q] * a.bg[1];
+                a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
+            } else {
+                a.out_color[pix] = C0[q] + T[q] * a.bg[0];
+                a.out_color[HW + pix] = C1[q] + T[q] * a.bg[1];
+                a.out_color[2 * HW + pix] = C2[q] + T[q] * a.bg[2];
+            }
         }
     }
     if (lane == 0 && a.surv && qallow == 15u) a.surv_n[tile] = scnt;
@@ -243,7 +269,15 @@ k_render_fwd(RenderFwdArgs a) {
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
     if (!tile_unit_fwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_fwd_tile(a, tile, qallow);
+    render_fwd_tile<false>(a, tile, qallow);
+}
+// exact mode (gsr_set_exact_blend): the registers its double-precision expf needs, no occupancy target
+__global__ void __launch_bounds__(64) k_render_fwd_exact(RenderFwdArgs a) {
+    unsigned tile;
+    uint32_t qallow;
+    zero_slice(a.zero, a.zero_n4);
+    if (!tile_unit_fwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
+    render_fwd_tile<true>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -270,7 +304,8 @@ void launch_render_fwd(const RenderFwdArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0) return;
     // one block per unit of the longest band (heavy tiles count four); the rest exit
-    hipLaunchKernelGGL(k_render_fwd, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
+    if (a.exact) hipLaunchKernelGGL(k_render_fwd_exact, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
+    else hipLaunchKernelGGL(k_render_fwd, dim3(tile_pass_blocks(ntile, FWD_TAIL_SPLIT)), dim3(64), 0, s, a);
 }
 
 }  // namespace gsr

@@ -27,7 +27,8 @@ namespace gsr {
 
 // NCH: channels composited (<= 4 NC4; render()'s layout has 14, so its group skips the two
 // padding channels' FMAs and reduction slots)
-template <int NC4, int NCH = 4 * NC4>
+// EXACT: the reference's blend arithmetic bit for bit (gsr_tile.hpp "exact mode")
+template <int NC4, int NCH = 4 * NC4, bool EXACT = false>
 __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -42,6 +43,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
     __shared__ float4 s_a[64], s_b[64];
     __shared__ float4 s_f[NC4][64];
     __shared__ uint32_t s_q[64], s_e[64];  // quadrant mask, entry index
+    __shared__ unsigned long long s_gexp[EXACT ? 32 : 1];  // exact mode: glibc_expf's table
+    if (EXACT) gexp_table_init(s_gexp);
     float T[4], Cc[4][NCH], lim[4];
     uint32_t last[4];
     uint32_t live = 0;
@@ -74,8 +77,8 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             qm = wt.reach(r, j, nullptr, qallow);  // (a quadrant unit tests its own only)
-            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
-            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
+            ra = EXACT ? r.a : make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(EXACT ? r.b.x : TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
@@ -117,15 +120,21 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
                 const float dx = A.x - pxq[q & 1], dy = A.y - pyq[q >> 1];
-                const float power = gauss_power(A.z, A.w, B.x, dx, dy);
-                const float alpha = fminf(0.99f, B.y * tile_exp2(power));
+                float power, alpha;
+                if (EXACT) {
+#pragma clang fp contract(off)
+                    power = ref_power(A.z, A.w, B.x, dx, dy);
+                    alpha = fminf(0.99f, B.y * glibc_expf(power, s_gexp));
+                } else {
+                    power = gauss_power(A.z, A.w, B.x, dx, dy);
+                    alpha = fminf(0.99f, B.y * tile_exp2(power));
+                }
                 // (compare results are 0 on inactive lanes, and the walk runs with every lane on:
                 // no exec masking; each mask op below is one SALU instruction)
                 const lmask hit = m_ge(alpha, lim[q]) & ~m_gt0(power);
                 const float test_T = T[q] * (1 - alpha);
                 const lmask lt = m_lt(test_T, 0.0001f);
                 const lmask blend = hit & ~lt, sat = hit & lt;
-                const float w = sel(blend, alpha * T[q], 0.f);
                 float Fs[4 * NC4];
 #pragma unroll
                 for (int g = 0; g < NC4; g++) {
@@ -134,8 +143,16 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
                     Fs[4 * g + 2] = F[g].z;
                     Fs[4 * g + 3] = F[g].w;
                 }
+                if (EXACT) {  // forward.cu:359: C += feature * alpha * T, left to right
+#pragma clang fp contract(off)
 #pragma unroll
-                for (int c = 0; c < NCH; c++) Cc[q][c] += Fs[c] * w;
+                    for (int c = 0; c < NCH; c++)
+                        Cc[q][c] = sel(blend, Cc[q][c] + Fs[c] * alpha * T[q], Cc[q][c]);
+                } else {
+                    const float w = sel(blend, alpha * T[q], 0.f);
+#pragma unroll
+                    for (int c = 0; c < NCH; c++) Cc[q][c] += Fs[c] * w;
+                }
                 T[q] = sel(blend, test_T, T[q]);
                 last[q] = sel(blend, pos1, last[q]);
                 blended |= blend;
@@ -160,7 +177,14 @@ __device__ __forceinline__ void render_fwd_mc_tile(const RenderMcArgs& a, const 
             }
 #pragma unroll
             for (int c = 0; c < NCH; c++)
-                if (c < a.nch) a.out[c * HW + pix] = Cc[q][c] + T[q] * a.bg[c];
+                if (c < a.nch) {
+                    if (EXACT) {
+#pragma clang fp contract(off)
+                        a.out[c * HW + pix] = Cc[q][c] + T[q] * a.bg[c];
+                    } else {
+                        a.out[c * HW + pix] = Cc[q][c] + T[q] * a.bg[c];
+                    }
+                }
         }
     }
     if (a.tile_nmax) {
@@ -189,7 +213,7 @@ struct McBwdLds {
 };
 
 // The back-to-front walk of one tile over its NL = NCH channels.
-template <int NC4, int NCH, bool DET>
+template <int NC4, int NCH, bool DET, bool EXACT>
 __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigned tile, const WaveTile& wt,
                                             McBwdLds<NC4>& sm, float (&T)[4], const float (&Tb)[4],
                                             const float (&dpl)[4][NCH], const uint32_t (&last)[4],
@@ -229,6 +253,8 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
     if (!lst)
         tl.init(a.ent, a.st_ranges[st], tile, a.grid_x, sth, nmax ? a.tile_emax[tile] : 0u, nmax ? a.tile_nmax[tile] : 0u);
     const uint32_t rbase = DET ? a.ranges[tile].x : 0u;
+    __shared__ unsigned long long s_gexp[EXACT ? 32 : 1];  // exact mode: glibc_expf's table
+    if (EXACT) gexp_table_init(s_gexp);
     for (;;) {
         uint32_t id = 0, nb, p, qm = 0;  // p: list position (back to front)
         if (lst) {
@@ -258,8 +284,8 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
         if ((uint32_t)lane < nb) {
             const Rec r = a.rec[id];
             if (!lst) qm = wt.reach(r, p, qlim);
-            ra = make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
-            rb = make_float4(TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
+            ra = EXACT ? r.a : make_float4(r.a.x, r.a.y, TILE_STAGE_AC * r.a.z, TILE_STAGE_B * r.a.w);
+            rb = make_float4(EXACT ? r.b.x : TILE_STAGE_AC * r.b.x, r.b.y, 0.f, 0.f);
 #pragma unroll
             for (int g = 0; g < NC4; g++) f[g] = a.feat[(size_t)id * a.fstride4 + g];
         }
@@ -298,9 +324,17 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
             for (int q = 0; q < 4; q++) {
                 if (!((m >> q) & 1u)) continue;
                 const float dx = ax - pxq[q & 1], dy = ay - pyq[q >> 1];
-                const float power = gauss_power(ka, kb, kc, dx, dy);
-                const float G = tile_exp2(power);
-                const float alpha = fminf(0.99f, op * G);
+                float power, G, alpha;
+                if (EXACT) {
+#pragma clang fp contract(off)
+                    power = ref_power(ka, kb, kc, dx, dy);
+                    G = glibc_expf(power, s_gexp);
+                    alpha = fminf(0.99f, op * G);
+                } else {
+                    power = gauss_power(ka, kb, kc, dx, dy);
+                    G = tile_exp2(power);
+                    alpha = fminf(0.99f, op * G);
+                }
                 // (compare results are 0 on inactive lanes, and every lane is on: no exec masking)
                 const lmask act = (m_ult(pos, last[q]) & ~m_gt0(power)) & ~m_lt(alpha, 1.0f / 255.0f);
                 if (act == 0ull) continue;
@@ -368,7 +402,7 @@ __device__ __forceinline__ void mc_bwd_walk(const RenderMcArgs& a, const unsigne
 // (Round 5 also measured a split into two launches, one walking the tiles with at most 10 live
 // channels over those only: k_render_bwd_mc 0.60 -> 0.79 ms per view at cfg4,
 // profiles/r5x_mc_live_ab.txt.)
-template <int NC4, int NCH, bool DET>
+template <int NC4, int NCH, bool DET, bool EXACT>
 __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const unsigned tile, const uint32_t qallow) {
     WaveTile wt;
     wt.init(tile, a.grid_x, a.W, a.H);
@@ -394,16 +428,16 @@ __device__ __forceinline__ void render_bwd_mc_tile(const RenderMcArgs& a, const 
         qlim[q] = ((qallow >> q) & 1u) ? wave_max_u32(last[q]) : 0u;
         nmax = qlim[q] > nmax ? qlim[q] : nmax;
     }
-    mc_bwd_walk<NC4, NCH, DET>(a, tile, wt, sm, T, Tb, dp, last, qlim, nmax);
+    mc_bwd_walk<NC4, NCH, DET, EXACT>(a, tile, wt, sm, T, Tb, dp, last, qlim, nmax);
 }
 
-template <int NC4, int NCH = 4 * NC4>
+template <int NC4, int NCH = 4 * NC4, bool EXACT = false>
 __global__ void __launch_bounds__(64) k_render_fwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
     zero_slice(a.zero, a.zero_n4);
     if (!tile_unit_fwd(a.grid_x * a.grid_y, a.order, a.nheavy, tile, qallow)) return;
-    render_fwd_mc_tile<NC4, NCH>(a, tile, qallow);
+    render_fwd_mc_tile<NC4, NCH, EXACT>(a, tile, qallow);
 }
 
 #ifdef GSR_RENDER_STATS
@@ -423,7 +457,7 @@ extern "C" int gsr_debug_mcb_times(unsigned long long* out, int n, int reset) {
 }
 #endif
 
-template <int NC4, int NCH = 4 * NC4, bool DET = false>
+template <int NC4, int NCH = 4 * NC4, bool DET = false, bool EXACT = false>
 __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
     unsigned tile;
     uint32_t qallow;
@@ -431,7 +465,7 @@ __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
 #ifdef GSR_RENDER_STATS
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    render_bwd_mc_tile<NC4, NCH, DET>(a, tile, qallow);
+    render_bwd_mc_tile<NC4, NCH, DET, EXACT>(a, tile, qallow);
 #ifdef GSR_RENDER_STATS
     if (threadIdx.x == 0 && blockIdx.x < (unsigned)MCB_UNITS) {
         unsigned long long* r = g_mcb_times[0] + 4 * (size_t)blockIdx.x;
@@ -443,33 +477,36 @@ __global__ void __launch_bounds__(64) k_render_bwd_mc(RenderMcArgs a) {
 #endif
 }
 
-void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
-    const unsigned ntile = a.grid_x * a.grid_y;
-    if (ntile == 0 || a.nch <= 0) return;
-    const dim3 grid(tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
+template <bool EXACT>
+static void launch_fwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s) {
     switch ((a.nch + 3) / 4) {
-        case 1: hipLaunchKernelGGL(k_render_fwd_mc<1>, grid, dim3(64), 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_render_fwd_mc<2>, grid, dim3(64), 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_render_fwd_mc<3>, grid, dim3(64), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_render_fwd_mc<1, 4, EXACT>), grid, dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_render_fwd_mc<2, 8, EXACT>), grid, dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_render_fwd_mc<3, 12, EXACT>), grid, dim3(64), 0, s, a); break;
         default:
-            if (a.nch == 14) hipLaunchKernelGGL((k_render_fwd_mc<4, 14>), grid, dim3(64), 0, s, a);
-            else hipLaunchKernelGGL(k_render_fwd_mc<4>, grid, dim3(64), 0, s, a);
+            if (a.nch == 14) hipLaunchKernelGGL((k_render_fwd_mc<4, 14, EXACT>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_render_fwd_mc<4, 16, EXACT>), grid, dim3(64), 0, s, a);
             break;
     }
 }
 
-template <bool DET>
+void launch_render_fwd_mc(const RenderMcArgs& a, hipStream_t s) {
+    const unsigned ntile = a.grid_x * a.grid_y;
+    if (ntile == 0 || a.nch <= 0) return;
+    const dim3 grid(tile_pass_blocks(ntile, FWD_TAIL_SPLIT));
+    if (a.exact) launch_fwd_mc<true>(a, grid, s);
+    else launch_fwd_mc<false>(a, grid, s);
+}
+
+template <bool DET, bool EXACT>
 static void launch_bwd_mc(const RenderMcArgs& a, const dim3 grid, hipStream_t s) {
     switch ((a.nch + 3) / 4) {
-        case 1: hipLaunchKernelGGL((k_render_bwd_mc<1, 4, DET>), grid, dim3(64), 0, s, a); break;
-        case 2: hipLaunchKernelGGL((k_render_bwd_mc<2, 8, DET>), grid, dim3(64), 0, s, a); break;
-        case 3: hipLaunchKernelGGL((k_render_bwd_mc<3, 12, DET>), grid, dim3(64), 0, s, a); break;
+        case 1: hipLaunchKernelGGL((k_render_bwd_mc<1, 4, DET, EXACT>), grid, dim3(64), 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_render_bwd_mc<2, 8, DET, EXACT>), grid, dim3(64), 0, s, a); break;
+        case 3: hipLaunchKernelGGL((k_render_bwd_mc<3, 12, DET, EXACT>), grid, dim3(64), 0, s, a); break;
         default:
-            if (a.nch == 14) {
-                hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET>), grid, dim3(64), 0, s, a);
-            } else {
-                hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET>), grid, dim3(64), 0, s, a);
-            }
+            if (a.nch == 14) hipLaunchKernelGGL((k_render_bwd_mc<4, 14, DET, EXACT>), grid, dim3(64), 0, s, a);
+            else hipLaunchKernelGGL((k_render_bwd_mc<4, 16, DET, EXACT>), grid, dim3(64), 0, s, a);
             break;
     }
 }
@@ -478,8 +515,13 @@ void launch_render_bwd_mc(const RenderMcArgs& a, hipStream_t s) {
     const unsigned ntile = a.grid_x * a.grid_y;
     if (ntile == 0 || a.nch <= 0) return;
     const dim3 grid(tile_pass_blocks_bal(ntile, 0u));
-    if (a.partial) launch_bwd_mc<true>(a, grid, s);
-    else launch_bwd_mc<false>(a, grid, s);
+    if (a.exact) {
+        if (a.partial) launch_bwd_mc<true, true>(a, grid, s);
+        else launch_bwd_mc<false, true>(a, grid, s);
+    } else {
+        if (a.partial) launch_bwd_mc<true, false>(a, grid, s);
+        else launch_bwd_mc<false, false>(a, grid, s);
+    }
 }
 
 }  // namespace gsr

@@ -420,6 +420,66 @@ __device__ __forceinline__ float gauss_power(float na, float nb, float nc, float
     return __builtin_fmaf(na * dx, dx, __builtin_fmaf(nc * dy, dy, (nb * dx) * dy));
 }
 
+// ---- exact mode: the reference's blend arithmetic bit for bit ------------------------------
+// The fast evaluation above (prescaled conic, two FMAs, v_exp_f32) decides a (pixel, Gaussian)
+// pair differently from the reference's float arithmetic only where the exponent is within
+// rounding of a threshold (alpha within ulps of 1/255, a transmittance within ulps of 1e-4): a
+// pixel or two per frame.  A guard band around the alpha threshold -- the pairs there
+// re-evaluated with the oracle's arithmetic -- measured +7.8 % on the 3-stream headline and +3 % on
+// the single call (round 6: the forward to five waves per SIMD, one add and one compare per
+// evaluation in both passes), and it cannot reach the transmittance decisions, which depend on
+// every earlier alpha of the pixel.  So bit-parity is a mode: with gsr_set_exact_blend(1) the tile
+// passes evaluate every pair as the reference does --
+//   power = -0.5f * (a dx dx + c dy dy) - b dx dy  in its operation order, no contraction
+//   G = expf(power)                                 glibc's algorithm (the oracle's libm), below
+//   alpha = min(0.99f, o * G),  C += (colour * alpha) * T,  out = C + T * bg
+// (forward.cu:335-359, oracle/gsr_oracle.c:437-456; every such block under `#pragma clang fp
+// contract(off)`) -- so the forward's colours, transmittance and
+// n_contrib equal the canonical oracle's bit for bit and the backward replays the same decisions
+// (its gradients differ by summation order only).
+// (plain operators under the pragma: HIP's __fmul_rn / __fadd_rn are operators in functions of
+// their own, compiled with contraction on, so LLVM may still fuse them into FMAs once inlined)
+__device__ __forceinline__ float ref_power(float a, float b, float c, float dx, float dy) {
+#pragma clang fp contract(off)
+    return -0.5f * (a * dx * dx + c * dy * dy) - b * dx * dy;
+}
+// glibc's expf (sysdeps/ieee754/flt-32/e_expf.c, the ARM optimized-routines algorithm the oracle's
+// libm runs; on FMA hosts the __expf_fma build, whose contractions are reproduced here): x = (k +
+// r) ln2 / 32 with k = round(x 32 / ln2), 2^(k/32) from a 32-entry table of asuint64(2^(i/32)) -
+// (i << 47), 2^(r/32) by a cubic, all in double.  Equal to the host libm's expf on every float in
+// [-104, 8] (2.2e9 inputs checked, tools/check_glibc_expf.c); below log(2^-150) it is 0, as glibc's
+// underflow path returns.  tab: the table in LDS (gexp_table_init).
+constexpr unsigned long long GEXP_TAB[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+__device__ __forceinline__ void gexp_table_init(unsigned long long* tab) {
+    const int lane = threadIdx.x & 63;
+    if (lane < 32) tab[lane] = GEXP_TAB[lane];
+}
+__device__ __forceinline__ float glibc_expf(float x, const unsigned long long* tab) {
+#pragma clang fp contract(off)
+    constexpr double INVLN2N = 0x1.71547652b82fep+5, SHIFT = 0x1.8p+52;
+    const double xd = (double)x;
+    double kd = __builtin_fma(xd, INVLN2N, SHIFT);
+    const unsigned long long ki = __double_as_longlong(kd);
+    kd -= SHIFT;
+    const double r = __builtin_fma(xd, INVLN2N, -kd);
+    const unsigned long long t = tab[ki & 31u] + (ki << 47);
+    const double s = __longlong_as_double((long long)t);
+    const double zz = __builtin_fma(0x1.c6af84b912394p-20, r, 0x1.ebfce50fac4f3p-13);
+    const double r2 = r * r;
+    double y = __builtin_fma(r, 0x1.62e42ff0c52d6p-6, 1.0);
+    y = __builtin_fma(zz, r2, y);
+    y = y * s;
+    return x < -0x1.9fe368p6f ? 0.f : (float)y;
+}
+
 // Lane masks in SGPR pairs and selects on them (v_cmp_*_e64 / v_cndmask_b32_e64).  On
 // gfx950 a v_cndmask_b32 that reads its mask from VCC (the VOP2 form the compiler picks
 // for `c ? a : b`) issues ~5x slower than the VOP3 form reading any other SGPR pair
@@ -433,6 +493,11 @@ __device__ __forceinline__ lmask m_gt0(float a) {  // a > 0
 __device__ __forceinline__ lmask m_ge(float a, float b) {  // a >= b (false on NaN)
     lmask m;
     asm("v_cmp_ge_f32_e64 %0, %1, %2" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ lmask m_lt1(float a) {  // a < 1
+    lmask m;
+    asm("v_cmp_gt_f32_e64 %0, 1.0, %1" : "=s"(m) : "v"(a));
     return m;
 }
 __device__ __forceinline__ lmask m_lt(float a, float b) {  // a < b

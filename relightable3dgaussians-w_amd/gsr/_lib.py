@@ -3,6 +3,7 @@
 The product path: every call lands in hand-written HIP for gfx950.  There is no CPU or
 PyTorch fallback -- if the library or a GPU is missing, calls raise.
 """
+import contextlib
 import ctypes as C
 import os
 import subprocess
@@ -104,6 +105,7 @@ def _declare(lib):
     lib.gsr_profile_read.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_longlong), i, i]
     lib.gsr_set_deterministic.argtypes = [i]
     lib.gsr_set_survivor_lists.argtypes = [i]
+    lib.gsr_set_exact_blend.argtypes = [i]
     lib.gsr_set_backward_heavy_bits.argtypes = [i]
     lib.gsr_check_buffers.argtypes = [i, i, i, i, vp, vp, vp, vp, vp]
     lib.gsr_materialize_lists.argtypes = [i, i, i, vp, vp, vp, vp]
@@ -119,7 +121,7 @@ def _declare(lib):
                "gsr_view_regularisers_tail_backward", "gsr_densify_stats", "gsr_sh_basis", "gsr_sky_xyz_forward",
                "gsr_sky_xyz_backward", "gsr_activations_forward", "gsr_activations_backward",
                "gsr_texture2d_forward", "gsr_texture2d_backward", "gsr_get_layout", "gsr_set_deterministic",
-               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_set_backward_heavy_bits", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
+               "gsr_get_deterministic", "gsr_set_survivor_lists", "gsr_get_survivor_lists", "gsr_set_exact_blend", "gsr_get_exact_blend", "gsr_set_backward_heavy_bits", "gsr_debug_build", "gsr_check_buffers", "gsr_materialize_lists"):
         getattr(lib, fn).restype = C.c_int
 
 
@@ -192,6 +194,29 @@ def set_survivor_lists(on=True):
 
 def survivor_lists():
     return bool(lib().gsr_get_survivor_lists())
+
+
+def set_exact_blend(on=True):
+    """Exact blend mode (gsr_set_exact_blend): the tile passes evaluate every (pixel, Gaussian)
+    pair with the reference's float arithmetic bit for bit (forward colours, transmittance and
+    n_contrib equal the canonical oracle's; slower).  Takes effect at the next forward; its
+    backward replays that forward's mode."""
+    check(lib().gsr_set_exact_blend(int(bool(on))), "gsr_set_exact_blend")
+
+
+def exact_blend():
+    return bool(lib().gsr_get_exact_blend())
+
+
+@contextlib.contextmanager
+def exact_blend_mode(on=True):
+    """with _lib.exact_blend_mode(): ... -- exact blend mode inside the block, restored after."""
+    before = exact_blend()
+    set_exact_blend(on)
+    try:
+        yield
+    finally:
+        set_exact_blend(before)
 
 
 def set_backward_heavy_bits(bits=-1):

@@ -73,8 +73,14 @@ def test_full_preprocess_bit_exact(full):
     np.testing.assert_array_equal(st["depth_key"][vis], ref["depths"][vis].view(np.uint32))
 
 
-def test_cfg2_binning_invariants(cfg2):
-    cam, gs, c, st = cfg2
+def test_full_binning_invariants(full):
+    """The binning at size on every full-size cloud (cfg2 uniform, cfg2c clustered with
+    screen-filling splats, cfg5 at 4K with 8x8 super-tiles), through the reference's point_list
+    and ranges materialised from the super-tile lists (rasterizer_impl.cu:70-138): every visible
+    Gaussian listed exactly tiles_touched times (tiles_touched is bit-exact against the oracle in
+    test_full_preprocess_bit_exact), every listed rect covering its tile, (depth, index) order
+    inside each tile.  A Gaussian dropped from a super-tile list would fail the counts."""
+    cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
     R, pl, rg = st["R"], st["point_list"].astype(np.int64), st["ranges"].astype(np.int64)
@@ -174,13 +180,43 @@ def test_full_sampled_tiles_forward(full):
     assert rel_l2(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m]) <= 1e-6
 
 
+def test_full_sampled_tiles_exact(full):
+    """Exact blend mode at full size (cfg2, the clustered cfg2c with pixels blending ~2.7k
+    Gaussians, cfg5 at 4K): the oracle's colours, final transmittance and n_contrib on the sampled
+    tiles bit for bit -- no decision within ulps of alpha = 1/255 or T = 1e-4 taken the other way
+    -- and the backward's sampled gradients within 1e-4."""
+    from gsr import _lib
+    cam, gs, c, _ = full
+    W, H = cam.image_width, cam.image_height
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    with _lib.exact_blend_mode():
+        st = run_gpu(cam, gs, mode="sh", sh_degree=c["sh_degree"])
+    tiles = _sample_tiles(gx, gy, ranges=st["ranges"])
+    rec = st["rec"]
+    out, fT, nc = orc.render_fwd(st["ranges"], st["point_list"], rec[:, 0:2], rec[:, 6:9], rec[:, 2:6],
+                                 np.zeros(3, np.float32), W, H, tiles=tiles)
+    m = _tile_mask(tiles, gx, W, H)
+    np.testing.assert_array_equal(st["n_contrib"].reshape(H, W)[m], nc.reshape(H, W)[m])
+    np.testing.assert_array_equal(st["final_T"].reshape(H, W)[m], fT.reshape(H, W)[m])
+    np.testing.assert_array_equal(st["color"].cpu().numpy()[:, m], out[:, m])
+    if c.get("clustered"):
+        _sampled_backward_check(cam, gs, c, st, tiles, m)
+    del st
+
+
 def test_full_sampled_tiles_backward(full):
     cam, gs, c, st = full
     W, H = cam.image_width, cam.image_height
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    P = gs["means3D"].shape[0]
     tiles = _sample_tiles(gx, gy, ranges=st["ranges"])
-    m = _tile_mask(tiles, gx, W, H)
+    _sampled_backward_check(cam, gs, c, st, tiles, _tile_mask(tiles, gx, W, H))
+
+
+def _sampled_backward_check(cam, gs, c, st, tiles, m):
+    """The backward with dL/dpix zero outside the sampled tiles against the oracle's backward of
+    the same tiles (from the GPU's lists and records): every gradient within 1e-4."""
+    W, H = cam.image_width, cam.image_height
+    P = gs["means3D"].shape[0]
     dout = np.random.default_rng(9).standard_normal((3, H, W)).astype(np.float32) * m[None]
     g = _grads(cam, gs, st, torch.tensor(dout, device="cuda"), c["sh_degree"])
     torch.cuda.synchronize()

@@ -187,6 +187,24 @@ def test_forward_parity(case):
 
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_forward_parity_exact(case):
+    """Exact blend mode (gsr_set_exact_blend; gsr_tile.hpp "exact mode"): the forward's colours,
+    final transmittance and n_contrib equal the canonical oracle's bit for bit, on every case."""
+    from gsr import _lib
+    cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
+                        camera=case.get("camera", "identity"))
+    gs = mutate(gs, case.get("mutate"))
+    kw = dict(mode=case["mode"], bg=case.get("bg", (0.0, 0.0, 0.0)), scale_modifier=case.get("scale_modifier", 1.0),
+              sh_degree=case.get("sh_degree", 0))
+    with _lib.exact_blend_mode():
+        st = run_gpu(cam, gs, cov=case.get("cov", False), **kw)
+    ref = run_oracle(cam, gs, cov3=st["cov3"].cpu().numpy() if case.get("cov") else None, **kw)
+    check_forward(st, ref, cam.image_width, cam.image_height)
+    np.testing.assert_array_equal(st["color"].cpu().numpy(), ref["color"])
+    np.testing.assert_array_equal(st["final_T"], ref["final_T"])
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_backward_parity(case):
     _, _C, _ = _dgr()
     cam, gs = make_case(P=case["P"], W=case["W"], H=case["H"], sh_degree=case.get("sh_degree", 0),
@@ -246,6 +264,17 @@ def test_backward_parity_quadrant_units(name, bits):
         test_backward_parity(case)
     finally:
         _lib.set_backward_heavy_bits(-1)
+
+
+@pytest.mark.parametrize("name", ["faint_opacity", "sh3_orbit_bg", "heavy_tiles", "opaque_stack", "wide_strip_520_tiles"])
+def test_backward_parity_exact(name):
+    """The backward over an exact-mode forward replays its arithmetic (the mode recorded with the
+    image buffer): every gradient within the same 1e-4 of the oracle.  faint_opacity puts
+    alpha ~ 1/255 everywhere, opaque_stack saturates most pixels early."""
+    _, _, _lib = _dgr()
+    case = next(c for c in CASES if c["name"] == name)
+    with _lib.exact_blend_mode():
+        test_backward_parity(case)
 
 
 def test_autograd_module_path():
