@@ -21,9 +21,6 @@
  *                      render()'s per-Gaussian colour preparation (normals, shade, sky
  *                      colour, depth; gaussian_renderer/__init__.py:120-200) fused into
  *                      the composite's feature rows
- *   gsr_forward_channels_relit
- *                      the same shade inside the composite's forward, for the visible
- *                      Gaussians only
  *   gsr_adam_step      torch.optim.Adam.step over the per-Gaussian param groups
  *   gsr_adam_step_range  the same over one element range (the pipelined data-parallel step)
  *                      (train.py:191, relit3DGW_model.py:149) as one fused launch over a
@@ -176,50 +173,16 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
  * the backward (it holds the foreground normals).  features must be 16-B aligned (each
  * 64-B row is written whole by one kernel). */
 size_t gsr_relit_workspace_bytes(int P, int N_fg, int deg, int sky_deg);
-/* The shade inputs of gsr_relit_features as one struct (gsr_forward_channels_relit). */
-typedef struct gsr_relit_spec {
-    int N_fg, deg, specular, sky_deg;
-    const float* xyz;
-    const float* rotation;
-    const float* scaling;
-    const int* fg_rank;
-    const int* fg_rows;
-    const float* albedo;
-    const float* roughness;
-    const float* metalness;
-    const float* base;
-    const float* fg_lut;
-    const float* sky_sh;
-    const float* campos;
-    const float* viewmatrix;
-    void* workspace;
-} gsr_relit_spec;
 int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
                        const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
                        const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
                        int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
                        float* features, void* workspace, void* stream);
-/* Visible-only relit forward: gsr_forward_channels whose features
- * [P][16] are shaded inside the call, after the preprocess and only for the Gaussians it
- * kept (radii > 0), on a second stream overlapped with the depth sort and the binning and
- * joined before the composite.  The rows of culled Gaussians are not written (nothing
- * reads them).  Outputs equal gsr_relit_features + gsr_forward_channels bit for bit.
- * feature_stride must be 16; shade->workspace pairs with gsr_relit_features_backward. */
-int gsr_forward_channels_relit(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
-                               void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int nch,
-                               int feature_stride, float* features, const float* background, int width, int height,
-                               const float* means3D, const float* opacities, const float* scales,
-                               float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                               const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
-                               float tan_fovy, int prefiltered, float* out, int* radii, void* stream,
-                               int* num_rendered, const gsr_relit_spec* shade);
 /* Backward: dL_dfeatures [P][16] -> d_xyz [P,3], d_rotation [P,4], d_albedo [N_fg,3],
  * d_roughness / d_metalness [N_fg] (may be NULL), d_base, d_sky_sh (may be NULL).  The
  * scaling gets no gradient (the axis is an argmin).  `accumulate`: bits GSR_ACC_MEAN3D
  * (d_xyz), GSR_ACC_ROT (d_rotation), GSR_ACC_ALBEDO / _ROUGH / _METAL add into those
- * buffers instead of overwriting them.  radii (may be NULL): after
- * gsr_forward_channels_relit, its radii -- the culled Gaussians (zero gradient rows, no
- * shaded normal) then load nothing; every output is the same. */
+ * buffers instead of overwriting them. */
 #define GSR_ACC_ALBEDO 16u
 #define GSR_ACC_ROUGH 32u
 #define GSR_ACC_METAL 64u
@@ -227,9 +190,9 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
                                 const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
                                 const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
                                 int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
-                                const float* dL_dfeatures, const int* radii, float* d_xyz, float* d_rotation,
-                                float* d_albedo, float* d_roughness, float* d_metalness, float* d_base,
-                                float* d_sky_sh, void* workspace, unsigned accumulate, void* stream);
+                                const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
+                                float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
+                                void* workspace, unsigned accumulate, void* stream);
 
 /* render()'s image-space tail over the composite's images ([H,W] planes, [3,H,W] for n01):
  *   normal     = ((n01 - 0.5) * 2 * (normal_view ? -1 : 1)) * sky + (1 - sky)

@@ -16,7 +16,6 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
-#include <map>
 #include <mutex>
 #include <unordered_set>
 #include <string>
@@ -488,32 +487,8 @@ struct McSpec {
     float* out;          // forward: [nch][H][W]
     const float* dL_dout;  // backward: [nch][H][W]
     float* dL_dfeat;       // backward: [P][fstride]
-    const gsr_relit_spec* shade = nullptr;  // forward: shade the visible rows of `features` first
 };
 constexpr int MC_GROUP = 16;
-
-// A second stream per caller stream (gsr_forward_channels_relit: the visible-only shade runs
-// beside the depth sort and the binning), with its fork / join events.  Created on first use
-// on the caller's current device and kept.
-struct SideStream {
-    hipStream_t s = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-};
-int side_stream(hipStream_t caller, SideStream*& out) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, SideStream> streams;
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    std::lock_guard<std::mutex> lk(mu);
-    SideStream& ss = streams[{dev, caller}];
-    if (!ss.s) {
-        HIP_OK(hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking));
-        HIP_OK(hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming));
-        HIP_OK(hipEventCreateWithFlags(&ss.join, hipEventDisableTiming));
-    }
-    out = &ss;
-    return GSR_OK;
-}
 
 gsr::RenderMcArgs mc_args(int W, int H, unsigned gx, unsigned gy, unsigned gsx, const uint2* st_ranges, const uint2* ent,
                           const gsr::Rec* rec, const uint32_t* order, const uint32_t* nheavy, uint32_t* tile_nmax,
@@ -664,8 +639,6 @@ int gsr_get_layout(int P, long long R, int width, int height, gsr_layout* out) {
     return GSR_OK;
 }
 
-static int relit_launch(int P, const gsr_relit_spec& sp, float* features, const int* vis, hipStream_t s);
-
 static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
                         void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int D, int M,
                         const float* background, int width, int height, const float* means3D, const float* shs,
@@ -728,21 +701,6 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
         gsr::launch_preprocess(pa, s);
     }
     GSR_LAUNCH_CHECK();
-    // visible-only relit shade (gsr_forward_channels_relit), right behind the preprocess that
-    // wrote the radii
-    SideStream* side = nullptr;
-    if (mc && mc->shade && getenv("GSR_RELIT_SIDE")) {
-        int rc_side = side_stream(s, side);
-        if (rc_side != GSR_OK) return rc_side;
-        HIP_OK(hipEventRecord(side->fork, s));
-        HIP_OK(hipStreamWaitEvent(side->s, side->fork, 0));
-        rc_side = relit_launch(P, *mc->shade, const_cast<float*>(mc->features), radii, side->s);
-        if (rc_side != GSR_OK) return rc_side;
-        HIP_OK(hipEventRecord(side->join, side->s));
-    } else if (mc && mc->shade) {
-        const int rc_sh = relit_launch(P, *mc->shade, const_cast<float*>(mc->features), radii, s);
-        if (rc_sh != GSR_OK) return rc_sh;
-    }
 
     // The forward's one host synchronisation (the reference's, rasterizer_impl.cu:281) reads
     // P_v, R and S: one workgroup sums the preprocess's per-workgroup totals into host-mapped
@@ -882,10 +840,6 @@ static int forward_impl(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_r
     ra.zero = reinterpret_cast<float4*>(at<float>(geom, gl.acc));
     ra.zero_n4 = (long long)gsr::ACC_STRIDE * P / 4;
     auto render_pass = [&]() -> int {
-        if (side) {  // the shaded features
-            HIP_OK(hipStreamWaitEvent(s, side->join, 0));
-            side = nullptr;
-        }
         ra.st_ranges = at<uint2>(bin, bl.st_ranges);
         ra.ent = at<uint2>(bin, bl.ent);
         GSR_STAGE(ST_RENDER_FWD);
@@ -991,35 +945,6 @@ int gsr_forward_channels(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_
         HIP_OK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)nch * width * height, s));
         return GSR_OK;
     }
-    return forward_impl(geometry_buffer, geometry_ctx, binning_buffer, binning_ctx, image_buffer, image_ctx, P, 0, 0,
-                        background, width, height, means3D, nullptr, nullptr, opacities, scales, scale_modifier,
-                        rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
-                        nullptr, radii, stream_, num_rendered, &mc);
-}
-
-int gsr_forward_channels_relit(gsr_resize_fn geometry_buffer, void* geometry_ctx, gsr_resize_fn binning_buffer,
-                               void* binning_ctx, gsr_resize_fn image_buffer, void* image_ctx, int P, int nch,
-                               int feature_stride, float* features, const float* background, int width, int height,
-                               const float* means3D, const float* opacities, const float* scales,
-                               float scale_modifier, const float* rotations, const float* cov3D_precomp,
-                               const float* viewmatrix, const float* projmatrix, const float* cam_pos, float tan_fovx,
-                               float tan_fovy, int prefiltered, float* out, int* radii, void* stream_,
-                               int* num_rendered, const gsr_relit_spec* shade) {
-    if (num_rendered) *num_rendered = 0;
-    if (!shade) return fail(GSR_E_ARG, "gsr_forward_channels_relit: missing shade inputs");
-    if (feature_stride != gsr::RELIT_STRIDE)
-        return fail(GSR_E_ARG, "gsr_forward_channels_relit: feature_stride must be %d (got %d)", gsr::RELIT_STRIDE,
-                    feature_stride);
-    if (P > 0 || features) {
-        const int e = check_mc("gsr_forward_channels_relit", nch, feature_stride, features);
-        if (e != GSR_OK) return e;
-    }
-    if (!background || !out) return fail(GSR_E_ARG, "gsr_forward_channels_relit: missing background or output");
-    if (P == 0) {
-        HIP_OK(hipMemsetAsync(out, 0, sizeof(float) * (size_t)nch * width * height, reinterpret_cast<hipStream_t>(stream_)));
-        return GSR_OK;
-    }
-    McSpec mc{nch, feature_stride, features, background, out, nullptr, nullptr, shade};
     return forward_impl(geometry_buffer, geometry_ctx, binning_buffer, binning_ctx, image_buffer, image_ctx, P, 0, 0,
                         background, width, height, means3D, nullptr, nullptr, opacities, scales, scale_modifier,
                         rotations, cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
@@ -1353,35 +1278,35 @@ size_t gsr_relit_workspace_bytes(int P, int N_fg, int deg, int sky_deg) {
     return relit_ws_layout(P, N_fg, deg, sky_deg).total;
 }
 
-// The fused relit features of P Gaussians into features [P][16]; vis (the forward's radii, or
-// null) restricts them to the Gaussians the rasterizer kept.
-static int relit_launch(int P, const gsr_relit_spec& sp, float* features, const int* vis, hipStream_t s) {
-    const int N_fg = sp.N_fg, deg = sp.deg, sky_deg = sp.sky_deg;
+int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
+                       const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
+                       const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
+                       int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
+                       float* features, void* workspace, void* stream_) {
     if (P < 0 || N_fg < 0 || N_fg > P || deg < 2 || deg > 5 || sky_deg < -1 || sky_deg > 3)
         return fail(GSR_E_ARG, "gsr_relit_features: bad sizes P=%d N_fg=%d deg=%d sky_deg=%d", P, N_fg, deg, sky_deg);
     if (P == 0) return GSR_OK;
-    if (!sp.xyz || !sp.rotation || !sp.scaling || !sp.fg_rank || !features || !sp.workspace || !sp.campos ||
-        !sp.viewmatrix || (N_fg > 0 && (!sp.fg_rows || !sp.albedo || !sp.base || !sp.fg_lut || (sp.specular && !sp.roughness))) ||
-        (sky_deg >= 0 && !sp.sky_sh))
+    if (!xyz || !rotation || !scaling || !fg_rank || !features || !workspace || !campos || !viewmatrix ||
+        (N_fg > 0 && (!fg_rows || !albedo || !base || !fg_lut || (specular && !roughness))) ||
+        (sky_deg >= 0 && !sky_sh))
         return fail(GSR_E_ARG, "gsr_relit_features: missing inputs");
     if ((reinterpret_cast<uintptr_t>(features) & 15u) != 0)
         return fail(GSR_E_ARG, "gsr_relit_features: features must be 16-B aligned");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
-    char* ws = align_base(sp.workspace);
-    gsr::RelitArgs ra{P, sp.xyz, sp.rotation, sp.scaling, sp.fg_rank, sky_deg, sp.sky_sh, sp.campos, sp.viewmatrix,
-                      features, at<float>(ws, wl.normal_fg)};
-    ra.vis = vis;
+    char* ws = align_base(workspace);
+    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, features,
+                      at<float>(ws, wl.normal_fg)};
     {
         GSR_STAGE(ST_SHADE_FWD);
         gsr::launch_relit_prep(ra, s);
         if (N_fg > 0) {
-            gsr::ShadeArgs a{N_fg, deg, sp.xyz, at<float>(ws, wl.normal_fg), sp.albedo, sp.campos, sp.roughness,
-                             sp.metalness, sp.base, sp.fg_lut, sp.specular};
-            a.rows = sp.fg_rows;
+            gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
+                             fg_lut, specular};
+            a.rows = fg_rows;
             a.io_stride = gsr::RELIT_STRIDE;
             a.vp_stride = 0;
-            a.viewmatrix = sp.viewmatrix;  // whole rows (k_relit_prep skips the shaded ones)
-            a.vis = vis;
+            a.viewmatrix = viewmatrix;  // whole rows (k_relit_prep skips the shaded ones)
             gsr::launch_shade_fwd(a, features, features + 3, features + 6, s);
         }
     }
@@ -1389,23 +1314,13 @@ static int relit_launch(int P, const gsr_relit_spec& sp, float* features, const 
     return GSR_OK;
 }
 
-int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
-                       const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
-                       const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
-                       int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
-                       float* features, void* workspace, void* stream_) {
-    const gsr_relit_spec sp{N_fg,  deg,     specular, sky_deg,   xyz,  rotation, scaling, fg_rank, fg_rows,
-                            albedo, roughness, metalness, base, fg_lut, sky_sh, campos,  viewmatrix, workspace};
-    return relit_launch(P, sp, features, nullptr, reinterpret_cast<hipStream_t>(stream_));
-}
-
 int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
                                 const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
                                 const float* metalness, int deg, const float* base, const float* fg_lut, int specular,
                                 int sky_deg, const float* sky_sh, const float* campos, const float* viewmatrix,
-                                const float* dL_dfeatures, const int* radii, float* d_xyz, float* d_rotation,
-                                float* d_albedo, float* d_roughness, float* d_metalness, float* d_base,
-                                float* d_sky_sh, void* workspace, unsigned accumulate, void* stream_) {
+                                const float* dL_dfeatures, float* d_xyz, float* d_rotation, float* d_albedo,
+                                float* d_roughness, float* d_metalness, float* d_base, float* d_sky_sh,
+                                void* workspace, unsigned accumulate, void* stream_) {
     if (P < 0 || N_fg < 0 || N_fg > P || deg < 2 || deg > 5 || sky_deg < -1 || sky_deg > 3)
         return fail(GSR_E_ARG, "gsr_relit_features_backward: bad sizes");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
@@ -1419,7 +1334,6 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
     char* ws = align_base(workspace);
     gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, nullptr,
                       at<float>(ws, wl.normal_fg)};
-    ra.vis = radii;
     {
         GSR_STAGE(ST_SHADE_BWD);
         if (N_fg > 0) {
@@ -1428,7 +1342,6 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
             a.rows = fg_rows;
             a.io_stride = gsr::RELIT_STRIDE;
             a.vp_stride = 0;
-            a.vis = radii;
             gsr::ShadeGrads g{dL_dfeatures, dL_dfeatures + 3, specular ? dL_dfeatures + 6 : nullptr,
                               at<float>(ws, wl.d_pos_fg), at<float>(ws, wl.d_normal_fg), d_albedo, nullptr,
                               specular ? d_roughness : nullptr, specular ? d_metalness : nullptr, d_base};

@@ -295,8 +295,6 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
     __syncthreads();
     const int i = blockIdx.x * SHADE_THREADS + threadIdx.x;
     if (i >= a.N) return;
-    const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
-    if (a.vis && a.vis[row] == 0) return;  // culled: no row is read for it
     const float3 n = ld3(a.normal, i);
     const float3 al = ld3(a.albedo, i);
     const float x = n.x, y = n.y, z = n.z;
@@ -311,6 +309,7 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         dh[c] = alc[c] * irr;
         dl[c] = gamma_f(dh[c]);
     }
+    const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
     // the relit features' whole row: rgb, diffuse, specular, depth, 0.5 n + 0.5, 1, 0, 0 as four
     // 16-B stores (k_relit_prep leaves the shaded rows to this kernel)
     auto store_row = [&](const float (&r)[3], const float (&d)[3], const float (&sp)[3]) {
@@ -390,13 +389,9 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
     const bool valid = i < a.N;
     const int ii = valid ? i : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const size_t row = a.rows ? (size_t)a.rows[ii] : (size_t)ii;
-    // a culled Gaussian (visible-only mode) has a zero gradient row and no forward normal: it
-    // runs with zero inputs, so every value it adds below is a zero as it was with its own
-    const bool live = valid && !(a.vis && a.vis[row] == 0);
 
-    const float3 n = live ? ld3(a.normal, ii) : make_float3(0.f, 0.f, 0.f);
-    const float3 al = live ? ld3(a.albedo, ii) : make_float3(0.f, 0.f, 0.f);
+    const float3 n = ld3(a.normal, ii);
+    const float3 al = ld3(a.albedo, ii);
     const float x = n.x, y = n.y, z = n.z;
     const float alc[3] = {al.x, al.y, al.z};
     float irr_raw[3], irr[3], dh[3];
@@ -409,7 +404,8 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         dh[c] = alc[c] * irr[c];
     }
     float grgb[3] = {0.f, 0.f, 0.f}, gdif[3] = {0.f, 0.f, 0.f}, gspe[3] = {0.f, 0.f, 0.f};
-    if (live) {
+    const size_t row = a.rows ? (size_t)a.rows[ii] : (size_t)ii;
+    if (valid) {
         if (g.g_rgb) { const float3 t = ld3s(g.g_rgb, row, a.io_stride); grgb[0] = t.x; grgb[1] = t.y; grgb[2] = t.z; }
         if (g.g_diffuse) {
             const float3 t = ld3s(g.g_diffuse, row, a.io_stride);
@@ -420,16 +416,9 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
             gspe[0] = t.x; gspe[1] = t.y; gspe[2] = t.z;
         }
     }
-    float g_a[3] = {0.f, 0.f, 0.f}, g_n[3] = {0.f, 0.f, 0.f}, g_p[3] = {0.f, 0.f, 0.f};
+    float g_dh[3], g_a[3] = {0.f, 0.f, 0.f}, g_n[3] = {0.f, 0.f, 0.f}, g_p[3] = {0.f, 0.f, 0.f};
     float g_vp[3] = {0.f, 0.f, 0.f}, g_si[3] = {0.f, 0.f, 0.f};
     float g_kr = 0.f, g_km = 0.f;
-    // a wave of culled Gaussians only (visible-only mode) adds zeros everywhere: it skips the
-    // evaluation and stores the zeros
-    if (__ballot(live) == 0ull) {
-        if (g.d_base)
-            for (int t = lane; t < 3 * K; t += 64) sred[wave][t] = 0.f;
-    } else {
-    float g_dh[3];
 #pragma unroll
     for (int c = 0; c < 3; c++) g_dh[c] = gdif[c] * gamma_d(dh[c]);
     float Y[K], gw[DEG + 1], gi[3];
@@ -460,7 +449,7 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
                     v = Y[k] * gw[l] * g_si[c];
                     if (k < 9) v += gi[c] * dco[k < 9 ? k : 0];
                 }
-                vb[t] = live ? v : 0.f;
+                vb[t] = valid ? v : 0.f;
             }
             const float red = wave_multi_sum<12>(vb);
             if ((lane & 15) < 3 && e0 + vi < 3 * K) sred[wave][e0 + vi] = red;
@@ -476,10 +465,10 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         diffuse_gi();
         base_partials();
     } else {
-        const float3 p = live ? ld3s(a.pos, row, 3) : make_float3(0.f, 0.f, 0.f);
+        const float3 p = ld3s(a.pos, row, 3);
         const float3 vp = ld3s(a.view_pos, ii, a.vp_stride);
-        const float kr = live ? a.kr[ii] : 0.f;
-        const float km = (a.km && live) ? a.km[ii] : 0.f;
+        const float kr = a.kr[ii];
+        const float km = a.km ? a.km[ii] : 0.f;
         const float wv[3] = {vp.x - p.x, vp.y - p.y, vp.z - p.z};
         const float l2 = wv[0] * wv[0] + wv[1] * wv[1] + wv[2] * wv[2];
         const bool lclamp = l2 < 1e-20f;
@@ -581,7 +570,6 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
         g_n[1] += gi[c] * (-LC1 * sb[24 + c] * 2 * y + LC1x2 * sb[12 + c] * x + LC1x2 * sb[15 + c] * z + LC2x2 * sb[3 + c]);
         g_n[2] += gi[c] * (LC3 * sb[18 + c] * 2 * z + LC1x2 * sb[21 + c] * x + LC1x2 * sb[15 + c] * y + LC2x2 * sb[6 + c]);
     }
-    }  // the wave's evaluation
     if (valid) {
         if (g.d_pos) st3(g.d_pos, i, g_p[0], g_p[1], g_p[2]);
         if (g.d_normal) st3(g.d_normal, i, g_n[0], g_n[1], g_n[2]);
@@ -675,7 +663,6 @@ template <int SDEG>
 __global__ void __launch_bounds__(256) k_relit_prep(RelitArgs a) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= a.P) return;
-    if (a.vis && a.vis[i] == 0) return;  // culled: its row and normal are never read
     const float3 xyz = ld3(a.xyz, i);
     const RelitGeom g = relit_geom(a, i, xyz);
     const int rank = a.fg_rank[i];
@@ -702,8 +689,6 @@ __global__ void __launch_bounds__(256) k_relit_prep(RelitArgs a) {
 // foreground rows), dL/drotation (through the flipped minimum axis and build_rotation's
 // normalisation), per-workgroup partial dL/dsky_sh.  dL/dscaling is zero (the axis choice
 // is an argmin).
-__device__ const float kZeroRow[RELIT_STRIDE] = {};
-
 template <int SDEG>
 __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads gr) {
     constexpr int KS = SDEG >= 0 ? (SDEG + 1) * (SDEG + 1) : 1;
@@ -712,29 +697,17 @@ __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads 
     const bool valid = i < a.P;
     const int ii = valid ? i : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    // a culled Gaussian (visible-only mode) reads a zero row instead of its own zero gradient
-    // row, and no shade gradients (the shade backward wrote none for it); a wave of culled
-    // Gaussians only stores its zeros without the evaluation
-    const bool live = valid && !(a.vis && a.vis[ii] == 0);
-    float Yk[KS];
-    float gcol[3] = {0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < KS; k++) Yk[k] = 0.f;
-    if (__ballot(live) == 0ull) {
-        if (valid && !(gr.acc & ACC_MEAN3D)) st3(gr.d_xyz, i, 0.f, 0.f, 0.f);
-        if (valid && !(gr.acc & ACC_ROT))
-            *reinterpret_cast<float4*>(gr.d_rotation + 4 * (size_t)i) = make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {
     const float3 xyz = ld3(a.xyz, ii);
     const RelitGeom g = relit_geom(a, ii, xyz);
-    const float* gf = live ? gr.dL_dfeatures + (size_t)ii * RELIT_STRIDE : kZeroRow;
+    const float* gf = gr.dL_dfeatures + (size_t)ii * RELIT_STRIDE;
     const float* V = a.viewmatrix;
     float gx = gf[9] * V[2], gy = gf[9] * V[6], gz = gf[9] * V[10];
     float3 gn = make_float3(0.5f * gf[10], 0.5f * gf[11], 0.5f * gf[12]);
     const int rank = a.fg_rank[ii];
+    float Yk[KS];
+    float gcol[3] = {0.f, 0.f, 0.f};
     if (rank >= 0) {
-        const float3 dn = live ? ld3(gr.d_normal_fg, rank) : make_float3(0.f, 0.f, 0.f);
-        const float3 dpos = live ? ld3(gr.d_pos_fg, rank) : make_float3(0.f, 0.f, 0.f);
+        const float3 dn = ld3(gr.d_normal_fg, rank), dpos = ld3(gr.d_pos_fg, rank);
         gn.x += dn.x; gn.y += dn.y; gn.z += dn.z;
         gx += dpos.x; gy += dpos.y; gz += dpos.z;
 #pragma unroll
@@ -803,7 +776,6 @@ __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads 
         }
         *rp = dr;
     }
-    }  // the wave's evaluation
     if (SDEG < 0 || !gr.d_sky_sh) return;
     // dL/dsky_sh[k][c] = sum over sky Gaussians of Y_k(dir) gcol[c]: per-workgroup slab
     const int vi = wave_multi_sum_index(lane);

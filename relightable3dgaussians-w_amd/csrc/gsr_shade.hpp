@@ -27,10 +27,6 @@ struct ShadeArgs {
     // row offsets 0/3/6): also the row's depth (viewmatrix column 2, device), 0.5 n + 0.5, alpha
     // 1 and the padding, so every 64-B feature row is written by one kernel in full.
     const float* viewmatrix = nullptr;
-    // Visible-only mode (the fused relit path): vis[row] == 0 marks a Gaussian the rasterizer
-    // culled (its radius); the forward skips it (its row is never read), the backward reads a
-    // zero gradient row for it instead of its own (zero) one.  Null: every Gaussian.
-    const int* vis = nullptr;
 };
 
 struct ShadeGrads {
@@ -61,7 +57,6 @@ struct RelitArgs {
     const float* viewmatrix;  // world_view_transform, row-major [4,4]
     float* features;        // [P][RELIT_STRIDE]
     float* normal_fg;       // [N_fg,3]
-    const int* vis = nullptr;  // [P] radii: 0 = culled, skipped (ShadeArgs::vis); null: all
 };
 struct RelitGrads {
     const float* dL_dfeatures;  // [P][RELIT_STRIDE]

@@ -191,18 +191,7 @@ def rasterize_gaussians_channels(background, means3D, features, opacity, scales,
                          f"background {tuple(background.shape)})")
     radii = torch.empty(P, dtype=torch.int32, device=dev)  # preprocess writes every entry (0 when culled)
     bs = _lib.BufferSet(dev)
-    # relit_features(defer=True) rows: shaded inside this call for the visible Gaussians
-    # (gsr_forward_channels_relit), or first, in full, when they cannot be used as they are
-    defer = getattr(features, "_gsr_relit_defer", None)
-    if defer is not None and defer.done:
-        defer = None
-    feat = pack_features(features if features.dtype == torch.float32 else features.float(), nch) \
-        if defer is None else features
-    if defer is not None and not (feat.dtype == torch.float32 and feat.is_contiguous() and feat.size(1) == 16 and
-                                  feat.data_ptr() % 16 == 0 and nch <= 16):
-        defer.materialize(features)
-        defer = None
-        feat = pack_features(features, nch)
+    feat = pack_features(features if features.dtype == torch.float32 else features.float(), nch)
     out = torch.empty((nch, H, W), dtype=torch.float32, device=dev)
     keep = [_f32(x) for x in (background, means3D, opacity, scales, rotations, cov3D_precomp, viewmatrix, projmatrix,
                               campos)]
@@ -213,21 +202,15 @@ def rasterize_gaussians_channels(background, means3D, features, opacity, scales,
     rc = _lib.ResizeContexts(bs)
     nr = C.c_int(0)
     try:
-        args = (_lib.RESIZE, rc.ctx[0], _lib.RESIZE, rc.ctx[1], _lib.RESIZE, rc.ctx[2], P, nch, feat.size(1),
-                _lib.fptr(feat), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(op_), _lib.fptr(sc_),
-                float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_),
-                _lib.fptr(cp_), float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out.data_ptr(),
-                radii.data_ptr(), _lib.stream_of(dev), C.byref(nr))
-        if defer is None:
-            ret = _lib.lib().gsr_forward_channels(*args)
-        else:
-            ret = _lib.lib().gsr_forward_channels_relit(*args, C.byref(defer.spec))
+        ret = _lib.lib().gsr_forward_channels(
+            _lib.RESIZE, rc.ctx[0], _lib.RESIZE, rc.ctx[1], _lib.RESIZE, rc.ctx[2], P, nch, feat.size(1),
+            _lib.fptr(feat), _lib.fptr(bg_), W, H, _lib.fptr(m_), _lib.fptr(op_), _lib.fptr(sc_),
+            float(scale_modifier), _lib.fptr(rot_), _lib.fptr(cov_), _lib.fptr(vm_), _lib.fptr(pm_), _lib.fptr(cp_),
+            float(tan_fovx), float(tan_fovy), int(bool(prefiltered)), out.data_ptr(), radii.data_ptr(),
+            _lib.stream_of(dev), C.byref(nr))
     finally:
         rc.close()
     _lib.check(ret, "rasterize_gaussians_channels")
-    if defer is not None:
-        defer.done = True
-        defer.radii = radii
     return int(nr.value), out, radii, bs.bufs[0], bs.bufs[1], bs.bufs[2], feat
 
 

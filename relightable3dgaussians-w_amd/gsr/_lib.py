@@ -29,13 +29,6 @@ class Layout(C.Structure):
         "img_surv_n", "img_surv", "surv_cap")]
 
 
-class RelitSpec(C.Structure):
-    """gsr_relit_spec (include/gsr.h): gsr_relit_features' inputs for gsr_forward_channels_relit."""
-    _fields_ = [("N_fg", C.c_int), ("deg", C.c_int), ("specular", C.c_int), ("sky_deg", C.c_int)] + [
-        (n, C.c_void_p) for n in ("xyz", "rotation", "scaling", "fg_rank", "fg_rows", "albedo", "roughness",
-                                  "metalness", "base", "fg_lut", "sky_sh", "campos", "viewmatrix", "workspace")]
-
-
 DEBUG_LIB_PATH = os.path.join(PKG_DIR, "lib", "debug", "libgsr.so")
 
 
@@ -65,10 +58,7 @@ def _declare(lib):
     lib.gsr_relit_workspace_bytes.restype = sz
     lib.gsr_relit_features.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp, vp, vp]
     lib.gsr_relit_features_backward.argtypes = [i, i, vp, vp, vp, vp, vp, vp, vp, vp, i, vp, vp, i, i, vp, vp, vp, vp,
-                                                vp, vp, vp, vp, vp, vp, vp, vp, vp, C.c_uint, vp]
-    lib.gsr_forward_channels_relit.argtypes = [RESIZE_FN, vp, RESIZE_FN, vp, RESIZE_FN, vp, i, i, i, vp, vp, i, i, vp,
-                                               vp, vp, f, vp, vp, vp, vp, vp, f, f, i, vp, vp, vp, C.POINTER(C.c_int),
-                                               C.POINTER(RelitSpec)]
+                                                vp, vp, vp, vp, vp, vp, vp, vp, C.c_uint, vp]
     lib.gsr_relit_epilogue.argtypes = [i, i, vp, vp, vp, vp, vp, i, vp, vp, vp]
     lib.gsr_relit_epilogue_backward.argtypes = [i, i, vp, vp, vp, vp, i, vp, vp, vp, vp, vp]
     lib.gsr_texture2d_forward.argtypes = [i, i, i, i, i, i, vp, vp, i, i, vp, vp]
@@ -122,7 +112,7 @@ def _declare(lib):
     lib.gsr_last_error.restype = C.c_char_p
     lib.gsr_version.restype = C.c_char_p
     for fn in ("gsr_forward", "gsr_forward_reuse", "gsr_knn_mean_dist", "gsr_backward", "gsr_mark_visible", "gsr_shade_forward",
-               "gsr_shade_backward", "gsr_forward_channels", "gsr_forward_channels_relit", "gsr_backward_channels",
+               "gsr_shade_backward", "gsr_forward_channels", "gsr_backward_channels",
                "gsr_relit_features", "gsr_relit_features_backward", "gsr_relit_epilogue",
                "gsr_relit_epilogue_backward", "gsr_adam_step", "gsr_adam_step_range", "gsr_ssim_forward", "gsr_ssim_backward",
                "gsr_ssim_l1_backward",

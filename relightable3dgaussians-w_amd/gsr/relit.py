@@ -288,18 +288,13 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
     sky_mask = viewpoint_camera.sky_mask.to(dev).squeeze()
     is_sky = pc.get_is_sky.squeeze()
 
+    feat = relit_shade.relit_features(means3D, pc.get_rotation, pc.get_scaling, is_sky, pc.get_albedo,
+                                      pc.get_roughness, pc.get_metalness, envlight, viewpoint_camera.camera_center,
+                                      viewpoint_camera.world_view_transform, sky_sh, sky_sh_degree, specular, fix_sky)
+    bg = bg_color.reshape(-1).float()
     # A value repeated over three channels (depth, alpha, roughness, metalness) is one
     # composite channel when the background is grey; otherwise three.
     grey = _is_grey(bg_color)
-    # Without extras and with a grey background the relit rows go to the rasterizer as they are:
-    # it then shades them itself, after its preprocess and for the visible Gaussians only
-    # (relit_shade.DeferredShade, gsr_forward_channels_relit).
-    direct = not debug and grey
-    feat = relit_shade.relit_features(means3D, pc.get_rotation, pc.get_scaling, is_sky, pc.get_albedo,
-                                      pc.get_roughness, pc.get_metalness, envlight, viewpoint_camera.camera_center,
-                                      viewpoint_camera.world_view_transform, sky_sh, sky_sh_degree, specular, fix_sky,
-                                      defer=direct and relit_shade.visible_only_default())
-    bg = bg_color.reshape(-1).float()
     zero3 = _zero_rows(None, dev, 3)
     # (name, columns [P, k], background [k]); alpha is rendered with a black background
     chans = [("render", feat[:, 0:3], bg), ("diffuse_color", feat[:, 3:6], bg), ("specular_color", feat[:, 6:9], bg),
@@ -324,7 +319,8 @@ def render(viewpoint_camera, pc, envlight, sky_sh, sky_sh_degree, pipe, bg_color
         bgs.append(b[:k])
         widths.append(k)
     nch = sum(widths)
-    features = feat if direct else torch.cat(cols, 1)
+    # without extras and with a grey background the relit rows are the features as they are
+    features = feat if (not debug and grey) else torch.cat(cols, 1)
     image, radii = dgr.rasterize_channels(means3D, screenspace_points, features, opacity, scales, rotations,
                                           cov3D_precomp, _bg_cat(bg_color, widths, bgs), settings, nch=nch)
     H, W = settings.image_height, settings.image_width

@@ -120,56 +120,18 @@ RELIT_CHANNELS = {"render": (0, 3), "diffuse_color": (3, 6), "specular_color": (
                   "normal": (10, 13), "alpha": (13, 14)}
 
 
-class DeferredShade:
-    """A relit_features(defer=True) result not shaded yet: the rasterizer's multi-channel forward
-    (diff_gaussian_rasterization._C.rasterize_gaussians_channels) shades it inside its call, after
-    the preprocess and for the Gaussians it keeps only (gsr_forward_channels_relit), and records
-    its radii here for the shade backward.  Anything else that needs the values first calls
-    materialize(), which shades every Gaussian as relit_features does without defer."""
-
-    def __init__(self, spec, keep):
-        self.spec, self.keep = spec, keep  # keep: the tensors the spec points into
-        self.done = False
-        self.radii = None
-
-    def materialize(self, feat):
-        """Shade every row of feat (the [P, 16] tensor this shade belongs to) now."""
-        if self.done:
-            return
-        sp = self.spec
-        _lib.check(_lib.lib().gsr_relit_features(
-            feat.shape[0], sp.N_fg, sp.xyz, sp.rotation, sp.scaling, sp.fg_rank, sp.fg_rows, sp.albedo, sp.roughness,
-            sp.metalness, sp.deg, sp.base, sp.fg_lut, sp.specular, sp.sky_deg, sp.sky_sh, sp.campos, sp.viewmatrix,
-            feat.data_ptr(), sp.workspace, _lib.stream_of(feat.device)), "gsr_relit_features")
-        self.done = True
-
-
-def visible_only_default():
-    """Whether relit.render defers the shade into the rasterizer (GSR_RELIT_VISIBLE, default on)."""
-    return os.environ.get("GSR_RELIT_VISIBLE", "1") != "0"
-
-
 class RelitFeaturesFunction(torch.autograd.Function):
     """gsr_relit_features: render()'s per-Gaussian channels as [P, 16] feature rows."""
 
     @staticmethod
     def forward(ctx, xyz, rotation, scaling, albedo, roughness, metalness, base, sky_sh, fg_rank, fg_rows, campos,
-                viewmatrix, lut, deg, sky_deg, specular, sink_in=None, defer=False):
+                viewmatrix, lut, deg, sky_deg, specular, sink_in=None):
         P, N = xyz.shape[0], fg_rows.shape[0]
         dev = xyz.device
         feat = torch.empty((P, 16), dtype=torch.float32, device=dev)
         ws = torch.empty(int(_lib.lib().gsr_relit_workspace_bytes(P, N, deg, sky_deg)), dtype=torch.uint8, device=dev)
         ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
-        ctx.defer = None
-        if P and defer:
-            spec = _lib.RelitSpec(N, deg, int(specular), sky_deg, xyz.data_ptr(), rotation.data_ptr(),
-                                  scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows), ptr(albedo), ptr(roughness),
-                                  ptr(metalness), base.data_ptr(), lut.data_ptr(), ptr(sky_sh), campos.data_ptr(),
-                                  viewmatrix.data_ptr(), ws.data_ptr())
-            ctx.defer = DeferredShade(spec, (xyz, rotation, scaling, albedo, roughness, metalness, base, sky_sh,
-                                             fg_rank, fg_rows, campos, viewmatrix, lut, ws))
-            feat._gsr_relit_defer = ctx.defer  # read by the rasterizer call it is passed to
-        elif P:
+        if P:
             _lib.check(_lib.lib().gsr_relit_features(
                 P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),
                 ptr(albedo), ptr(roughness), ptr(metalness), deg, base.data_ptr(), lut.data_ptr(), int(specular),
@@ -211,13 +173,10 @@ class RelitFeaturesFunction(torch.autograd.Function):
         d_base = torch.empty_like(base)
         d_sky = torch.empty_like(sky_sh) if ctx.has[2] and ctx.sky_deg >= 0 else None
         ptr = lambda t: None if t is None or t.numel() == 0 else t.data_ptr()
-        # visible-only: the rasterizer that shaded the rows also told which Gaussians it kept
-        radii = ctx.defer.radii if ctx.defer is not None else None
         _lib.check(_lib.lib().gsr_relit_features_backward(
             P, N, xyz.data_ptr(), rotation.data_ptr(), scaling.data_ptr(), fg_rank.data_ptr(), ptr(fg_rows),
             ptr(albedo), ptr(roughness), ptr(metalness), ctx.deg, base.data_ptr(), lut.data_ptr(), int(ctx.specular),
-            ctx.sky_deg, ptr(sky_sh), campos.data_ptr(), viewmatrix.data_ptr(), g_feat.data_ptr(), ptr(radii),
-            d_xyz.data_ptr(),
+            ctx.sky_deg, ptr(sky_sh), campos.data_ptr(), viewmatrix.data_ptr(), g_feat.data_ptr(), d_xyz.data_ptr(),
             d_rot.data_ptr(), ptr(d_alb), ptr(d_kr), ptr(d_km), d_base.data_ptr(), ptr(d_sky), ws.data_ptr(), acc,
             _lib.stream_of(dev)), "gsr_relit_features_backward")
         if sk is not None:
@@ -226,7 +185,7 @@ class RelitFeaturesFunction(torch.autograd.Function):
             d_xyz, d_rot, d_alb, d_kr, d_km = (keep(d_xyz, 0), keep(d_rot, 1), keep(d_alb, 2), keep(d_kr, 3),
                                                keep(d_km, 4))
         return (d_xyz, d_rot, None, d_alb, d_kr, d_km, d_base, d_sky, None, None, None, None, None, None, None, None,
-                None, None)
+                None)
 
 
 _FG_CACHE = {}
@@ -255,7 +214,7 @@ def _fg_index(is_sky, P, dev):
 
 
 def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness, light, campos, viewmatrix,
-                   sky_sh=None, sky_sh_degree=1, specular=True, fix_sky=False, defer=False):
+                   sky_sh=None, sky_sh_degree=1, specular=True, fix_sky=False):
     """render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) as
     one fused op: returns features [P, 16] with the columns of RELIT_CHANNELS -- the shaded
     colour (sky colour for sky Gaussians), diffuse and specular (0 for sky), view-space
@@ -264,10 +223,7 @@ def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness,
     (get_xyz), rotation [P,4] (get_rotation), scaling [P,3] (get_scaling), is_sky [P] or
     [P,1] bool, albedo [N_fg,3], roughness / metalness [N_fg,1], sky_sh [1, K, 3] (the
     sky SH; ignored with fix_sky), campos [3], viewmatrix = world_view_transform.
-    Differentiable w.r.t. xyz, rotation, albedo, roughness, metalness, light.base, sky_sh.
-    defer=True: the rows are shaded later, inside the rasterizer's multi-channel forward that
-    receives them and for the Gaussians it keeps only (DeferredShade; gsr.relit.render passes
-    them straight to it) -- same values for every row the composite reads, same gradients."""
+    Differentiable w.r.t. xyz, rotation, albedo, roughness, metalness, light.base, sky_sh."""
     _lib.require_gpu_tensor(xyz, "xyz")
     dev = xyz.device
     fg_rows, fg_rank = _fg_index(is_sky, xyz.shape[0], dev)
@@ -285,7 +241,7 @@ def relit_features(xyz, rotation, scaling, is_sky, albedo, roughness, metalness,
     return RelitFeaturesFunction.apply(f(xyz), f(rotation), f(scaling), f(albedo), _flat1(roughness),
                                        _flat1(metalness), base, sk, fg_rank, fg_rows, _f32(campos), _f32(viewmatrix),
                                        fg_lut(dev), deg, sky_deg, bool(specular),
-                                       (xyz, rotation, albedo, roughness, metalness), bool(defer))
+                                       (xyz, rotation, albedo, roughness, metalness))
 
 
 class EnvironmentLight(torch.nn.Module):

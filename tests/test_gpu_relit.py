@@ -280,81 +280,3 @@ def test_epilogue_matches_torch_restatement(normal_view):
     want = run(torch_tail)
     for name, a, b in zip(("normal", "normal_ref", "d_n01", "d_depth"), got, want):
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
-
-
-@pytest.mark.parametrize("fix_sky,specular", [(False, True), (True, True), (False, False)])
-def test_visible_only_shade_bit_identical(monkeypatch, fix_sky, specular):
-    """The fused render() shading only the Gaussians the rasterizer keeps (relit_features
-    defer=True -> gsr_forward_channels_relit, the shade on a second stream after the
-    preprocess; the shade backward given the radii) against shading every Gaussian first:
-    every image and every gradient equal bit for bit, on a scene whose camera culls a third of
-    the Gaussians.  Deterministic backward on both sides
-    (the default's float atomics sum in a run-dependent order)."""
-    import relit_shade
-    from gsr import relit
-    xyz, q, s, is_sky, mat, sky_sh, _, _ = _scene(P=6000, n_sky=600, seed=5)
-    xyz = xyz.clone()
-    xyz[::3, 0] += 60.0  # off to the side: outside the frustum, radius 0
-    cam, _ = make_case(P=10, W=160, H=120, camera="orbit")
-    g = torch.Generator().manual_seed(9)
-    sky_mask = (torch.rand(1, 120, 160, generator=g) > 0.2).float()
-    view = types.SimpleNamespace(image_width=160, image_height=120, FoVx=cam.FoVx, FoVy=cam.FoVy,
-                                 world_view_transform=cam.world_view_transform.cuda(),
-                                 full_proj_transform=cam.full_proj_transform.cuda(),
-                                 camera_center=cam.camera_center.cuda(), sky_mask=sky_mask)
-    opacity = torch.rand(xyz.shape[0], 1, generator=g).cuda() * 0.9 + 0.05
-    light = _light()
-    pipe = types.SimpleNamespace(compute_cov3D_python=False)
-    bgt = torch.zeros(3, device="cuda")
-    wts = {}
-    made = []
-    real_init = relit_shade.DeferredShade.__init__
-
-    def count_init(self, *a):
-        made.append(1)
-        real_init(self, *a)
-
-    monkeypatch.setattr(relit_shade.DeferredShade, "__init__", count_init)
-
-    def run(visible_only):
-        monkeypatch.setenv("GSR_RELIT_VISIBLE", "1" if visible_only else "0")
-        leaves = [t.clone().requires_grad_(True) for t in (xyz, q, mat["albedo"], light.base, opacity,
-                                                           mat["roughness"], mat["metalness"], sky_sh)]
-        pc = _Model(leaves[0], leaves[1], s, is_sky, dict(albedo=leaves[2], roughness=leaves[5],
-                                                          metalness=leaves[6]), leaves[4])
-        lt = relit_shade.EnvironmentLight(leaves[3], sh_degree=4)
-        out = relit.render(view, pc, lt, leaves[7], 1, pipe, bgt, debug=False, specular=specular, fix_sky=fix_sky)
-        loss = 0.0
-        gen = torch.Generator(device="cuda").manual_seed(4)
-        for k in sorted(out):
-            if k in ("viewspace_points", "visibility_filter", "radii"):
-                continue
-            wts.setdefault(k, torch.randn(out[k].shape, device="cuda", generator=gen))
-            loss = loss + (out[k] * wts[k]).sum()
-        loss.backward()
-        torch.cuda.synchronize()
-        return out, [t.grad for t in leaves] + [out["viewspace_points"].grad]
-
-    from gsr import _lib
-    was = _lib.deterministic()
-    _lib.set_deterministic(True)  # fixed-order gradient sums: two runs are comparable bit for bit
-    try:
-        o_all, g_all = run(False)
-        assert not made
-        o_vis, g_vis = run(True)
-    finally:
-        _lib.set_deterministic(was)
-    assert made  # the deferred path ran
-    culled = float((o_vis["radii"] == 0).float().mean())
-    assert culled > 0.3, culled
-    assert torch.equal(o_vis["radii"], o_all["radii"])
-    for k in o_all:
-        if k in ("viewspace_points", "visibility_filter", "radii"):
-            continue
-        assert torch.equal(o_vis[k], o_all[k]), k
-    names = ["xyz", "rotation", "albedo", "base", "opacity", "roughness", "metalness", "sky_sh", "means2D"]
-    for name, a, b in zip(names, g_vis, g_all):
-        if b is None:
-            assert a is None, name
-            continue
-        assert torch.equal(a, b), (name, float((a - b).abs().max()))
