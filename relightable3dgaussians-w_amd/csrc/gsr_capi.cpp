@@ -1299,16 +1299,15 @@ int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation,
                       at<float>(ws, wl.normal_fg)};
     {
         GSR_STAGE(ST_SHADE_FWD);
-        gsr::launch_relit_prep(ra, s);
-        if (N_fg > 0) {
-            gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
-                             fg_lut, specular};
-            a.rows = fg_rows;
-            a.io_stride = gsr::RELIT_STRIDE;
-            a.vp_stride = 0;
-            a.viewmatrix = viewmatrix;  // whole rows (k_relit_prep skips the shaded ones)
-            gsr::launch_shade_fwd(a, features, features + 3, features + 6, s);
-        }
+        // one pass over all P: geometry, sky rows, and the foreground shade in place
+        // (gsr_shade.hip k_relit_fwd; the shade's rows are the Gaussians themselves)
+        gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
+                         fg_lut, specular};
+        a.rows = fg_rows;
+        a.io_stride = gsr::RELIT_STRIDE;
+        a.vp_stride = 0;
+        a.viewmatrix = viewmatrix;
+        gsr::launch_relit_fwd(ra, a, s);
     }
     GSR_LAUNCH_CHECK();
     return GSR_OK;

@@ -287,15 +287,16 @@ __device__ __forceinline__ void st3(float* p, int i, float a, float b, float c) 
     p[3 * i + 2] = c;
 }
 
+// The base SH as staged in LDS, typed so that its reads stay ds_ instructions inside the
+// per-Gaussian functions below (a generic pointer compiles to flat loads with 64-bit addresses)
+using LdsCF = const __attribute__((address_space(3))) float*;
+
+// One Gaussian's shade: normal n, position p (rows `row` of the outputs, index i of the
+// per-Gaussian inputs albedo / kr / km / view_pos), base SH in LDS (sb).
 template <int DEG>
-__global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float* rgb, float* dif, float* spe) {
+__device__ __forceinline__ void shade_fwd_one(const ShadeArgs& a, LdsCF sb, int i, size_t row, float3 n,
+                                              float3 p, float* rgb, float* dif, float* spe) {
     constexpr int K = (DEG + 1) * (DEG + 1);
-    __shared__ float sb[K * 3];
-    for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS) sb[t] = a.base[t];
-    __syncthreads();
-    const int i = blockIdx.x * SHADE_THREADS + threadIdx.x;
-    if (i >= a.N) return;
-    const float3 n = ld3(a.normal, i);
     const float3 al = ld3(a.albedo, i);
     const float x = n.x, y = n.y, z = n.z;
     float dh[3], dl[3];
@@ -309,13 +310,11 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         dh[c] = alc[c] * irr;
         dl[c] = gamma_f(dh[c]);
     }
-    const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
     // the relit features' whole row: rgb, diffuse, specular, depth, 0.5 n + 0.5, 1, 0, 0 as four
-    // 16-B stores (k_relit_prep leaves the shaded rows to this kernel)
+    // 16-B stores (the sky rows are written by the relit kernel itself)
     auto store_row = [&](const float (&r)[3], const float (&d)[3], const float (&sp)[3]) {
-        const float3 q = ld3s(a.pos, row, 3);
         const float* V = a.viewmatrix;
-        const float depth = q.x * V[2] + q.y * V[6] + q.z * V[10] + V[14];
+        const float depth = p.x * V[2] + p.y * V[6] + p.z * V[10] + V[14];
         float4* o = reinterpret_cast<float4*>(rgb + row * (size_t)a.io_stride);
         o[0] = make_float4(r[0], r[1], r[2], d[0]);
         o[1] = make_float4(d[1], d[2], sp[0], sp[1]);
@@ -334,7 +333,6 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
         return;
     }
     if (!a.viewmatrix) st3s(dif, row, a.io_stride, dl[0], dl[1], dl[2]);
-    const float3 p = ld3s(a.pos, row, 3);
     const float3 vp = ld3s(a.view_pos, i, a.vp_stride);
     const float kr = a.kr[i];
     const float km = a.km ? a.km[i] : 0.f;
@@ -376,6 +374,18 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float*
     }
     st3s(rgb, row, a.io_stride, out_rgb[0], out_rgb[1], out_rgb[2]);
     st3s(spe, row, a.io_stride, out_spe[0], out_spe[1], out_spe[2]);
+}
+
+template <int DEG>
+__global__ void __launch_bounds__(SHADE_THREADS) k_shade_fwd(ShadeArgs a, float* rgb, float* dif, float* spe) {
+    constexpr int K = (DEG + 1) * (DEG + 1);
+    __shared__ float sb[K * 3];
+    for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS) sb[t] = a.base[t];
+    __syncthreads();
+    const int i = blockIdx.x * SHADE_THREADS + threadIdx.x;
+    if (i >= a.N) return;
+    const size_t row = a.rows ? (size_t)a.rows[i] : (size_t)i;
+    shade_fwd_one<DEG>(a, (LdsCF)sb, i, row, ld3(a.normal, i), ld3s(a.pos, row, 3), rgb, dif, spe);
 }
 
 template <int DEG>
@@ -602,15 +612,15 @@ __global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const
 }
 
 // ---- fused relit features ------------------------------------------------
-// render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) in two
-// kernels around the shade, writing the multi-channel composite's feature rows directly:
+// render()'s per-Gaussian colour preparation (gaussian_renderer/__init__.py:120-200) in one
+// kernel, writing the multi-channel composite's feature rows directly:
 //   row i = [rgb 0-2, diffuse 3-5, specular 6-8, depth 9, 0.5 n + 0.5 10-12, alpha 13, 0, 0]
-// k_relit_prep: view direction (safe_normalize(xyz - campos), NVDIFFREC/util.py:27-31),
+// k_relit_fwd: view direction (safe_normalize(xyz - campos), NVDIFFREC/util.py:27-31),
 // normal = minimum-scale axis of build_rotation(q) flipped towards the camera
 // (gaussian_model.py:115-122, general_utils.py:98-170), depth = view-space z
 // (gaussian_model.py:125-130), sky colour clamp_min(eval_sh(sky_deg, sky_sh, dir) + 0.5, 0)
-// or 1 with fix_sky (__init__.py:143-148); the foreground normals go to a compact array for
-// the shade kernel, which writes rows 0-8 of the foreground Gaussians (ShadeArgs.rows).
+// or 1 with fix_sky (__init__.py:143-148), and the foreground shade (shade_fwd_one); the
+// foreground normals also go to a compact array for the shade backward.
 template <int SDEG>
 __device__ __forceinline__ float3 sky_colour(float3 d, const float* sky) {
     constexpr int K = (SDEG + 1) * (SDEG + 1);
@@ -659,26 +669,37 @@ __device__ __forceinline__ RelitGeom relit_geom(const RelitArgs& a, int i, float
     return g;
 }
 
-template <int SDEG>
-__global__ void __launch_bounds__(256) k_relit_prep(RelitArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.P) return;
-    const float3 xyz = ld3(a.xyz, i);
-    const RelitGeom g = relit_geom(a, i, xyz);
-    const int rank = a.fg_rank[i];
-    if (rank >= 0) {  // the shade writes this Gaussian's whole row (ShadeArgs.viewmatrix)
-        st3(a.normal_fg, rank, g.n.x, g.n.y, g.n.z);
+// The relit features of every Gaussian in one pass: the geometry, depth and sky colour, and for
+// a foreground Gaussian the shade (shade_fwd_one) on the normal it has just computed -- one
+// launch, and the shade reads neither the normal back nor the position again (round 5 ran a
+// separate preparation kernel before the shade: the same rows bit for bit, the same
+// expressions in a TU built without FMA contraction).  The foreground normals still go to
+// normal_fg for the shade backward.
+template <int DEG, int SDEG>
+__global__ void __launch_bounds__(SHADE_THREADS) k_relit_fwd(RelitArgs ra, ShadeArgs a) {
+    constexpr int K = (DEG + 1) * (DEG + 1);
+    __shared__ float sb[K * 3];
+    if (a.N > 0)
+        for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS) sb[t] = a.base[t];
+    __syncthreads();
+    const int i = blockIdx.x * SHADE_THREADS + threadIdx.x;
+    if (i >= ra.P) return;
+    const float3 xyz = ld3(ra.xyz, i);
+    const RelitGeom g = relit_geom(ra, i, xyz);
+    const int rank = ra.fg_rank[i];
+    if (rank >= 0) {
+        st3(ra.normal_fg, rank, g.n.x, g.n.y, g.n.z);
+        shade_fwd_one<DEG>(a, (LdsCF)sb, rank, (size_t)i, g.n, xyz, ra.features, ra.features + 3, ra.features + 6);
         return;
     }
-    // depth: row 2 of W2V = column 2 of world_view_transform (gaussian_model.py:125-130)
-    const float* V = a.viewmatrix;
+    const float* V = ra.viewmatrix;
     const float depth = xyz.x * V[2] + xyz.y * V[6] + xyz.z * V[10] + V[14];
     float3 c = make_float3(1.f, 1.f, 1.f);
     if (SDEG >= 0) {
-        c = sky_colour<(SDEG < 0 ? 0 : SDEG)>(g.dir, a.sky_sh);
+        c = sky_colour<(SDEG < 0 ? 0 : SDEG)>(g.dir, ra.sky_sh);
         c = make_float3(fmaxf(c.x, 0.f), fmaxf(c.y, 0.f), fmaxf(c.z, 0.f));
     }
-    float4* o = reinterpret_cast<float4*>(a.features + (size_t)i * RELIT_STRIDE);
+    float4* o = reinterpret_cast<float4*>(ra.features + (size_t)i * RELIT_STRIDE);
     o[0] = make_float4(c.x, c.y, c.z, 0.f);
     o[1] = make_float4(0.f, 0.f, 0.f, 0.f);
     o[2] = make_float4(0.f, depth, 0.5f * g.n.x + 0.5f, 0.5f * g.n.y + 0.5f);
@@ -801,16 +822,27 @@ size_t relit_workspace_bytes(int P, int sky_deg) {
     return nb * 3 * KS * sizeof(float) + 256;
 }
 
-void launch_relit_prep(const RelitArgs& a, hipStream_t s) {
-    if (a.P == 0) return;
-    const dim3 grid((a.P + 255) / 256), blk(256);
-    switch (a.sky_deg) {
-        case 0: hipLaunchKernelGGL(k_relit_prep<0>, grid, blk, 0, s, a); break;
-        case 1: hipLaunchKernelGGL(k_relit_prep<1>, grid, blk, 0, s, a); break;
-        case 2: hipLaunchKernelGGL(k_relit_prep<2>, grid, blk, 0, s, a); break;
-        case 3: hipLaunchKernelGGL(k_relit_prep<3>, grid, blk, 0, s, a); break;
-        default: hipLaunchKernelGGL(k_relit_prep<-1>, grid, blk, 0, s, a); break;
+void launch_relit_fwd(const RelitArgs& ra, const ShadeArgs& a, hipStream_t s) {
+    if (ra.P == 0) return;
+    const dim3 grid((ra.P + SHADE_THREADS - 1) / SHADE_THREADS), blk(SHADE_THREADS);
+#define CALLR(D, S) hipLaunchKernelGGL((k_relit_fwd<D, S>), grid, blk, 0, s, ra, a)
+#define SKY(D)                          \
+    switch (ra.sky_deg) {               \
+        case 0: CALLR(D, 0); break;     \
+        case 1: CALLR(D, 1); break;     \
+        case 2: CALLR(D, 2); break;     \
+        case 3: CALLR(D, 3); break;     \
+        default: CALLR(D, -1); break;   \
     }
+    switch (a.deg) {
+        case 2: SKY(2) break;
+        case 3: SKY(3) break;
+        case 4: SKY(4) break;
+        case 5: SKY(5) break;
+        default: break;
+    }
+#undef SKY
+#undef CALLR
 }
 
 void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s) {

@@ -43,7 +43,7 @@ struct ShadeGrads {
     unsigned acc;  // ACC_ALBEDO / ACC_ROUGH / ACC_METAL: add into d_albedo / d_kr / d_km
 };
 
-// Fused relit features (gsr_shade.hip k_relit_prep / k_relit_prep_bwd).
+// Fused relit features (gsr_shade.hip k_relit_fwd / k_relit_prep_bwd).
 constexpr int RELIT_STRIDE = 16;  // feature row: rgb, diffuse, specular, depth, normal01, alpha, 0, 0
 struct RelitArgs {
     int P;
@@ -69,7 +69,9 @@ struct RelitGrads {
     unsigned acc;               // ACC_MEAN3D / ACC_ROT: add into d_xyz / d_rotation
 };
 size_t relit_workspace_bytes(int P, int sky_deg);
-void launch_relit_prep(const RelitArgs& a, hipStream_t s);
+// the relit features of all P in one launch (a: the foreground shade's arguments, whole-row
+// mode; a.N = N_fg, its rows are the Gaussians themselves)
+void launch_relit_fwd(const RelitArgs& ra, const ShadeArgs& a, hipStream_t s);
 void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s);
 
 constexpr int SHADE_THREADS = 256;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Times relit_shade.relit_features alone (forward, and forward + backward of a weighted sum of
 its 14 columns) at P Gaussians on one stream: HIP events over 50 back-to-back iterations each
-(tools only, GPU box).  The kernels: k_relit_prep, k_shade_fwd, k_shade_bwd,
+(tools only, GPU box).  The kernels: k_relit_fwd, k_shade_bwd,
 k_shade_base_reduce, k_relit_prep_bwd.
 
     GSR_LIB_PATH=... python tools/bench_relit.py [P]
