@@ -672,9 +672,8 @@ __device__ __forceinline__ RelitGeom relit_geom(const RelitArgs& a, int i, float
 // The relit features of every Gaussian in one pass: the geometry, depth and sky colour, and for
 // a foreground Gaussian the shade (shade_fwd_one) on the normal it has just computed -- one
 // launch, and the shade reads neither the normal back nor the position again (round 5 ran a
-// separate preparation kernel before the shade: the same rows bit for bit, the same
-// expressions in a TU built without FMA contraction).  The foreground normals still go to
-// normal_fg for the shade backward.
+// separate preparation kernel before the shade, with the same expressions in this
+// no-contraction TU).  The foreground normals still go to normal_fg for the shade backward.
 template <int DEG, int SDEG>
 __global__ void __launch_bounds__(SHADE_THREADS) k_relit_fwd(RelitArgs ra, ShadeArgs a) {
     constexpr int K = (DEG + 1) * (DEG + 1);
