@@ -1258,16 +1258,13 @@ int gsr_shade_backward(int N, int deg, const float* pos, const float* normal, co
 // ---- fused relit features ----------------------------------------------
 namespace {
 struct RelitWs {
-    size_t normal_fg, d_normal_fg, d_pos_fg, shade_ws, relit_ws, total;
+    size_t shade_ws, relit_ws, total;
 };
 RelitWs relit_ws_layout(int P, int N_fg, int deg, int sky_deg) {
     RelitWs w{};
     size_t t = 0;
     auto take = [&](size_t b) { const size_t o = t; t += (b + 255) & ~(size_t)255; return o; };
-    w.normal_fg = take(12 * (size_t)N_fg);
-    w.d_normal_fg = take(12 * (size_t)N_fg);
-    w.d_pos_fg = take(12 * (size_t)N_fg);
-    w.shade_ws = take(gsr::shade_workspace_bytes(N_fg, deg));
+    w.shade_ws = take(gsr::shade_workspace_bytes(P, deg));  // d_base partials per 256 Gaussians of all P
     w.relit_ws = take(gsr::relit_workspace_bytes(P, sky_deg));
     w.total = t + 256;
     return w;
@@ -1295,15 +1292,12 @@ int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation,
     hipStream_t s = reinterpret_cast<hipStream_t>(stream_);
     const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
     char* ws = align_base(workspace);
-    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, features,
-                      at<float>(ws, wl.normal_fg)};
+    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, features};
     {
         GSR_STAGE(ST_SHADE_FWD);
         // one pass over all P: geometry, sky rows, and the foreground shade in place
         // (gsr_shade.hip k_relit_fwd; the shade's rows are the Gaussians themselves)
-        gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
-                         fg_lut, specular};
-        a.rows = fg_rows;
+        gsr::ShadeArgs a{N_fg, deg, xyz, nullptr, albedo, campos, roughness, metalness, base, fg_lut, specular};
         a.io_stride = gsr::RELIT_STRIDE;
         a.vp_stride = 0;
         a.viewmatrix = viewmatrix;
@@ -1331,27 +1325,22 @@ int gsr_relit_features_backward(int P, int N_fg, const float* xyz, const float* 
     if (!dL_dfeatures || !d_xyz || !d_rotation || !workspace) return fail(GSR_E_ARG, "gsr_relit_features_backward: missing buffers");
     const RelitWs wl = relit_ws_layout(P, N_fg, deg, sky_deg);
     char* ws = align_base(workspace);
-    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, nullptr,
-                      at<float>(ws, wl.normal_fg)};
+    gsr::RelitArgs ra{P, xyz, rotation, scaling, fg_rank, sky_deg, sky_sh, campos, viewmatrix, nullptr};
     {
         GSR_STAGE(ST_SHADE_BWD);
-        if (N_fg > 0) {
-            gsr::ShadeArgs a{N_fg, deg, xyz, at<float>(ws, wl.normal_fg), albedo, campos, roughness, metalness, base,
-                             fg_lut, specular};
-            a.rows = fg_rows;
-            a.io_stride = gsr::RELIT_STRIDE;
-            a.vp_stride = 0;
-            gsr::ShadeGrads g{dL_dfeatures, dL_dfeatures + 3, specular ? dL_dfeatures + 6 : nullptr,
-                              at<float>(ws, wl.d_pos_fg), at<float>(ws, wl.d_normal_fg), d_albedo, nullptr,
-                              specular ? d_roughness : nullptr, specular ? d_metalness : nullptr, d_base};
-            g.acc = accumulate & (gsr::ACC_ALBEDO | gsr::ACC_ROUGH | gsr::ACC_METAL);
-            gsr::launch_shade_bwd(a, g, at<void>(ws, wl.shade_ws), s);
-        } else if (d_base) {
-            HIP_OK(hipMemsetAsync(d_base, 0, sizeof(float) * 3 * (deg + 1) * (deg + 1), s));
-        }
-        gsr::RelitGrads rg{dL_dfeatures, at<float>(ws, wl.d_normal_fg), at<float>(ws, wl.d_pos_fg), d_xyz, d_rotation,
-                           d_sky_sh, at<float>(ws, wl.relit_ws), accumulate & (gsr::ACC_MEAN3D | gsr::ACC_ROT)};
-        gsr::launch_relit_prep_bwd(ra, rg, s);
+        // one pass over all P (gsr_shade.hip k_relit_bwd): the foreground shade backward on the
+        // recomputed normal, then the preparation's chain; d_base / d_sky_sh by fixed-order
+        // reductions of its per-workgroup partials
+        gsr::ShadeArgs a{N_fg, deg, xyz, nullptr, albedo, campos, roughness, metalness, base, fg_lut, specular};
+        a.io_stride = gsr::RELIT_STRIDE;
+        a.vp_stride = 0;
+        gsr::ShadeGrads g{dL_dfeatures, dL_dfeatures + 3, specular ? dL_dfeatures + 6 : nullptr, nullptr, nullptr,
+                          N_fg > 0 ? d_albedo : nullptr, nullptr, (specular && N_fg > 0) ? d_roughness : nullptr,
+                          (specular && N_fg > 0) ? d_metalness : nullptr, d_base};
+        g.acc = accumulate & (gsr::ACC_ALBEDO | gsr::ACC_ROUGH | gsr::ACC_METAL);
+        gsr::RelitGrads rg{dL_dfeatures, d_xyz, d_rotation, d_sky_sh, at<float>(ws, wl.relit_ws),
+                           accumulate & (gsr::ACC_MEAN3D | gsr::ACC_ROT)};
+        gsr::launch_relit_bwd(ra, rg, a, g, at<void>(ws, wl.shade_ws), s);
     }
     GSR_LAUNCH_CHECK();
     return GSR_OK;

@@ -619,8 +619,10 @@ __global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const
 // normal = minimum-scale axis of build_rotation(q) flipped towards the camera
 // (gaussian_model.py:115-122, general_utils.py:98-170), depth = view-space z
 // (gaussian_model.py:125-130), sky colour clamp_min(eval_sh(sky_deg, sky_sh, dir) + 0.5, 0)
-// or 1 with fix_sky (__init__.py:143-148), and the foreground shade (shade_fwd_one); the
-// foreground normals also go to a compact array for the shade backward.
+// or 1 with fix_sky (__init__.py:143-148), and the foreground shade (shade_fwd_one).
+// k_relit_bwd: the shade backward and dL/dxyz (depth, sky direction, shade position),
+// dL/drotation (through the flipped minimum axis and build_rotation's normalisation),
+// dL/dsky_sh.  dL/dscaling is zero (the axis choice is an argmin).
 template <int SDEG>
 __device__ __forceinline__ float3 sky_colour(float3 d, const float* sky) {
     constexpr int K = (SDEG + 1) * (SDEG + 1);
@@ -673,7 +675,7 @@ __device__ __forceinline__ RelitGeom relit_geom(const RelitArgs& a, int i, float
 // a foreground Gaussian the shade (shade_fwd_one) on the normal it has just computed -- one
 // launch, and the shade reads neither the normal back nor the position again (round 5 ran a
 // separate preparation kernel before the shade, with the same expressions in this
-// no-contraction TU).  The foreground normals still go to normal_fg for the shade backward.
+// no-contraction TU).  k_relit_bwd recomputes the normals, so none are stored.
 template <int DEG, int SDEG>
 __global__ void __launch_bounds__(SHADE_THREADS) k_relit_fwd(RelitArgs ra, ShadeArgs a) {
     constexpr int K = (DEG + 1) * (DEG + 1);
@@ -687,7 +689,6 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_relit_fwd(RelitArgs ra, Shade
     const RelitGeom g = relit_geom(ra, i, xyz);
     const int rank = ra.fg_rank[i];
     if (rank >= 0) {
-        st3(ra.normal_fg, rank, g.n.x, g.n.y, g.n.z);
         shade_fwd_one<DEG>(a, (LdsCF)sb, rank, (size_t)i, g.n, xyz, ra.features, ra.features + 3, ra.features + 6);
         return;
     }
@@ -705,71 +706,271 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_relit_fwd(RelitArgs ra, Shade
     o[3] = make_float4(0.5f * g.n.z + 0.5f, 1.f, 0.f, 0.f);
 }
 
-// Backward of the preparation: dL/dxyz (depth, sky direction, + the shade's dL/dpos of the
-// foreground rows), dL/drotation (through the flipped minimum axis and build_rotation's
-// normalisation), per-workgroup partial dL/dsky_sh.  dL/dscaling is zero (the axis choice
-// is an argmin).
-template <int SDEG>
-__global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads gr) {
+// The relit features' backward in one pass over all P: the foreground shade backward on the
+// normal and position recomputed here (no normal / position gradient arrays between two
+// kernels), then the preparation's chain (depth, sky colour, the flipped minimum axis,
+// build_rotation's normalisation).  The d_base partials are per workgroup of 256 Gaussians
+// (sky lanes add zeros), reduced in fixed order by k_shade_base_reduce; d_sky_sh likewise.
+template <int DEG, int SDEG>
+__global__ void __launch_bounds__(SHADE_THREADS) __attribute__((amdgpu_waves_per_eu(4)))
+k_relit_bwd(RelitArgs ra, RelitGrads rg, ShadeArgs a, ShadeGrads g,
+                                                             float* ws_base) {
+    constexpr int K = (DEG + 1) * (DEG + 1);
     constexpr int KS = SDEG >= 0 ? (SDEG + 1) * (SDEG + 1) : 1;
-    __shared__ float sred[4][3 * KS];
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool valid = i < a.P;
+    __shared__ float sb[K * 3];
+    __shared__ float sred[4][K * 3];
+    __shared__ float sred2[4][3 * KS];
+    if (a.N > 0)
+        for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS) sb[t] = a.base[t];
+    __syncthreads();
+    const int i = blockIdx.x * SHADE_THREADS + threadIdx.x;
+    const bool valid = i < ra.P;
     const int ii = valid ? i : 0;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const float3 xyz = ld3(a.xyz, ii);
-    const RelitGeom g = relit_geom(a, ii, xyz);
-    const float* gf = gr.dL_dfeatures + (size_t)ii * RELIT_STRIDE;
-    const float* V = a.viewmatrix;
+    const float3 xyz = ld3(ra.xyz, ii);
+    const int rank = ra.fg_rank[ii];
+    const bool isfg = valid && rank >= 0;
+    const int ri = isfg ? rank : 0;
+    const float* gf = rg.dL_dfeatures + (size_t)ii * RELIT_STRIDE;
+    float g_p[3] = {0.f, 0.f, 0.f}, g_n[3] = {0.f, 0.f, 0.f};
+    {
+    // the shade backward (k_shade_bwd's body; a sky or invalid lane runs it on zeros)
+    const float3 n = relit_geom(ra, ii, xyz).n;
+    const float3 al = isfg ? ld3(a.albedo, ri) : make_float3(0.f, 0.f, 0.f);
+    const float x = n.x, y = n.y, z = n.z;
+    const float alc[3] = {al.x, al.y, al.z};
+    float irr_raw[3], irr[3], dh[3];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        irr_raw[c] = LC1 * sb[24 + c] * (x * x - y * y) + LC3 * sb[18 + c] * (z * z) + LC4 * sb[c] - LC5 * sb[18 + c] +
+                     LC1x2 * sb[12 + c] * x * y + LC1x2 * sb[21 + c] * x * z + LC1x2 * sb[15 + c] * y * z +
+                     LC2x2 * sb[9 + c] * x + LC2x2 * sb[3 + c] * y + LC2x2 * sb[6 + c] * z;
+        irr[c] = irr_raw[c] < 1e-4f ? 1e-4f : irr_raw[c];
+        dh[c] = alc[c] * irr[c];
+    }
+    float grgb[3] = {0.f, 0.f, 0.f}, gdif[3] = {0.f, 0.f, 0.f}, gspe[3] = {0.f, 0.f, 0.f};
+    if (isfg) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            grgb[c] = gf[c];
+            gdif[c] = gf[3 + c];
+            gspe[c] = a.specular ? gf[6 + c] : 0.f;
+        }
+    }
+    float g_dh[3], g_a[3] = {0.f, 0.f, 0.f};
+    float g_vp[3] = {0.f, 0.f, 0.f}, g_si[3] = {0.f, 0.f, 0.f};
+    float g_kr = 0.f, g_km = 0.f;
+#pragma unroll
+    for (int c = 0; c < 3; c++) g_dh[c] = gdif[c] * gamma_d(dh[c]);
+    float Y[K], gw[DEG + 1], gi[3];
+    // dL/d(diffuse irradiance) once g_dh is final
+    auto diffuse_gi = [&]() {
+#pragma unroll
+        for (int c = 0; c < 3; c++) gi[c] = irr_raw[c] >= 1e-4f ? g_dh[c] * alc[c] : 0.f;
+    };
+    // d_base[k][c] = sum_i Y_k gw_l g_si[c] (+ diffuse coefficients for k < 9): this
+    // workgroup's partial sums into sred, taken while Y is live and before the SH-gradient
+    // phase (so that Y and that phase's registers are never live together)
+    auto base_partials = [&]() {
+        if (!g.d_base) return;
+        const float dco[9] = {LC4, LC2x2 * y, LC2x2 * z, LC2x2 * x, LC1x2 * x * y, LC1x2 * y * z, LC3 * z * z - LC5,
+                              LC1x2 * x * z, LC1 * (x * x - y * y)};
+        // the 3K wave sums in chunks of 12 values, each one transposed butterfly
+        // (gsr_tile.hpp wave_multi_sum; chunks keep the live registers small)
+        const int vi = wave_multi_sum_index(lane);
+#pragma unroll
+        for (int e0 = 0; e0 < 3 * K; e0 += 12) {
+            float vb[12];
+#pragma unroll
+            for (int t = 0; t < 12; t++) {
+                const int e = e0 + t, k = e / 3, c = e - 3 * k;
+                float v = 0.f;
+                if (e < 3 * K) {
+                    const int l = k < 1 ? 0 : k < 4 ? 1 : k < 9 ? 2 : k < 16 ? 3 : k < 25 ? 4 : 5;
+                    v = Y[k] * gw[l] * g_si[c];
+                    if (k < 9) v += gi[c] * dco[k < 9 ? k : 0];
+                }
+                vb[t] = isfg ? v : 0.f;
+            }
+            const float red = wave_multi_sum<12>(vb);
+            if ((lane & 15) < 3 && e0 + vi < 3 * K) sred[wave][e0 + vi] = red;
+        }
+    };
+    if (!a.specular) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) g_dh[c] += grgb[c] * gamma_d(dh[c]);
+#pragma unroll
+        for (int k = 0; k < K; k++) Y[k] = 0.f;
+#pragma unroll
+        for (int l = 0; l <= DEG; l++) gw[l] = 0.f;
+        diffuse_gi();
+        base_partials();
+    } else {
+        const float3 p = xyz;
+        const float3 vp = ld3s(a.view_pos, ri, a.vp_stride);
+        const float kr = isfg ? a.kr[ri] : 0.f;
+        const float km = (a.km && isfg) ? a.km[ri] : 0.f;
+        const float wv[3] = {vp.x - p.x, vp.y - p.y, vp.z - p.z};
+        const float l2 = wv[0] * wv[0] + wv[1] * wv[1] + wv[2] * wv[2];
+        const bool lclamp = l2 < 1e-20f;
+        const float len = sqrtf(lclamp ? 1e-20f : l2);
+        const float wo[3] = {wv[0] / len, wv[1] / len, wv[2] / len};
+        const float nn[3] = {x, y, z};
+        const float dwn = wo[0] * x + wo[1] * y + wo[2] * z;
+        float rv[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) rv[c] = 2 * dwn * nn[c] - wo[c];
+        const float rl2 = rv[0] * rv[0] + rv[1] * rv[1] + rv[2] * rv[2];
+        const bool rclamp = rl2 < 1e-20f;
+        const float rlen = sqrtf(rclamp ? 1e-20f : rl2);
+        const float r[3] = {rv[0] / rlen, rv[1] / rlen, rv[2] / rlen};
+        const float ndv = dwn < 1e-4f ? 1e-4f : dwn;
+        float fg[2], fgu[2], fgv[2];
+        lut_fetch<true>(a.lut, ndv, kr, fg, fgu, fgv);
+        sh_basis<DEG, false>(r[0], r[1], r[2], Y, nullptr, nullptr, nullptr);
+#pragma unroll
+        for (int l = 0; l <= DEG; l++) gw[l] = __expf((float)(-l * (l + 1)) * (0.3f * kr));
+        float g_fg0 = 0.f, g_fg1 = 0.f, g_r[3] = {0.f, 0.f, 0.f};
+        float g_gw[DEG + 1];
+#pragma unroll
+        for (int l = 0; l <= DEG; l++) g_gw[l] = 0.f;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            float si_raw = 0.f;
+#pragma unroll
+            for (int l = 0, k = 0; l <= DEG; l++)
+#pragma unroll
+                for (int m = 0; m < 2 * l + 1; m++, k++) si_raw += Y[k] * (gw[l] * sb[3 * k + c]);
+            const float si = si_raw < 1e-4f ? 1e-4f : si_raw;
+            const float F0 = a.km ? (1.0f - km) * 0.04f + alc[c] * km : 0.04f;
+            const float refl = F0 * fg[0] + fg[1];
+            const float sh_hdr = si * refl;
+            const float shaded = a.km ? (1 - km) * dh[c] + sh_hdr : dh[c] + sh_hdr;
+            const float g_sh = grgb[c] * gamma_d(shaded);
+            const float g_hdr = g_sh + gspe[c] * gamma_d(sh_hdr);
+            if (a.km) {
+                g_dh[c] += (1 - km) * g_sh;
+                g_km += -dh[c] * g_sh;
+            } else {
+                g_dh[c] += g_sh;
+            }
+            g_si[c] = si_raw >= 1e-4f ? g_hdr * refl : 0.f;
+            const float g_refl = g_hdr * si;
+            const float g_F0 = g_refl * fg[0];
+            g_fg0 += g_refl * F0;
+            g_fg1 += g_refl;
+            if (a.km) {
+                g_km += (alc[c] - 0.04f) * g_F0;
+                g_a[c] += km * g_F0;
+            }
+        }
+        diffuse_gi();
+        base_partials();
+        {
+            float sk[K];
+#pragma unroll
+            for (int l = 0, k = 0; l <= DEG; l++)
+#pragma unroll
+                for (int m = 0; m < 2 * l + 1; m++, k++) {
+                    const float bs = sb[3 * k] * g_si[0] + sb[3 * k + 1] * g_si[1] + sb[3 * k + 2] * g_si[2];
+                    g_gw[l] += Y[k] * bs;
+                    sk[k] = gw[l] * bs;
+                }
+            // d si / d r through the basis gradients, accumulated term by term
+            sh_grad_dot<DEG>(r[0], r[1], r[2], sk, g_r[0], g_r[1], g_r[2]);
+        }
+#pragma unroll
+        for (int l = 0; l <= DEG; l++) g_kr += g_gw[l] * gw[l] * ((float)(-l * (l + 1)) * 0.3f);
+        const float g_ndv = g_fg0 * fgu[0] + g_fg1 * fgu[1];
+        g_kr += g_fg0 * fgv[0] + g_fg1 * fgv[1];
+        const float rdg = r[0] * g_r[0] + r[1] * g_r[1] + r[2] * g_r[2];
+        float g_rv[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) g_rv[c] = rclamp ? g_r[c] / rlen : (g_r[c] - r[c] * rdg) / rlen;
+        float g_dwn = 2 * (x * g_rv[0] + y * g_rv[1] + z * g_rv[2]);
+        if (dwn >= 1e-4f) g_dwn += g_ndv;
+        float g_wo[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            g_n[c] += 2 * dwn * g_rv[c] + g_dwn * wo[c];
+            g_wo[c] = -g_rv[c] + g_dwn * nn[c];
+        }
+        const float wdg = wo[0] * g_wo[0] + wo[1] * g_wo[1] + wo[2] * g_wo[2];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            const float gwv = lclamp ? g_wo[c] / len : (g_wo[c] - wo[c] * wdg) / len;
+            g_vp[c] += gwv;
+            g_p[c] -= gwv;
+        }
+    }
+    // diffuse irradiance backward
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        g_a[c] += g_dh[c] * irr[c];
+        g_n[0] += gi[c] * (LC1 * sb[24 + c] * 2 * x + LC1x2 * sb[12 + c] * y + LC1x2 * sb[21 + c] * z + LC2x2 * sb[9 + c]);
+        g_n[1] += gi[c] * (-LC1 * sb[24 + c] * 2 * y + LC1x2 * sb[12 + c] * x + LC1x2 * sb[15 + c] * z + LC2x2 * sb[3 + c]);
+        g_n[2] += gi[c] * (LC3 * sb[18 + c] * 2 * z + LC1x2 * sb[21 + c] * x + LC1x2 * sb[15 + c] * y + LC2x2 * sb[6 + c]);
+    }
+    if (isfg) {
+        if (g.d_albedo) {
+            if (g.acc & ACC_ALBEDO) st3(g.d_albedo, ri, g.d_albedo[3 * ri] + g_a[0], g.d_albedo[3 * ri + 1] + g_a[1],
+                                        g.d_albedo[3 * ri + 2] + g_a[2]);
+            else st3(g.d_albedo, ri, g_a[0], g_a[1], g_a[2]);
+        }
+        if (g.d_kr) g.d_kr[ri] = (g.acc & ACC_ROUGH) ? g.d_kr[ri] + g_kr : g_kr;
+        if (g.d_km) g.d_km[ri] = (g.acc & ACC_METAL) ? g.d_km[ri] + g_km : g_km;
+    }
+    }
+    // the preparation's backward, geometry recomputed
+    const RelitGeom geo = relit_geom(ra, ii, xyz);
+    const float* V = ra.viewmatrix;
     float gx = gf[9] * V[2], gy = gf[9] * V[6], gz = gf[9] * V[10];
     float3 gn = make_float3(0.5f * gf[10], 0.5f * gf[11], 0.5f * gf[12]);
-    const int rank = a.fg_rank[ii];
     float Yk[KS];
     float gcol[3] = {0.f, 0.f, 0.f};
     if (rank >= 0) {
-        const float3 dn = ld3(gr.d_normal_fg, rank), dpos = ld3(gr.d_pos_fg, rank);
-        gn.x += dn.x; gn.y += dn.y; gn.z += dn.z;
-        gx += dpos.x; gy += dpos.y; gz += dpos.z;
+        gn.x += g_n[0]; gn.y += g_n[1]; gn.z += g_n[2];
+        gx += g_p[0]; gy += g_p[1]; gz += g_p[2];
 #pragma unroll
         for (int k = 0; k < KS; k++) Yk[k] = 0.f;
     } else if (SDEG >= 0) {
         constexpr int SD = SDEG < 0 ? 0 : SDEG;
-        sh_basis<SD, false>(g.dir.x, g.dir.y, g.dir.z, Yk, nullptr, nullptr, nullptr);
+        sh_basis<SD, false>(geo.dir.x, geo.dir.y, geo.dir.z, Yk, nullptr, nullptr, nullptr);
         float raw[3];
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) {
             float v = 0.f;
 #pragma unroll
-            for (int k = 0; k < KS; k++) v = __builtin_fmaf(Yk[k], a.sky_sh[3 * k + ch], v);
+            for (int k = 0; k < KS; k++) v = __builtin_fmaf(Yk[k], ra.sky_sh[3 * k + ch], v);
             raw[ch] = v + 0.5f;
             gcol[ch] = raw[ch] >= 0.f ? gf[ch] : 0.f;  // clamp_min backward passes at the bound
         }
         float s[KS];
 #pragma unroll
         for (int k = 0; k < KS; k++)
-            s[k] = a.sky_sh[3 * k] * gcol[0] + a.sky_sh[3 * k + 1] * gcol[1] + a.sky_sh[3 * k + 2] * gcol[2];
+            s[k] = ra.sky_sh[3 * k] * gcol[0] + ra.sky_sh[3 * k + 1] * gcol[1] + ra.sky_sh[3 * k + 2] * gcol[2];
         float gd[3];
-        sh_grad_dot<SD>(g.dir.x, g.dir.y, g.dir.z, s, gd[0], gd[1], gd[2]);
+        sh_grad_dot<SD>(geo.dir.x, geo.dir.y, geo.dir.z, s, gd[0], gd[1], gd[2]);
         // safe_normalize backward (x / sqrt(clamp(x.x, 1e-20)))
-        const float dg = g.dir.x * gd[0] + g.dir.y * gd[1] + g.dir.z * gd[2];
-        const bool clamped = g.len * g.len < 1e-20f;
-        gx += clamped ? gd[0] / g.len : (gd[0] - g.dir.x * dg) / g.len;
-        gy += clamped ? gd[1] / g.len : (gd[1] - g.dir.y * dg) / g.len;
-        gz += clamped ? gd[2] / g.len : (gd[2] - g.dir.z * dg) / g.len;
+        const float dg = geo.dir.x * gd[0] + geo.dir.y * gd[1] + geo.dir.z * gd[2];
+        const bool clamped = geo.len * geo.len < 1e-20f;
+        gx += clamped ? gd[0] / geo.len : (gd[0] - geo.dir.x * dg) / geo.len;
+        gy += clamped ? gd[1] / geo.len : (gd[1] - geo.dir.y * dg) / geo.len;
+        gz += clamped ? gd[2] / geo.len : (gd[2] - geo.dir.z * dg) / geo.len;
     } else {
 #pragma unroll
         for (int k = 0; k < KS; k++) Yk[k] = 0.f;
     }
     // normal -> axis (undo the flip) -> column of R -> q -> rotation
-    const float ga0 = g.keep ? gn.x : -gn.x, ga1 = g.keep ? gn.y : -gn.y, ga2 = g.keep ? gn.z : -gn.z;
-    const float qr = g.q.x, qx = g.q.y, qy = g.q.z, qz = g.q.w;
+    const float ga0 = geo.keep ? gn.x : -gn.x, ga1 = geo.keep ? gn.y : -gn.y, ga2 = geo.keep ? gn.z : -gn.z;
+    const float qr = geo.q.x, qx = geo.q.y, qy = geo.q.z, qz = geo.q.w;
     float gqr, gqx, gqy, gqz;
-    if (g.axis == 0) {  // (1 - 2(y^2 + z^2), 2(xy + rz), 2(xz - ry))
+    if (geo.axis == 0) {  // (1 - 2(y^2 + z^2), 2(xy + rz), 2(xz - ry))
         gqr = 2 * (qz * ga1 - qy * ga2);
         gqx = 2 * (qy * ga1 + qz * ga2);
         gqy = -4 * qy * ga0 + 2 * (qx * ga1 - qr * ga2);
         gqz = -4 * qz * ga0 + 2 * (qr * ga1 + qx * ga2);
-    } else if (g.axis == 1) {  // (2(xy - rz), 1 - 2(x^2 + z^2), 2(yz + rx))
+    } else if (geo.axis == 1) {  // (2(xy - rz), 1 - 2(x^2 + z^2), 2(yz + rx))
         gqr = 2 * (-qz * ga0 + qx * ga2);
         gqx = 2 * (qy * ga0 + qr * ga2) - 4 * qx * ga1;
         gqy = 2 * (qx * ga0 + qz * ga2);
@@ -783,36 +984,42 @@ __global__ void __launch_bounds__(256) k_relit_prep_bwd(RelitArgs a, RelitGrads 
     // q = r / |r|
     const float qg = qr * gqr + qx * gqx + qy * gqy + qz * gqz;
     if (valid) {
-        if (gr.acc & ACC_MEAN3D)
-            st3(gr.d_xyz, i, gr.d_xyz[3 * i] + gx, gr.d_xyz[3 * i + 1] + gy, gr.d_xyz[3 * i + 2] + gz);
+        if (rg.acc & ACC_MEAN3D)
+            st3(rg.d_xyz, i, rg.d_xyz[3 * i] + gx, rg.d_xyz[3 * i + 1] + gy, rg.d_xyz[3 * i + 2] + gz);
         else
-            st3(gr.d_xyz, i, gx, gy, gz);
-        float4 dr = make_float4((gqr - qr * qg) / g.qn, (gqx - qx * qg) / g.qn, (gqy - qy * qg) / g.qn,
-                                (gqz - qz * qg) / g.qn);
-        float4* rp = reinterpret_cast<float4*>(gr.d_rotation + 4 * (size_t)i);
-        if (gr.acc & ACC_ROT) {
+            st3(rg.d_xyz, i, gx, gy, gz);
+        float4 dr = make_float4((gqr - qr * qg) / geo.qn, (gqx - qx * qg) / geo.qn, (gqy - qy * qg) / geo.qn,
+                                (gqz - qz * qg) / geo.qn);
+        float4* rp = reinterpret_cast<float4*>(rg.d_rotation + 4 * (size_t)i);
+        if (rg.acc & ACC_ROT) {
             const float4 o = *rp;
             dr = make_float4(o.x + dr.x, o.y + dr.y, o.z + dr.z, o.w + dr.w);
         }
         *rp = dr;
     }
-    if (SDEG < 0 || !gr.d_sky_sh) return;
-    // dL/dsky_sh[k][c] = sum over sky Gaussians of Y_k(dir) gcol[c]: per-workgroup slab
-    const int vi = wave_multi_sum_index(lane);
+    if (SDEG >= 0 && rg.d_sky_sh) {
+        // dL/dsky_sh[k][c] = sum over sky Gaussians of Y_k(dir) gcol[c]
+        const int vi = wave_multi_sum_index(lane);
 #pragma unroll
-    for (int e0 = 0; e0 < 3 * KS; e0 += 12) {
-        float vb[12];
+        for (int e0 = 0; e0 < 3 * KS; e0 += 12) {
+            float vb[12];
 #pragma unroll
-        for (int t = 0; t < 12; t++) {
-            const int e = e0 + t, k = e / 3, c = e - 3 * k;
-            vb[t] = (valid && e < 3 * KS) ? Yk[k < KS ? k : 0] * gcol[c] : 0.f;
+            for (int t = 0; t < 12; t++) {
+                const int e = e0 + t, k = e / 3, c = e - 3 * k;
+                vb[t] = (valid && e < 3 * KS) ? Yk[k < KS ? k : 0] * gcol[c] : 0.f;
+            }
+            const float red = wave_multi_sum<12>(vb);
+            if ((lane & 15) < 3 && e0 + vi < 3 * KS) sred2[wave][e0 + vi] = red;
         }
-        const float red = wave_multi_sum<12>(vb);
-        if ((lane & 15) < 3 && e0 + vi < 3 * KS) sred[wave][e0 + vi] = red;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < 3 * KS; t += 256)
-        gr.workspace[(size_t)t * gridDim.x + blockIdx.x] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+    if (g.d_base)
+        for (int t = threadIdx.x; t < K * 3; t += SHADE_THREADS)
+            ws_base[(size_t)t * gridDim.x + blockIdx.x] = sred[0][t] + sred[1][t] + sred[2][t] + sred[3][t];
+    if (SDEG >= 0 && rg.d_sky_sh)
+        for (int t = threadIdx.x; t < 3 * KS; t += SHADE_THREADS)
+            rg.workspace[(size_t)t * gridDim.x + blockIdx.x] =
+                sred2[0][t] + sred2[1][t] + sred2[2][t] + sred2[3][t];
 }
 
 size_t relit_workspace_bytes(int P, int sky_deg) {
@@ -844,24 +1051,42 @@ void launch_relit_fwd(const RelitArgs& ra, const ShadeArgs& a, hipStream_t s) {
 #undef CALLR
 }
 
-void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s) {
-    if (a.P == 0) {
-        if (g.d_sky_sh && a.sky_deg >= 0)
-            (void)hipMemsetAsync(g.d_sky_sh, 0, sizeof(float) * 3 * (a.sky_deg + 1) * (a.sky_deg + 1), s);
+void launch_relit_bwd(const RelitArgs& ra, const RelitGrads& rg, const ShadeArgs& a, const ShadeGrads& g,
+                      void* ws_base, hipStream_t s) {
+    if (ra.P == 0) {
+        if (g.d_base) (void)hipMemsetAsync(g.d_base, 0, sizeof(float) * 3 * (a.deg + 1) * (a.deg + 1), s);
+        if (rg.d_sky_sh && ra.sky_deg >= 0)
+            (void)hipMemsetAsync(rg.d_sky_sh, 0, sizeof(float) * 3 * (ra.sky_deg + 1) * (ra.sky_deg + 1), s);
         return;
     }
-    const int nb = (a.P + 255) / 256;
-    const dim3 grid(nb), blk(256);
-    switch (a.sky_deg) {
-        case 0: hipLaunchKernelGGL(k_relit_prep_bwd<0>, grid, blk, 0, s, a, g); break;
-        case 1: hipLaunchKernelGGL(k_relit_prep_bwd<1>, grid, blk, 0, s, a, g); break;
-        case 2: hipLaunchKernelGGL(k_relit_prep_bwd<2>, grid, blk, 0, s, a, g); break;
-        case 3: hipLaunchKernelGGL(k_relit_prep_bwd<3>, grid, blk, 0, s, a, g); break;
-        default: hipLaunchKernelGGL(k_relit_prep_bwd<-1>, grid, blk, 0, s, a, g); break;
+    const int nb = (ra.P + SHADE_THREADS - 1) / SHADE_THREADS;
+    const dim3 grid(nb), blk(SHADE_THREADS);
+    float* wsb = reinterpret_cast<float*>(ws_base);
+#define CALLR(D, S) hipLaunchKernelGGL((k_relit_bwd<D, S>), grid, blk, 0, s, ra, rg, a, g, wsb)
+#define SKY(D)                          \
+    switch (ra.sky_deg) {               \
+        case 0: CALLR(D, 0); break;     \
+        case 1: CALLR(D, 1); break;     \
+        case 2: CALLR(D, 2); break;     \
+        case 3: CALLR(D, 3); break;     \
+        default: CALLR(D, -1); break;   \
     }
-    if (g.d_sky_sh && a.sky_deg >= 0) {
-        const int KC = 3 * (a.sky_deg + 1) * (a.sky_deg + 1);
-        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, g.workspace, g.d_sky_sh);
+    switch (a.deg) {
+        case 2: SKY(2) break;
+        case 3: SKY(3) break;
+        case 4: SKY(4) break;
+        case 5: SKY(5) break;
+        default: break;
+    }
+#undef SKY
+#undef CALLR
+    if (g.d_base) {
+        const int KC = 3 * (a.deg + 1) * (a.deg + 1);
+        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, wsb, g.d_base);
+    }
+    if (rg.d_sky_sh && ra.sky_deg >= 0) {
+        const int KC = 3 * (ra.sky_deg + 1) * (ra.sky_deg + 1);
+        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, rg.workspace, rg.d_sky_sh);
     }
 }
 

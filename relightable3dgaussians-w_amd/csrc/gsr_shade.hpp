@@ -43,7 +43,7 @@ struct ShadeGrads {
     unsigned acc;  // ACC_ALBEDO / ACC_ROUGH / ACC_METAL: add into d_albedo / d_kr / d_km
 };
 
-// Fused relit features (gsr_shade.hip k_relit_fwd / k_relit_prep_bwd).
+// Fused relit features (gsr_shade.hip k_relit_fwd / k_relit_bwd).
 constexpr int RELIT_STRIDE = 16;  // feature row: rgb, diffuse, specular, depth, normal01, alpha, 0, 0
 struct RelitArgs {
     int P;
@@ -56,12 +56,9 @@ struct RelitArgs {
     const float* campos;    // [3]
     const float* viewmatrix;  // world_view_transform, row-major [4,4]
     float* features;        // [P][RELIT_STRIDE]
-    float* normal_fg;       // [N_fg,3]
 };
 struct RelitGrads {
     const float* dL_dfeatures;  // [P][RELIT_STRIDE]
-    const float* d_normal_fg;   // [N_fg,3] from the shade backward
-    const float* d_pos_fg;      // [N_fg,3] from the shade backward
     float* d_xyz;               // [P,3]
     float* d_rotation;          // [P,4]
     float* d_sky_sh;            // [(sky_deg+1)^2][3] or null
@@ -72,7 +69,10 @@ size_t relit_workspace_bytes(int P, int sky_deg);
 // the relit features of all P in one launch (a: the foreground shade's arguments, whole-row
 // mode; a.N = N_fg, its rows are the Gaussians themselves)
 void launch_relit_fwd(const RelitArgs& ra, const ShadeArgs& a, hipStream_t s);
-void launch_relit_prep_bwd(const RelitArgs& a, const RelitGrads& g, hipStream_t s);
+// the relit features' backward over all P in one launch (+ the fixed-order d_base and d_sky_sh
+// reductions): ws_base holds shade_workspace_bytes(P, deg)
+void launch_relit_bwd(const RelitArgs& ra, const RelitGrads& rg, const ShadeArgs& a, const ShadeGrads& g,
+                      void* ws_base, hipStream_t s);
 
 constexpr int SHADE_THREADS = 256;
 size_t shade_workspace_bytes(int N, int deg);
