@@ -600,15 +600,24 @@ __global__ void __launch_bounds__(SHADE_THREADS) k_shade_bwd(ShadeArgs a, ShadeG
 
 // fixed-order reduction of the per-workgroup d_base slabs: one workgroup per output value; the
 // slabs are stored value-major (ws[value][workgroup]), so each reads one contiguous row
-__global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const float* ws, float* d_base) {
+// KC2 / ws2 / out2: a second slab set reduced by the blocks past KC (the relit backward's
+// dL/dsky_sh beside its dL/dbase: one launch for both)
+__global__ void __launch_bounds__(256) k_shade_base_reduce(int nb, int KC, const float* ws, float* d_base, int KC2 = 0,
+                                                           const float* ws2 = nullptr, float* out2 = nullptr) {
     __shared__ float sh[4];
     float v = 0.f;
-    const float* row = ws + (size_t)blockIdx.x * nb;
+    int blk = blockIdx.x;
+    if (blk >= KC) {  // the second set
+        blk -= KC;
+        ws = ws2;
+        d_base = out2;
+    }
+    const float* row = ws + (size_t)blk * nb;
     for (int b = threadIdx.x; b < nb; b += 256) v += row[b];
     v = wave_reduce_sum(v);
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
     __syncthreads();
-    if (threadIdx.x == 0) d_base[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+    if (threadIdx.x == 0) d_base[blk] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
 // ---- fused relit features ------------------------------------------------
@@ -1080,14 +1089,12 @@ void launch_relit_bwd(const RelitArgs& ra, const RelitGrads& rg, const ShadeArgs
     }
 #undef SKY
 #undef CALLR
-    if (g.d_base) {
-        const int KC = 3 * (a.deg + 1) * (a.deg + 1);
-        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, wsb, g.d_base);
-    }
-    if (rg.d_sky_sh && ra.sky_deg >= 0) {
-        const int KC = 3 * (ra.sky_deg + 1) * (ra.sky_deg + 1);
-        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KC), dim3(256), 0, s, nb, KC, rg.workspace, rg.d_sky_sh);
-    }
+    // both fixed-order reductions in one launch
+    const int KB = g.d_base ? 3 * (a.deg + 1) * (a.deg + 1) : 0;
+    const int KSK = (rg.d_sky_sh && ra.sky_deg >= 0) ? 3 * (ra.sky_deg + 1) * (ra.sky_deg + 1) : 0;
+    if (KB + KSK > 0)
+        hipLaunchKernelGGL(k_shade_base_reduce, dim3(KB + KSK), dim3(256), 0, s, nb, KB, wsb, g.d_base, KSK,
+                           (const float*)rg.workspace, rg.d_sky_sh);
 }
 
 size_t shade_workspace_bytes(int N, int deg) {
