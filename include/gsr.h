@@ -169,9 +169,10 @@ int gsr_backward_channels(int P, int nch, int feature_stride, const float* featu
  *           nullable), and for sky Gaussians clamp_min(eval_sh(sky_deg, sky_sh, dir) + 0.5, 0)
  *           (sky_deg = -1: 1, fix_sky) with diffuse = specular = 0.
  * fg_rank [P] holds each Gaussian's rank among the foreground ones (-1: sky) and fg_rows
- * [N_fg] the inverse map.  workspace: gsr_relit_workspace_bytes, kept from the forward to
- * the backward (it holds the foreground normals).  features must be 16-B aligned (each
- * 64-B row is written whole by one kernel). */
+ * [N_fg] the inverse map (validated, not read: one kernel runs over all P by fg_rank).
+ * workspace: gsr_relit_workspace_bytes, scratch for the backward's per-workgroup partial
+ * sums (the forward leaves it untouched; the backward recomputes the normals).  features
+ * must be 16-B aligned (each 64-B row is written whole by one thread). */
 size_t gsr_relit_workspace_bytes(int P, int N_fg, int deg, int sky_deg);
 int gsr_relit_features(int P, int N_fg, const float* xyz, const float* rotation, const float* scaling,
                        const int* fg_rank, const int* fg_rows, const float* albedo, const float* roughness,
