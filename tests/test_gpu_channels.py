@@ -89,6 +89,16 @@ def test_channels_match_separate_calls(ks):
         assert _rel(a, b) < 1e-5, (name, _rel(a, b))
 
 
+@pytest.mark.parametrize("ks", [(3, 3, 3, 1, 3, 1), (3, 2)])
+def test_channels_match_separate_calls_exact(ks):
+    """Exact blend mode (gsr_set_exact_blend) in both: the composite's channels equal the separate
+    exact-mode 3-channel calls bit for bit (their blend arithmetic is the same expression per
+    channel), the gradients as in the default mode."""
+    from gsr import _lib
+    with _lib.exact_blend_mode():
+        test_channels_match_separate_calls(ks)
+
+
 def test_channels_heavy_tiles_and_ragged():
     """Dense centre (heavy-tile quadrant split) on a ragged image size."""
     dgr, g, s = _setup(P=40000, W=133, H=77, seed=5, camera="identity")
