@@ -1,8 +1,7 @@
 #!/usr/bin/env python
 """Times relit_shade.relit_features alone (forward, and forward + backward of a weighted sum of
 its 14 columns) at P Gaussians on one stream: HIP events over 50 back-to-back iterations each
-(tools only, GPU box).  The kernels: k_relit_fwd, k_shade_bwd,
-k_shade_base_reduce, k_relit_prep_bwd.
+(tools only, GPU box).  The kernels: k_relit_fwd, then k_relit_bwd and k_shade_base_reduce.
 
     GSR_LIB_PATH=... python tools/bench_relit.py [P]
 """
