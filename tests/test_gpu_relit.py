@@ -88,11 +88,16 @@ def _composition(xyz, q, s, is_sky, mat, sky_sh, light, campos, wvt, specular=Tr
     n = axis * torch.where(keep, 1, -1)
     fg = ~is_sky
     P = xyz.shape[0]
-    rgb, ex = relit_shade.shade(light, xyz[fg][None, None], n[fg][None, None], mat["albedo"][None, None],
-                                campos.expand(int(fg.sum()), 3)[None, None], mat["roughness"][None, None],
-                                mat["metalness"][None, None], specular=specular)
     cols = torch.zeros(P, 3, device="cuda")
-    cols[fg] = rgb[0, 0]
+    dif = torch.zeros(P, 3, device="cuda")
+    spe = torch.zeros(P, 3, device="cuda")
+    if fg.any():  # render() shades only when it has foreground Gaussians
+        rgb, ex = relit_shade.shade(light, xyz[fg][None, None], n[fg][None, None], mat["albedo"][None, None],
+                                    campos.expand(int(fg.sum()), 3)[None, None], mat["roughness"][None, None],
+                                    mat["metalness"][None, None], specular=specular)
+        cols[fg] = rgb[0, 0]
+        dif[fg] = ex["diffuse"][0, 0]
+        spe[fg] = ex["specular"][0, 0]
     if fix_sky:
         cols[is_sky] = 1.0
     else:
@@ -100,19 +105,21 @@ def _composition(xyz, q, s, is_sky, mat, sky_sh, light, campos, wvt, specular=Tr
         sh = sky_sh[0]
         v = C0 * sh[0] - C1 * dd[:, 1:2] * sh[1] + C1 * dd[:, 2:3] * sh[2] - C1 * dd[:, 0:1] * sh[3]
         cols[is_sky] = torch.clamp_min(v + 0.5, 0.0)
-    dif = torch.zeros(P, 3, device="cuda")
-    dif[fg] = ex["diffuse"][0, 0]
-    spe = torch.zeros(P, 3, device="cuda")
-    spe[fg] = ex["specular"][0, 0]
     p_hom = torch.cat([xyz, torch.ones_like(xyz[:, :1])], -1).unsqueeze(-1)
     depth = torch.matmul(wvt.transpose(0, 1), p_hom)[:, 2]
     return torch.cat([cols, dif, spe, depth, 0.5 * n + 0.5, torch.ones(P, 1, device="cuda")], 1)
 
 
-@pytest.mark.parametrize("specular,fix_sky", [(True, False), (False, False), (True, True)])
-def test_relit_features_match_composition(specular, fix_sky):
+@pytest.mark.parametrize("specular,fix_sky,P,n_sky", [(True, False, 4000, 400), (False, False, 4000, 400),
+                                                      (True, True, 4000, 400),
+                                                      # edge cases of the fused kernels' fg/sky ranks: no sky,
+                                                      # a ragged last workgroup, a lone foreground Gaussian,
+                                                      # no foreground at all
+                                                      (True, False, 4000, 0), (True, False, 257, 1),
+                                                      (True, False, 300, 299), (True, False, 300, 300)])
+def test_relit_features_match_composition(specular, fix_sky, P, n_sky):
     import relit_shade
-    xyz, q, s, is_sky, mat, sky_sh, campos, wvt = _scene()
+    xyz, q, s, is_sky, mat, sky_sh, campos, wvt = _scene(P=P, n_sky=n_sky)
     light = _light()
     leaves = lambda: [t.clone().requires_grad_(True) for t in (xyz, q, mat["albedo"], mat["roughness"],
                                                                  mat["metalness"], light.base, sky_sh)]
